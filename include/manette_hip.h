@@ -1,0 +1,161 @@
+/*
+ * manette_hip.h — C ABI of libmanette_hip.so, the MI355X (gfx950) device side of the
+ * PAAC+FiGAR rollout/update hot path.
+ *
+ * Conventions (every entry point):
+ *   - returns int status, MT_OK (0) on success; mt_last_error() gives the message of the
+ *     last failure on the calling thread;
+ *   - every buffer is a caller-owned DEVICE pointer unless the name says _host; the library
+ *     never allocates or synchronises inside a launch function, so each call can be captured
+ *     into a hipGraph (mt_graph_*);
+ *   - `stream` is a hipStream_t (NULL = the legacy default stream);
+ *   - tensors are dense, row-major, NHWC for images, TF variable layouts for parameters
+ *     (conv HWIO, dense (in, out)), fp32 arithmetic.
+ *
+ * Which reference interface each entry point replaces is cited per function
+ * (paths relative to the reference repo andres-quintela/manette).
+ */
+#ifndef MANETTE_HIP_H
+#define MANETTE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *mt_stream_t; /* hipStream_t */
+
+enum {
+  MT_OK = 0,
+  MT_ERR_ARG = 1,         /* bad argument (shape, null pointer, out of range) */
+  MT_ERR_HIP = 2,         /* a HIP runtime call failed */
+  MT_ERR_UNSUPPORTED = 3, /* configuration not built into this library */
+  MT_ERR_WORKSPACE = 4    /* workspace smaller than mt_net_workspace_bytes() */
+};
+
+/* --arch values of train.py:100 (networks.py:178-278). */
+enum { MT_ARCH_NIPS = 0, MT_ARCH_NATURE = 1, MT_ARCH_PWYX = 2, MT_ARCH_LSTM = 3 };
+/* --activation values of train.py:117 (networks.py:27-31). */
+enum { MT_ACT_RELU = 0, MT_ACT_LEAKY = 1 };
+/* --clip_norm_type values of train.py:96 (actor_learner.py:55-72). */
+enum { MT_CLIP_IGNORE = 0, MT_CLIP_GLOBAL = 1 };
+
+/* Number of fp32 partial sums mt_grad_sumsq writes (and mt_clip_rmsprop reads). */
+#define MT_NORM_PARTIALS 512
+
+/* Network configuration: the `network_conf` dict of train.py:52-63. */
+typedef struct mt_net_config {
+  int32_t arch;          /* MT_ARCH_* */
+  int32_t depth;         /* 1 = gray, 3 = --rgb; input channels = 4*depth (networks.py:152) */
+  int32_t num_actions;   /* A: ALE minimal action set size (environment_creator.py:28) */
+  int32_t num_reps;      /* R = --nb_choices (exploration_policy.py:48) */
+  int32_t activation;    /* MT_ACT_* */
+  float alpha_leaky;     /* --alpha_leaky_relu */
+  float softmax_temp;    /* --softmax_temp (networks.py:91-98) */
+} mt_net_config;
+
+typedef struct mt_net mt_net;
+
+const char *mt_last_error(void);
+int mt_version(void);
+
+/* ---- network description / parameter layout -------------------------------------------
+ * Replaces the TF graph construction of networks.py:130-278 + policy_v_network.py:19-57.
+ * Parameters live in ONE flat fp32 buffer, variables in TF creation order (trunk, critic,
+ * actor, repetition), each (weights, biases) pair contiguous, each pair 64-float aligned.
+ * The gradient, RMSProp `ms` and `mom` slot buffers share that layout. */
+int mt_net_create(const mt_net_config *cfg, mt_net **out);
+void mt_net_destroy(mt_net *net);
+int mt_net_num_params(const mt_net *net, size_t *n_floats);
+int mt_net_num_vars(const mt_net *net, int *n);
+/* TF variable name (e.g. "Network/conv1/conv1_weights"), shape, offset into the flat buffer,
+ * and the uniform init bound d (networks.py:34-89: U(-d, d)); d < 0 means N(0,1) init. */
+int mt_net_var_info(const mt_net *net, int i, char *name, int name_len, int64_t *shape4,
+                    int *ndim, size_t *offset, float *init_bound);
+int mt_net_feature_dim(const mt_net *net, int *f); /* width of the trunk output (256/512/...) */
+/* Bytes of device workspace a forward/backward on `batch` rows needs. */
+int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes);
+
+/* ---- forward (A5-A7) ----------------------------------------------------------------------
+ * Replaces session.run([output_layer_v, output_layer_pi, output_layer_rep], {input_ph: s})
+ * (paac.py:144-146, :219-224) and the forward half of train_step (paac.py:254-256).
+ * obs: [batch][84][84][4*depth] uint8 (for LSTM: [batch][5][84][84][4*depth]).
+ * Outputs v [batch], pi [batch][A], rep [batch][R] (softmax probabilities).
+ * Activations are kept in `ws` for a following mt_loss_backward on the same rows. */
+int mt_forward(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
+               size_t ws_bytes, float *v, float *pi, float *rep, mt_stream_t stream);
+
+/* ---- device multinomial sampling (perf mode of A3) -----------------------------------------
+ * Replaces ExplorationPolicy.multinomial_choose (exploration_policy.py:108-116) with an
+ * inverse-CDF draw on (p - float32 epsneg), the last category taking the remainder — the
+ * distribution numpy's multinomial(1, p - epsneg) draws from. Uniforms come from a
+ * counter-based hash of (seed, row, counters[row]); counters (device, one uint64 per row) are
+ * incremented by the call, so a captured graph draws fresh numbers on every replay.
+ * Writes int32 indices a_idx [batch], r_idx [batch]. */
+int mt_sample(const float *pi, const float *rep, int batch, int num_actions, int num_reps,
+              uint64_t seed, uint64_t *counters, int32_t *a_idx, int32_t *r_idx,
+              mt_stream_t stream);
+
+/* ---- n-step return / advantage scan (A9) ---------------------------------------------------
+ * Replaces paac.py:219-231 (+ flatten :237-238). rewards/masks/values: [T][E] fp32,
+ * v_boot: [E] (V(s_T)). Writes y, adv: [T][E] fp32 (row t*E+e). Arithmetic follows the
+ * reference's numpy dtypes exactly (first product in fp32, the rest fp64, fp32 output). */
+int mt_returns(const float *rewards, const float *masks, const float *values, const float *v_boot,
+               float gamma, int T, int E, float *y, float *adv, mt_stream_t stream);
+
+/* ---- fused loss + backward (A10) ------------------------------------------------------------
+ * Replaces optimizer.compute_gradients(network.loss) (actor_learner.py:49) with the loss of
+ * policy_v_network.py:25-74. Requires the activations of mt_forward(obs, batch) in `ws`
+ * (pi, rep, v as that call returned them). a_idx/r_idx: selected action / repetition index
+ * (argmax of the one-hot feeds, paac.py:239-240). Writes the full flat gradient `grad`
+ * (every variable; alignment padding zeroed) and per-row loss terms
+ * loss_terms [batch][4] = (critic 0.25(y-v)^2, -adv*(logpi_a+logrep_r), entropy_pi, entropy_rep). */
+int mt_loss_backward(const mt_net *net, const float *params, const uint8_t *obs, int batch,
+                     void *ws, size_t ws_bytes, const float *pi, const float *rep, const float *v,
+                     const int32_t *a_idx, const int32_t *r_idx, const float *y, const float *adv,
+                     float entropy_beta, float *grad, float *loss_terms, mt_stream_t stream);
+
+/* ---- global-norm clip + TF1 ApplyRMSProp (A11) ----------------------------------------------
+ * Replaces clip_by_global_norm (actor_learner.py:59-63) + ApplyRMSProp (actor_learner.py:47-48,74).
+ * mt_grad_sumsq writes MT_NORM_PARTIALS fp32 partial sums of (inv_scale*g)^2.
+ * mt_clip_rmsprop: g' = inv_scale*g; norm = sqrt(sum partials);
+ *   clip_type GLOBAL: g' *= clip * min(1/norm, 1/clip);
+ *   ms += (g'^2 - ms)*(1 - decay); mom = momentum*mom + g'*lr/sqrt(ms + eps); w -= mom.
+ * lr is read from device memory (*lr_dev) so a captured graph picks up the schedule
+ * (actor_learner.py:132-136). norm_out (device, may be NULL) receives the pre-clip norm.
+ * inv_scale folds the 1/world of a data-parallel all-reduce (sum) into the update. */
+int mt_grad_sumsq(const float *g, size_t n, float inv_scale, float *partials, mt_stream_t stream);
+int mt_clip_rmsprop(float *w, float *ms, float *mom, const float *g, size_t n,
+                    const float *partials, const float *lr_dev, float decay, float momentum,
+                    float eps, float clip, int clip_type, float inv_scale, float *norm_out,
+                    mt_stream_t stream);
+
+/* ---- frame preprocess + 4-frame stack (A2) --------------------------------------------------
+ * Replaces AtariEmulator.__process_frame_pool / ObservationPool (atari_emulator.py:79-88,
+ * environment.py:58-80): per env, each "push" is the pair of the last two ALE screens of one
+ * emulator.next() (atari_emulator.py:90-100): pooled = max(f0, f1) (np.amax), resized to 84x84
+ * with the nearest LUT (row_lut[84], col_lut[84] = source row/col), appended to the 4-deep
+ * observation stack. Per env e: push_offset[e], push_count[e] (1..4) index the pushes (oldest
+ * first) in `raw` = [total_pushes][2][210][160][depth] uint8. prev/out: [E][84][84][4*depth];
+ * out[c] = prev[c+p] for c < 4-p, else the (c-(4-p))-th new push; RGB interleaves channels as
+ * [R_t0..R_t3, G_t0..G_t3, B_t0..B_t3] (environment.py:75). out may not alias prev. */
+int mt_preprocess(const uint8_t *raw, const int32_t *push_offset, const int32_t *push_count,
+                  int E, int depth, const int32_t *row_lut, const int32_t *col_lut,
+                  const uint8_t *prev, uint8_t *out, mt_stream_t stream);
+
+/* ---- small helpers ----------------------------------------------------------------------- */
+/* out[i] = sum_z parts[z*n + i] (deterministic order); used for split reductions. */
+int mt_sum_slabs(const float *parts, int nslabs, size_t n, float *out, mt_stream_t stream);
+
+/* hipGraph capture of everything launched on `stream` between begin and end. */
+int mt_graph_begin(mt_stream_t stream);
+int mt_graph_end(mt_stream_t stream, void **graph_exec);
+int mt_graph_launch(void *graph_exec, mt_stream_t stream);
+int mt_graph_destroy(void *graph_exec);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MANETTE_HIP_H */

@@ -1,0 +1,418 @@
+// fp32 MFMA (v_mfma_f32_16x16x4_f32) tiled GEMM core with pluggable operand loaders.
+//
+//   C[m][n] = sum_k A(m, k) * B(k, n)
+//
+// Every conv / dense forward and backward product of the trunk is one instantiation: the
+// loaders gather their operand (im2col of an NHWC activation, a dense matrix, a transposed
+// dense matrix, the transposed-conv gather of a backward-data pass) straight from HBM into
+// LDS, so no im2col buffer is ever materialised. fp32 in / fp32 accumulate: the MFMA is an
+// exact k-ordered fmaf chain (cdna_hip_programming.md §3), the numerics TF's fp32 path has.
+//
+// Tile: 256 threads = 4 waves laid out WM x WN; each wave owns TM x TN 16x16 accumulators.
+// K is walked in BK=32 chunks staged through LDS. Split-K over blockIdx.z.
+//
+// LDS operand layouts (per loader, chosen to mirror the operand's memory layout):
+//   KMAJOR  : L[row][BK + 4]   (k contiguous)  -> fragment = one ds_read_b128
+//   !KMAJOR : L[k][ROWS + 4]   (row contiguous) -> fragment = four ds_read_b32
+// Fragment element s of lane l (r = l&15, g = l>>4) holds k = kc*16 + g*4 + s for BOTH
+// operands, so MFMA s multiplies A[r][k] by B[k][r'] with the same k (the k order inside a
+// 16-chunk is permuted, which a sum does not see).
+#pragma once
+#include "common.h"
+
+namespace mt {
+
+template <int BM_, int BN_, int WM_, int WN_>
+struct Tile {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BK = 32;
+  static constexpr int TM = BM / (WM * 16);
+  static constexpr int TN = BN / (WN * 16);
+  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(TM >= 1 && TN >= 1 && TM * WM * 16 == BM && TN * WN * 16 == BN, "tile shape");
+};
+
+template <bool KMAJOR, int ROWS, int BK>
+struct LdsShape {
+  static constexpr int LD = KMAJOR ? (BK + 4) : (ROWS + 4);
+  static constexpr int SIZE = KMAJOR ? ROWS * (BK + 4) : BK * (ROWS + 4);
+};
+
+template <bool KMAJOR, int ROWS, int BK>
+__device__ __forceinline__ f32x4 load_frag(const float *L, int row, int k) {
+  if constexpr (KMAJOR) {
+    return *reinterpret_cast<const f32x4 *>(L + row * (BK + 4) + k);
+  } else {
+    constexpr int LD = ROWS + 4;
+    f32x4 v;
+    v[0] = L[(k + 0) * LD + row];
+    v[1] = L[(k + 1) * LD + row];
+    v[2] = L[(k + 2) * LD + row];
+    v[3] = L[(k + 3) * LD + row];
+    return v;
+  }
+}
+
+// Store 4 consecutive-k values of one row (KMAJOR) or 4 consecutive rows at one k (!KMAJOR).
+template <bool KMAJOR, int ROWS, int BK>
+__device__ __forceinline__ void lds_put4(float *L, int row, int k, f32x4 v) {
+  if constexpr (KMAJOR) {
+    *reinterpret_cast<f32x4 *>(L + row * (BK + 4) + k) = v;
+  } else {
+    *reinterpret_cast<f32x4 *>(L + k * (ROWS + 4) + row) = v;
+  }
+}
+
+template <class T, class LA, class LB, class EP>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EP ep, int M, int N, int K,
+                                                       int kchunk) {
+  using SA = LdsShape<LA::KMAJOR, T::BM, T::BK>;
+  using SB = LdsShape<LB::KMAJOR, T::BN, T::BK>;
+  __shared__ __attribute__((aligned(16))) float smem[SA::SIZE + SB::SIZE];
+  float *As = smem;
+  float *Bs = smem + SA::SIZE;
+
+  const int m0 = blockIdx.x * T::BM;
+  const int n0 = blockIdx.y * T::BN;
+  const int kb = blockIdx.z * kchunk;
+  const int ke = min(K, kb + kchunk);
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int wm = w / T::WN, wn = w % T::WN;
+  const int r = lane & 15, g = lane >> 4;
+
+  f32x4 acc[T::TM][T::TN];
+#pragma unroll
+  for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = kb; k0 < ke; k0 += T::BK) {
+    la.template fill<T::BM, T::BK>(As, m0, k0, ke, M);
+    lb.template fill<T::BN, T::BK>(Bs, n0, k0, ke, N);
+    __syncthreads();
+#pragma unroll
+    for (int kc = 0; kc < T::BK / 16; ++kc) {
+      f32x4 a[T::TM], b[T::TN];
+#pragma unroll
+      for (int i = 0; i < T::TM; ++i)
+        a[i] = load_frag<LA::KMAJOR, T::BM, T::BK>(As, (wm * T::TM + i) * 16 + r, kc * 16 + g * 4);
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j)
+        b[j] = load_frag<LB::KMAJOR, T::BN, T::BK>(Bs, (wn * T::TN + j) * 16 + r, kc * 16 + g * 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < T::TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TN; ++j) {
+      const int n = n0 + (wn * T::TN + j) * 16 + r;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = m0 + (wm * T::TM + i) * 16 + g * 4 + q;
+        if (m < M && n < N) ep(m, n, (int)blockIdx.z, acc[i][j][q]);
+      }
+    }
+}
+
+template <class T, class LA, class LB, class EP>
+inline int launch_gemm(const LA &la, const LB &lb, const EP &ep, int M, int N, int K, int splits,
+                       hipStream_t s) {
+  if (M <= 0 || N <= 0) return MT_OK;
+  const int nchunks = cdiv(K, T::BK);
+  if (splits < 1) splits = 1;
+  if (splits > nchunks) splits = nchunks;
+  const int kchunk = cdiv(nchunks, splits) * T::BK;
+  splits = cdiv(K, kchunk);
+  dim3 grid(cdiv(M, T::BM), cdiv(N, T::BN), splits);
+  hipLaunchKernelGGL((gemm_f32_kernel<T, LA, LB, EP>), grid, dim3(256), 0, s, la, lb, ep, M, N, K,
+                     kchunk);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+// Number of K splits gemm will actually use (for sizing slab workspaces).
+template <class T>
+inline int gemm_splits(int K, int splits) {
+  const int nchunks = cdiv(K, T::BK);
+  if (splits < 1) splits = 1;
+  if (splits > nchunks) splits = nchunks;
+  const int kchunk = cdiv(nchunks, splits) * T::BK;
+  return cdiv(K, kchunk);
+}
+
+// ------------------------------------------------------------------------------------------
+// Loaders. fill<ROWS, BK>(L, row0, k0, ke, nrows): stage rows [row0, row0+ROWS) x k [k0, k0+BK)
+// of the operand into LDS, zero outside [0, nrows) x [k0, ke). All 256 threads participate.
+// ------------------------------------------------------------------------------------------
+
+// Dense row-major operand X[row][k] (k contiguous, leading dim ld), fp32. KMAJOR.
+struct LdRowMajor {
+  static constexpr bool KMAJOR = true;
+  const float *X;
+  int ld;
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
+    constexpr int Q = BK / 4;
+    for (int it = threadIdx.x; it < ROWS * Q; it += 256) {
+      const int rr = it / Q, q = it % Q;
+      const int row = row0 + rr, k = k0 + q * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (row < nrows) {
+        const float *p = X + (size_t)row * ld + k;
+        if (k + 3 < ke) {
+          v = *reinterpret_cast<const f32x4 *>(p);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (k + e < ke) v[e] = p[e];
+        }
+      }
+      lds_put4<true, ROWS, BK>(L, rr, q * 4, v);
+    }
+  }
+};
+
+// Dense operand stored [k][row] (row contiguous, leading dim ld), fp32. !KMAJOR.
+// ones_row < 0: every row < nrows comes from X. ones_row >= 0: rows < ones_row come from X,
+// row ones_row reads 1.0 (for k < ke) and later rows read 0 — the bias row of a [X, 1]^T
+// product, so one GEMM yields dW and db together.
+struct LdColMajor {
+  static constexpr bool KMAJOR = false;
+  const float *X;
+  int ld;
+  int ones_row;
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
+    constexpr int Q = ROWS / 4;
+    const int nx = ones_row >= 0 ? ones_row : nrows;
+    for (int it = threadIdx.x; it < BK * Q; it += 256) {
+      const int kk = it / Q, q = it % Q;
+      const int k = k0 + kk, row = row0 + q * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (k < ke) {
+        const float *p = X + (size_t)k * ld + row;
+        if (row + 3 < nx && (ld & 3) == 0) {
+          v = *reinterpret_cast<const f32x4 *>(p);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rw = row + e;
+            if (rw < nx) v[e] = p[e];
+            else if (rw == ones_row) v[e] = 1.f;
+          }
+        }
+      }
+      lds_put4<false, ROWS, BK>(L, q * 4, kk, v);
+    }
+  }
+};
+
+// Compile-time conv geometry (NHWC input [B][H][W][CIN], HWIO weights, TF padding).
+template <int CIN_, int COUT_, int KS_, int S_, int H_, int W_, bool SAME_>
+struct ConvGeom {
+  static constexpr int CIN = CIN_, COUT = COUT_, KH = KS_, KW = KS_, S = S_, H = H_, W = W_;
+  static constexpr bool SAME = SAME_;
+  static constexpr int OH = SAME ? (H + S - 1) / S : (H - KH) / S + 1;
+  static constexpr int OW = SAME ? (W + S - 1) / S : (W - KW) / S + 1;
+  // TF SAME: pad_total = max((O-1)*S + K - I, 0), pad_before = pad_total / 2.
+  static constexpr int PADT_TOTAL = SAME ? (((OH - 1) * S + KH - H) > 0 ? ((OH - 1) * S + KH - H) : 0) : 0;
+  static constexpr int PADL_TOTAL = SAME ? (((OW - 1) * S + KW - W) > 0 ? ((OW - 1) * S + KW - W) : 0) : 0;
+  static constexpr int PT = PADT_TOTAL / 2, PL = PADL_TOTAL / 2;
+  static constexpr int KK = KH * KW * CIN;  // GEMM-K of the forward product
+  static_assert(CIN % 4 == 0 && COUT % 4 == 0, "channel quads");
+};
+
+template <bool U8>
+struct InElem;
+template <>
+struct InElem<true> {
+  typedef uint8_t T;
+  __device__ static __forceinline__ f32x4 load4(const uint8_t *p) {
+    const uint32_t u = *reinterpret_cast<const uint32_t *>(p);
+    const float s = 1.0f / 255.0f;  // networks.py:155 scalar_mul(1/255, cast)
+    return f32x4{(float)(u & 0xff) * s, (float)((u >> 8) & 0xff) * s,
+                 (float)((u >> 16) & 0xff) * s, (float)(u >> 24) * s};
+  }
+};
+template <>
+struct InElem<false> {
+  typedef float T;
+  __device__ static __forceinline__ f32x4 load4(const float *p) {
+    return *reinterpret_cast<const f32x4 *>(p);
+  }
+};
+
+// Implicit im2col of the forward conv: A(m = (b, oy, ox), k = (ky, kx, ci)). KMAJOR.
+template <class G, bool U8>
+struct LdIm2col {
+  static constexpr bool KMAJOR = true;
+  const typename InElem<U8>::T *X;
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
+    constexpr int Q = BK / 4;
+    for (int it = threadIdx.x; it < ROWS * Q; it += 256) {
+      const int rr = it / Q, q = it % Q;
+      const int m = row0 + rr, k = k0 + q * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (m < nrows && k < ke) {
+        const int b = m / (G::OH * G::OW);
+        const int rem = m - b * (G::OH * G::OW);
+        const int oy = rem / G::OW, ox = rem - oy * G::OW;
+        const int ky = k / (G::KW * G::CIN);
+        const int r2 = k - ky * (G::KW * G::CIN);
+        const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
+        const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
+        if (iy >= 0 && iy < G::H && ix >= 0 && ix < G::W)
+          v = InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
+      }
+      lds_put4<true, ROWS, BK>(L, rr, q * 4, v);
+    }
+  }
+};
+
+// Transposed im2col for the weight gradient: A(row = k (+ bias row KK), gk = m). !KMAJOR.
+template <class G, bool U8>
+struct LdIm2colT {
+  static constexpr bool KMAJOR = false;
+  const typename InElem<U8>::T *X;
+  int nm;  // number of GEMM-k rows (= B*OH*OW)
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
+    constexpr int Q = ROWS / 4;
+    for (int it = threadIdx.x; it < BK * Q; it += 256) {
+      const int kk = it / Q, q = it % Q;
+      const int m = k0 + kk, kr = row0 + q * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (m < ke) {
+        if (kr < G::KK) {
+          const int b = m / (G::OH * G::OW);
+          const int rem = m - b * (G::OH * G::OW);
+          const int oy = rem / G::OW, ox = rem - oy * G::OW;
+          const int ky = kr / (G::KW * G::CIN);
+          const int r2 = kr - ky * (G::KW * G::CIN);
+          const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
+          const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
+          if (iy >= 0 && iy < G::H && ix >= 0 && ix < G::W)
+            v = InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
+        } else if (kr == G::KK) {
+          v[0] = 1.f;  // bias row
+        }
+      }
+      lds_put4<false, ROWS, BK>(L, q * 4, kk, v);
+    }
+  }
+};
+
+// Backward-data of a conv, A side: rows = input pixels (b, iy, ix), gk = (ky, kx, co);
+// A = dY[b][oy][ox][co] with oy = (iy + PT - ky)/S when that divides and lands in range. KMAJOR.
+template <class G>
+struct LdConvBwdA {
+  static constexpr bool KMAJOR = true;
+  const float *dY;  // [B][OH][OW][COUT]
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
+    constexpr int Q = BK / 4;
+    for (int it = threadIdx.x; it < ROWS * Q; it += 256) {
+      const int rr = it / Q, q = it % Q;
+      const int m = row0 + rr, k = k0 + q * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (m < nrows && k < ke) {
+        const int b = m / (G::H * G::W);
+        const int rem = m - b * (G::H * G::W);
+        const int iy = rem / G::W, ix = rem - iy * G::W;
+        const int ky = k / (G::KW * G::COUT);
+        const int r2 = k - ky * (G::KW * G::COUT);
+        const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
+        const int ty = iy + G::PT - ky, tx = ix + G::PL - kx;
+        if (ty >= 0 && tx >= 0 && (ty % G::S) == 0 && (tx % G::S) == 0) {
+          const int oy = ty / G::S, ox = tx / G::S;
+          if (oy < G::OH && ox < G::OW)
+            v = *reinterpret_cast<const f32x4 *>(
+                dY + (((size_t)b * G::OH + oy) * G::OW + ox) * G::COUT + co);
+        }
+      }
+      lds_put4<true, ROWS, BK>(L, rr, q * 4, v);
+    }
+  }
+};
+
+// Backward-data of a conv, B side: rows = ci, gk = (ky, kx, co): W[ky][kx][ci][co]. KMAJOR.
+template <class G>
+struct LdConvBwdB {
+  static constexpr bool KMAJOR = true;
+  const float *Wt;  // HWIO
+  template <int ROWS, int BK>
+  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
+    constexpr int Q = BK / 4;
+    for (int it = threadIdx.x; it < ROWS * Q; it += 256) {
+      const int rr = it / Q, q = it % Q;
+      const int ci = row0 + rr, k = k0 + q * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (ci < nrows && k < ke) {
+        const int ky = k / (G::KW * G::COUT);
+        const int r2 = k - ky * (G::KW * G::COUT);
+        const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
+        v = *reinterpret_cast<const f32x4 *>(Wt + (((size_t)(ky * G::KW + kx) * G::CIN + ci) * G::COUT + co));
+      }
+      lds_put4<true, ROWS, BK>(L, rr, q * 4, v);
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// Epilogues: ep(m, n, z, value)
+// ------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ float act_fwd(float x, int act, float alpha) {
+  // networks.py:27-31 relu / max(x, alpha*x)
+  return act == MT_ACT_RELU ? fmaxf(x, 0.f) : fmaxf(x, alpha * x);
+}
+// Gradient factor from the post-activation output y (TF ReluGrad: y > 0; Maximum grad for
+// max(x, a*x): x >= a*x, i.e. y >= 0 for 0 < a < 1).
+__device__ __forceinline__ float act_bwd(float y, int act, float alpha) {
+  return act == MT_ACT_RELU ? (y > 0.f ? 1.f : 0.f) : (y >= 0.f ? 1.f : alpha);
+}
+
+struct EpBiasAct {
+  float *Y;
+  const float *bias;
+  int ld;
+  int act;
+  float alpha;
+  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
+    Y[(size_t)m * ld + n] = act_fwd(v + bias[n], act, alpha);
+  }
+};
+
+struct EpSlab {
+  float *P;
+  int M, N;
+  __device__ __forceinline__ void operator()(int m, int n, int z, float v) const {
+    P[((size_t)z * M + m) * N + n] = v;
+  }
+};
+
+// dX = v * act'(Yact) (Yact = post-activation output of the layer that produced X).
+struct EpMasked {
+  float *dX;
+  const float *Yact;
+  int ld;
+  int act;
+  float alpha;
+  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
+    const size_t i = (size_t)m * ld + n;
+    dX[i] = v * act_bwd(Yact[i], act, alpha);
+  }
+};
+
+}  // namespace mt

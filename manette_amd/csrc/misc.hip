@@ -1,0 +1,307 @@
+// Streaming kernels of the PAAC hot path on gfx950 (all HBM-bound, no MFMA):
+//   A2  frame preprocess + 4-frame stack      (atari_emulator.py:79-124, environment.py:42-80)
+//   A3  device multinomial sampling (perf mode) (exploration_policy.py:108-116)
+//   A9  n-step return / advantage scan         (paac.py:219-231)
+//   A11 global-norm clip + TF1 ApplyRMSProp    (actor_learner.py:47-74)
+// plus error reporting and hipGraph capture helpers of the C ABI.
+#include <atomic>
+#include <cmath>
+
+#include "common.h"
+
+namespace mt {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// ---------------------------------------------------------------------------------------------
+// A9: y_t = R_t, R_t = r_t + gamma * R_{t+1} * mask_t, R_T = V(s_T); adv_t = R_t - V_t.
+// dtype trail of paac.py:226-231 under numpy's promotion rules: estimated_return starts as the
+// float32 bootstrap; `self.gamma * estimated_return` is a python float times a float32 array,
+// i.e. a float32 product; every later operation meets float64 arrays (rewards, masks, values),
+// so the rest runs in float64; the feed casts y/adv to float32 (placeholders are float32).
+// ---------------------------------------------------------------------------------------------
+__global__ void returns_kernel(const float *__restrict__ r, const float *__restrict__ mask,
+                               const float *__restrict__ V, const float *__restrict__ VT,
+                               float gamma, int T, int E, float *__restrict__ y,
+                               float *__restrict__ adv) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  // t = T-1: float32 product gamma*R_T, then float64 with the mask and reward.
+  const float g32 = __fmul_rn(gamma, VT[e]);
+  double R = (double)r[(size_t)(T - 1) * E + e] + (double)g32 * (double)mask[(size_t)(T - 1) * E + e];
+  y[(size_t)(T - 1) * E + e] = (float)R;
+  adv[(size_t)(T - 1) * E + e] = (float)(R - (double)V[(size_t)(T - 1) * E + e]);
+  const double gd = (double)gamma;
+  for (int t = T - 2; t >= 0; --t) {
+    const size_t i = (size_t)t * E + e;
+    R = (double)r[i] + (gd * R) * (double)mask[i];
+    y[i] = (float)R;
+    adv[i] = (float)(R - (double)V[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// A11, pass 1: partial sums of (s*g)^2, MT_NORM_PARTIALS blocks, deterministic.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sumsq_kernel(const float *__restrict__ g, size_t n, float s,
+                                                    float *__restrict__ partials) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  const size_t n4 = n / 4;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const f32x4 v = reinterpret_cast<const f32x4 *>(g)[i] * s;
+    acc += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
+  }
+  for (size_t i = n4 * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float v = g[i] * s;
+    acc += (double)(v * v);
+  }
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = (float)(red[0] + red[1] + red[2] + red[3]);
+}
+
+// A11, pass 2: every block reduces the partials (fixed order), then clip + ApplyRMSProp.
+// TF1 training_ops ApplyRMSProp (CPU functor):
+//   ms  += (grad^2 - ms) * (1 - rho)
+//   mom  = mom * momentum + (grad * lr) / sqrt(ms + epsilon)
+//   var -= mom
+// clip_by_global_norm: scale = clip * min(1/norm, 1/clip) (both factors fp32).
+__global__ __launch_bounds__(256) void clip_rmsprop_kernel(
+    float *__restrict__ w, float *__restrict__ ms, float *__restrict__ mom,
+    const float *__restrict__ g, size_t n, const float *__restrict__ partials,
+    const float *__restrict__ lr_dev, float decay, float momentum, float eps, float clip,
+    int clip_type, float s, float *__restrict__ norm_out) {
+  __shared__ float sh_scale;
+  if (threadIdx.x < 64) {
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < MT_NORM_PARTIALS; i += 64) acc += (double)partials[i];
+    acc = wave_sum_d(acc);
+    if (threadIdx.x == 0) {
+      const float norm = sqrtf((float)acc);
+      float scale = s;
+      if (clip_type == MT_CLIP_GLOBAL) {
+        const float inv_clip = (float)(1.0 / (double)clip);
+        scale = s * (clip * fminf(1.0f / norm, inv_clip));
+      }
+      sh_scale = scale;
+      if (norm_out && blockIdx.x == 0) *norm_out = norm;
+    }
+  }
+  __syncthreads();
+  const float scale = sh_scale;
+  const float lr = *lr_dev;
+  const float one_m_rho = 1.0f - decay;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    // with s != 1 (data parallel), g is the SUM over ranks: scale folds 1/world and the clip.
+    const float gi = (clip_type == MT_CLIP_GLOBAL) ? g[i] * scale : g[i] * s;
+    float m = ms[i];
+    m = m + (gi * gi - m) * one_m_rho;
+    const float mo = mom[i] * momentum + (gi * lr) / sqrtf(m + eps);
+    ms[i] = m;
+    mom[i] = mo;
+    w[i] = w[i] - mo;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// A2: one thread per (env, y, x) output pixel; writes the 4*depth stacked channels.
+// ---------------------------------------------------------------------------------------------
+template <int DEPTH>
+__global__ __launch_bounds__(256) void preprocess_kernel(
+    const uint8_t *__restrict__ raw, const int32_t *__restrict__ push_offset,
+    const int32_t *__restrict__ push_count, int E, const int32_t *__restrict__ row_lut,
+    const int32_t *__restrict__ col_lut, const uint8_t *__restrict__ prev, uint8_t *__restrict__ out) {
+  constexpr int SH = 210, SW = 160, FR = SH * SW * DEPTH;  // one ALE screen
+  constexpr int C = 4 * DEPTH;
+  __shared__ int rl[84], cl[84];
+  if (threadIdx.x < 84) {
+    rl[threadIdx.x] = row_lut[threadIdx.x];
+    cl[threadIdx.x] = col_lut[threadIdx.x];
+  }
+  __syncthreads();
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= E * 84 * 84) return;
+  const int e = idx / (84 * 84);
+  const int pix = idx - e * (84 * 84);
+  const int yy = pix / 84, xx = pix - yy * 84;
+  const int p = push_count[e];
+  const int off = push_offset[e];
+  const uint8_t *pv = prev + (size_t)idx * C;
+  uint8_t *po = out + (size_t)idx * C;
+  const size_t src = ((size_t)rl[yy] * SW + cl[xx]) * DEPTH;
+#pragma unroll
+  for (int col = 0; col < DEPTH; ++col) {
+    uint8_t v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c < 4 - p) {
+        v[c] = pv[col * 4 + c + p];
+      } else {
+        const uint8_t *f = raw + (size_t)(off + c - (4 - p)) * 2 * FR;
+        const uint8_t a = f[src + col], b = f[FR + src + col];
+        v[c] = a > b ? a : b;  // np.amax over the 2-frame pool
+      }
+    }
+    *reinterpret_cast<uint32_t *>(po + col * 4) =
+        (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// A3 perf mode: counter-based uniforms, inverse CDF over (p - epsneg(float32)).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int draw_index(const float *p, int n, double u) {
+  const double epsneg = 5.9604644775390625e-08;  // np.finfo(np.float32).epsneg
+  double cum = 0.0;
+  for (int j = 0; j < n - 1; ++j) {
+    cum += (double)(p[j] - (float)epsneg);
+    if (u < cum) return j;
+  }
+  return n - 1;
+}
+
+__global__ void sample_kernel(const float *__restrict__ pi, const float *__restrict__ rep, int B,
+                              int A, int R, uint64_t seed, uint64_t *__restrict__ counters,
+                              int32_t *__restrict__ a_idx, int32_t *__restrict__ r_idx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t c = counters[b];
+  counters[b] = c + 1;
+  const uint64_t h = mix64(seed ^ mix64(((uint64_t)b << 40) ^ c));
+  const uint64_t h2 = mix64(h ^ 0x9e3779b97f4a7c15ULL);
+  const double ua = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+  const double ur = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+  a_idx[b] = draw_index(pi + (size_t)b * A, A, ua);
+  r_idx[b] = draw_index(rep + (size_t)b * R, R, ur);
+}
+
+}  // namespace mt
+
+using namespace mt;
+
+extern "C" const char *mt_last_error(void) { return g_err; }
+
+extern "C" int mt_version(void) { return 1; }
+
+extern "C" int mt_returns(const float *rewards, const float *masks, const float *values,
+                          const float *v_boot, float gamma, int T, int E, float *y, float *adv,
+                          mt_stream_t stream) {
+  MT_CHECK_ARG(rewards && masks && values && v_boot && y && adv, "null argument");
+  MT_CHECK_ARG(T >= 1 && E >= 1, "T and E must be >= 1");
+  hipLaunchKernelGGL(returns_kernel, dim3(cdiv(E, 64)), dim3(64), 0, (hipStream_t)stream, rewards,
+                     masks, values, v_boot, gamma, T, E, y, adv);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+extern "C" int mt_grad_sumsq(const float *g, size_t n, float inv_scale, float *partials,
+                             mt_stream_t stream) {
+  MT_CHECK_ARG(g && partials, "null argument");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(MT_NORM_PARTIALS), dim3(256), 0, (hipStream_t)stream, g, n,
+                     inv_scale, partials);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+extern "C" int mt_clip_rmsprop(float *w, float *ms, float *mom, const float *g, size_t n,
+                               const float *partials, const float *lr_dev, float decay,
+                               float momentum, float eps, float clip, int clip_type,
+                               float inv_scale, float *norm_out, mt_stream_t stream) {
+  MT_CHECK_ARG(w && ms && mom && g && partials && lr_dev, "null argument");
+  MT_CHECK_ARG(clip_type == MT_CLIP_IGNORE || clip_type == MT_CLIP_GLOBAL,
+               "clip_type %d not supported (reference 'local' is broken: actor_learner.py:66-67)",
+               clip_type);
+  MT_CHECK_ARG(clip_type != MT_CLIP_GLOBAL || clip > 0.f, "clip must be > 0");
+  int blocks = (int)std::min<size_t>((n + 255) / 256, 1024);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(clip_rmsprop_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, ms,
+                     mom, g, n, partials, lr_dev, decay, momentum, eps, clip, clip_type, inv_scale,
+                     norm_out);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+extern "C" int mt_preprocess(const uint8_t *raw, const int32_t *push_offset,
+                             const int32_t *push_count, int E, int depth, const int32_t *row_lut,
+                             const int32_t *col_lut, const uint8_t *prev, uint8_t *out,
+                             mt_stream_t stream) {
+  MT_CHECK_ARG(raw && push_offset && push_count && row_lut && col_lut && prev && out,
+               "null argument");
+  MT_CHECK_ARG(E >= 1, "E must be >= 1");
+  MT_CHECK_ARG(prev != out, "out may not alias prev");
+  const int total = E * 84 * 84;
+  if (depth == 1) {
+    hipLaunchKernelGGL(preprocess_kernel<1>, dim3(cdiv(total, 256)), dim3(256), 0,
+                       (hipStream_t)stream, raw, push_offset, push_count, E, row_lut, col_lut, prev,
+                       out);
+  } else if (depth == 3) {
+    hipLaunchKernelGGL(preprocess_kernel<3>, dim3(cdiv(total, 256)), dim3(256), 0,
+                       (hipStream_t)stream, raw, push_offset, push_count, E, row_lut, col_lut, prev,
+                       out);
+  } else {
+    set_error("depth must be 1 or 3");
+    return MT_ERR_ARG;
+  }
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+extern "C" int mt_sample(const float *pi, const float *rep, int batch, int num_actions,
+                         int num_reps, uint64_t seed, uint64_t *counters, int32_t *a_idx,
+                         int32_t *r_idx, mt_stream_t stream) {
+  MT_CHECK_ARG(pi && rep && counters && a_idx && r_idx, "null argument");
+  MT_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_reps >= 1, "bad sizes");
+  hipLaunchKernelGGL(sample_kernel, dim3(cdiv(batch, 64)), dim3(64), 0, (hipStream_t)stream, pi,
+                     rep, batch, num_actions, num_reps, seed, counters, a_idx, r_idx);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+extern "C" int mt_graph_begin(mt_stream_t stream) {
+  MT_CHECK_ARG(stream != nullptr, "graph capture needs a non-default stream");
+  MT_HIP(hipStreamBeginCapture((hipStream_t)stream, hipStreamCaptureModeThreadLocal));
+  return MT_OK;
+}
+
+extern "C" int mt_graph_end(mt_stream_t stream, void **graph_exec) {
+  MT_CHECK_ARG(stream && graph_exec, "null argument");
+  hipGraph_t g = nullptr;
+  MT_HIP(hipStreamEndCapture((hipStream_t)stream, &g));
+  hipGraphExec_t ex = nullptr;
+  hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    set_error("hipGraphInstantiate failed: %s", hipGetErrorString(e));
+    return MT_ERR_HIP;
+  }
+  *graph_exec = (void *)ex;
+  return MT_OK;
+}
+
+extern "C" int mt_graph_launch(void *graph_exec, mt_stream_t stream) {
+  MT_CHECK_ARG(graph_exec, "null graph");
+  MT_HIP(hipGraphLaunch((hipGraphExec_t)graph_exec, (hipStream_t)stream));
+  return MT_OK;
+}
+
+extern "C" int mt_graph_destroy(void *graph_exec) {
+  if (graph_exec) MT_HIP(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
+  return MT_OK;
+}

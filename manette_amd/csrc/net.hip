@@ -1,0 +1,667 @@
+// Policy/value network of the PAAC hot path on gfx950: parameter layout, forward (A5-A7) and
+// fused loss + backward (A10).
+//
+// Reference: networks.py:130-278 (trunks), policy_v_network.py:19-74 (heads + loss).
+// Trunk products run on the fp32 MFMA GEMM core (gemm.h) with implicit im2col loaders; the
+// small heads (critic 1, actor A, repetition R outputs) and the loss are one workgroup per row.
+#include <string>
+#include <vector>
+#include <cmath>
+#include <algorithm>
+
+#include "gemm.h"
+
+namespace mt {
+
+// ---------------------------------------------------------------------------------------------
+// Architectures (compile-time geometry). C = 4*depth input channels.
+// ---------------------------------------------------------------------------------------------
+template <int C>
+struct NipsArch {  // networks.py:178-192
+  using G1 = ConvGeom<C, 16, 8, 4, 84, 84, false>;
+  using G2 = ConvGeom<16, 32, 4, 2, 20, 20, false>;
+  using G3 = G2;  // unused
+  static constexpr int NCONV = 2;
+  static constexpr int FLAT = G2::OH * G2::OW * G2::COUT;  // 2592
+  static constexpr int F = 256;
+  static constexpr const char *FC = "fc3";
+};
+template <int C>
+struct NatureArch {  // networks.py:261-278
+  using G1 = ConvGeom<C, 32, 8, 4, 84, 84, false>;
+  using G2 = ConvGeom<32, 64, 4, 2, 20, 20, false>;
+  using G3 = ConvGeom<64, 64, 3, 1, 9, 9, false>;
+  static constexpr int NCONV = 3;
+  static constexpr int FLAT = G3::OH * G3::OW * G3::COUT;  // 3136
+  static constexpr int F = 512;
+  static constexpr const char *FC = "fc4";
+};
+
+}  // namespace mt
+
+struct VarInfo {
+  std::string name;
+  int ndim;
+  int64_t shape[4];
+  size_t offset;
+  float bound;
+};
+
+struct mt_net {
+  mt_net_config cfg;
+  int C;       // input channels (4*depth)
+  int F;       // trunk feature width
+  int O;       // 1 + A + R head outputs
+  int nconv;
+  int flat;
+  std::vector<VarInfo> vars;
+  size_t nparams;
+  size_t off_conv[3];  // weights offset of each conv (biases follow)
+  size_t off_fc, off_critic, off_actor, off_rep;
+};
+
+namespace mt {
+
+static size_t align64(size_t x) { return (x + 63) & ~size_t(63); }
+
+static void add_pair(mt_net *n, size_t &off, const std::string &scope, const std::string &nm,
+                     std::vector<int64_t> wshape, int64_t nb, float bw, float bb, size_t *woff) {
+  off = align64(off);
+  VarInfo w{};
+  w.name = scope + "/" + nm + "/" + nm + "_weights";
+  w.ndim = (int)wshape.size();
+  size_t ws = 1;
+  for (int i = 0; i < w.ndim; ++i) {
+    w.shape[i] = wshape[i];
+    ws *= (size_t)wshape[i];
+  }
+  w.offset = off;
+  w.bound = bw;
+  VarInfo b{};
+  b.name = scope + "/" + nm + "/" + nm + "_biases";
+  b.ndim = 1;
+  b.shape[0] = nb;
+  b.offset = off + ws;
+  b.bound = bb;
+  *woff = off;
+  n->vars.push_back(w);
+  n->vars.push_back(b);
+  off = off + ws + (size_t)nb;
+}
+
+template <class G>
+static void add_conv(mt_net *n, size_t &off, int idx) {
+  // networks.py:34-55: weights U(+-1/sqrt(filters*k*k)) (shape[3] is the OUTPUT channel count),
+  // biases U(+-1/sqrt(in_channels*k*k)).
+  const float bw = 1.0f / std::sqrt((float)(G::COUT * G::KH * G::KW));
+  const float bb = 1.0f / std::sqrt((float)(G::CIN * G::KH * G::KW));
+  std::string nm = "conv" + std::to_string(idx + 1);
+  add_pair(n, off, "Network", nm, {G::KH, G::KW, G::CIN, G::COUT}, G::COUT, bw, bb,
+           &n->off_conv[idx]);
+}
+
+template <class Ar>
+static void build_layout(mt_net *n) {
+  size_t off = 0;
+  add_conv<typename Ar::G1>(n, off, 0);
+  add_conv<typename Ar::G2>(n, off, 1);
+  if constexpr (Ar::NCONV == 3) add_conv<typename Ar::G3>(n, off, 2);
+  const float bf = 1.0f / std::sqrt((float)Ar::FLAT);  // networks.py:72-89
+  add_pair(n, off, "Network", Ar::FC, {Ar::FLAT, Ar::F}, Ar::F, bf, bf, &n->off_fc);
+  const float bh = 1.0f / std::sqrt((float)Ar::F);
+  const int A = n->cfg.num_actions, R = n->cfg.num_reps;
+  // policy_v_network.py:22 (critic), :31 (actor), :47 (repetition) — TF creation order.
+  add_pair(n, off, "Training/Critic", "critic_output", {Ar::F, 1}, 1, bh, bh, &n->off_critic);
+  add_pair(n, off, "Training/Actor", "actor_output", {Ar::F, A}, A, bh, bh, &n->off_actor);
+  add_pair(n, off, "Training/Repetition", "repetition_output", {Ar::F, R}, R, bh, bh, &n->off_rep);
+  n->nparams = align64(off);
+  n->F = Ar::F;
+  n->flat = Ar::FLAT;
+  n->nconv = Ar::NCONV;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Workspace layout (floats), a pure function of (net, batch).
+// ---------------------------------------------------------------------------------------------
+struct WsLayout {
+  size_t act[3], dact[3], fcslab, H, dz, dH, wslab, total;
+  int fc_splits;
+};
+
+template <int N>
+struct TileFor {
+  using T = Tile<64, 64, 2, 2>;
+};
+template <>
+struct TileFor<16> {
+  using T = Tile<64, 16, 4, 1>;
+};
+template <>
+struct TileFor<32> {
+  using T = Tile<64, 32, 4, 1>;
+};
+
+using TileFc = Tile<32, 64, 2, 2>;    // dense forward, M = batch (small)
+using TileDense = Tile<64, 64, 2, 2>;  // dense dW / dX
+
+static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
+  int s = target / (grid_mn > 0 ? grid_mn : 1);
+  if (s < 1) s = 1;
+  const int chunks = cdiv(K, bk);
+  if (s > chunks) s = chunks;
+  return s;
+}
+
+template <class G>
+static int conv_wgrad_splits(int B) {
+  using T = typename TileFor<G::COUT>::T;
+  const int M = G::KK + 1;
+  const int K = B * G::OH * G::OW;
+  const int s = pick_splits(cdiv(M, T::BM) * cdiv(G::COUT, T::BN), K, T::BK);
+  return gemm_splits<T>(K, s);
+}
+
+template <class G>
+static size_t conv_wgrad_slab(int B) {
+  const int s = conv_wgrad_splits<G>(B);
+  return s > 1 ? (size_t)s * (G::KK + 1) * G::COUT : 0;
+}
+
+template <class Ar>
+static int fc_splits(int B, int F) {
+  const int s = pick_splits(cdiv(B, TileFc::BM) * cdiv(F, TileFc::BN), Ar::FLAT, TileFc::BK, 256);
+  return gemm_splits<TileFc>(Ar::FLAT, s);
+}
+
+template <class Ar>
+static WsLayout ws_layout(const mt_net *n, int B) {
+  WsLayout L{};
+  size_t off = 0;
+  auto take = [&](size_t nf) {
+    size_t o = off;
+    off = align64(off + nf);
+    return o;
+  };
+  using G1 = typename Ar::G1;
+  using G2 = typename Ar::G2;
+  using G3 = typename Ar::G3;
+  const size_t a1 = (size_t)B * G1::OH * G1::OW * G1::COUT;
+  const size_t a2 = (size_t)B * G2::OH * G2::OW * G2::COUT;
+  const size_t a3 = Ar::NCONV == 3 ? (size_t)B * G3::OH * G3::OW * G3::COUT : 0;
+  L.act[0] = take(a1);
+  L.act[1] = take(a2);
+  L.act[2] = take(a3);
+  L.dact[0] = take(a1);
+  L.dact[1] = take(a2);
+  L.dact[2] = take(a3);
+  L.fc_splits = fc_splits<Ar>(B, Ar::F);
+  L.fcslab = take((size_t)L.fc_splits * B * Ar::F);
+  L.H = take((size_t)B * Ar::F);
+  L.dz = take((size_t)B * n->O);
+  L.dH = take((size_t)B * Ar::F);
+  size_t ws = conv_wgrad_slab<G1>(B);
+  ws = std::max(ws, conv_wgrad_slab<G2>(B));
+  if constexpr (Ar::NCONV == 3) ws = std::max(ws, conv_wgrad_slab<G3>(B));
+  L.wslab = take(ws);
+  L.total = off;
+  return L;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kernels: slab sum, heads forward, loss + heads backward, heads weight gradient.
+// ---------------------------------------------------------------------------------------------
+__global__ void sum_slabs_kernel(const float *__restrict__ P, int S, size_t n, float *__restrict__ out) {
+  const size_t n4 = n / 4;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 acc = reinterpret_cast<const f32x4 *>(P)[i];
+    for (int z = 1; z < S; ++z) acc += reinterpret_cast<const f32x4 *>(P + (size_t)z * n)[i];
+    reinterpret_cast<f32x4 *>(out)[i] = acc;
+  }
+  for (size_t i = n4 * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float acc = P[i];
+    for (int z = 1; z < S; ++z) acc += P[(size_t)z * n + i];
+    out[i] = acc;
+  }
+}
+
+static int sum_slabs(const float *P, int S, size_t n, float *out, hipStream_t s) {
+  if (n == 0) return MT_OK;
+  int blocks = (int)std::min<size_t>((n / 4 + 255) / 256 + 1, 2048);
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(blocks), dim3(256), 0, s, P, S, n, out);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+struct HeadParams {
+  const float *Wc, *bc, *Wa, *ba, *Wr, *br;
+  int A, R, F;
+};
+
+static HeadParams head_params(const mt_net *n, const float *P) {
+  HeadParams h;
+  h.F = n->F;
+  h.A = n->cfg.num_actions;
+  h.R = n->cfg.num_reps;
+  h.Wc = P + n->off_critic;
+  h.bc = h.Wc + h.F;
+  h.Wa = P + n->off_actor;
+  h.ba = h.Wa + (size_t)h.F * h.A;
+  h.Wr = P + n->off_rep;
+  h.br = h.Wr + (size_t)h.F * h.R;
+  return h;
+}
+
+// Weight of head output o (0 = critic, 1..A = actor, 1+A.. = repetition) for feature f
+// (f == F is the bias).
+__device__ __forceinline__ float head_w(const HeadParams &hp, int f, int o) {
+  if (o == 0) return f < hp.F ? hp.Wc[f] : hp.bc[0];
+  if (o <= hp.A) return f < hp.F ? hp.Wa[(size_t)f * hp.A + (o - 1)] : hp.ba[o - 1];
+  const int rr = o - 1 - hp.A;
+  return f < hp.F ? hp.Wr[(size_t)f * hp.R + rr] : hp.br[rr];
+}
+
+// Softmax over n logits held in lanes [0, n) of one wave (x/temp, TF: exp(x-max)/sum).
+__device__ __forceinline__ float wave_softmax(float x, int lane, int n) {
+  const float xm = lane < n ? x : -INFINITY;
+  const float mx = wave_max(xm);
+  const float e = lane < n ? expf(x - mx) : 0.f;
+  const float s = wave_sum(e);
+  return e / s;
+}
+
+constexpr int kMaxHeads = 64;  // 1 + A + R <= 64
+
+// One workgroup per row: h = act(sum_z slabs + b); logits = h . [Wc|Wa|Wr] + b;
+// v = logit_0; pi = softmax(logits_a / temp); rep = softmax(logits_r / temp).
+__global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict__ slabs, int S, int B,
+                                                        const float *__restrict__ fc_b, int act,
+                                                        float alpha, HeadParams hp, float temp,
+                                                        float *__restrict__ H, float *__restrict__ v,
+                                                        float *__restrict__ pi,
+                                                        float *__restrict__ rep) {
+  __shared__ float hs[512];
+  __shared__ float part[4][kMaxHeads];
+  const int b = blockIdx.x;
+  const int F = hp.F, O = 1 + hp.A + hp.R;
+  for (int f = threadIdx.x; f < F; f += 256) {
+    float acc = 0.f;
+    for (int z = 0; z < S; ++z) acc += slabs[((size_t)z * B + b) * F + f];
+    const float h = act_fwd(acc + fc_b[f], act, alpha);
+    hs[f] = h;
+    H[(size_t)b * F + f] = h;
+  }
+  __syncthreads();
+  const int o = threadIdx.x & 63, qt = threadIdx.x >> 6;
+  if (o < O) {
+    const int f0 = qt * (F / 4), f1 = f0 + F / 4;
+    float acc = 0.f;
+    for (int f = f0; f < f1; ++f) acc += hs[f] * head_w(hp, f, o);
+    part[qt][o] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    float z = 0.f;
+    if (lane < O) z = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane] + head_w(hp, F, lane);
+    if (lane == 0) v[b] = z;
+    // actor logits sit in lanes 1..A, repetition logits in lanes 1+A..A+R: shift them to 0..
+    const float za = __shfl(z, (lane + 1) & 63, 64) / temp;
+    const float pa = wave_softmax(za, lane, hp.A);
+    if (lane < hp.A) pi[(size_t)b * hp.A + lane] = pa;
+    const float zr = __shfl(z, (lane + 1 + hp.A) & 63, 64) / temp;
+    const float pr = wave_softmax(zr, lane, hp.R);
+    if (lane < hp.R) rep[(size_t)b * hp.R + lane] = pr;
+  }
+}
+
+// dL/dlogit for one softmax head (policy_v_network.py:29-57, :59-74), one wave, lanes [0, n):
+// objective = adv*log(p_sel + 1e-30) + beta*H,  H = -sum p*log(p + 1e-30),  L = -scale*objective.
+// Chain rule exactly as TF differentiates it: g_k = dL/dp_k, dz_k = p_k (g_k - sum_j p_j g_j),
+// dlogit_k = dz_k / temp. Returns lane's dlogit; *ent, *lsel receive H and log(p_sel+eps).
+__device__ __forceinline__ float head_softmax_grad(float p, int lane, int n, int sel, float adv,
+                                                   float beta, float scale, float temp, float *ent,
+                                                   float *lsel) {
+  const float eps = 1e-30f;
+  const bool on = lane < n;
+  const float pe = p + eps;
+  const float lp = on ? logf(pe) : 0.f;
+  const float e = wave_sum(on ? -(p * lp) : 0.f);
+  *ent = e;
+  *lsel = __shfl(lp, sel, 64);
+  // d objective / dp_k = adv*[k==sel]/(p+eps) + beta * d(-sum p log(p+eps))/dp_k
+  //                    = adv*[k==sel]/(p+eps) - beta*(log(p+eps) + p/(p+eps))
+  float dobj = on ? ((lane == sel ? adv / pe : 0.f) - beta * (lp + p / pe)) : 0.f;
+  const float g = -scale * dobj;
+  const float sg = wave_sum(on ? p * g : 0.f);
+  return on ? p * (g - sg) / temp : 0.f;
+}
+
+// One workgroup per row b: head gradients dz[b][0..O) and dH[b][f] = act'(H) * sum_o dz_o W[f][o].
+__global__ __launch_bounds__(256) void loss_bwd_kernel(
+    HeadParams hp, const float *__restrict__ H, const float *__restrict__ pi,
+    const float *__restrict__ rep, const float *__restrict__ v, const int32_t *__restrict__ a_idx,
+    const int32_t *__restrict__ r_idx, const float *__restrict__ y, const float *__restrict__ adv,
+    float beta, float scale, float temp, int act, float alpha, float *__restrict__ dz,
+    float *__restrict__ dH, float *__restrict__ loss_terms) {
+  __shared__ float dzs[kMaxHeads];
+  const int b = blockIdx.x;
+  const int A = hp.A, R = hp.R, O = 1 + A + R, F = hp.F;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const float ad = adv[b];
+    const float pa = lane < A ? pi[(size_t)b * A + lane] : 0.f;
+    const float pr = lane < R ? rep[(size_t)b * R + lane] : 0.f;
+    float ent_a, ls_a, ent_r, ls_r;
+    const float ga = head_softmax_grad(pa, lane, A, a_idx[b], ad, beta, scale, temp, &ent_a, &ls_a);
+    const float gr = head_softmax_grad(pr, lane, R, r_idx[b], ad, beta, scale, temp, &ent_r, &ls_r);
+    const float diff = y[b] - v[b];
+    // d/dv of scale * 0.25 * (y - v)^2  (policy_v_network.py:25-26)
+    const float gv = scale * 0.25f * 2.0f * (v[b] - y[b]);
+    if (lane == 0) dzs[0] = gv;
+    if (lane < A) dzs[1 + lane] = ga;
+    if (lane < R) dzs[1 + A + lane] = gr;
+    if (lane == 0 && loss_terms) {
+      loss_terms[(size_t)b * 4 + 0] = 0.25f * diff * diff;
+      loss_terms[(size_t)b * 4 + 1] = -((ls_a + ls_r) * ad);
+      loss_terms[(size_t)b * 4 + 2] = ent_a;
+      loss_terms[(size_t)b * 4 + 3] = ent_r;
+    }
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < O; o += 256) dz[(size_t)b * O + o] = dzs[o];
+  for (int f = threadIdx.x; f < F; f += 256) {
+    float acc = dzs[0] * hp.Wc[f];
+    const float *wa = hp.Wa + (size_t)f * A;
+    for (int k = 0; k < A; ++k) acc += dzs[1 + k] * wa[k];
+    const float *wr = hp.Wr + (size_t)f * R;
+    for (int k = 0; k < R; ++k) acc += dzs[1 + A + k] * wr[k];
+    const float h = H[(size_t)b * F + f];
+    dH[(size_t)b * F + f] = acc * act_bwd(h, act, alpha);
+  }
+}
+
+// Head weight/bias gradient: G[f][o] = sum_b [H,1][b][f] * dz[b][o] scattered into the three
+// (w, b) variable pairs of the flat gradient.
+__global__ void head_wgrad_kernel(const float *__restrict__ H, const float *__restrict__ dz, int B,
+                                  int F, int A, int R, float *__restrict__ gc,
+                                  float *__restrict__ ga, float *__restrict__ gr) {
+  const int O = 1 + A + R;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (F + 1) * O) return;
+  const int f = idx / O, o = idx % O;
+  float acc = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float h = f < F ? H[(size_t)b * F + f] : 1.f;
+    acc += h * dz[(size_t)b * O + o];
+  }
+  if (o == 0)
+    gc[f] = acc;  // [F][1] weights then the bias at index F
+  else if (o <= A)
+    ga[(size_t)f * A + (o - 1)] = acc;
+  else
+    gr[(size_t)f * R + (o - 1 - A)] = acc;
+}
+
+struct EpStore {
+  float *P;
+  int ld;
+  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
+    P[(size_t)m * ld + n] = v;
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Layer drivers
+// ---------------------------------------------------------------------------------------------
+template <class G, bool U8>
+static int conv_forward(const void *X, const float *Wt, const float *bias, float *Y, int B, int act,
+                        float alpha, hipStream_t s) {
+  using T = typename TileFor<G::COUT>::T;
+  LdIm2col<G, U8> la{reinterpret_cast<const typename InElem<U8>::T *>(X)};
+  LdColMajor lb{Wt, G::COUT, -1};
+  EpBiasAct ep{Y, bias, G::COUT, act, alpha};
+  return launch_gemm<T>(la, lb, ep, B * G::OH * G::OW, G::COUT, G::KK, 1, s);
+}
+
+// dW (+db) of a conv: [im2col(X), 1]^T . dY  -> grad[(KK+1) x COUT] (weights then biases).
+template <class G, bool U8>
+static int conv_wgrad(const void *X, const float *dY, float *slab, float *gwb, int B,
+                      hipStream_t s) {
+  using T = typename TileFor<G::COUT>::T;
+  const int M = G::KK + 1, K = B * G::OH * G::OW;
+  const int S = conv_wgrad_splits<G>(B);
+  LdIm2colT<G, U8> la{reinterpret_cast<const typename InElem<U8>::T *>(X), K};
+  LdColMajor lb{dY, G::COUT, -1};
+  if (S == 1) return launch_gemm<T>(la, lb, EpStore{gwb, G::COUT}, M, G::COUT, K, 1, s);
+  int rc = launch_gemm<T>(la, lb, EpSlab{slab, M, G::COUT}, M, G::COUT, K, S, s);
+  if (rc) return rc;
+  return sum_slabs(slab, S, (size_t)M * G::COUT, gwb, s);
+}
+
+// dX of a conv (transposed-conv gather), masked by the activation derivative of X.
+template <class G>
+static int conv_dgrad(const float *dY, const float *Wt, const float *Xact, float *dX, int B,
+                      int act, float alpha, hipStream_t s) {
+  using T = typename TileFor<G::CIN>::T;
+  LdConvBwdA<G> la{dY};
+  LdConvBwdB<G> lb{Wt};
+  EpMasked ep{dX, Xact, G::CIN, act, alpha};
+  return launch_gemm<T>(la, lb, ep, B * G::H * G::W, G::CIN, G::KH * G::KW * G::COUT, 1, s);
+}
+
+#define MT_TRY(x)              \
+  do {                         \
+    int rc_ = (x);             \
+    if (rc_ != MT_OK) return rc_; \
+  } while (0)
+
+template <class Ar>
+static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
+                        float *v, float *pi, float *rep, hipStream_t s) {
+  const WsLayout L = ws_layout<Ar>(n, B);
+  const int act = n->cfg.activation;
+  const float al = n->cfg.alpha_leaky;
+  using G1 = typename Ar::G1;
+  using G2 = typename Ar::G2;
+  using G3 = typename Ar::G3;
+  float *a1 = ws + L.act[0], *a2 = ws + L.act[1], *a3 = ws + L.act[2];
+  MT_TRY((conv_forward<G1, true>(obs, P + n->off_conv[0], P + n->off_conv[0] + G1::KK * G1::COUT,
+                                 a1, B, act, al, s)));
+  MT_TRY((conv_forward<G2, false>(a1, P + n->off_conv[1], P + n->off_conv[1] + G2::KK * G2::COUT,
+                                  a2, B, act, al, s)));
+  const float *flat = a2;
+  if constexpr (Ar::NCONV == 3) {
+    MT_TRY((conv_forward<G3, false>(a2, P + n->off_conv[2], P + n->off_conv[2] + G3::KK * G3::COUT,
+                                    a3, B, act, al, s)));
+    flat = a3;
+  }
+  // dense layer (networks.py:57-70), split-K partial slabs; heads kernel finishes bias + act.
+  const float *Wfc = P + n->off_fc;
+  MT_TRY((launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1},
+                              EpSlab{ws + L.fcslab, B, Ar::F}, B, Ar::F, Ar::FLAT, L.fc_splits, s)));
+  HeadParams hp = head_params(n, P);
+  hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, L.fc_splits, B,
+                     Wfc + (size_t)Ar::FLAT * Ar::F, act, al, hp, n->cfg.softmax_temp, ws + L.H, v,
+                     pi, rep);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+template <class Ar>
+static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
+                         const float *pi, const float *rep, const float *v, const int32_t *a_idx,
+                         const int32_t *r_idx, const float *y, const float *adv, float beta,
+                         float *grad, float *loss_terms, hipStream_t s) {
+  const WsLayout L = ws_layout<Ar>(n, B);
+  const int act = n->cfg.activation;
+  const float al = n->cfg.alpha_leaky;
+  using G1 = typename Ar::G1;
+  using G2 = typename Ar::G2;
+  using G3 = typename Ar::G3;
+  float *a1 = ws + L.act[0], *a2 = ws + L.act[1], *a3 = ws + L.act[2];
+  float *d1 = ws + L.dact[0], *d2 = ws + L.dact[1], *d3 = ws + L.dact[2];
+  MT_HIP(hipMemsetAsync(grad, 0, n->nparams * sizeof(float), s));
+
+  // loss scaling 5.0 and the batch mean (policy_v_network.py:70-74): scale = 5/B.
+  const float scale = 5.0f / (float)B;
+  HeadParams hp = head_params(n, P);
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3(B), dim3(256), 0, s, hp, ws + L.H, pi, rep, v, a_idx,
+                     r_idx, y, adv, beta, scale, n->cfg.softmax_temp, act, al, ws + L.dz, ws + L.dH,
+                     loss_terms);
+  MT_LAUNCHED();
+  {
+    const int tot = (Ar::F + 1) * n->O;
+    hipLaunchKernelGGL(head_wgrad_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, s, ws + L.H,
+                       ws + L.dz, B, Ar::F, n->cfg.num_actions, n->cfg.num_reps,
+                       grad + n->off_critic, grad + n->off_actor, grad + n->off_rep);
+    MT_LAUNCHED();
+  }
+  const float *flat = Ar::NCONV == 3 ? a3 : a2;
+  float *dflat = Ar::NCONV == 3 ? d3 : d2;
+  const float *Wfc = P + n->off_fc;
+  // dense dW, db: [flat, 1]^T . dH -> grad[(FLAT+1) x F]
+  MT_TRY((launch_gemm<TileDense>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
+                                 EpStore{grad + n->off_fc, Ar::F}, Ar::FLAT + 1, Ar::F, B, 1, s)));
+  // dense dX: dH . W^T, masked by the last conv's activation
+  MT_TRY((launch_gemm<TileDense>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+                                 EpMasked{dflat, flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1, s)));
+  float *slab = ws + L.wslab;
+  if constexpr (Ar::NCONV == 3) {
+    MT_TRY((conv_wgrad<G3, false>(a2, d3, slab, grad + n->off_conv[2], B, s)));
+    MT_TRY((conv_dgrad<G3>(d3, P + n->off_conv[2], a2, d2, B, act, al, s)));
+  }
+  MT_TRY((conv_wgrad<G2, false>(a1, d2, slab, grad + n->off_conv[1], B, s)));
+  MT_TRY((conv_dgrad<G2>(d2, P + n->off_conv[1], a1, d1, B, act, al, s)));
+  MT_TRY((conv_wgrad<G1, true>(obs, d1, slab, grad + n->off_conv[0], B, s)));
+  return MT_OK;
+}
+
+}  // namespace mt
+
+// ---------------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------------
+using namespace mt;
+
+#define MT_ARCH_SWITCH(net, ...)                                                   \
+  do {                                                                              \
+    const int arch_ = (net)->cfg.arch, d_ = (net)->cfg.depth;                       \
+    if (arch_ == MT_ARCH_NIPS && d_ == 1) { using Ar = NipsArch<4>; __VA_ARGS__; }         \
+    else if (arch_ == MT_ARCH_NIPS && d_ == 3) { using Ar = NipsArch<12>; __VA_ARGS__; }   \
+    else if (arch_ == MT_ARCH_NATURE && d_ == 1) { using Ar = NatureArch<4>; __VA_ARGS__; } \
+    else if (arch_ == MT_ARCH_NATURE && d_ == 3) { using Ar = NatureArch<12>; __VA_ARGS__; } \
+    else { set_error("arch %d depth %d not built", arch_, d_); return MT_ERR_UNSUPPORTED; } \
+  } while (0)
+
+extern "C" int mt_net_create(const mt_net_config *cfg, mt_net **out) {
+  MT_CHECK_ARG(cfg && out, "null argument");
+  MT_CHECK_ARG(cfg->depth == 1 || cfg->depth == 3, "depth must be 1 or 3");
+  MT_CHECK_ARG(cfg->num_actions >= 1 && cfg->num_actions <= 32, "num_actions out of range [1,32]");
+  MT_CHECK_ARG(cfg->num_reps >= 1 && cfg->num_reps <= 31, "num_reps out of range [1,31]");
+  MT_CHECK_ARG(cfg->activation == MT_ACT_RELU || cfg->activation == MT_ACT_LEAKY, "bad activation");
+  MT_CHECK_ARG(cfg->softmax_temp > 0.f, "softmax_temp must be > 0");
+  mt_net *n = new mt_net();
+  n->cfg = *cfg;
+  n->C = 4 * cfg->depth;
+  n->O = 1 + cfg->num_actions + cfg->num_reps;
+  const int arch = cfg->arch, d = cfg->depth;
+  if (arch == MT_ARCH_NIPS && d == 1) build_layout<NipsArch<4>>(n);
+  else if (arch == MT_ARCH_NIPS && d == 3) build_layout<NipsArch<12>>(n);
+  else if (arch == MT_ARCH_NATURE && d == 1) build_layout<NatureArch<4>>(n);
+  else if (arch == MT_ARCH_NATURE && d == 3) build_layout<NatureArch<12>>(n);
+  else {
+    delete n;
+    set_error("arch %d not built into this library", arch);
+    return MT_ERR_UNSUPPORTED;
+  }
+  *out = n;
+  return MT_OK;
+}
+
+extern "C" void mt_net_destroy(mt_net *net) { delete net; }
+
+extern "C" int mt_net_num_params(const mt_net *net, size_t *n) {
+  MT_CHECK_ARG(net && n, "null argument");
+  *n = net->nparams;
+  return MT_OK;
+}
+
+extern "C" int mt_net_num_vars(const mt_net *net, int *n) {
+  MT_CHECK_ARG(net && n, "null argument");
+  *n = (int)net->vars.size();
+  return MT_OK;
+}
+
+extern "C" int mt_net_var_info(const mt_net *net, int i, char *name, int name_len, int64_t *shape4,
+                               int *ndim, size_t *offset, float *init_bound) {
+  MT_CHECK_ARG(net, "null net");
+  MT_CHECK_ARG(i >= 0 && i < (int)net->vars.size(), "var index %d out of range", i);
+  const VarInfo &v = net->vars[i];
+  if (name && name_len > 0) {
+    std::strncpy(name, v.name.c_str(), name_len - 1);
+    name[name_len - 1] = 0;
+  }
+  if (shape4)
+    for (int k = 0; k < 4; ++k) shape4[k] = k < v.ndim ? v.shape[k] : 0;
+  if (ndim) *ndim = v.ndim;
+  if (offset) *offset = v.offset;
+  if (init_bound) *init_bound = v.bound;
+  return MT_OK;
+}
+
+extern "C" int mt_net_feature_dim(const mt_net *net, int *f) {
+  MT_CHECK_ARG(net && f, "null argument");
+  *f = net->F;
+  return MT_OK;
+}
+
+extern "C" int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes) {
+  MT_CHECK_ARG(net && bytes, "null argument");
+  MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
+  MT_ARCH_SWITCH(net, { *bytes = ws_layout<Ar>(net, batch).total * sizeof(float); });
+  return MT_OK;
+}
+
+extern "C" int mt_forward(const mt_net *net, const float *params, const uint8_t *obs, int batch,
+                          void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
+                          mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && obs && ws && v && pi && rep, "null argument");
+  MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
+  MT_ARCH_SWITCH(net, {
+    const WsLayout L = ws_layout<Ar>(net, batch);
+    if (ws_bytes < L.total * sizeof(float)) {
+      set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
+      return MT_ERR_WORKSPACE;
+    }
+    return forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, (hipStream_t)stream);
+  });
+  return MT_OK;
+}
+
+extern "C" int mt_loss_backward(const mt_net *net, const float *params, const uint8_t *obs,
+                                int batch, void *ws, size_t ws_bytes, const float *pi,
+                                const float *rep, const float *v, const int32_t *a_idx,
+                                const int32_t *r_idx, const float *y, const float *adv,
+                                float entropy_beta, float *grad, float *loss_terms,
+                                mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && obs && ws && pi && rep && v && a_idx && r_idx && y && adv && grad,
+               "null argument");
+  MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
+  MT_ARCH_SWITCH(net, {
+    const WsLayout L = ws_layout<Ar>(net, batch);
+    if (ws_bytes < L.total * sizeof(float)) {
+      set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
+      return MT_ERR_WORKSPACE;
+    }
+    return backward_impl<Ar>(net, params, obs, batch, (float *)ws, pi, rep, v, a_idx, r_idx, y, adv,
+                             entropy_beta, grad, loss_terms, (hipStream_t)stream);
+  });
+  return MT_OK;
+}
+
+extern "C" int mt_sum_slabs(const float *parts, int nslabs, size_t n, float *out,
+                            mt_stream_t stream) {
+  MT_CHECK_ARG(parts && out && nslabs >= 1, "bad argument");
+  return sum_slabs(parts, nslabs, n, out, (hipStream_t)stream);
+}
