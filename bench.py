@@ -1,0 +1,243 @@
+"""Benchmark of the PAAC+FiGAR rollout/update hot path on MI355X (BASELINE.json metric).
+
+One "step" = one PAAC update: T rollout macro-steps over every env of the rank (device
+forward, sampling, native emulator step, H2D of the pushed screens, device preprocess, host
+bookkeeping) + bootstrap forward + n-step returns + fused loss backward + [RCCL all-reduce] +
+clip/RMSProp. value = env-steps/s of the whole job = world * ec * T * K / max-over-ranks time.
+Workload (N=1 default): BASELINE.json configs[1], Pong NIPS ec=32 ew=8 t_max=5, synthetic
+84x84 frames (manette_amd/synthetic.py), random-init weights.
+
+  python bench.py [--gpus N --steps K --warmup W --config pong-nips --sampling device]
+  N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # BASELINE.json configs[1..4]; per-rank ec (weak scaling: ec per GPU fixed)
+    'pong-nips': dict(game='pong', arch='NIPS', ec=32, ew=8, max_repetition=0, nb_choices=1, rgb=False),
+    'breakout-nature-figar': dict(game='breakout', arch='NATURE', ec=64, ew=8, max_repetition=10,
+                                  nb_choices=11, rgb=False),
+    'seaquest-nature': dict(game='seaquest', arch='NATURE', ec=32, ew=8, max_repetition=0, nb_choices=1,
+                            rgb=False),
+}
+MI355X_FP32_TFLOPS = 157.3   # dense fp32 (vector = MFMA), MI355X_MICROARCH.md
+MI355X_HBM_GBS = 8000.0      # HBM3E peak, MI355X_MICROARCH.md
+
+
+def conv_out(h, k, s):
+    return (h - k) // s + 1
+
+
+def arch_flops(arch, depth, A, R):
+    """Forward FLOPs per sample per layer (2*MACs) for NIPS/NATURE, and weights (floats)."""
+    C = 4 * depth
+    if arch == 'NIPS':
+        convs = [(8, 4, C, 16), (4, 2, 16, 32)]
+        F = 256
+    else:
+        convs = [(8, 4, C, 32), (4, 2, 32, 64), (3, 1, 64, 64)]
+        F = 512
+    h = 84
+    layers = []
+    for (k, s, cin, cout) in convs:
+        h = conv_out(h, k, s)
+        layers.append(('conv', 2.0 * h * h * cout * k * k * cin, k * k * cin * cout + cout, h * h * cout))
+    flat = h * h * convs[-1][3]
+    layers.append(('fc', 2.0 * flat * F, flat * F + F, F))
+    layers.append(('heads', 2.0 * F * (1 + A + R), F * (1 + A + R) + 1 + A + R, 1 + A + R))
+    return layers
+
+
+def train_pass_flops(layers, N):
+    """forward + backward (dW everywhere, dX everywhere except the input conv)."""
+    fwd = sum(l[1] for l in layers)
+    return N * (3 * fwd - layers[0][1])
+
+
+def build_args(cfg, T, sampling, seed):
+    import train as train_cli
+    a = train_cli.get_arg_parser().parse_args([])
+    a.game = cfg['game']
+    a.arch = cfg['arch']
+    a.emulator_counts = cfg['ec']
+    a.emulator_workers = cfg['ew']
+    a.max_repetition = cfg['max_repetition']
+    a.nb_choices = cfg['nb_choices']
+    a.rgb = cfg['rgb']
+    a.max_local_steps = T
+    a.max_global_steps = 1 << 62
+    a.checkpoint_interval = 1 << 62
+    a.sampling = sampling
+    a.runner = 'native'
+    a.seed = seed
+    a.debugging_folder = tempfile.mkdtemp(prefix='manette_bench_')
+    return a
+
+
+def cpu_baseline(cfg, T, seconds, rank):
+    """The oracle ("port") restated reference loop on host cores: numpy float32 network +
+    clip/RMSProp, the reference's host loop and process runners (mp.Queue barrier), the same
+    synthetic emulators with CPU preprocess. Bounded sample: as many updates as fit in ~seconds."""
+    from oracle import host_loop, policy
+    from manette_amd.environment_creator import MINIMAL_ACTIONS
+    from manette_amd.synthetic import SyntheticEmulator
+    A = MINIMAL_ACTIONS[cfg['game']]
+    ec, ew = cfg['ec'], cfg['ew']
+    tab = policy.tab_repetitions(cfg['max_repetition'], cfg['nb_choices'])
+    cores = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get('OMP_NUM_THREADS', cores))
+    cores = min(cores, omp)
+    emus = [SyntheticEmulator(i, A, rgb=cfg['rgb']) for i in range(ec)]
+    net = host_loop.OracleNetwork(cfg['arch'], 3 if cfg['rgb'] else 1, A, cfg['nb_choices'], seed=0)
+    np.random.seed(1234)
+
+    class Timed(host_loop.HostLoop):
+        pass
+
+    loop = Timed(emus, net, tab, A, max_local_steps=T, workers=ew, record=False)
+    # warm up one update, then time whole updates until `seconds` elapse (at most 200)
+    steps_per_update = ec * T
+    t_start = [None]
+    n_upd = [0]
+    orig_train = net.train
+
+    def train_hook(*a, **k):
+        orig_train(*a, **k)
+        n_upd[0] += 1
+        if n_upd[0] == 1:
+            t_start[0] = time.perf_counter()
+        elif time.perf_counter() - t_start[0] > seconds or n_upd[0] >= 201:
+            loop.global_step = 1 << 62  # stop after this update
+    net.train = train_hook
+    loop.run(1 << 61)
+    elapsed = time.perf_counter() - t_start[0]
+    timed = n_upd[0] - 1
+    return dict(value=timed * steps_per_update / elapsed, unit='env-steps/s', cores=cores, kind='port',
+                sample='%d PAAC updates (ec=%d, t_max=%d, %s) after 1 warm-up, %d emulator worker '
+                       'processes, numpy fp32 network, %.1f s' % (timed, ec, T, cfg['arch'], ew, elapsed))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=60)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--config', default='pong-nips', choices=sorted(CONFIGS))
+    ap.add_argument('--t_max', type=int, default=5)
+    ap.add_argument('--sampling', default='device', choices=['device', 'host'])
+    ap.add_argument('--cpu_seconds', type=float, default=15.0)
+    ap.add_argument('--no_cpu_baseline', action='store_true')
+    ap.add_argument('--seed', type=int, default=0)
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    cfg = CONFIGS[a.config]
+    T = a.t_max
+    args = build_args(cfg, T, a.sampling, a.seed)
+    args.env_id_offset = rank * cfg['ec']
+
+    from manette_amd.exploration_policy import ExplorationPolicy
+    from manette_amd.paac import PAACLearner
+    import train as train_cli
+    np.random.seed(1234 + rank)
+    explo = ExplorationPolicy(args)
+    net_creator, env_creator = train_cli.get_network_and_environment_creator(args, explo)
+    learner = PAACLearner(net_creator, env_creator, explo, args)
+    learner.is_chief = False  # no checkpoint writes from the benchmark
+    learner.start()
+
+    def one_update():
+        learner.book.new_update()
+        for t in range(T):
+            learner.step(t)
+        learner.update()
+
+    for _ in range(a.warmup):
+        one_update()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    learner.profile = {}
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        one_update()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    prof = {k: [s.elapsed_time(e) for (s, e) in v] for k, v in learner.profile.items()}
+    learner.profile = None
+    ec = cfg['ec']
+    value = world * ec * T * a.steps / elapsed
+
+    if rank == 0:
+        depth = 3 if cfg['rgb'] else 1
+        A = args.num_actions
+        layers = arch_flops(cfg['arch'], depth, A, cfg['nb_choices'])
+        N = ec * T
+        tp_ms = float(np.mean(prof['train_pass']))
+        tp_flops = train_pass_flops(layers, N)
+        rf_ms = float(np.mean(prof['rollout_forward']))
+        fwd_flops = ec * sum(l[1] for l in layers)
+        fwd_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in layers) + 4 * ec * sum(l[3] for l in layers)
+        achieved = tp_flops / (tp_ms * 1e-3) / 1e12
+        line = {
+            'metric': 'env-steps/sec (ec x t_max frames per update)',
+            'value': round(value, 1),
+            'unit': 'env-steps/s',
+            'n_gpus': world,
+            'steps': a.steps,
+            'warmup': a.warmup,
+            'ms_per_step': round(elapsed / a.steps * 1e3, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'fp32',
+            'data': 'synthetic (seeded 210x160 screens, native emulator threads, GPU preprocess)',
+            'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling' % (
+                a.config, ec, cfg['ew'], T, a.sampling), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
+                'global_emulators': ec * world, 'parallelism': 'dp%d' % world},
+            'roofline': {'bound': 'mfma', 'kernel': 'train pass (fwd+bwd, %d rows)' % N,
+                         'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': round(achieved / MI355X_FP32_TFLOPS, 4), 'traffic': None,
+                         'ms_per_launch': round(tp_ms, 4), 'flop_per_launch': tp_flops},
+            'rollout_forward': {'ms': round(rf_ms, 4), 'tflops': round(fwd_flops / (rf_ms * 1e-3) / 1e12, 3),
+                                'hbm_gbs': round(fwd_bytes / (rf_ms * 1e-3) / 1e9, 1),
+                                'hbm_frac': round(fwd_bytes / (rf_ms * 1e-3) / 1e9 / MI355X_HBM_GBS, 4)},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            learner.cleanup()
+            learner = None
+            line['cpu_baseline'] = cpu_baseline(cfg, T, a.cpu_seconds, rank)
+        print(json.dumps(line), flush=True)
+    if learner is not None:
+        learner.cleanup()
+    shutil.rmtree(args.debugging_folder, ignore_errors=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

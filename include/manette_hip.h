@@ -101,9 +101,10 @@ int mt_sample(const float *pi, const float *rep, int batch, int num_actions, int
 /* ---- n-step return / advantage scan (A9) ---------------------------------------------------
  * Replaces paac.py:219-231 (+ flatten :237-238). rewards/masks/values: [T][E] fp32,
  * v_boot: [E] (V(s_T)). Writes y, adv: [T][E] fp32 (row t*E+e). Arithmetic follows the
- * reference's numpy dtypes exactly (first product in fp32, the rest fp64, fp32 output). */
+ * reference's numpy dtypes exactly (gamma is the python float: the first product gamma*V_T in
+ * fp32, the rest fp64, fp32 output). */
 int mt_returns(const float *rewards, const float *masks, const float *values, const float *v_boot,
-               float gamma, int T, int E, float *y, float *adv, mt_stream_t stream);
+               double gamma, int T, int E, float *y, float *adv, mt_stream_t stream);
 
 /* ---- fused loss + backward (A10) ------------------------------------------------------------
  * Replaces optimizer.compute_gradients(network.loss) (actor_learner.py:49) with the loss of

@@ -1,0 +1,59 @@
+/*
+ * manette_host.h — C ABI of libmanette_host.so: the native emulator runner of the PAAC hot
+ * path (host cores). Replaces runners.py:7-50 + emulator_runner.py:19-42 for native emulator
+ * banks: a pool of worker threads steps disjoint env blocks per macro-step (FiGAR repeats,
+ * reward sums, terminal resets) and writes the screens each env pushed into ONE compact
+ * pinned staging buffer that the caller hipMemcpyAsync's to HBM for mt_preprocess.
+ *
+ * The bank implemented here is the synthetic ALE stand-in (manette_amd/synthetic.py defines
+ * it and precomputes its streams from seeded numpy RandomStates, so the Python and native
+ * paths see identical screens and rewards):
+ *   next(a):  push screens (ring[2k % ring], ring[(2k+1) % ring]); reward = rewards[k % L];
+ *             k += 1; steps += 1; terminal = steps >= episode_len
+ *   initial:  4 pushes as next(0) without reward; steps = 0   (atari_emulator.py:102-110)
+ * Status codes as manette_hip.h (0 = ok); mh_last_error() describes the last failure.
+ */
+#ifndef MANETTE_HOST_H
+#define MANETTE_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mh_runner mh_runner;
+
+const char *mh_last_error(void);
+
+/* screens: [n_envs][ring][frame_bytes] uint8, rewards: [n_envs][reward_len] float32 (caller
+ * keeps both alive). tab_rep: FiGAR repetition table (exploration_policy.py:56-62). */
+int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_rep, int n_reps,
+                     const uint8_t *screens, int ring, size_t frame_bytes, const float *rewards,
+                     int reward_len, int episode_len, mh_runner **out);
+void mh_runner_destroy(mh_runner *r);
+
+/* get_initial_state() of every env: 4 pushes each. Outputs as mh_runner_step. */
+int mh_runner_reset(mh_runner *r, uint8_t *staging, int32_t *push_offset, int32_t *push_count,
+                    int *total_pushes);
+
+/* One macro-step (emulator_runner.py:24-41) of every env with action a_idx[e] repeated
+ * tab_rep[r_idx[e]] more times unless the episode ends. Outputs:
+ *   staging      [total_pushes][2][frame_bytes]: screens of the last <=4 pushes of each env,
+ *                env-major, oldest first (a terminal's reset pushes included);
+ *   push_offset  [E] first staging slot of env e; push_count [E] in 1..4;
+ *   reward       [E] float32 sum over the repeats (shared float32 array semantics);
+ *   over         [E] 1.0 if the episode ended (state is then the reset state).
+ * staging must hold 4*E slots. */
+int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx, uint8_t *staging,
+                   int32_t *push_offset, int32_t *push_count, float *reward, float *over,
+                   int *total_pushes);
+
+/* Per-env counters (for tests): k (next() calls incl. reset pushes) and steps in episode. */
+int mh_runner_env_state(const mh_runner *r, int e, int64_t *k, int32_t *steps);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MANETTE_HOST_H */

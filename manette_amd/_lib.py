@@ -1,0 +1,115 @@
+"""ctypes bindings of the two C-ABI libraries (include/manette_hip.h, include/manette_host.h).
+
+The HIP library is the only compute path: if it is missing or fails to load, every device
+call raises (there is no CPU fallback in the product).
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HIP_LIB = os.path.join(HERE, 'libmanette_hip.so')
+HOST_LIB = os.path.join(HERE, 'libmanette_host.so')
+
+MT_ARCH = {'NIPS': 0, 'NATURE': 1, 'PWYX': 2, 'LSTM': 3}
+MT_ACT = {'relu': 0, 'leaky_relu': 1}
+MT_CLIP = {'ignore': 0, 'global': 1}
+MT_NORM_PARTIALS = 512
+
+
+class MTError(RuntimeError):
+    pass
+
+
+class mt_net_config(C.Structure):
+    _fields_ = [('arch', C.c_int32), ('depth', C.c_int32), ('num_actions', C.c_int32),
+                ('num_reps', C.c_int32), ('activation', C.c_int32), ('alpha_leaky', C.c_float),
+                ('softmax_temp', C.c_float)]
+
+
+_P = C.c_void_p
+_I = C.c_int
+_F = C.c_float
+_SZ = C.c_size_t
+
+_HIP_SIGS = {
+    'mt_last_error': (C.c_char_p, []),
+    'mt_version': (_I, []),
+    'mt_net_create': (_I, [C.POINTER(mt_net_config), C.POINTER(_P)]),
+    'mt_net_destroy': (None, [_P]),
+    'mt_net_num_params': (_I, [_P, C.POINTER(_SZ)]),
+    'mt_net_num_vars': (_I, [_P, C.POINTER(_I)]),
+    'mt_net_var_info': (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_int64), C.POINTER(_I),
+                             C.POINTER(_SZ), C.POINTER(_F)]),
+    'mt_net_feature_dim': (_I, [_P, C.POINTER(_I)]),
+    'mt_net_workspace_bytes': (_I, [_P, _I, C.POINTER(_SZ)]),
+    'mt_forward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P]),
+    'mt_sample': (_I, [_P, _P, _I, _I, _I, C.c_uint64, _P, _P, _P, _P]),
+    'mt_returns': (_I, [_P, _P, _P, _P, C.c_double, _I, _I, _P, _P, _P]),
+    'mt_loss_backward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
+    'mt_grad_sumsq': (_I, [_P, _SZ, _F, _P, _P]),
+    'mt_clip_rmsprop': (_I, [_P, _P, _P, _P, _SZ, _P, _P, _F, _F, _F, _F, _I, _F, _P, _P]),
+    'mt_preprocess': (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    'mt_sum_slabs': (_I, [_P, _I, _SZ, _P, _P]),
+    'mt_graph_begin': (_I, [_P]),
+    'mt_graph_end': (_I, [_P, C.POINTER(_P)]),
+    'mt_graph_launch': (_I, [_P, _P]),
+    'mt_graph_destroy': (_I, [_P]),
+}
+
+_HOST_SIGS = {
+    'mh_last_error': (C.c_char_p, []),
+    'mh_runner_create': (_I, [_I, _I, _P, _I, _P, _I, _SZ, _P, _I, _I, C.POINTER(_P)]),
+    'mh_runner_destroy': (None, [_P]),
+    'mh_runner_reset': (_I, [_P, _P, _P, _P, C.POINTER(_I)]),
+    'mh_runner_step': (_I, [_P, _P, _P, _P, _P, _P, _P, _P, C.POINTER(_I)]),
+    'mh_runner_env_state': (_I, [_P, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+}
+
+_hip = None
+_host = None
+
+
+def _load(path, sigs):
+    if not os.path.exists(path):
+        raise MTError('%s is not built (run __graft_entry__.build() or python -m manette_amd.build)'
+                      % path)
+    lib = C.CDLL(path)
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        _hip = _load(HIP_LIB, _HIP_SIGS)
+    return _hip
+
+
+def host():
+    global _host
+    if _host is None:
+        _host = _load(HOST_LIB, _HOST_SIGS)
+    return _host
+
+
+def check(rc, what='call'):
+    if rc != 0:
+        msg = hip().mt_last_error()
+        raise MTError('%s failed (status %d): %s' % (what, rc, msg.decode() if msg else ''))
+
+
+def check_host(rc, what='call'):
+    if rc != 0:
+        msg = host().mh_last_error()
+        raise MTError('%s failed (status %d): %s' % (what, rc, msg.decode() if msg else ''))
+
+
+def hip_symbols():
+    return sorted(_HIP_SIGS)
+
+
+def host_symbols():
+    return sorted(_HOST_SIGS)

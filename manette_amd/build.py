@@ -1,0 +1,71 @@
+"""Build the native libraries in-tree (no JIT cache, so the .so files travel with the repo).
+
+  libmanette_hip.so   hipcc --offload-arch=gfx950: HIP kernels + C ABI (include/manette_hip.h)
+  libmanette_host.so  g++: native emulator runner + bookkeeping (include/manette_host.h)
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+HIP_SOURCES = ['net.hip', 'misc.hip']
+HIP_HEADERS = ['common.h', 'gemm.h']
+HOST_SOURCES = ['runner.cpp']
+HIP_LIB = os.path.join(HERE, 'libmanette_hip.so')
+HOST_LIB = os.path.join(HERE, 'libmanette_host.so')
+INCLUDE = os.path.join(os.path.dirname(HERE), 'include')
+
+
+def _hipcc():
+    for c in (os.environ.get('HIPCC'), '/opt/rocm/bin/hipcc', shutil.which('hipcc')):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError('hipcc not found')
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_hip(force=False, verbose=False):
+    srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
+    deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [os.path.join(INCLUDE, 'manette_hip.h')]
+    if not force and not _stale(HIP_LIB, deps):
+        return HIP_LIB
+    tmp = HIP_LIB + '.tmp'
+    cmd = [_hipcc(), '--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
+           '-Wno-unused-result', '-o', tmp] + srcs
+    if verbose:
+        print(' '.join(cmd))
+    subprocess.check_call(cmd, cwd=CSRC)
+    os.replace(tmp, HIP_LIB)
+    return HIP_LIB
+
+
+def build_host(force=False, verbose=False):
+    srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES]
+    deps = srcs + [os.path.join(INCLUDE, 'manette_host.h')]
+    if not force and not _stale(HOST_LIB, deps):
+        return HOST_LIB
+    tmp = HOST_LIB + '.tmp'
+    cmd = ['g++', '-O3', '-march=x86-64-v2', '-fPIC', '-shared', '-std=c++20', '-pthread', '-Wall',
+           '-o', tmp] + srcs
+    if verbose:
+        print(' '.join(cmd))
+    subprocess.check_call(cmd, cwd=CSRC)
+    os.replace(tmp, HOST_LIB)
+    return HOST_LIB
+
+
+def build_all(force=False, verbose=False):
+    build_host(force, verbose)
+    build_hip(force, verbose)
+
+
+if __name__ == '__main__':
+    build_all(force='--force' in sys.argv, verbose=True)

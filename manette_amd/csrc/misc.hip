@@ -29,16 +29,17 @@ void set_error(const char *fmt, ...) {
 // ---------------------------------------------------------------------------------------------
 __global__ void returns_kernel(const float *__restrict__ r, const float *__restrict__ mask,
                                const float *__restrict__ V, const float *__restrict__ VT,
-                               float gamma, int T, int E, float *__restrict__ y,
+                               double gamma, int T, int E, float *__restrict__ y,
                                float *__restrict__ adv) {
+#pragma clang fp contract(off)
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
   // t = T-1: float32 product gamma*R_T, then float64 with the mask and reward.
-  const float g32 = __fmul_rn(gamma, VT[e]);
+  const float g32 = __fmul_rn((float)gamma, VT[e]);
   double R = (double)r[(size_t)(T - 1) * E + e] + (double)g32 * (double)mask[(size_t)(T - 1) * E + e];
   y[(size_t)(T - 1) * E + e] = (float)R;
   adv[(size_t)(T - 1) * E + e] = (float)(R - (double)V[(size_t)(T - 1) * E + e]);
-  const double gd = (double)gamma;
+  const double gd = gamma;  // python float (float64)
   for (int t = T - 2; t >= 0; --t) {
     const size_t i = (size_t)t * E + e;
     R = (double)r[i] + (gd * R) * (double)mask[i];
@@ -81,6 +82,7 @@ __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
     const float *__restrict__ g, size_t n, const float *__restrict__ partials,
     const float *__restrict__ lr_dev, float decay, float momentum, float eps, float clip,
     int clip_type, float s, float *__restrict__ norm_out) {
+#pragma clang fp contract(off)  // TF's operation-by-operation rounding, no fused multiply-add
   __shared__ float sh_scale;
   if (threadIdx.x < 64) {
     double acc = 0.0;
@@ -201,7 +203,7 @@ extern "C" const char *mt_last_error(void) { return g_err; }
 extern "C" int mt_version(void) { return 1; }
 
 extern "C" int mt_returns(const float *rewards, const float *masks, const float *values,
-                          const float *v_boot, float gamma, int T, int E, float *y, float *adv,
+                          const float *v_boot, double gamma, int T, int E, float *y, float *adv,
                           mt_stream_t stream) {
   MT_CHECK_ARG(rewards && masks && values && v_boot && y && adv, "null argument");
   MT_CHECK_ARG(T >= 1 && E >= 1, "T and E must be >= 1");

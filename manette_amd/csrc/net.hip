@@ -93,8 +93,8 @@ template <class G>
 static void add_conv(mt_net *n, size_t &off, int idx) {
   // networks.py:34-55: weights U(+-1/sqrt(filters*k*k)) (shape[3] is the OUTPUT channel count),
   // biases U(+-1/sqrt(in_channels*k*k)).
-  const float bw = 1.0f / std::sqrt((float)(G::COUT * G::KH * G::KW));
-  const float bb = 1.0f / std::sqrt((float)(G::CIN * G::KH * G::KW));
+  const float bw = (float)(1.0 / std::sqrt((double)(G::COUT * G::KH * G::KW)));
+  const float bb = (float)(1.0 / std::sqrt((double)(G::CIN * G::KH * G::KW)));
   std::string nm = "conv" + std::to_string(idx + 1);
   add_pair(n, off, "Network", nm, {G::KH, G::KW, G::CIN, G::COUT}, G::COUT, bw, bb,
            &n->off_conv[idx]);
@@ -106,9 +106,9 @@ static void build_layout(mt_net *n) {
   add_conv<typename Ar::G1>(n, off, 0);
   add_conv<typename Ar::G2>(n, off, 1);
   if constexpr (Ar::NCONV == 3) add_conv<typename Ar::G3>(n, off, 2);
-  const float bf = 1.0f / std::sqrt((float)Ar::FLAT);  // networks.py:72-89
+  const float bf = (float)(1.0 / std::sqrt((double)Ar::FLAT));  // networks.py:72-89
   add_pair(n, off, "Network", Ar::FC, {Ar::FLAT, Ar::F}, Ar::F, bf, bf, &n->off_fc);
-  const float bh = 1.0f / std::sqrt((float)Ar::F);
+  const float bh = (float)(1.0 / std::sqrt((double)Ar::F));
   const int A = n->cfg.num_actions, R = n->cfg.num_reps;
   // policy_v_network.py:22 (critic), :31 (actor), :47 (repetition) — TF creation order.
   add_pair(n, off, "Training/Critic", "critic_output", {Ar::F, 1}, 1, bh, bh, &n->off_critic);

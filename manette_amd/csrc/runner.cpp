@@ -1,0 +1,268 @@
+// Native emulator runner (host cores) — see include/manette_host.h.
+//
+// Reference: runners.py:7-50 (np.split of the envs over `ew` workers, one go-Queue per
+// worker, one barrier Queue) and emulator_runner.py:19-42 (per env: Action, next(), repeats
+// while not terminal, reward sum, reset on terminal). Here the workers are persistent threads
+// released by a generation counter and joined by an arrival counter (spin, then futex wait via
+// std::atomic::wait), so a macro-step costs a few microseconds of synchronisation instead of
+// 2*ew Queue round trips. A step runs in two phases:
+//   A: each worker steps its envs and records which screens each env pushed (last <= 4);
+//   main: prefix sum of push counts -> compact staging offsets;
+//   B: each worker copies its envs' screens into the staging buffer (pinned, H2D'd whole).
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/manette_host.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+void set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+struct Env {
+  const uint8_t *screens;  // [ring][frame_bytes]
+  const float *rewards;    // [reward_len]
+  int64_t k = 0;           // pushes so far (next() + reset pushes)
+  int32_t steps = 0;       // next() calls in the current episode
+  int64_t last[4];         // k of the last pushes, ring
+  int npush = 0;           // pushes in the current macro-step (uncapped)
+};
+
+}  // namespace
+
+struct mh_runner {
+  int E = 0, W = 0;
+  std::vector<int32_t> tab;
+  int ring = 0;
+  size_t fb = 0;
+  int reward_len = 0, episode_len = 0;
+  std::vector<Env> env;
+  std::vector<std::thread> threads;
+  // job
+  std::atomic<uint32_t> gen{0};
+  std::atomic<int> arrived{0};
+  std::atomic<bool> quit{false};
+  int phase = 0;  // 0 = reset, 1 = step A, 2 = copy B
+  const int32_t *a_idx = nullptr, *r_idx = nullptr;
+  uint8_t *staging = nullptr;
+  int32_t *push_offset = nullptr, *push_count = nullptr;
+  float *reward = nullptr, *over = nullptr;
+
+  int block_begin(int w) const { return (int)((int64_t)E * w / W); }
+  int block_end(int w) const { return (int)((int64_t)E * (w + 1) / W); }
+
+  void push(Env &e) {
+    e.last[e.npush & 3] = e.k;
+    e.npush++;
+    e.k++;
+  }
+  // emulator.next(a): returns (reward, terminal); the screens are those of push k.
+  float next(Env &e, bool *term) {
+    const float r = e.rewards[e.k % reward_len];
+    push(e);
+    e.steps++;
+    *term = e.steps >= episode_len;
+    return r;
+  }
+  void initial(Env &e) {  // get_initial_state(): 4 noop action_repeats
+    for (int i = 0; i < 4; ++i) push(e);
+    e.steps = 0;
+  }
+
+  void run_phase(int w) {
+    const int b0 = block_begin(w), b1 = block_end(w);
+    if (phase == 0) {
+      for (int i = b0; i < b1; ++i) {
+        env[i].npush = 0;
+        initial(env[i]);
+      }
+    } else if (phase == 1) {
+      for (int i = b0; i < b1; ++i) {
+        Env &e = env[i];
+        e.npush = 0;
+        int left = tab[r_idx[i]];  // Action.init_from_list (exploration_policy.py:13-17)
+        bool term = false;
+        float rs = next(e, &term);  // emulator_runner.py:27
+        if (term) initial(e);       // :28-29
+        while (left > 0 && !term) {  // :33-40 (float32 accumulation of the shared array)
+          --left;
+          rs += next(e, &term);
+          if (term) initial(e);
+        }
+        reward[i] = rs;
+        over[i] = term ? 1.f : 0.f;
+      }
+    }
+    if (phase == 0 || phase == 2) {
+      for (int i = b0; i < b1; ++i) {
+        const Env &e = env[i];
+        const int n = std::min(e.npush, 4);
+        for (int j = 0; j < n; ++j) {
+          const int64_t kk = e.last[(e.npush - n + j) & 3];
+          uint8_t *dst = staging + (size_t)(push_offset[i] + j) * 2 * fb;
+          std::memcpy(dst, e.screens + (size_t)((2 * kk) % ring) * fb, fb);
+          std::memcpy(dst + fb, e.screens + (size_t)((2 * kk + 1) % ring) * fb, fb);
+        }
+      }
+    }
+  }
+
+  void worker(int w) {
+    uint32_t seen = 0;
+    for (;;) {
+      // spin briefly, then sleep on the generation word
+      int spins = 0;
+      uint32_t g;
+      while ((g = gen.load(std::memory_order_acquire)) == seen) {
+        if (++spins < 4000) {
+          cpu_relax();
+        } else {
+          gen.wait(seen, std::memory_order_acquire);
+        }
+      }
+      seen = g;
+      if (quit.load(std::memory_order_acquire)) return;
+      run_phase(w);
+      if (arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == W) arrived.notify_one();
+    }
+  }
+
+  void dispatch(int ph) {
+    phase = ph;
+    arrived.store(0, std::memory_order_relaxed);
+    gen.fetch_add(1, std::memory_order_acq_rel);
+    gen.notify_all();
+    int spins = 0;
+    int a;
+    while ((a = arrived.load(std::memory_order_acquire)) != W) {
+      if (++spins < 20000) cpu_relax();
+      else arrived.wait(a, std::memory_order_acquire);
+    }
+  }
+
+  int compact(int *total) {
+    int off = 0;
+    for (int i = 0; i < E; ++i) {
+      const int n = std::min(env[i].npush, 4);
+      push_offset[i] = off;
+      push_count[i] = n;
+      off += n;
+    }
+    *total = off;
+    return 0;
+  }
+};
+
+extern "C" const char *mh_last_error(void) { return g_err; }
+
+extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_rep, int n_reps,
+                                const uint8_t *screens, int ring, size_t frame_bytes,
+                                const float *rewards, int reward_len, int episode_len,
+                                mh_runner **out) {
+  if (!out || !tab_rep || !screens || !rewards) {
+    set_error("null argument");
+    return 1;
+  }
+  if (n_envs < 1 || n_workers < 1 || n_reps < 1 || ring < 2 || frame_bytes == 0 ||
+      reward_len < 1 || episode_len < 1) {
+    set_error("bad sizes");
+    return 1;
+  }
+  for (int i = 0; i < n_reps; ++i)
+    if (tab_rep[i] < 0) {
+      set_error("negative repetition");
+      return 1;
+    }
+  mh_runner *r = new mh_runner();
+  r->E = n_envs;
+  r->W = std::min(n_workers, n_envs);
+  r->tab.assign(tab_rep, tab_rep + n_reps);
+  r->ring = ring;
+  r->fb = frame_bytes;
+  r->reward_len = reward_len;
+  r->episode_len = episode_len;
+  r->env.resize(n_envs);
+  for (int i = 0; i < n_envs; ++i) {
+    r->env[i].screens = screens + (size_t)i * ring * frame_bytes;
+    r->env[i].rewards = rewards + (size_t)i * reward_len;
+  }
+  for (int w = 0; w < r->W; ++w) r->threads.emplace_back([r, w] { r->worker(w); });
+  *out = r;
+  return 0;
+}
+
+extern "C" void mh_runner_destroy(mh_runner *r) {
+  if (!r) return;
+  r->quit.store(true, std::memory_order_release);
+  r->gen.fetch_add(1, std::memory_order_acq_rel);
+  r->gen.notify_all();
+  for (auto &t : r->threads) t.join();
+  delete r;
+}
+
+extern "C" int mh_runner_reset(mh_runner *r, uint8_t *staging, int32_t *push_offset,
+                               int32_t *push_count, int *total_pushes) {
+  if (!r || !staging || !push_offset || !push_count || !total_pushes) {
+    set_error("null argument");
+    return 1;
+  }
+  r->staging = staging;
+  r->push_offset = push_offset;
+  r->push_count = push_count;
+  for (int i = 0; i < r->E; ++i) {
+    push_offset[i] = 4 * i;
+    push_count[i] = 4;
+  }
+  *total_pushes = 4 * r->E;
+  r->dispatch(0);
+  return 0;
+}
+
+extern "C" int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx,
+                              uint8_t *staging, int32_t *push_offset, int32_t *push_count,
+                              float *reward, float *over, int *total_pushes) {
+  if (!r || !a_idx || !r_idx || !staging || !push_offset || !push_count || !reward || !over ||
+      !total_pushes) {
+    set_error("null argument");
+    return 1;
+  }
+  const int nr = (int)r->tab.size();
+  for (int i = 0; i < r->E; ++i)
+    if (r_idx[i] < 0 || r_idx[i] >= nr) {
+      set_error("r_idx[%d] = %d out of range [0,%d)", i, r_idx[i], nr);
+      return 1;
+    }
+  r->a_idx = a_idx;
+  r->r_idx = r_idx;
+  r->staging = staging;
+  r->push_offset = push_offset;
+  r->push_count = push_count;
+  r->reward = reward;
+  r->over = over;
+  r->dispatch(1);
+  r->compact(total_pushes);
+  r->dispatch(2);
+  return 0;
+}
+
+extern "C" int mh_runner_env_state(const mh_runner *r, int e, int64_t *k, int32_t *steps) {
+  if (!r || e < 0 || e >= r->E) {
+    set_error("bad env index");
+    return 1;
+  }
+  if (k) *k = r->env[e].k;
+  if (steps) *steps = r->env[e].steps;
+  return 0;
+}

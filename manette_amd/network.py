@@ -1,0 +1,199 @@
+"""HIP-backed policy/value network: the device side of networks.py + policy_v_network.py +
+the optimizer of actor_learner.py:43-74, driven through libmanette_hip.so.
+
+torch tensors are used for device storage and the current stream only; every compute call is a
+C-ABI launch. One flat fp32 buffer holds all variables (TF creation order and names); the
+gradient and the RMSProp slots (`ms` initialised to ONES, `mom` to zeros — TF1
+RMSPropOptimizer, pinned by tests/golden/meta_graph.json) share its layout.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class DeviceNetwork(object):
+    """network_conf of train.py:52-63 -> device parameters + forward / backward / update."""
+
+    def __init__(self, conf, device='cuda'):
+        self.conf = dict(conf)
+        self.device = torch.device(device)
+        self.arch = conf.get('arch', 'NIPS')
+        self.depth = 3 if conf.get('rgb', False) else 1
+        self.num_actions = int(conf['num_actions'])
+        self.num_reps = int(conf.get('nb_choices', 1))
+        self.temp = float(conf.get('softmax_temp', 1.0))
+        self.beta = float(conf.get('entropy_regularisation_strength', 0.02))
+        self.clip_norm = float(conf.get('clip_norm', 3.0))
+        clip_type = conf.get('clip_norm_type', 'global')
+        if clip_type not in _lib.MT_CLIP:
+            # actor_learner.py:65-67 ('local' iterates (g, v) tuples and cannot run)
+            raise ValueError('clip_norm_type %r not supported' % clip_type)
+        self.clip_type = _lib.MT_CLIP[clip_type]
+        self.decay = float(conf.get('alpha', 0.99))
+        self.eps = float(conf.get('e', 0.1))
+        cfg = _lib.mt_net_config(_lib.MT_ARCH[self.arch], self.depth, self.num_actions,
+                                 self.num_reps, _lib.MT_ACT[conf.get('activation', 'relu')],
+                                 float(conf.get('alpha_leaky_relu', 0.1)), self.temp)
+        lib = _lib.hip()
+        h = C.c_void_p()
+        check(lib.mt_net_create(C.byref(cfg), C.byref(h)), 'mt_net_create')
+        self._h = h
+        n = C.c_size_t()
+        check(lib.mt_net_num_params(h, C.byref(n)))
+        self.nparams = n.value
+        nv = C.c_int()
+        check(lib.mt_net_num_vars(h, C.byref(nv)))
+        self.vars = []
+        for i in range(nv.value):
+            name = C.create_string_buffer(256)
+            shape = (C.c_int64 * 4)()
+            nd = C.c_int()
+            off = C.c_size_t()
+            bound = C.c_float()
+            check(lib.mt_net_var_info(h, i, name, 256, shape, C.byref(nd), C.byref(off), C.byref(bound)))
+            self.vars.append((name.value.decode(), tuple(shape[k] for k in range(nd.value)), off.value,
+                              bound.value))
+        f = C.c_int()
+        check(lib.mt_net_feature_dim(h, C.byref(f)))
+        self.feature_dim = f.value
+        dev = self.device
+        self.params = torch.zeros(self.nparams, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.params)
+        self.ms = torch.ones_like(self.params)
+        self.mom = torch.zeros_like(self.params)
+        self.partials = torch.zeros(_lib.MT_NORM_PARTIALS, dtype=torch.float32, device=dev)
+        self.lr_dev = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.norm_dev = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._lr_host = torch.zeros(1, dtype=torch.float32).pin_memory()
+        self._ws = {}
+        self._out = {}
+
+    def __del__(self):
+        h = getattr(self, '_h', None)
+        if h:
+            _lib.hip().mt_net_destroy(h)
+            self._h = None
+
+    # ---- parameters ------------------------------------------------------------------------
+    def init_params(self, seed=0):
+        """U(-d, d) per variable with the reference init bounds (networks.py:34-89)."""
+        rs = np.random.RandomState(seed)
+        flat = np.zeros(self.nparams, dtype=np.float32)
+        for name, shape, off, d in self.vars:
+            n = int(np.prod(shape))
+            flat[off:off + n] = rs.uniform(-d, d, size=n).astype(np.float32)
+        self.params.copy_(torch.from_numpy(flat))
+        self.ms.fill_(1.0)
+        self.mom.zero_()
+
+    def get_variables(self, which='params'):
+        flat = getattr(self, which).detach().cpu().numpy()
+        return {name: flat[off:off + int(np.prod(shape))].reshape(shape).copy()
+                for name, shape, off, _ in self.vars}
+
+    def set_variables(self, values, which='params'):
+        flat = getattr(self, which).detach().cpu().numpy().copy()
+        for name, shape, off, _ in self.vars:
+            if name in values:
+                a = np.asarray(values[name], dtype=np.float32)
+                assert a.shape == tuple(shape), (name, a.shape, shape)
+                flat[off:off + a.size] = a.reshape(-1)
+        getattr(self, which).copy_(torch.from_numpy(flat))
+
+    # ---- buffers -----------------------------------------------------------------------------
+    def workspace(self, batch, key=None):
+        """Device workspace for `batch` rows, cached under `key` (default: the batch size)."""
+        key = batch if key is None else key
+        n = C.c_size_t()
+        check(_lib.hip().mt_net_workspace_bytes(self._h, batch, C.byref(n)))
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < n.value:
+            ws = torch.empty(n.value, dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
+
+    def outputs(self, batch, key=None):
+        k = (batch, key)
+        o = self._out.get(k)
+        if o is None:
+            dev = self.device
+            o = (torch.empty(batch, dtype=torch.float32, device=dev),
+                 torch.empty(batch, self.num_actions, dtype=torch.float32, device=dev),
+                 torch.empty(batch, self.num_reps, dtype=torch.float32, device=dev))
+            self._out[k] = o
+        return o
+
+    # ---- compute -----------------------------------------------------------------------------
+    def forward(self, obs, batch=None, out=None, ws_key=None):
+        """obs: uint8 cuda tensor [B,84,84,4*depth]. Returns (v, pi, rep) device tensors.
+        The activations stay in the workspace of `ws_key or batch` for loss_backward."""
+        B = int(batch if batch is not None else obs.shape[0])
+        assert obs.dtype == torch.uint8 and obs.is_cuda and obs.is_contiguous()
+        assert obs.numel() >= B * 84 * 84 * 4 * self.depth
+        ws = self.workspace(B, ws_key)
+        v, pi, rep = out if out is not None else self.outputs(B)
+        check(_lib.hip().mt_forward(self._h, _ptr(self.params), _ptr(obs), B, _ptr(ws), ws.numel(),
+                                    _ptr(v), _ptr(pi), _ptr(rep), _stream()), 'mt_forward')
+        return v, pi, rep
+
+    def loss_backward(self, obs, B, v, pi, rep, a_idx, r_idx, y, adv, loss_terms=None, ws_key=None):
+        """Gradient of policy_v_network.py:25-74 into self.grad (needs forward() on obs first)."""
+        ws = self.workspace(B, ws_key)
+        for t in (a_idx, r_idx):
+            assert t.dtype == torch.int32 and t.is_cuda
+        check(_lib.hip().mt_loss_backward(
+            self._h, _ptr(self.params), _ptr(obs), B, _ptr(ws), ws.numel(), _ptr(pi), _ptr(rep),
+            _ptr(v), _ptr(a_idx), _ptr(r_idx), _ptr(y), _ptr(adv), self.beta, _ptr(self.grad),
+            _ptr(loss_terms), _stream()), 'mt_loss_backward')
+        return self.grad
+
+    def set_lr(self, lr):
+        """LR lives in device memory so captured graphs pick up the schedule."""
+        self._lr_host[0] = float(lr)
+        self.lr_dev.copy_(self._lr_host, non_blocking=True)
+
+    def apply_gradients(self, inv_scale=1.0):
+        """clip_by_global_norm + ApplyRMSProp on self.grad (actor_learner.py:47-74).
+        inv_scale folds the 1/world of a data-parallel gradient sum."""
+        lib = _lib.hip()
+        s = _stream()
+        check(lib.mt_grad_sumsq(_ptr(self.grad), self.nparams, float(inv_scale), _ptr(self.partials), s),
+              'mt_grad_sumsq')
+        check(lib.mt_clip_rmsprop(_ptr(self.params), _ptr(self.ms), _ptr(self.mom), _ptr(self.grad),
+                                  self.nparams, _ptr(self.partials), _ptr(self.lr_dev), self.decay, 0.0,
+                                  self.eps, self.clip_norm, self.clip_type, float(inv_scale),
+                                  _ptr(self.norm_dev), s), 'mt_clip_rmsprop')
+
+
+def sample(pi, rep, seed, counters, a_idx, r_idx):
+    """Device multinomial draw (perf mode of exploration_policy.py:108-116)."""
+    B, A = pi.shape
+    R = rep.shape[1]
+    check(_lib.hip().mt_sample(_ptr(pi), _ptr(rep), B, A, R, C.c_uint64(seed), _ptr(counters),
+                               _ptr(a_idx), _ptr(r_idx), _stream()), 'mt_sample')
+
+
+def returns(rewards, masks, values, v_boot, gamma, y, adv):
+    """paac.py:219-231 on device."""
+    T, E = rewards.shape
+    check(_lib.hip().mt_returns(_ptr(rewards), _ptr(masks), _ptr(values), _ptr(v_boot), float(gamma),
+                                T, E, _ptr(y), _ptr(adv), _stream()), 'mt_returns')
+
+
+def preprocess(raw, push_offset, push_count, E, depth, row_lut, col_lut, prev, out):
+    """atari_emulator.py:79-124 frame pool + resize + stack on device."""
+    check(_lib.hip().mt_preprocess(_ptr(raw), _ptr(push_offset), _ptr(push_count), E, depth,
+                                   _ptr(row_lut), _ptr(col_lut), _ptr(prev), _ptr(out), _stream()),
+          'mt_preprocess')

@@ -1,0 +1,246 @@
+"""PAACLearner: the PAAC+FiGAR rollout/update loop (paac.py:15-301) on one MI355X per process.
+
+train() = init_network; loop { for t in range(T): step(t); update(); log; save_vars }; cleanup
+(the reference has no step()/update(); these are the decomposition of paac.py:140-205 and
+:219-256). Data stays in HBM: the (T+1, E, 84, 84, C) uint8 rollout state ring, values,
+action/repetition indices, y/adv. Per macro-step only the sampled indices go device->host and
+only the emulators' screens (or finished observations) + rewards go host->device.
+
+Paths (args.runner):
+  'native'  emulators stepped by libmanette_host threads (NativeRunners); their raw screens go
+            H2D from one pinned staging buffer and mt_preprocess builds the stacks (A2).
+  'python'  reference-contract Python emulators (Runners / EmulatorRunner processes); finished
+            84x84xC observations go H2D.
+Sampling (args.sampling): 'host' = the reference's numpy multinomial stream (parity mode),
+'device' = mt_sample (perf mode, same distribution).
+Data parallel: one process per GPU (torch.distributed, RCCL); env ids are offset by rank
+(rank r owns global envs [r*ec, (r+1)*ec)), each rank rolls out its own shard and the flat
+gradient is summed by ONE all_reduce per update; 1/world is folded into mt_clip_rmsprop, so
+clip + RMSProp see the global-batch mean gradient and the replicas stay identical.
+"""
+import logging
+import time
+
+import numpy as np
+import torch
+
+from . import network as devnet
+from .actor_learner import ActorLearner
+from .bookkeeping import Bookkeeper
+from .environment import COL_LUT, ROW_LUT
+from .runners import NativeRunners, Runners
+from .emulator_runner import EmulatorRunner
+
+
+class PAACLearner(ActorLearner):
+    def __init__(self, network_creator, environment_creator, explo_policy, args):
+        self.seed = int(getattr(args, 'seed', 0))
+        super(PAACLearner, self).__init__(network_creator, environment_creator, explo_policy, args)
+        self.workers = args.emulator_workers
+        self.total_repetitions = args.nb_choices
+        self.lstm_bool = (args.arch == 'LSTM')
+        if self.lstm_bool:
+            raise NotImplementedError('LSTM arch: device kernels not built yet (DESIGN.md §next)')
+        self.tab_rep = explo_policy.tab_rep
+        self.runner_kind = getattr(args, 'runner', 'native')
+        self.sampling = getattr(args, 'sampling', 'host')
+        self.depth = 3 if getattr(args, 'rgb', False) else 1
+        self.C = 4 * self.depth
+        self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
+        self.world = torch.distributed.get_world_size() if self.dist else 1
+        self.rank = torch.distributed.get_rank() if self.dist else 0
+        self.is_chief = self.rank == 0
+        self.dev = self.network.device
+        E, T, C = self.emulator_counts, self.max_local_steps, self.C
+        dev = self.dev
+        self.states = torch.zeros(T + 1, E, 84, 84, C, dtype=torch.uint8, device=dev)
+        self.values = torch.zeros(T, E, dtype=torch.float32, device=dev)
+        self.a_idx = torch.zeros(T, E, dtype=torch.int32, device=dev)
+        self.r_idx = torch.zeros(T, E, dtype=torch.int32, device=dev)
+        self.rewards_d = torch.zeros(T, E, dtype=torch.float32, device=dev)
+        self.masks_d = torch.zeros(T, E, dtype=torch.float32, device=dev)
+        self.y = torch.zeros(T, E, dtype=torch.float32, device=dev)
+        self.adv = torch.zeros(T, E, dtype=torch.float32, device=dev)
+        self.pi_roll = torch.zeros(E, self.num_actions, dtype=torch.float32, device=dev)
+        self.rep_roll = torch.zeros(E, self.total_repetitions, dtype=torch.float32, device=dev)
+        self.v_boot = torch.zeros(E, dtype=torch.float32, device=dev)
+        self.loss_terms = torch.zeros(T * E, 4, dtype=torch.float32, device=dev)
+        self.counters = torch.zeros(E, dtype=torch.int64, device=dev)
+        pin = dict(pin_memory=True)
+        self.rewards_h = torch.zeros(T, E, dtype=torch.float32, **pin)
+        self.masks_h = torch.zeros(T, E, dtype=torch.float32, **pin)
+        self.a_h = torch.zeros(T, E, dtype=torch.int32, **pin)
+        self.r_h = torch.zeros(T, E, dtype=torch.int32, **pin)
+        self.pi_h = torch.zeros(E, self.num_actions, dtype=torch.float32, **pin)
+        self.rep_h = torch.zeros(E, self.total_repetitions, dtype=torch.float32, **pin)
+        self.row_lut = torch.from_numpy(ROW_LUT.astype(np.int32)).to(dev)
+        self.col_lut = torch.from_numpy(COL_LUT.astype(np.int32)).to(dev)
+        self.event = torch.cuda.Event()
+        self.book = Bookkeeper(E, self.num_actions, self.tab_rep)
+        self.runners = None
+        self.profile = None      # name -> [(start_event, end_event)] when profiling (bench.py)
+        self.sample_seed = (self.seed * 1000003 + self.rank * 7919 + 1) & 0xffffffffffff
+
+    # ------------------------------------------------------------------------------------------
+    def _start_runners(self):
+        E, C = self.emulator_counts, self.C
+        if self.runner_kind == 'native':
+            bank = self.environment_creator.create_bank(0, E)
+            self.runners = NativeRunners(bank, self.workers, self.tab_rep)
+            self.raw_d = torch.zeros(4 * E, 2, bank.frame_bytes, dtype=torch.uint8, device=self.dev)
+            self.off_d = torch.zeros(E, dtype=torch.int32, device=self.dev)
+            self.cnt_d = torch.zeros(E, dtype=torch.int32, device=self.dev)
+            total = self.runners.reset()
+            self._upload_pushes(total, self.states[0], self.states[0].clone())
+        else:
+            emus = [self.environment_creator.create_environment(i) for i in range(E)]
+            s0 = np.asarray([e.get_initial_state() for e in emus], dtype=np.uint8)
+            variables = [s0, np.zeros(E, np.float32), np.zeros(E, np.float32), np.zeros(E, np.int32),
+                         np.zeros(E, np.int32)]
+            self.runners = Runners(self.tab_rep, EmulatorRunner, emus, self.workers, variables)
+            self.runners.start()
+            self.shared = self.runners.get_shared_variables()
+            self.obs_h = torch.zeros(E, 84, 84, C, dtype=torch.uint8, pin_memory=True)
+            self.obs_h.numpy()[...] = self.shared[0]
+            self.states[0].copy_(self.obs_h, non_blocking=True)
+
+    def _upload_pushes(self, total, out, prev):
+        """H2D of the compact staging (only the pushed screens), then mt_preprocess."""
+        r = self.runners
+        self.raw_d[:total].copy_(r.staging[:total], non_blocking=True)
+        self.off_d.copy_(r.push_offset, non_blocking=True)
+        self.cnt_d.copy_(r.push_count, non_blocking=True)
+        devnet.preprocess(self.raw_d, self.off_d, self.cnt_d, self.emulator_counts, self.depth,
+                          self.row_lut, self.col_lut, prev, out)
+
+    def _mark(self, name):
+        if self.profile is None:
+            return None
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        self.profile.setdefault(name, []).append(ev)
+        return ev[1]
+
+    # ------------------------------------------------------------------------------------------
+    def step(self, t):
+        """One rollout macro-step (paac.py:140-205)."""
+        net = self.network
+        E = self.emulator_counts
+        end = self._mark('rollout_forward')
+        v, pi, rep = net.forward(self.states[t], E, out=(self.values[t], self.pi_roll, self.rep_roll),
+                                 ws_key='rollout')
+        if end is not None:
+            end.record()
+        if self.sampling == 'device':
+            devnet.sample(pi, rep, self.sample_seed, self.counters, self.a_idx[t], self.r_idx[t])
+            self.a_h[t].copy_(self.a_idx[t], non_blocking=True)
+            self.r_h[t].copy_(self.r_idx[t], non_blocking=True)
+            self.event.record()
+            self.event.synchronize()
+            a = self.a_h[t].numpy()
+            r = self.r_h[t].numpy()
+        else:
+            self.pi_h.copy_(pi, non_blocking=True)
+            self.rep_h.copy_(rep, non_blocking=True)
+            self.event.record()
+            self.event.synchronize()
+            a, r = self.explo_policy.choose_indices(self.pi_h.numpy(), self.rep_h.numpy())
+            self.a_h[t].numpy()[...] = a
+            self.r_h[t].numpy()[...] = r
+            self.a_idx[t].copy_(self.a_h[t], non_blocking=True)
+            self.r_idx[t].copy_(self.r_h[t], non_blocking=True)
+        if self.runner_kind == 'native':
+            total = self.runners.step(self.a_h[t], self.r_h[t])
+            reward = self.runners.reward.numpy()
+            over = self.runners.over.numpy()
+            self._upload_pushes(total, self.states[t + 1], self.states[t])
+        else:
+            sh = self.shared
+            sh[3][...] = a
+            sh[4][...] = r
+            self.runners.update_environments()
+            self.runners.wait_updated()
+            self.obs_h.numpy()[...] = sh[0]
+            self.states[t + 1].copy_(self.obs_h, non_blocking=True)
+            reward, over = sh[1], sh[2]
+        self.global_step = self.book.step(self.global_step, a, r, reward, over,
+                                          self.rewards_h[t].numpy(), self.masks_h[t].numpy())
+
+    def update(self):
+        """Bootstrap, n-step returns, fused loss backward, [all-reduce], clip + RMSProp
+        (paac.py:219-256)."""
+        net = self.network
+        E, T = self.emulator_counts, self.max_local_steps
+        N = E * T
+        net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout')
+        self.rewards_d.copy_(self.rewards_h, non_blocking=True)
+        self.masks_d.copy_(self.masks_h, non_blocking=True)
+        devnet.returns(self.rewards_d, self.masks_d, self.values, self.v_boot, self.gamma, self.y, self.adv)
+        lr = self.get_lr()
+        net.set_lr(lr)
+        obs = self.states[:T].reshape(N, 84, 84, self.C)
+        end = self._mark('train_pass')
+        v, pi, rep = net.forward(obs, N, ws_key='train')
+        net.loss_backward(obs, N, v, pi, rep, self.a_idx.view(N), self.r_idx.view(N), self.y.view(N),
+                          self.adv.view(N), loss_terms=self.loss_terms, ws_key='train')
+        if end is not None:
+            end.record()
+        inv = 1.0
+        if self.world > 1:
+            torch.distributed.all_reduce(net.grad)
+            inv = 1.0 / self.world
+        net.apply_gradients(inv)
+        self.states[0].copy_(self.states[T])
+        return lr
+
+    def loss_value(self):
+        """5*(mean(-(adv*logp + beta*H)) + mean(0.25(y-v)^2)) of the last update (host sync)."""
+        t = self.loss_terms.double().mean(0).cpu().numpy()
+        beta = self.network.beta
+        return float(5.0 * (t[0] + t[1] - beta * (t[2] + t[3])))
+
+    # ------------------------------------------------------------------------------------------
+    def start(self):
+        self.global_step = self.init_network()
+        if self.world > 1:
+            torch.distributed.broadcast(self.network.params, 0)
+            torch.distributed.broadcast(self.network.ms, 0)
+            torch.distributed.broadcast(self.network.mom, 0)
+        self.global_step_start = self.global_step
+        self._start_runners()
+
+    def train(self):
+        """Main actor learner loop (paac.py:86-297)."""
+        self.start()
+        counter = 0
+        start_time = time.time()
+        logging.debug('Starting training at Step %d', self.global_step)
+        try:
+            while self.global_step < self.max_global_steps:
+                loop_start_time = time.time()
+                self.book.new_update()
+                for t in range(self.max_local_steps):
+                    self.step(t)
+                self.update()
+                counter += 1
+                if counter % max(1, 2048 // self.emulator_counts) == 0:
+                    torch.cuda.synchronize()
+                    now = time.time()
+                    tr = self.book.total_rewards
+                    last_ten = 0.0 if len(tr) < 1 else float(np.mean(tr[-10:]))
+                    steps_per_sec = self.max_local_steps * self.emulator_counts / (now - loop_start_time)
+                    avg = (self.global_step - self.global_step_start) / (now - start_time)
+                    logging.info('Ran %d steps, at %f steps/s (%f steps/s avg), last 10 rewards avg %f',
+                                 self.global_step, steps_per_sec, avg, last_ten)
+                self.save_vars()
+        finally:
+            self.cleanup()
+
+    def cleanup(self):
+        try:
+            torch.cuda.synchronize()
+            super(PAACLearner, self).cleanup()
+        finally:
+            if self.runners is not None:
+                self.runners.stop()
+                self.runners = None

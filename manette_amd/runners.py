@@ -1,0 +1,142 @@
+"""Host-side emulator runners (A1): runners.py:7-50 + emulator_runner.py:19-42.
+
+NativeRunners  — the hot path: a libmanette_host.so thread pool steps a native emulator bank
+                 and writes every env's pushed screens into ONE compact pinned staging buffer,
+                 which the learner copies to HBM on its stream for mt_preprocess.
+Runners        — the reference interface for Python emulators (BaseEnvironment objects,
+                 e.g. an ALE wrapper): `ew` worker processes over shared memory, a go-queue per
+                 worker and a barrier queue; workers=0 runs the same loop in process.
+"""
+import ctypes as C
+import multiprocessing as mp
+from multiprocessing.sharedctypes import RawArray
+
+import numpy as np
+import torch
+
+from . import _lib
+from .emulator_runner import EmulatorRunner, run_emulators
+
+
+def _np(t):
+    return t.numpy()
+
+
+class NativeRunners(object):
+    def __init__(self, bank, n_workers, tab_rep):
+        self.bank = bank
+        self.E = bank.screens.shape[0]
+        self.tab = np.ascontiguousarray(np.asarray(tab_rep, dtype=np.int32))
+        self.frame_bytes = bank.frame_bytes
+        h = C.c_void_p()
+        lib = _lib.host()
+        _lib.check_host(lib.mh_runner_create(
+            self.E, int(n_workers), self.tab.ctypes.data_as(C.c_void_p), len(self.tab),
+            bank.screens.ctypes.data_as(C.c_void_p), bank.screens.shape[1], self.frame_bytes,
+            bank.rewards.ctypes.data_as(C.c_void_p), bank.rewards.shape[1], bank.episode_len,
+            C.byref(h)), 'mh_runner_create')
+        self._h = h
+        pin = torch.cuda.is_available()
+        mk = lambda *shape, dtype: torch.zeros(*shape, dtype=dtype, pin_memory=pin)
+        self.staging = mk(4 * self.E, 2, self.frame_bytes, dtype=torch.uint8)
+        self.push_offset = mk(self.E, dtype=torch.int32)
+        self.push_count = mk(self.E, dtype=torch.int32)
+        self.reward = mk(self.E, dtype=torch.float32)
+        self.over = mk(self.E, dtype=torch.float32)
+        self.total = 0
+
+    def _ptr(self, t):
+        return C.c_void_p(t.data_ptr())
+
+    def reset(self):
+        """get_initial_state() of every env (paac.py:98): 4 pushes each."""
+        tot = C.c_int()
+        _lib.check_host(_lib.host().mh_runner_reset(self._h, self._ptr(self.staging), self._ptr(self.push_offset),
+                                                    self._ptr(self.push_count), C.byref(tot)), 'mh_runner_reset')
+        self.total = tot.value
+        return self.total
+
+    def step(self, a_idx, r_idx):
+        """a_idx/r_idx: int32 host arrays/tensors [E]. Returns the number of staged pushes."""
+        a = a_idx if isinstance(a_idx, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a_idx, np.int32))
+        r = r_idx if isinstance(r_idx, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(r_idx, np.int32))
+        tot = C.c_int()
+        _lib.check_host(_lib.host().mh_runner_step(
+            self._h, self._ptr(a), self._ptr(r), self._ptr(self.staging), self._ptr(self.push_offset),
+            self._ptr(self.push_count), self._ptr(self.reward), self._ptr(self.over), C.byref(tot)),
+            'mh_runner_step')
+        self.total = tot.value
+        return self.total
+
+    def env_state(self, e):
+        k = C.c_int64()
+        s = C.c_int32()
+        _lib.check_host(_lib.host().mh_runner_env_state(self._h, e, C.byref(k), C.byref(s)))
+        return k.value, s.value
+
+    def stop(self):
+        if getattr(self, '_h', None):
+            _lib.host().mh_runner_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.stop()
+
+
+class Runners(object):
+    """runners.py:7-50 interface: Runners(tab_rep, EmulatorRunner, emulators, workers, variables)
+    with variables = [states, rewards, over, action indices, repetition indices]."""
+
+    def __init__(self, tab_rep, runner_cls, emulators, workers, variables):
+        self.workers = workers
+        if workers == 0:
+            self.variables = variables
+            self._inline = (tab_rep, list(emulators))
+            return
+        self.variables = [self._get_shared(v) for v in variables]
+        self.queues = [mp.Queue() for _ in range(workers)]
+        self.barrier = mp.Queue()
+        blocks = np.array_split(np.arange(len(emulators)), workers)
+        self.runners = [runner_cls(tab_rep, i, [emulators[j] for j in blk],
+                                   [v[blk[0]:blk[-1] + 1] for v in self.variables], self.queues[i],
+                                   self.barrier)
+                        for i, blk in enumerate(blocks)]
+
+    @staticmethod
+    def _get_shared(array):
+        ctype = {np.dtype(np.float32): C.c_float, np.dtype(np.float64): C.c_double,
+                 np.dtype(np.uint8): C.c_uint8, np.dtype(np.int32): C.c_int32}[array.dtype]
+        shared = RawArray(ctype, array.size)
+        out = np.frombuffer(shared, array.dtype).reshape(array.shape)
+        out[...] = array
+        return out
+
+    def start(self):
+        if self.workers:
+            for r in self.runners:
+                r.daemon = True
+                r.start()
+
+    def stop(self):
+        if self.workers:
+            for q in self.queues:
+                q.put(None)
+            for r in self.runners:
+                r.join(timeout=5)
+
+    def get_shared_variables(self):
+        return self.variables
+
+    def update_environments(self):
+        if self.workers == 0:
+            tab_rep, emus = self._inline
+            run_emulators(tab_rep, emus, self.variables)
+            return
+        for q in self.queues:
+            q.put(True)
+
+    def wait_updated(self):
+        if self.workers == 0:
+            return
+        for _ in range(self.workers):
+            self.barrier.get()

@@ -1,0 +1,231 @@
+"""numpy restatement of the policy/value networks, heads, loss and backward (oracle).
+
+networks.py:14-127 (Operations), :152-155 (input scale), :178-192 (NIPS), :206-225 (PWYX),
+:261-278 (NATURE); policy_v_network.py:19-74 (heads + loss). NHWC activations, HWIO conv
+weights, (in, out) dense weights, TF VALID/SAME padding, flatten in NHWC order.
+Backward is the hand-derived gradient of the same graph (TF's ops: Conv2DBackprop*, MatMul
+grads, ReluGrad on the activation output, Softmax/Log grads).
+"""
+import numpy as np
+from numpy.lib.stride_tricks import as_strided
+
+
+def arch_spec(arch, depth, num_actions, num_reps):
+    """Layer list + TF variable names/shapes/init bounds (networks.py:34-89, :178-278)."""
+    C = 4 * depth
+    if arch == 'NIPS':
+        convs = [('conv1', 8, 4, C, 16, 'VALID', False), ('conv2', 4, 2, 16, 32, 'VALID', False)]
+        fc = ('fc3', 256)
+    elif arch == 'NATURE':
+        convs = [('conv1', 8, 4, C, 32, 'VALID', False), ('conv2', 4, 2, 32, 64, 'VALID', False),
+                 ('conv3', 3, 1, 64, 64, 'VALID', False)]
+        fc = ('fc4', 512)
+    elif arch == 'PWYX':
+        convs = [('conv1', 5, 1, C, 32, 'SAME', True), ('conv2', 5, 1, 32, 32, 'SAME', True),
+                 ('conv3', 4, 1, 32, 64, 'SAME', True), ('conv4', 3, 1, 64, 64, 'SAME', False)]
+        fc = ('fc5', 512)
+    else:
+        raise ValueError(arch)
+    H = 84
+    for (_, k, s, cin, cout, pad, pool) in convs:
+        H = (H - k) // s + 1 if pad == 'VALID' else -(-H // s)
+        if pool:
+            H = H // 2
+    flat = H * H * convs[-1][4]
+    F = fc[1]
+    vars_ = []
+    for (name, k, s, cin, cout, pad, pool) in convs:
+        vars_.append(('Network/%s/%s_weights' % (name, name), (k, k, cin, cout), 1.0 / np.sqrt(cout * k * k)))
+        vars_.append(('Network/%s/%s_biases' % (name, name), (cout,), 1.0 / np.sqrt(cin * k * k)))
+    vars_.append(('Network/%s/%s_weights' % (fc[0], fc[0]), (flat, F), 1.0 / np.sqrt(flat)))
+    vars_.append(('Network/%s/%s_biases' % (fc[0], fc[0]), (F,), 1.0 / np.sqrt(flat)))
+    for scope, nm, n in [('Training/Critic', 'critic_output', 1), ('Training/Actor', 'actor_output', num_actions),
+                         ('Training/Repetition', 'repetition_output', num_reps)]:
+        vars_.append(('%s/%s/%s_weights' % (scope, nm, nm), (F, n), 1.0 / np.sqrt(F)))
+        vars_.append(('%s/%s/%s_biases' % (scope, nm, nm), (n,), 1.0 / np.sqrt(F)))
+    return dict(convs=convs, fc=fc, flat=flat, F=F, vars=vars_, A=num_actions, R=num_reps)
+
+
+def _pads(H, k, s, padding):
+    if padding == 'VALID':
+        return (H - k) // s + 1, 0, 0
+    O = -(-H // s)
+    tot = max((O - 1) * s + k - H, 0)
+    return O, tot // 2, tot - tot // 2  # TF SAME: extra padding after
+
+
+def im2col(x, k, s, padding):
+    """x [B,H,W,C] -> cols [B*OH*OW, k*k*C] (k order ky, kx, c)."""
+    B, H, W, C = x.shape
+    OH, pt, pb = _pads(H, k, s, padding)
+    OW, pl, pr = _pads(W, k, s, padding)
+    if pt or pb or pl or pr:
+        x = np.pad(x, ((0, 0), (pt, pb), (pl, pr), (0, 0)))
+    x = np.ascontiguousarray(x)
+    sb, sh, sw, sc = x.strides
+    win = as_strided(x, shape=(B, OH, OW, k, k, C), strides=(sb, sh * s, sw * s, sh, sw, sc))
+    return win.reshape(B * OH * OW, k * k * C), (OH, OW, pt, pl)
+
+
+def col2im(dcols, xshape, k, s, padding):
+    B, H, W, C = xshape
+    OH, pt, pb = _pads(H, k, s, padding)
+    OW, pl, pr = _pads(W, k, s, padding)
+    d = dcols.reshape(B, OH, OW, k, k, C)
+    dx = np.zeros((B, H + pt + pb, W + pl + pr, C), dtype=dcols.dtype)
+    for ky in range(k):
+        for kx in range(k):
+            dx[:, ky:ky + s * (OH - 1) + 1:s, kx:kx + s * (OW - 1) + 1:s, :] += d[:, :, :, ky, kx, :]
+    return dx[:, pt:pt + H, pl:pl + W, :]
+
+
+def act_fwd(x, act, alpha):
+    return np.maximum(x, 0) if act == 'relu' else np.maximum(x, alpha * x)
+
+
+def act_bwd(y, act, alpha):
+    # TF ReluGrad: grad * (y > 0); tf.maximum(x, a*x) grad: x >= a*x  <=>  y >= 0.
+    if act == 'relu':
+        return (y > 0).astype(y.dtype)
+    return np.where(y >= 0, 1.0, alpha).astype(y.dtype)
+
+
+def maxpool2(x):
+    """2x2/2 VALID max pool (networks.py:108-110). Returns (y, argmax mask)."""
+    B, H, W, C = x.shape
+    OH, OW = H // 2, W // 2
+    xc = x[:, :OH * 2, :OW * 2, :].reshape(B, OH, 2, OW, 2, C)
+    y = xc.max(axis=(2, 4))
+    return y
+
+
+def maxpool2_bwd(x, y, dy):
+    # TF MaxPoolGrad routes the gradient to the first max in the window (row-major scan).
+    B, H, W, C = x.shape
+    OH, OW = H // 2, W // 2
+    dx = np.zeros_like(x)
+    taken = np.zeros((B, OH, OW, C), dtype=bool)
+    for dy_ in range(2):
+        for dx_ in range(2):
+            xs = x[:, dy_:OH * 2:2, dx_:OW * 2:2, :]
+            hit = (xs == y) & ~taken
+            dx[:, dy_:OH * 2:2, dx_:OW * 2:2, :] += np.where(hit, dy, 0)
+            taken |= hit
+    return dx
+
+
+def softmax(z):
+    m = z.max(axis=1, keepdims=True)
+    e = np.exp(z - m)
+    return e / e.sum(axis=1, keepdims=True)
+
+
+def forward(spec, P, obs, act='relu', alpha=0.1, temp=1.0, dtype=np.float64):
+    """P: dict name -> array. obs uint8 [B,84,84,C]. Returns (v, pi, rep, cache)."""
+    x = obs.astype(dtype) * dtype(1.0 / 255.0)  # networks.py:155
+    cache = dict(layers=[])
+    for (name, k, s, cin, cout, pad, pool) in spec['convs']:
+        W = P['Network/%s/%s_weights' % (name, name)].astype(dtype)
+        b = P['Network/%s/%s_biases' % (name, name)].astype(dtype)
+        cols, (OH, OW, _, _) = im2col(x, k, s, pad)
+        y = act_fwd(cols @ W.reshape(-1, cout) + b, act, alpha).reshape(x.shape[0], OH, OW, cout)
+        entry = dict(x=x, y=y, k=k, s=s, pad=pad, pool=pool, cout=cout, name=name)
+        if pool:
+            y2 = maxpool2(y)
+            entry['yp'] = y2
+            y = y2
+        cache['layers'].append(entry)
+        x = y
+    B = x.shape[0]
+    flat = x.reshape(B, -1)
+    fc = spec['fc'][0]
+    Wf = P['Network/%s/%s_weights' % (fc, fc)].astype(dtype)
+    bf = P['Network/%s/%s_biases' % (fc, fc)].astype(dtype)
+    h = act_fwd(flat @ Wf + bf, act, alpha)
+    cache.update(flat=flat, h=h)
+    Wc = P['Training/Critic/critic_output/critic_output_weights'].astype(dtype)
+    bc = P['Training/Critic/critic_output/critic_output_biases'].astype(dtype)
+    Wa = P['Training/Actor/actor_output/actor_output_weights'].astype(dtype)
+    ba = P['Training/Actor/actor_output/actor_output_biases'].astype(dtype)
+    Wr = P['Training/Repetition/repetition_output/repetition_output_weights'].astype(dtype)
+    br = P['Training/Repetition/repetition_output/repetition_output_biases'].astype(dtype)
+    v = (h @ Wc + bc).reshape(-1)                       # policy_v_network.py:22-23
+    pi = softmax((h @ Wa + ba) / dtype(temp))           # :31, networks.py:97
+    rep = softmax((h @ Wr + br) / dtype(temp))          # :47
+    return v, pi, rep, cache
+
+
+def loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1, temp=1.0,
+                   dtype=np.float64):
+    """Loss of policy_v_network.py:25-74 and its gradient for every variable (dict)."""
+    v, pi, rep, c = forward(spec, P, obs, act, alpha, temp, dtype)
+    B = len(v)
+    y = np.asarray(y, dtype)
+    adv = np.asarray(adv, dtype)
+    eps = dtype(1e-30)
+    lpi = np.log(pi + eps)
+    lrep = np.log(rep + eps)
+    ent_pi = -(pi * lpi).sum(1)
+    ent_rep = -(rep * lrep).sum(1)
+    sel_pi = lpi[np.arange(B), a_idx]
+    sel_rep = lrep[np.arange(B), r_idx]
+    actor_obj = (sel_pi + sel_rep) * adv + beta * (ent_pi + ent_rep)
+    critic = 0.25 * (y - v) ** 2
+    loss = 5.0 * (np.mean(-actor_obj) + np.mean(critic))
+    scale = 5.0 / B
+    # critic
+    dv = scale * 0.5 * (v - y)
+    # softmax heads: dL/dp then the softmax Jacobian, then / temp
+    def head_grad(p, lp, sel):
+        oh = np.zeros_like(p)
+        oh[np.arange(B), sel] = 1.0
+        pe = p + eps
+        dobj = oh * (adv[:, None] / pe) - beta * (lp + p / pe)
+        g = -scale * dobj
+        dz = p * (g - (p * g).sum(1, keepdims=True))
+        return dz / temp
+    dza = head_grad(pi, lpi, a_idx)
+    dzr = head_grad(rep, lrep, r_idx)
+    h = c['h']
+    G = {}
+    G['Training/Critic/critic_output/critic_output_weights'] = h.T @ dv[:, None]
+    G['Training/Critic/critic_output/critic_output_biases'] = dv.sum(keepdims=True)
+    G['Training/Actor/actor_output/actor_output_weights'] = h.T @ dza
+    G['Training/Actor/actor_output/actor_output_biases'] = dza.sum(0)
+    G['Training/Repetition/repetition_output/repetition_output_weights'] = h.T @ dzr
+    G['Training/Repetition/repetition_output/repetition_output_biases'] = dzr.sum(0)
+    Wc = P['Training/Critic/critic_output/critic_output_weights'].astype(dtype)
+    Wa = P['Training/Actor/actor_output/actor_output_weights'].astype(dtype)
+    Wr = P['Training/Repetition/repetition_output/repetition_output_weights'].astype(dtype)
+    dh = (dv[:, None] @ Wc.T + dza @ Wa.T + dzr @ Wr.T) * act_bwd(h, act, alpha)
+    fc = spec['fc'][0]
+    Wf = P['Network/%s/%s_weights' % (fc, fc)].astype(dtype)
+    G['Network/%s/%s_weights' % (fc, fc)] = c['flat'].T @ dh
+    G['Network/%s/%s_biases' % (fc, fc)] = dh.sum(0)
+    dflat = dh @ Wf.T
+    layers = c['layers']
+    last = layers[-1]
+    dx = dflat.reshape(last['yp'].shape if last['pool'] else last['y'].shape)
+    for li in range(len(layers) - 1, -1, -1):
+        L = layers[li]
+        if L['pool']:
+            dx = maxpool2_bwd(L['y'], L['yp'], dx)
+        dy = dx * act_bwd(L['y'], act, alpha)
+        cols, _ = im2col(L['x'], L['k'], L['s'], L['pad'])
+        dy2 = dy.reshape(-1, L['cout'])
+        name = L['name']
+        W = P['Network/%s/%s_weights' % (name, name)].astype(dtype)
+        G['Network/%s/%s_weights' % (name, name)] = (cols.T @ dy2).reshape(W.shape)
+        G['Network/%s/%s_biases' % (name, name)] = dy2.sum(0)
+        if li > 0:
+            dcols = dy2 @ W.reshape(-1, L['cout']).T
+            dx = col2im(dcols, L['x'].shape, L['k'], L['s'], L['pad'])
+    terms = np.stack([critic, -((sel_pi + sel_rep) * adv), ent_pi, ent_rep], axis=1)
+    return loss, G, dict(v=v, pi=pi, rep=rep, terms=terms)
+
+
+def init_params(spec, seed):
+    """U(-d, d) with the TF init bounds of networks.py:34-89 (the TF RNG stream itself is not
+    reproducible without TF; parity is on the bounds)."""
+    rs = np.random.RandomState(seed)
+    return {n: rs.uniform(-d, d, size=shape).astype(np.float32) for (n, shape, d) in spec['vars']}

@@ -172,10 +172,10 @@ class FakeSession(object):
             self.train.append(dict(
                 state_sha=sha(inp),
                 state_shape=np.asarray(np.shape(inp), dtype=np.int64),
-                y=np.asarray(fd[n.critic_target_ph], dtype=np.float64),
-                adv=np.asarray(fd[n.adv_actor_ph], dtype=np.float64),
-                a_onehot=np.asarray(fd[n.selected_action_ph], dtype=np.float64),
-                r_onehot=np.asarray(fd[n.selected_repetition_ph], dtype=np.float64),
+                y=np.array(fd[n.critic_target_ph], dtype=np.float64, copy=True),
+                adv=np.array(fd[n.adv_actor_ph], dtype=np.float64, copy=True),
+                a_onehot=np.array(fd[n.selected_action_ph], dtype=np.float64, copy=True),
+                r_onehot=np.array(fd[n.selected_repetition_ph], dtype=np.float64, copy=True),
                 lr=np.float64(fd[self.learner.learning_rate]),
                 global_step=np.int64(self.learner.global_step)))
             return None, None
@@ -266,7 +266,7 @@ def run_host_loop(ref, ec, ew, T, A, max_rep, nb_choices, n_updates, lstm):
     out['episode_reward'] = np.asarray([v for s, tag, v in sv if tag == 'rl/reward'], np.float64)
     out['episode_length'] = np.asarray([v for s, tag, v in sv if tag == 'rl/episode_length'], np.float64)
     for i, (tag, vals) in enumerate(hist):
-        out['hist_%s_%d' % (tag, i // 2)] = vals.astype(np.int64)
+        out["hist_%s_%d" % (tag, i // 2)] = np.array(vals, dtype=np.int64)
     out['final_global_step'] = np.int64(L.global_step)
     return out
 

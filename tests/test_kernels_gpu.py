@@ -1,0 +1,183 @@
+"""Parity of every libmanette_hip.so kernel against the oracle, through the C ABI (GPU box).
+
+Tolerances: integer/byte work (preprocess, returns from identical inputs, sampling indices)
+bit-exact; fp32 network math vs the float64 oracle within 2e-5 relative (forward) and
+2e-4 relative L2 per variable (gradients) — the fp32 accumulation-order budget for K <= 3136.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nets, optim, preprocess, returns
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [('NIPS', 1, 6, 1), ('NIPS', 3, 4, 11), ('NATURE', 1, 4, 11), ('NATURE', 3, 18, 1)]
+
+
+def _net(arch, depth, A, R, seed=0, act='relu'):
+    from manette_amd.network import DeviceNetwork
+    conf = dict(arch=arch, rgb=depth == 3, num_actions=A, nb_choices=R, softmax_temp=1.0,
+                entropy_regularisation_strength=0.02, clip_norm=3.0, clip_norm_type='global',
+                activation=act, alpha_leaky_relu=0.1)
+    net = DeviceNetwork(conf)
+    net.init_params(seed)
+    return net
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(np.asarray(a, np.float64) - b) / max(np.linalg.norm(b), 1e-12))
+
+
+@pytest.mark.parametrize('arch,depth,A,R', CONFIGS)
+@pytest.mark.parametrize('B', [3, 37])
+def test_forward_parity(arch, depth, A, R, B):
+    net = _net(arch, depth, A, R, seed=B)
+    rs = np.random.RandomState(B)
+    obs = rs.randint(0, 256, size=(B, 84, 84, 4 * depth)).astype(np.uint8)
+    v, pi, rep = net.forward(torch.from_numpy(obs).cuda())
+    torch.cuda.synchronize()
+    spec = nets.arch_spec(arch, depth, A, R)
+    P = net.get_variables()
+    v0, pi0, rep0, _ = nets.forward(spec, P, obs)
+    np.testing.assert_allclose(v.cpu().numpy(), v0, rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(pi.cpu().numpy(), pi0, rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(rep.cpu().numpy(), rep0, rtol=2e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize('arch,depth,A,R', CONFIGS)
+@pytest.mark.parametrize('B', [5, 40])
+def test_loss_backward_parity(arch, depth, A, R, B):
+    net = _net(arch, depth, A, R, seed=7 + B)
+    rs = np.random.RandomState(100 + B)
+    obs = rs.randint(0, 256, size=(B, 84, 84, 4 * depth)).astype(np.uint8)
+    a_idx = rs.randint(0, A, size=B).astype(np.int32)
+    r_idx = rs.randint(0, R, size=B).astype(np.int32)
+    y = rs.randn(B).astype(np.float32)
+    adv = rs.randn(B).astype(np.float32)
+    d = lambda x: torch.from_numpy(x).cuda()
+    obs_d = d(obs)
+    v, pi, rep = net.forward(obs_d)
+    terms = torch.zeros(B, 4, device='cuda')
+    net.loss_backward(obs_d, B, v, pi, rep, d(a_idx), d(r_idx), d(y), d(adv), loss_terms=terms)
+    torch.cuda.synchronize()
+    spec = nets.arch_spec(arch, depth, A, R)
+    P = net.get_variables()
+    loss, G, aux = nets.loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, 0.02)
+    got = net.get_variables('grad')
+    for name, _, _ in spec['vars']:
+        assert _rel(got[name], G[name]) < 2e-4, (name, _rel(got[name], G[name]))
+    np.testing.assert_allclose(terms.cpu().numpy(), aux['terms'], rtol=1e-4, atol=1e-5)
+    # alignment padding of the flat gradient is zero
+    flat = net.grad.cpu().numpy()
+    mask = np.ones(net.nparams, bool)
+    for _, shape, off, _ in net.vars:
+        mask[off:off + int(np.prod(shape))] = False
+    assert not flat[mask].any()
+
+
+def test_leaky_relu_backward():
+    net = _net('NIPS', 1, 6, 3, seed=3, act='leaky_relu')
+    rs = np.random.RandomState(3)
+    B = 9
+    obs = rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)
+    a_idx = rs.randint(0, 6, size=B).astype(np.int32)
+    r_idx = rs.randint(0, 3, size=B).astype(np.int32)
+    y = rs.randn(B).astype(np.float32)
+    adv = rs.randn(B).astype(np.float32)
+    d = lambda x: torch.from_numpy(x).cuda()
+    v, pi, rep = net.forward(d(obs))
+    net.loss_backward(d(obs), B, v, pi, rep, d(a_idx), d(r_idx), d(y), d(adv))
+    spec = nets.arch_spec('NIPS', 1, 6, 3)
+    _, G, _ = nets.loss_and_grads(spec, net.get_variables(), obs, a_idx, r_idx, y, adv, 0.02,
+                                  act='leaky_relu', alpha=0.1)
+    got = net.get_variables('grad')
+    for name, _, _ in spec['vars']:
+        assert _rel(got[name], G[name]) < 2e-4, name
+
+
+@pytest.mark.parametrize('T,E', [(5, 4), (5, 32), (20, 1000)])
+def test_returns_bit_exact(T, E):
+    from manette_amd.network import returns as dev_returns
+    rs = np.random.RandomState(T * E)
+    r = rs.choice([-1.0, 0.0, 1.0], size=(T, E)).astype(np.float32)
+    m = (rs.rand(T, E) > 0.1).astype(np.float32)
+    V = rs.randn(T, E).astype(np.float32)
+    VT = rs.randn(E).astype(np.float32)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    y = torch.empty(T, E, device='cuda')
+    adv = torch.empty(T, E, device='cuda')
+    dev_returns(d(r), d(m), d(V), d(VT), 0.99, y, adv)
+    y0, adv0 = returns.nstep_returns(r.astype(np.float64), m.astype(np.float64), V.astype(np.float64),
+                                     VT, 0.99)
+    np.testing.assert_array_equal(y.cpu().numpy(), y0.astype(np.float32))
+    np.testing.assert_array_equal(adv.cpu().numpy(), adv0.astype(np.float32))
+
+
+@pytest.mark.parametrize('clip_type', ['global', 'ignore'])
+@pytest.mark.parametrize('gscale', [1e-3, 10.0])
+def test_clip_rmsprop(clip_type, gscale):
+    net = _net('NIPS', 1, 6, 1)
+    net.clip_type = 1 if clip_type == 'global' else 0
+    rs = np.random.RandomState(1)
+    n = net.nparams
+    g = (rs.randn(n) * gscale).astype(np.float32)
+    w0 = net.params.cpu().numpy().copy()
+    ms0 = (1.0 + rs.rand(n)).astype(np.float32)
+    mom0 = (rs.randn(n) * 1e-3).astype(np.float32)
+    net.grad.copy_(torch.from_numpy(g))
+    net.ms.copy_(torch.from_numpy(ms0))
+    net.mom.copy_(torch.from_numpy(mom0))
+    net.set_lr(0.0224)
+    net.apply_gradients()
+    torch.cuda.synchronize()
+    norm = optim.global_norm([g])
+    assert abs(float(net.norm_dev.item()) - norm) <= 1e-5 * norm
+    s = optim.clip_scale(net.norm_dev.item(), 3.0) if clip_type == 'global' else np.float32(1.0)
+    w, ms, mom = w0.copy(), ms0.copy(), np.zeros_like(mom0)
+    mom[...] = mom0
+    optim.rmsprop_apply(w, ms, mom, g * s, np.float32(0.0224), 0.99, 0.0, 0.1)
+    np.testing.assert_array_equal(net.ms.cpu().numpy(), ms)
+    np.testing.assert_array_equal(net.mom.cpu().numpy(), mom)
+    np.testing.assert_array_equal(net.params.cpu().numpy(), w)
+
+
+@pytest.mark.parametrize('depth', [1, 3])
+def test_preprocess_bit_exact(depth):
+    from manette_amd.network import preprocess as dev_pre
+    rs = np.random.RandomState(depth)
+    E = 7
+    counts = np.array([1, 4, 2, 3, 1, 4, 1], np.int32)
+    offs = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32)
+    raw = rs.randint(0, 256, size=(int(counts.sum()), 2, 210, 160, depth)).astype(np.uint8)
+    prev = rs.randint(0, 256, size=(E, 84, 84, 4 * depth)).astype(np.uint8)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    out = torch.empty(E, 84, 84, 4 * depth, dtype=torch.uint8, device='cuda')
+    dev_pre(d(raw), d(offs), d(counts), E, depth, d(preprocess.ROW_LUT.astype(np.int32)),
+            d(preprocess.COL_LUT.astype(np.int32)), d(prev), out)
+    got = out.cpu().numpy()
+    for e in range(E):
+        pushes = [preprocess.pool_and_resize(raw[offs[e] + j, 0], raw[offs[e] + j, 1]) for j in range(counts[e])]
+        np.testing.assert_array_equal(got[e], preprocess.stack_update(prev[e], pushes, depth))
+
+
+def test_sample_distribution():
+    from manette_amd.network import sample
+    B, A, R = 4096, 6, 3
+    rs = np.random.RandomState(0)
+    p = rs.dirichlet(np.ones(A)).astype(np.float32)
+    q = rs.dirichlet(np.ones(R)).astype(np.float32)
+    pi = torch.from_numpy(np.tile(p, (B, 1))).cuda()
+    rep = torch.from_numpy(np.tile(q, (B, 1))).cuda()
+    ctr = torch.zeros(B, dtype=torch.int64, device='cuda')
+    a = torch.empty(B, dtype=torch.int32, device='cuda')
+    r = torch.empty(B, dtype=torch.int32, device='cuda')
+    counts = np.zeros(A)
+    for _ in range(8):
+        sample(pi, rep, 1234, ctr, a, r)
+        counts += np.bincount(a.cpu().numpy(), minlength=A)
+    assert (ctr.cpu().numpy() == 8).all()
+    freq = counts / counts.sum()
+    assert np.abs(freq - p).max() < 0.01
+    ah = a.cpu().numpy()
+    assert ah.min() >= 0 and ah.max() < A and r.cpu().numpy().max() < R

@@ -1,0 +1,22 @@
+#!/bin/bash
+# GPU-box sequence: smoke, gpu tests, bench. Each step has its own time limit; a fault-like
+# exit (timeout 124/137, abort 134, segfault 139) stops the sequence, a test failure does not.
+set -u
+OUT=${OUT:-gpurun_out}
+mkdir -p "$OUT"
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/suite.log"
+  case $rc in 124|137|134|139) echo "fault-like exit in $name, stopping" | tee -a "$OUT/suite.log"; exit $rc;; esac
+  return 0
+}
+: > "$OUT/suite.log"
+for step in ${STEPS:-smoke tests bench}; do
+  case $step in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run tests 900 python -m pytest tests -q -m gpu ;;
+    bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+  esac
+done
