@@ -86,8 +86,9 @@ def build_args(cfg, T, sampling, seed):
 
 
 def cpu_baseline(cfg, T, seconds, rank):
-    """The oracle ("port") restated reference loop on host cores: numpy float32 network +
-    clip/RMSProp, the reference's host loop and process runners (mp.Queue barrier), the same
+    """The oracle ("port") restated reference loop on host cores: the reference's host loop and
+    process runners (mp.Queue barrier) from oracle/host_loop.py, a torch-CPU fp32 network with the
+    TF1 clip/RMSProp update (oracle/torch_cpu.py, standing in for TF1's CPU kernels), the same
     synthetic emulators with CPU preprocess. Bounded sample: as many updates as fit in ~seconds."""
     from oracle import host_loop, policy
     from manette_amd.environment_creator import MINIMAL_ACTIONS
@@ -99,7 +100,8 @@ def cpu_baseline(cfg, T, seconds, rank):
     omp = int(os.environ.get('OMP_NUM_THREADS', cores))
     cores = min(cores, omp)
     emus = [SyntheticEmulator(i, A, rgb=cfg['rgb']) for i in range(ec)]
-    net = host_loop.OracleNetwork(cfg['arch'], 3 if cfg['rgb'] else 1, A, cfg['nb_choices'], seed=0)
+    from oracle.torch_cpu import TorchCPUNetwork
+    net = TorchCPUNetwork(cfg['arch'], 3 if cfg['rgb'] else 1, A, cfg['nb_choices'], seed=0, threads=cores)
     np.random.seed(1234)
 
     class Timed(host_loop.HostLoop):
@@ -125,7 +127,7 @@ def cpu_baseline(cfg, T, seconds, rank):
     timed = n_upd[0] - 1
     return dict(value=timed * steps_per_update / elapsed, unit='env-steps/s', cores=cores, kind='port',
                 sample='%d PAAC updates (ec=%d, t_max=%d, %s) after 1 warm-up, %d emulator worker '
-                       'processes, numpy fp32 network, %.1f s' % (timed, ec, T, cfg['arch'], ew, elapsed))
+                       'processes, torch-CPU fp32 network on %d threads, %.1f s' % (timed, ec, T, cfg['arch'], ew, cores, elapsed))
 
 
 def main():

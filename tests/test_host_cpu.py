@@ -1,0 +1,181 @@
+"""Host-side product components on CPU: native runner, bookkeeping, exploration policy and the
+Python runner path, each against the oracle / the reference's golden vectors."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from golden_env import GoldenEnv
+from oracle import host_loop as ohl
+from oracle import policy as opol
+from oracle import preprocess as opre
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+def _args(max_rep, nb):
+    import argparse
+    return argparse.Namespace(egreedy=False, epsilon=0.05, softmax_temp=1.0, keep_percentage=0.9,
+                              annealed=False, max_repetition=max_rep, nb_choices=nb)
+
+
+def test_product_tab_rep_g3():
+    from manette_amd.exploration_policy import ExplorationPolicy
+    for case in json.load(open(os.path.join(GOLDEN, 'tab_rep.json'))):
+        assert ExplorationPolicy(_args(case['max_repetition'], case['nb_choices'])).tab_rep == case['tab_rep']
+
+
+def test_product_sampler_is_reference_stream():
+    """Parity mode draws exactly the reference's numpy multinomial stream."""
+    from manette_amd.exploration_policy import ExplorationPolicy
+    g = dict(np.load(os.path.join(GOLDEN, 'host_loop_figar_r11.npz')))
+    pol = ExplorationPolicy(_args(10, 11))
+    np.random.seed(1234)
+    ours = [pol.choose_indices(g['roll_pi_%d' % i], g['roll_rep_%d' % i]) for i in range(5)]
+    np.random.seed(1234)
+    ref = [(opol.multinomial_choose(g['roll_pi_%d' % i]), opol.multinomial_choose(g['roll_rep_%d' % i]))
+           for i in range(5)]
+    for (a, r), (a0, r0) in zip(ours, ref):
+        assert a.tolist() == a0 and r.tolist() == r0
+    # and they are the actions the reference fed to its first train_step
+    a_first = np.argmax(g['train_a_onehot_0'], 1).reshape(5, 4)
+    assert [a.tolist() for a, _ in ours] == a_first.tolist()
+
+
+@pytest.mark.parametrize('name', ['host_loop_nips_r1', 'host_loop_figar_r11'])
+def test_bookkeeper_and_python_runners_g1(name):
+    """Product Runners(workers=0) + ExplorationPolicy + Bookkeeper reproduce the reference's
+    episode summaries, histograms, global_step and train feeds' actions."""
+    from manette_amd.bookkeeping import Bookkeeper
+    from manette_amd.emulator_runner import EmulatorRunner
+    from manette_amd.exploration_policy import ExplorationPolicy
+    from manette_amd.runners import Runners
+    g = dict(np.load(os.path.join(GOLDEN, name + '.npz')))
+    ec, ew, T, A, max_rep, nb, n_updates, lstm = [int(x) for x in g['config']]
+    pol = ExplorationPolicy(_args(max_rep, nb))
+    emus = [GoldenEnv(i) for i in range(ec)]
+    s0 = np.asarray([e.get_initial_state() for e in emus], np.uint8)
+    variables = [s0, np.zeros(ec, np.float32), np.zeros(ec, np.float32), np.zeros(ec, np.int32),
+                 np.zeros(ec, np.int32)]
+    runners = Runners(pol.tab_rep, EmulatorRunner, emus, 0, variables)
+    sh = runners.get_shared_variables()
+    book = Bookkeeper(ec, A, pol.tab_rep)
+    np.random.seed(1234)
+    gs = 0
+    i = 0
+    rewards = np.zeros((T, ec), np.float32)
+    masks = np.zeros((T, ec), np.float32)
+    for u in range(n_updates):
+        book.new_update()
+        acts = []
+        for t in range(T):
+            a, r = pol.choose_indices(g['roll_pi_%d' % i], g['roll_rep_%d' % i])
+            i += 1
+            sh[3][...] = a
+            sh[4][...] = r
+            runners.update_environments()
+            runners.wait_updated()
+            gs = book.step(gs, a, r, sh[1], sh[2], rewards[t], masks[t])
+            acts.append(a)
+        assert gs == g['train_global_step_%d' % u]
+        np.testing.assert_array_equal(np.concatenate(acts), np.argmax(g['train_a_onehot_%d' % u], 1))
+        ha, hr = book.histograms()
+        np.testing.assert_array_equal(ha, g['hist_actions_%d' % u])
+        np.testing.assert_array_equal(hr, g['hist_repetitions_%d' % u])
+    ep = np.asarray(book.episodes)
+    np.testing.assert_array_equal(ep[:, 0], g['episode_step'])
+    np.testing.assert_array_equal(ep[:, 1], g['episode_reward'])
+    np.testing.assert_array_equal(ep[:, 2], g['episode_length'])
+
+
+def test_python_runner_processes_g2():
+    from manette_amd.emulator_runner import EmulatorRunner
+    from manette_amd.runners import Runners
+    case = json.load(open(os.path.join(GOLDEN, 'runner.json')))[0]
+    ec = 4
+    emus = [GoldenEnv(i) for i in range(ec)]
+    s0 = np.asarray([e.get_initial_state() for e in emus], np.uint8)
+    variables = [s0, np.zeros(ec, np.float32), np.zeros(ec, np.float32), np.zeros(ec, np.int32),
+                 np.zeros(ec, np.int32)]
+    runners = Runners(case['tab_rep'], EmulatorRunner, emus, 2, variables)
+    runners.start()
+    try:
+        sh = runners.get_shared_variables()
+        import hashlib
+        for st in case['steps']:
+            sh[3][...] = st['a']
+            sh[4][...] = st['r']
+            runners.update_environments()
+            runners.wait_updated()
+            assert sh[1].tolist() == st['reward']
+            assert sh[2].tolist() == st['over']
+            assert [hashlib.sha1(sh[0][e].tobytes()).hexdigest() for e in range(ec)] == st['state_sha']
+    finally:
+        runners.stop()
+
+
+@pytest.mark.parametrize('max_rep,nb,workers', [(0, 1, 2), (10, 11, 3), (10, 6, 1)])
+def test_native_runner_matches_python_emulator(max_rep, nb, workers):
+    """libmanette_host's threads reproduce SyntheticEmulator (the reference contract) exactly:
+    rewards, terminals, and the observation the device preprocess builds from the staged pushes."""
+    from manette_amd.runners import NativeRunners
+    from manette_amd.synthetic import SyntheticBank, SyntheticEmulator
+    E, ep_len = 5, 7
+    tab = opol.tab_repetitions(max_rep, nb)
+    bank = SyntheticBank(0, E, episode_len=ep_len)
+    nr = NativeRunners(bank, workers, tab)
+    emus = [SyntheticEmulator(i, 6, episode_len=ep_len) for i in range(E)]
+    try:
+        tot = nr.reset()
+        stacks = []
+        for e in range(E):
+            prev = np.zeros((84, 84, 4), np.uint8)
+            st = _apply(nr, e, prev)
+            np.testing.assert_array_equal(st, emus[e].get_initial_state())
+            stacks.append(st)
+        rs = np.random.RandomState(nb)
+        states = np.asarray(stacks)
+        rewards = np.zeros(E, np.float32)
+        over = np.zeros(E, np.float32)
+        for step in range(25):
+            a = rs.randint(0, 6, E).astype(np.int32)
+            r = rs.randint(0, nb, E).astype(np.int32)
+            ohl.emulator_runner_step(tab, emus, states, rewards, over, a, r)
+            nr.step(a, r)
+            np.testing.assert_array_equal(nr.reward.numpy(), rewards)
+            np.testing.assert_array_equal(nr.over.numpy(), over)
+            for e in range(E):
+                stacks[e] = _apply(nr, e, stacks[e])
+                np.testing.assert_array_equal(stacks[e], states[e])
+                assert nr.env_state(e) == (emus[e].k, emus[e].steps)
+    finally:
+        nr.stop()
+
+
+def _apply(nr, e, prev):
+    off = int(nr.push_offset[e])
+    cnt = int(nr.push_count[e])
+    assert 1 <= cnt <= 4
+    fr = nr.staging.numpy()[off:off + cnt].reshape(cnt, 2, 210, 160, 1)
+    pushes = [opre.pool_and_resize(fr[j, 0], fr[j, 1]) for j in range(cnt)]
+    return opre.stack_update(prev, pushes)
+
+
+def test_native_runner_rejects_bad_index():
+    from manette_amd import _lib
+    from manette_amd.runners import NativeRunners
+    from manette_amd.synthetic import SyntheticBank
+    nr = NativeRunners(SyntheticBank(0, 2), 1, [0, 3])
+    try:
+        with pytest.raises(_lib.MTError):
+            nr.step(np.zeros(2, np.int32), np.array([0, 2], np.int32))
+    finally:
+        nr.stop()
+
+
+def test_lut_product_matches_pil_fixture():
+    from manette_amd.environment import COL_LUT, ROW_LUT
+    p = np.load(os.path.join(GOLDEN, 'preprocess.npz'))
+    np.testing.assert_array_equal(ROW_LUT, p['row_lut'])
+    np.testing.assert_array_equal(COL_LUT, p['col_lut'])
