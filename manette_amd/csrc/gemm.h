@@ -6,10 +6,13 @@
 // loaders gather their operand (im2col of an NHWC activation, a dense matrix, a transposed
 // dense matrix, the transposed-conv gather of a backward-data pass) straight from HBM into
 // LDS, so no im2col buffer is ever materialised. fp32 in / fp32 accumulate: the MFMA is an
-// exact k-ordered fmaf chain (cdna_hip_programming.md §3), the numerics TF's fp32 path has.
+// exact k-ordered fmaf chain (cdna_hip_programming.md §3), the numerics of TF's fp32 path.
 //
 // Tile: 256 threads = 4 waves laid out WM x WN; each wave owns TM x TN 16x16 accumulators.
-// K is walked in BK=32 chunks staged through LDS. Split-K over blockIdx.z.
+// K is walked in BK-deep chunks staged through LDS with a register-staged prefetch: the global
+// loads of chunk i+1 are issued before the MFMAs of chunk i (all of a thread's loads of a chunk
+// are in flight together). Small-K layers (conv fwd, K <= 256) use BK = K: one fill, one
+// latency. Split-K over blockIdx.z.
 //
 // LDS operand layouts (per loader, chosen to mirror the operand's memory layout):
 //   KMAJOR  : L[row][BK + 4]   (k contiguous)  -> fragment = one ds_read_b128
@@ -22,20 +25,21 @@
 
 namespace mt {
 
-template <int BM_, int BN_, int WM_, int WN_>
+template <int BM_, int BN_, int WM_, int WN_, int BK_ = 32>
 struct Tile {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
-  static constexpr int BK = 32;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = BK_;
   static constexpr int TM = BM / (WM * 16);
   static constexpr int TN = BN / (WN * 16);
   static_assert(WM * WN == 4, "4 waves per workgroup");
   static_assert(TM >= 1 && TN >= 1 && TM * WM * 16 == BM && TN * WN * 16 == BN, "tile shape");
+  static_assert(BK % 16 == 0, "BK multiple of 16");
 };
 
 template <bool KMAJOR, int ROWS, int BK>
 struct LdsShape {
-  static constexpr int LD = KMAJOR ? (BK + 4) : (ROWS + 4);
   static constexpr int SIZE = KMAJOR ? ROWS * (BK + 4) : BK * (ROWS + 4);
+  static constexpr int QUADS = ROWS * BK / 4;             // f32x4 items per fill
+  static constexpr int ITEMS = (QUADS + 255) / 256;        // per thread
 };
 
 template <bool KMAJOR, int ROWS, int BK>
@@ -53,22 +57,76 @@ __device__ __forceinline__ f32x4 load_frag(const float *L, int row, int k) {
   }
 }
 
-// Store 4 consecutive-k values of one row (KMAJOR) or 4 consecutive rows at one k (!KMAJOR).
+// Item it of a fill -> (row offset, k offset) inside the tile, by layout.
 template <bool KMAJOR, int ROWS, int BK>
-__device__ __forceinline__ void lds_put4(float *L, int row, int k, f32x4 v) {
+__device__ __forceinline__ void item_pos(int it, int &rr, int &kk) {
   if constexpr (KMAJOR) {
-    *reinterpret_cast<f32x4 *>(L + row * (BK + 4) + k) = v;
+    rr = it / (BK / 4);
+    kk = (it % (BK / 4)) * 4;  // 4 consecutive k of one row
   } else {
-    *reinterpret_cast<f32x4 *>(L + k * (ROWS + 4) + row) = v;
+    kk = it / (ROWS / 4);
+    rr = (it % (ROWS / 4)) * 4;  // 4 consecutive rows at one k
   }
 }
+
+template <bool KMAJOR, int ROWS, int BK>
+__device__ __forceinline__ void lds_put(float *L, int rr, int kk, f32x4 v) {
+  if constexpr (KMAJOR)
+    *reinterpret_cast<f32x4 *>(L + rr * (BK + 4) + kk) = v;
+  else
+    *reinterpret_cast<f32x4 *>(L + kk * (ROWS + 4) + rr) = v;
+}
+
+// Stage of one operand: registers for one chunk.
+template <class LD, int ROWS, int BK>
+struct Stage {
+  using S = LdsShape<LD::KMAJOR, ROWS, BK>;
+  f32x4 r[S::ITEMS];
+  // Interior tiles (uniform per workgroup) take the branch-free fetch: every load of the chunk
+  // is issued back to back and waited for once (a per-element guarded load would make hipcc
+  // wait vmcnt(0) per element — cdna_hip_programming.md §5 trap (c)).
+  __device__ __forceinline__ void load(const LD &ld, int row0, int k0, int ke, int nrows) {
+    if (ld.interior(row0, ROWS, k0, BK, ke, nrows)) {
+#pragma unroll
+      for (int i = 0; i < S::ITEMS; ++i) {
+        const int it = threadIdx.x + i * 256;
+        if (S::QUADS % 256 == 0 || it < S::QUADS) {
+          int rr, kk;
+          item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
+          r[i] = ld.fetch_fast(row0 + rr, k0 + kk);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < S::ITEMS; ++i) {
+        const int it = threadIdx.x + i * 256;
+        if (S::QUADS % 256 == 0 || it < S::QUADS) {
+          int rr, kk;
+          item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
+          r[i] = ld.fetch(row0, rr, k0, kk, ke, nrows);
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float *L) const {
+#pragma unroll
+    for (int i = 0; i < S::ITEMS; ++i) {
+      const int it = threadIdx.x + i * 256;
+      if (S::QUADS % 256 == 0 || it < S::QUADS) {
+        int rr, kk;
+        item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
+        lds_put<LD::KMAJOR, ROWS, BK>(L, rr, kk, r[i]);
+      }
+    }
+  }
+};
 
 template <class T, class LA, class LB, class EP>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EP ep, int M, int N, int K,
                                                        int kchunk) {
   using SA = LdsShape<LA::KMAJOR, T::BM, T::BK>;
   using SB = LdsShape<LB::KMAJOR, T::BN, T::BK>;
-  __shared__ __attribute__((aligned(16))) float smem[SA::SIZE + SB::SIZE];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   float *As = smem;
   float *Bs = smem + SA::SIZE;
 
@@ -87,12 +145,24 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EP ep, int 
 #pragma unroll
     for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  Stage<LA, T::BM, T::BK> sa;
+  Stage<LB, T::BN, T::BK> sb;
+  if (kb < ke) {
+    sa.load(la, m0, kb, ke, M);
+    sb.load(lb, n0, kb, ke, N);
+  }
   for (int k0 = kb; k0 < ke; k0 += T::BK) {
-    la.template fill<T::BM, T::BK>(As, m0, k0, ke, M);
-    lb.template fill<T::BN, T::BK>(Bs, n0, k0, ke, N);
+    sa.store(As);
+    sb.store(Bs);
     __syncthreads();
+    if (k0 + T::BK < ke) {  // prefetch the next chunk while this one is multiplied
+      sa.load(la, m0, k0 + T::BK, ke, M);
+      sb.load(lb, n0, k0 + T::BK, ke, N);
+    }
+    const int kcn = min(T::BK, ke - k0);  // valid k in this chunk (rest is zero-filled)
 #pragma unroll
     for (int kc = 0; kc < T::BK / 16; ++kc) {
+      if (kc * 16 >= kcn) break;
       f32x4 a[T::TM], b[T::TN];
 #pragma unroll
       for (int i = 0; i < T::TM; ++i)
@@ -124,23 +194,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EP ep, int 
     }
 }
 
-template <class T, class LA, class LB, class EP>
-inline int launch_gemm(const LA &la, const LB &lb, const EP &ep, int M, int N, int K, int splits,
-                       hipStream_t s) {
-  if (M <= 0 || N <= 0) return MT_OK;
-  const int nchunks = cdiv(K, T::BK);
-  if (splits < 1) splits = 1;
-  if (splits > nchunks) splits = nchunks;
-  const int kchunk = cdiv(nchunks, splits) * T::BK;
-  splits = cdiv(K, kchunk);
-  dim3 grid(cdiv(M, T::BM), cdiv(N, T::BN), splits);
-  hipLaunchKernelGGL((gemm_f32_kernel<T, LA, LB, EP>), grid, dim3(256), 0, s, la, lb, ep, M, N, K,
-                     kchunk);
-  MT_LAUNCHED();
-  return MT_OK;
+template <class T, class LA, class LB>
+constexpr size_t gemm_lds_bytes() {
+  return sizeof(float) * (LdsShape<LA::KMAJOR, T::BM, T::BK>::SIZE + LdsShape<LB::KMAJOR, T::BN, T::BK>::SIZE);
 }
 
-// Number of K splits gemm will actually use (for sizing slab workspaces).
+// Number of K splits the launch will actually use (chunks are whole BK multiples).
 template <class T>
 inline int gemm_splits(int K, int splits) {
   const int nchunks = cdiv(K, T::BK);
@@ -150,9 +209,34 @@ inline int gemm_splits(int K, int splits) {
   return cdiv(K, kchunk);
 }
 
+template <class T, class LA, class LB, class EP>
+inline int launch_gemm(const LA &la, const LB &lb, const EP &ep, int M, int N, int K, int splits,
+                       hipStream_t s) {
+  if (M <= 0 || N <= 0) return MT_OK;
+  const int nchunks = cdiv(K, T::BK);
+  if (splits < 1) splits = 1;
+  if (splits > nchunks) splits = nchunks;
+  const int kchunk = cdiv(nchunks, splits) * T::BK;
+  splits = cdiv(K, kchunk);
+  constexpr size_t lds = gemm_lds_bytes<T, LA, LB>();
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;  // per instantiation: allow > 64 KB dynamic LDS once
+  if (!attr_set && lds > 64 * 1024) {
+    MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_f32_kernel<T, LA, LB, EP>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr_set = true;
+  }
+  dim3 grid(cdiv(M, T::BM), cdiv(N, T::BN), splits);
+  hipLaunchKernelGGL((gemm_f32_kernel<T, LA, LB, EP>), grid, dim3(256), lds, s, la, lb, ep, M, N,
+                     K, kchunk);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
 // ------------------------------------------------------------------------------------------
-// Loaders. fill<ROWS, BK>(L, row0, k0, ke, nrows): stage rows [row0, row0+ROWS) x k [k0, k0+BK)
-// of the operand into LDS, zero outside [0, nrows) x [k0, ke). All 256 threads participate.
+// Loaders: fetch(row0, rr, k0, kk, ke, nrows) returns the 4 values of item (row0+rr, k0+kk)
+// — 4 consecutive k (KMAJOR) or 4 consecutive rows (!KMAJOR) — zero outside
+// [0, nrows) x [.., ke).
 // ------------------------------------------------------------------------------------------
 
 // Dense row-major operand X[row][k] (k contiguous, leading dim ld), fp32. KMAJOR.
@@ -160,25 +244,26 @@ struct LdRowMajor {
   static constexpr bool KMAJOR = true;
   const float *X;
   int ld;
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
-    constexpr int Q = BK / 4;
-    for (int it = threadIdx.x; it < ROWS * Q; it += 256) {
-      const int rr = it / Q, q = it % Q;
-      const int row = row0 + rr, k = k0 + q * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (row < nrows) {
-        const float *p = X + (size_t)row * ld + k;
-        if (k + 3 < ke) {
-          v = *reinterpret_cast<const f32x4 *>(p);
-        } else {
+  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
+    return row0 + rows <= nrows && k0 + bk <= ke;
+  }
+  __device__ __forceinline__ f32x4 fetch_fast(int row, int k) const {
+    return *reinterpret_cast<const f32x4 *>(X + (size_t)row * ld + k);
+  }
+  __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
+    const int row = row0 + rr, k = k0 + kk;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < nrows) {
+      const float *p = X + (size_t)row * ld + k;
+      if (k + 3 < ke) {
+        v = *reinterpret_cast<const f32x4 *>(p);
+      } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (k + e < ke) v[e] = p[e];
-        }
+        for (int e = 0; e < 4; ++e)
+          if (k + e < ke) v[e] = p[e];
       }
-      lds_put4<true, ROWS, BK>(L, rr, q * 4, v);
     }
+    return v;
   }
 };
 
@@ -191,29 +276,31 @@ struct LdColMajor {
   const float *X;
   int ld;
   int ones_row;
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
-    constexpr int Q = ROWS / 4;
+  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
     const int nx = ones_row >= 0 ? ones_row : nrows;
-    for (int it = threadIdx.x; it < BK * Q; it += 256) {
-      const int kk = it / Q, q = it % Q;
-      const int k = k0 + kk, row = row0 + q * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (k < ke) {
-        const float *p = X + (size_t)k * ld + row;
-        if (row + 3 < nx && (ld & 3) == 0) {
-          v = *reinterpret_cast<const f32x4 *>(p);
-        } else {
+    return row0 + rows <= nx && k0 + bk <= ke && (ld & 3) == 0;
+  }
+  __device__ __forceinline__ f32x4 fetch_fast(int row, int k) const {
+    return *reinterpret_cast<const f32x4 *>(X + (size_t)k * ld + row);
+  }
+  __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
+    const int row = row0 + rr, k = k0 + kk;
+    const int nx = ones_row >= 0 ? ones_row : nrows;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (k < ke) {
+      const float *p = X + (size_t)k * ld + row;
+      if (row + 3 < nx && (ld & 3) == 0) {
+        v = *reinterpret_cast<const f32x4 *>(p);
+      } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int rw = row + e;
-            if (rw < nx) v[e] = p[e];
-            else if (rw == ones_row) v[e] = 1.f;
-          }
+        for (int e = 0; e < 4; ++e) {
+          const int rw = row + e;
+          if (rw < nx) v[e] = p[e];
+          else if (rw == ones_row) v[e] = 1.f;
         }
       }
-      lds_put4<false, ROWS, BK>(L, q * 4, kk, v);
     }
+    return v;
   }
 };
 
@@ -257,26 +344,42 @@ template <class G, bool U8>
 struct LdIm2col {
   static constexpr bool KMAJOR = true;
   const typename InElem<U8>::T *X;
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
-    constexpr int Q = BK / 4;
-    for (int it = threadIdx.x; it < ROWS * Q; it += 256) {
-      const int rr = it / Q, q = it % Q;
-      const int m = row0 + rr, k = k0 + q * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (m < nrows && k < ke) {
-        const int b = m / (G::OH * G::OW);
-        const int rem = m - b * (G::OH * G::OW);
-        const int oy = rem / G::OW, ox = rem - oy * G::OW;
-        const int ky = k / (G::KW * G::CIN);
-        const int r2 = k - ky * (G::KW * G::CIN);
-        const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
-        const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
-        if (iy >= 0 && iy < G::H && ix >= 0 && ix < G::W)
-          v = InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
-      }
-      lds_put4<true, ROWS, BK>(L, rr, q * 4, v);
+  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
+    return row0 + rows <= nrows && k0 + bk <= ke;
+  }
+  // Padding (SAME) handled branch-free: clamped address, zero by select.
+  __device__ __forceinline__ f32x4 fetch_fast(int m, int k) const {
+    const int b = m / (G::OH * G::OW);
+    const int rem = m - b * (G::OH * G::OW);
+    const int oy = rem / G::OW, ox = rem - oy * G::OW;
+    const int ky = k / (G::KW * G::CIN);
+    const int r2 = k - ky * (G::KW * G::CIN);
+    const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
+    const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
+    if constexpr (G::SAME) {
+      const bool ok = iy >= 0 && iy < G::H && ix >= 0 && ix < G::W;
+      const int iyc = min(max(iy, 0), G::H - 1), ixc = min(max(ix, 0), G::W - 1);
+      const f32x4 v = InElem<U8>::load4(X + (((size_t)b * G::H + iyc) * G::W + ixc) * G::CIN + ci);
+      return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      return InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
     }
+  }
+  __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
+    const int m = row0 + rr, k = k0 + kk;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m < nrows && k < ke) {
+      const int b = m / (G::OH * G::OW);
+      const int rem = m - b * (G::OH * G::OW);
+      const int oy = rem / G::OW, ox = rem - oy * G::OW;
+      const int ky = k / (G::KW * G::CIN);
+      const int r2 = k - ky * (G::KW * G::CIN);
+      const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
+      const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
+      if (iy >= 0 && iy < G::H && ix >= 0 && ix < G::W)
+        v = InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
+    }
+    return v;
   }
 };
 
@@ -285,31 +388,45 @@ template <class G, bool U8>
 struct LdIm2colT {
   static constexpr bool KMAJOR = false;
   const typename InElem<U8>::T *X;
-  int nm;  // number of GEMM-k rows (= B*OH*OW)
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
-    constexpr int Q = ROWS / 4;
-    for (int it = threadIdx.x; it < BK * Q; it += 256) {
-      const int kk = it / Q, q = it % Q;
-      const int m = k0 + kk, kr = row0 + q * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (m < ke) {
-        if (kr < G::KK) {
-          const int b = m / (G::OH * G::OW);
-          const int rem = m - b * (G::OH * G::OW);
-          const int oy = rem / G::OW, ox = rem - oy * G::OW;
-          const int ky = kr / (G::KW * G::CIN);
-          const int r2 = kr - ky * (G::KW * G::CIN);
-          const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
-          const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
-          if (iy >= 0 && iy < G::H && ix >= 0 && ix < G::W)
-            v = InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
-        } else if (kr == G::KK) {
-          v[0] = 1.f;  // bias row
-        }
-      }
-      lds_put4<false, ROWS, BK>(L, q * 4, kk, v);
+  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
+    return row0 + rows <= G::KK && k0 + bk <= ke;  // the bias-row tile takes the guarded path
+  }
+  __device__ __forceinline__ f32x4 fetch_fast(int kr, int m) const {
+    const int b = m / (G::OH * G::OW);
+    const int rem = m - b * (G::OH * G::OW);
+    const int oy = rem / G::OW, ox = rem - oy * G::OW;
+    const int ky = kr / (G::KW * G::CIN);
+    const int r2 = kr - ky * (G::KW * G::CIN);
+    const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
+    const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
+    if constexpr (G::SAME) {
+      const bool ok = iy >= 0 && iy < G::H && ix >= 0 && ix < G::W;
+      const int iyc = min(max(iy, 0), G::H - 1), ixc = min(max(ix, 0), G::W - 1);
+      const f32x4 v = InElem<U8>::load4(X + (((size_t)b * G::H + iyc) * G::W + ixc) * G::CIN + ci);
+      return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      return InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
     }
+  }
+  __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
+    const int m = k0 + kk, kr = row0 + rr;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m < ke) {
+      if (kr < G::KK) {
+        const int b = m / (G::OH * G::OW);
+        const int rem = m - b * (G::OH * G::OW);
+        const int oy = rem / G::OW, ox = rem - oy * G::OW;
+        const int ky = kr / (G::KW * G::CIN);
+        const int r2 = kr - ky * (G::KW * G::CIN);
+        const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
+        const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
+        if (iy >= 0 && iy < G::H && ix >= 0 && ix < G::W)
+          v = InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
+      } else if (kr == G::KK) {
+        v[0] = 1.f;  // bias row
+      }
+    }
+    return v;
   }
 };
 
@@ -319,30 +436,43 @@ template <class G>
 struct LdConvBwdA {
   static constexpr bool KMAJOR = true;
   const float *dY;  // [B][OH][OW][COUT]
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
-    constexpr int Q = BK / 4;
-    for (int it = threadIdx.x; it < ROWS * Q; it += 256) {
-      const int rr = it / Q, q = it % Q;
-      const int m = row0 + rr, k = k0 + q * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (m < nrows && k < ke) {
-        const int b = m / (G::H * G::W);
-        const int rem = m - b * (G::H * G::W);
-        const int iy = rem / G::W, ix = rem - iy * G::W;
-        const int ky = k / (G::KW * G::COUT);
-        const int r2 = k - ky * (G::KW * G::COUT);
-        const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
-        const int ty = iy + G::PT - ky, tx = ix + G::PL - kx;
-        if (ty >= 0 && tx >= 0 && (ty % G::S) == 0 && (tx % G::S) == 0) {
-          const int oy = ty / G::S, ox = tx / G::S;
-          if (oy < G::OH && ox < G::OW)
-            v = *reinterpret_cast<const f32x4 *>(
-                dY + (((size_t)b * G::OH + oy) * G::OW + ox) * G::COUT + co);
-        }
+  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
+    return row0 + rows <= nrows && k0 + bk <= ke;
+  }
+  // The stride-S holes of the transposed conv are data-dependent: clamped address + select.
+  __device__ __forceinline__ f32x4 fetch_fast(int m, int k) const {
+    const int b = m / (G::H * G::W);
+    const int rem = m - b * (G::H * G::W);
+    const int iy = rem / G::W, ix = rem - iy * G::W;
+    const int ky = k / (G::KW * G::COUT);
+    const int r2 = k - ky * (G::KW * G::COUT);
+    const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
+    const int ty = iy + G::PT - ky, tx = ix + G::PL - kx;
+    const int oy = ty / G::S, ox = tx / G::S;  // only used when ty, tx >= 0
+    const bool ok = ty >= 0 && tx >= 0 && (ty - oy * G::S) == 0 && (tx - ox * G::S) == 0 &&
+                    oy < G::OH && ox < G::OW;
+    const int oyc = min(max(oy, 0), G::OH - 1), oxc = min(max(ox, 0), G::OW - 1);
+    const f32x4 v = *reinterpret_cast<const f32x4 *>(dY + (((size_t)b * G::OH + oyc) * G::OW + oxc) * G::COUT + co);
+    return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
+    const int m = row0 + rr, k = k0 + kk;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m < nrows && k < ke) {
+      const int b = m / (G::H * G::W);
+      const int rem = m - b * (G::H * G::W);
+      const int iy = rem / G::W, ix = rem - iy * G::W;
+      const int ky = k / (G::KW * G::COUT);
+      const int r2 = k - ky * (G::KW * G::COUT);
+      const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
+      const int ty = iy + G::PT - ky, tx = ix + G::PL - kx;
+      if (ty >= 0 && tx >= 0 && (ty % G::S) == 0 && (tx % G::S) == 0) {
+        const int oy = ty / G::S, ox = tx / G::S;
+        if (oy < G::OH && ox < G::OW)
+          v = *reinterpret_cast<const f32x4 *>(dY + (((size_t)b * G::OH + oy) * G::OW + ox) * G::COUT + co);
       }
-      lds_put4<true, ROWS, BK>(L, rr, q * 4, v);
     }
+    return v;
   }
 };
 
@@ -351,21 +481,25 @@ template <class G>
 struct LdConvBwdB {
   static constexpr bool KMAJOR = true;
   const float *Wt;  // HWIO
-  template <int ROWS, int BK>
-  __device__ __forceinline__ void fill(float *L, int row0, int k0, int ke, int nrows) const {
-    constexpr int Q = BK / 4;
-    for (int it = threadIdx.x; it < ROWS * Q; it += 256) {
-      const int rr = it / Q, q = it % Q;
-      const int ci = row0 + rr, k = k0 + q * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (ci < nrows && k < ke) {
-        const int ky = k / (G::KW * G::COUT);
-        const int r2 = k - ky * (G::KW * G::COUT);
-        const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
-        v = *reinterpret_cast<const f32x4 *>(Wt + (((size_t)(ky * G::KW + kx) * G::CIN + ci) * G::COUT + co));
-      }
-      lds_put4<true, ROWS, BK>(L, rr, q * 4, v);
+  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
+    return row0 + rows <= nrows && k0 + bk <= ke;
+  }
+  __device__ __forceinline__ f32x4 fetch_fast(int ci, int k) const {
+    const int ky = k / (G::KW * G::COUT);
+    const int r2 = k - ky * (G::KW * G::COUT);
+    const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
+    return *reinterpret_cast<const f32x4 *>(Wt + (((size_t)(ky * G::KW + kx) * G::CIN + ci) * G::COUT + co));
+  }
+  __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
+    const int ci = row0 + rr, k = k0 + kk;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (ci < nrows && k < ke) {
+      const int ky = k / (G::KW * G::COUT);
+      const int r2 = k - ky * (G::KW * G::COUT);
+      const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
+      v = *reinterpret_cast<const f32x4 *>(Wt + (((size_t)(ky * G::KW + kx) * G::CIN + ci) * G::COUT + co));
     }
+    return v;
   }
 };
 
@@ -399,6 +533,14 @@ struct EpSlab {
   int M, N;
   __device__ __forceinline__ void operator()(int m, int n, int z, float v) const {
     P[((size_t)z * M + m) * N + n] = v;
+  }
+};
+
+struct EpStore {
+  float *P;
+  int ld;
+  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
+    P[(size_t)m * ld + n] = v;
   }
 };
 

@@ -128,21 +128,37 @@ struct WsLayout {
   int fc_splits;
 };
 
-template <int N>
+// Tile by output width N (16 / 32 / >= 64 columns) and K-chunk depth BK.
+template <int N, int BK>
 struct TileFor {
-  using T = Tile<64, 64, 2, 2>;
+  using T = Tile<64, 64, 2, 2, BK>;
 };
-template <>
-struct TileFor<16> {
-  using T = Tile<64, 16, 4, 1>;
+template <int BK>
+struct TileFor<16, BK> {
+  using T = Tile<64, 16, 4, 1, BK>;
 };
-template <>
-struct TileFor<32> {
-  using T = Tile<64, 32, 4, 1>;
+template <int BK>
+struct TileFor<32, BK> {
+  using T = Tile<64, 32, 4, 1, BK>;
 };
 
-using TileFc = Tile<32, 64, 2, 2>;    // dense forward, M = batch (small)
-using TileDense = Tile<64, 64, 2, 2>;  // dense dW / dX
+// K-chunk of a forward conv: the whole K when it fits 256, else the largest of 256/192/128
+// dividing it (one fill per chunk, all loads of a chunk in flight together).
+template <int K>
+constexpr int conv_bk() {
+  return K <= 256 ? ((K + 15) / 16) * 16 : (K % 256 == 0 ? 256 : (K % 192 == 0 ? 192 : 128));
+}
+
+template <class G>
+using TileConvFwd = typename TileFor<G::COUT, conv_bk<G::KK>()>::T;
+template <class G>
+using TileConvWgrad = typename TileFor<G::COUT, 64>::T;
+template <class G>
+using TileConvDgrad = typename TileFor<G::CIN, 128>::T;
+
+using TileFc = Tile<32, 64, 2, 2, 64>;       // dense forward, M = batch (small), split-K
+using TileDenseW = Tile<64, 64, 2, 2, 32>;   // dense dW (GEMM-K = batch)
+using TileDenseX = Tile<64, 64, 2, 2, 128>;  // dense dX (GEMM-K = F)
 
 static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
   int s = target / (grid_mn > 0 ? grid_mn : 1);
@@ -154,7 +170,7 @@ static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
 
 template <class G>
 static int conv_wgrad_splits(int B) {
-  using T = typename TileFor<G::COUT>::T;
+  using T = TileConvWgrad<G>;
   const int M = G::KK + 1;
   const int K = B * G::OH * G::OW;
   const int s = pick_splits(cdiv(M, T::BM) * cdiv(G::COUT, T::BN), K, T::BK);
@@ -169,7 +185,7 @@ static size_t conv_wgrad_slab(int B) {
 
 template <class Ar>
 static int fc_splits(int B, int F) {
-  const int s = pick_splits(cdiv(B, TileFc::BM) * cdiv(F, TileFc::BN), Ar::FLAT, TileFc::BK, 256);
+  const int s = pick_splits(cdiv(B, TileFc::BM) * cdiv(F, TileFc::BN), Ar::FLAT, TileFc::BK, 128);
   return gemm_splits<TileFc>(Ar::FLAT, s);
 }
 
@@ -210,24 +226,47 @@ static WsLayout ws_layout(const mt_net *n, int B) {
 // ---------------------------------------------------------------------------------------------
 // Kernels: slab sum, heads forward, loss + heads backward, heads weight gradient.
 // ---------------------------------------------------------------------------------------------
-__global__ void sum_slabs_kernel(const float *__restrict__ P, int S, size_t n, float *__restrict__ out) {
+// out[i] = sum_z P[z*n + i], fixed order. A block owns 64 float4 columns; its 4 waves sum
+// interleaved slab subsets (z = w, w+4, ...) and the 4 partials are added in wave order.
+__global__ __launch_bounds__(256) void sum_slabs_kernel(const float *__restrict__ P, int S, size_t n,
+                                                        float *__restrict__ out) {
+  __shared__ f32x4 part[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const size_t n4 = n / 4;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    f32x4 acc = reinterpret_cast<const f32x4 *>(P)[i];
-    for (int z = 1; z < S; ++z) acc += reinterpret_cast<const f32x4 *>(P + (size_t)z * n)[i];
-    reinterpret_cast<f32x4 *>(out)[i] = acc;
+  const size_t c = (size_t)blockIdx.x * 64 + lane;  // float4 column
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (c < n4) {
+    const f32x4 *p = reinterpret_cast<const f32x4 *>(P) + c;
+    int z = w;
+    for (; z + 12 < S; z += 16) {
+      const f32x4 a0 = p[(size_t)z * n4], a1 = p[(size_t)(z + 4) * n4];
+      const f32x4 a2 = p[(size_t)(z + 8) * n4], a3 = p[(size_t)(z + 12) * n4];
+      acc += a0;
+      acc += a1;
+      acc += a2;
+      acc += a3;
+    }
+    for (; z < S; z += 4) acc += p[(size_t)z * n4];
   }
-  for (size_t i = n4 * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float acc = P[i];
-    for (int z = 1; z < S; ++z) acc += P[(size_t)z * n + i];
-    out[i] = acc;
+  part[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && c < n4) {
+    const f32x4 t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    reinterpret_cast<f32x4 *>(out)[c] = t;
+  }
+  // scalar tail (n not a multiple of 4)
+  if (blockIdx.x == 0) {
+    for (size_t i = n4 * 4 + threadIdx.x; i < n; i += 256) {
+      float t = 0.f;
+      for (int z = 0; z < S; ++z) t += P[(size_t)z * n + i];
+      out[i] = t;
+    }
   }
 }
 
 static int sum_slabs(const float *P, int S, size_t n, float *out, hipStream_t s) {
   if (n == 0) return MT_OK;
-  int blocks = (int)std::min<size_t>((n / 4 + 255) / 256 + 1, 2048);
+  const int blocks = (int)std::max<size_t>((n / 4 + 63) / 64, 1);
   hipLaunchKernelGGL(sum_slabs_kernel, dim3(blocks), dim3(256), 0, s, P, S, n, out);
   MT_LAUNCHED();
   return MT_OK;
@@ -272,8 +311,13 @@ __device__ __forceinline__ float wave_softmax(float x, int lane, int n) {
 
 constexpr int kMaxHeads = 64;  // 1 + A + R <= 64
 
-// One workgroup per row: h = act(sum_z slabs + b); logits = h . [Wc|Wa|Wr] + b;
-// v = logit_0; pi = softmax(logits_a / temp); rep = softmax(logits_r / temp).
+// One workgroup per row b (4 waves):
+//  1. h = act(sum_z slabs[z][b] + b_fc) — the split-K dense layer finished here
+//     (networks.py:57-70); every thread owns F/256 features, the slab loads of a feature are
+//     issued 8 at a time;
+//  2. logits_o = [h, 1] . W_o for the 1+A+R head outputs (policy_v_network.py:22, :31, :47):
+//     wave w takes outputs o = w, w+4, ...; lanes split F and reduce with shuffles;
+//  3. wave 0: v = logit_0, pi = softmax(logits_A / temp), rep = softmax(logits_R / temp).
 __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict__ slabs, int S, int B,
                                                         const float *__restrict__ fc_b, int act,
                                                         float alpha, HeadParams hp, float temp,
@@ -281,38 +325,45 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict_
                                                         float *__restrict__ pi,
                                                         float *__restrict__ rep) {
   __shared__ float hs[512];
-  __shared__ float part[4][kMaxHeads];
+  __shared__ float zs[64];
   const int b = blockIdx.x;
   const int F = hp.F, O = 1 + hp.A + hp.R;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int f = threadIdx.x; f < F; f += 256) {
+    const float *p = slabs + (size_t)b * F + f;
+    const size_t zs_stride = (size_t)B * F;
     float acc = 0.f;
-    for (int z = 0; z < S; ++z) acc += slabs[((size_t)z * B + b) * F + f];
+    int z = 0;
+    for (; z + 7 < S; z += 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = p[(size_t)(z + u) * zs_stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    for (; z < S; ++z) acc += p[(size_t)z * zs_stride];
     const float h = act_fwd(acc + fc_b[f], act, alpha);
     hs[f] = h;
     H[(size_t)b * F + f] = h;
   }
   __syncthreads();
-  const int o = threadIdx.x & 63, qt = threadIdx.x >> 6;
-  if (o < O) {
-    const int f0 = qt * (F / 4), f1 = f0 + F / 4;
+  for (int o = w; o < O; o += 4) {
     float acc = 0.f;
-    for (int f = f0; f < f1; ++f) acc += hs[f] * head_w(hp, f, o);
-    part[qt][o] = acc;
+    for (int f = lane; f < F; f += 64) acc += hs[f] * head_w(hp, f, o);
+    acc = wave_sum(acc);
+    if (lane == 0) zs[o] = acc + head_w(hp, F, o);
   }
   __syncthreads();
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    float z = 0.f;
-    if (lane < O) z = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane] + head_w(hp, F, lane);
-    if (lane == 0) v[b] = z;
-    // actor logits sit in lanes 1..A, repetition logits in lanes 1+A..A+R: shift them to 0..
-    const float za = __shfl(z, (lane + 1) & 63, 64) / temp;
-    const float pa = wave_softmax(za, lane, hp.A);
-    if (lane < hp.A) pi[(size_t)b * hp.A + lane] = pa;
-    const float zr = __shfl(z, (lane + 1 + hp.A) & 63, 64) / temp;
-    const float pr = wave_softmax(zr, lane, hp.R);
-    if (lane < hp.R) rep[(size_t)b * hp.R + lane] = pr;
-  }
+  if (w != 0) return;
+  const float z = lane < O ? zs[lane] : 0.f;
+  if (lane == 0) v[b] = z;
+  // actor logits sit in lanes 1..A, repetition logits in lanes 1+A..A+R: shift them to 0..
+  const float za = __shfl(z, (lane + 1) & 63, 64) / temp;
+  const float pa = wave_softmax(za, lane, hp.A);
+  if (lane < hp.A) pi[(size_t)b * hp.A + lane] = pa;
+  const float zr = __shfl(z, (lane + 1 + hp.A) & 63, 64) / temp;
+  const float pr = wave_softmax(zr, lane, hp.R);
+  if (lane < hp.R) rep[(size_t)b * hp.R + lane] = pr;
 }
 
 // dL/dlogit for one softmax head (policy_v_network.py:29-57, :59-74), one wave, lanes [0, n):
@@ -381,35 +432,39 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
   }
 }
 
-// Head weight/bias gradient: G[f][o] = sum_b [H,1][b][f] * dz[b][o] scattered into the three
-// (w, b) variable pairs of the flat gradient.
-__global__ void head_wgrad_kernel(const float *__restrict__ H, const float *__restrict__ dz, int B,
-                                  int F, int A, int R, float *__restrict__ gc,
-                                  float *__restrict__ ga, float *__restrict__ gr) {
+// Head weight/bias gradient: G[f][o] = sum_b [H,1][b][f] * dz[b][o], scattered into the three
+// (w, b) variable pairs of the flat gradient. A block owns 64 features x all O outputs; dz is
+// staged in LDS, H is read coalesced (consecutive lanes = consecutive features).
+__global__ __launch_bounds__(256) void head_wgrad_kernel(const float *__restrict__ H,
+                                                         const float *__restrict__ dz, int B, int F,
+                                                         int A, int R, float *__restrict__ gc,
+                                                         float *__restrict__ ga, float *__restrict__ gr) {
+  extern __shared__ __attribute__((aligned(16))) float dzs[];  // [B][O]
   const int O = 1 + A + R;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (F + 1) * O) return;
-  const int f = idx / O, o = idx % O;
-  float acc = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const float h = f < F ? H[(size_t)b * F + f] : 1.f;
-    acc += h * dz[(size_t)b * O + o];
+  for (int i = threadIdx.x; i < B * O; i += 256) dzs[i] = dz[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + lane;  // f == F is the bias row
+  if (f > F) return;
+  for (int o = w; o < O; o += 4) {
+    float a0 = 0.f, a1 = 0.f;
+    int b = 0;
+    for (; b + 1 < B; b += 2) {
+      const float h0 = f < F ? H[(size_t)b * F + f] : 1.f;
+      const float h1 = f < F ? H[(size_t)(b + 1) * F + f] : 1.f;
+      a0 += h0 * dzs[b * O + o];
+      a1 += h1 * dzs[(b + 1) * O + o];
+    }
+    for (; b < B; ++b) a0 += (f < F ? H[(size_t)b * F + f] : 1.f) * dzs[b * O + o];
+    const float acc = a0 + a1;
+    if (o == 0)
+      gc[f] = acc;  // [F][1] weights then the bias at index F
+    else if (o <= A)
+      ga[(size_t)f * A + (o - 1)] = acc;
+    else
+      gr[(size_t)f * R + (o - 1 - A)] = acc;
   }
-  if (o == 0)
-    gc[f] = acc;  // [F][1] weights then the bias at index F
-  else if (o <= A)
-    ga[(size_t)f * A + (o - 1)] = acc;
-  else
-    gr[(size_t)f * R + (o - 1 - A)] = acc;
 }
-
-struct EpStore {
-  float *P;
-  int ld;
-  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
-    P[(size_t)m * ld + n] = v;
-  }
-};
 
 // ---------------------------------------------------------------------------------------------
 // Layer drivers
@@ -417,7 +472,7 @@ struct EpStore {
 template <class G, bool U8>
 static int conv_forward(const void *X, const float *Wt, const float *bias, float *Y, int B, int act,
                         float alpha, hipStream_t s) {
-  using T = typename TileFor<G::COUT>::T;
+  using T = TileConvFwd<G>;
   LdIm2col<G, U8> la{reinterpret_cast<const typename InElem<U8>::T *>(X)};
   LdColMajor lb{Wt, G::COUT, -1};
   EpBiasAct ep{Y, bias, G::COUT, act, alpha};
@@ -428,10 +483,10 @@ static int conv_forward(const void *X, const float *Wt, const float *bias, float
 template <class G, bool U8>
 static int conv_wgrad(const void *X, const float *dY, float *slab, float *gwb, int B,
                       hipStream_t s) {
-  using T = typename TileFor<G::COUT>::T;
+  using T = TileConvWgrad<G>;
   const int M = G::KK + 1, K = B * G::OH * G::OW;
   const int S = conv_wgrad_splits<G>(B);
-  LdIm2colT<G, U8> la{reinterpret_cast<const typename InElem<U8>::T *>(X), K};
+  LdIm2colT<G, U8> la{reinterpret_cast<const typename InElem<U8>::T *>(X)};
   LdColMajor lb{dY, G::COUT, -1};
   if (S == 1) return launch_gemm<T>(la, lb, EpStore{gwb, G::COUT}, M, G::COUT, K, 1, s);
   int rc = launch_gemm<T>(la, lb, EpSlab{slab, M, G::COUT}, M, G::COUT, K, S, s);
@@ -443,7 +498,7 @@ static int conv_wgrad(const void *X, const float *dY, float *slab, float *gwb, i
 template <class G>
 static int conv_dgrad(const float *dY, const float *Wt, const float *Xact, float *dX, int B,
                       int act, float alpha, hipStream_t s) {
-  using T = typename TileFor<G::CIN>::T;
+  using T = TileConvDgrad<G>;
   LdConvBwdA<G> la{dY};
   LdConvBwdB<G> lb{Wt};
   EpMasked ep{dX, Xact, G::CIN, act, alpha};
@@ -511,8 +566,18 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
                      loss_terms);
   MT_LAUNCHED();
   {
-    const int tot = (Ar::F + 1) * n->O;
-    hipLaunchKernelGGL(head_wgrad_kernel, dim3(cdiv(tot, 256)), dim3(256), 0, s, ws + L.H,
+    static bool wg_attr = false;
+    if (!wg_attr) {
+      MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&head_wgrad_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      wg_attr = true;
+    }
+    if ((size_t)B * n->O * sizeof(float) > 160 * 1024) {
+      set_error("batch %d x %d head outputs exceeds the head-gradient LDS stage", B, n->O);
+      return MT_ERR_ARG;
+    }
+    hipLaunchKernelGGL(head_wgrad_kernel, dim3(cdiv(Ar::F + 1, 64)), dim3(256),
+                       sizeof(float) * (size_t)B * n->O, s, ws + L.H,
                        ws + L.dz, B, Ar::F, n->cfg.num_actions, n->cfg.num_reps,
                        grad + n->off_critic, grad + n->off_actor, grad + n->off_rep);
     MT_LAUNCHED();
@@ -521,10 +586,10 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
   float *dflat = Ar::NCONV == 3 ? d3 : d2;
   const float *Wfc = P + n->off_fc;
   // dense dW, db: [flat, 1]^T . dH -> grad[(FLAT+1) x F]
-  MT_TRY((launch_gemm<TileDense>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
+  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
                                  EpStore{grad + n->off_fc, Ar::F}, Ar::FLAT + 1, Ar::F, B, 1, s)));
   // dense dX: dH . W^T, masked by the last conv's activation
-  MT_TRY((launch_gemm<TileDense>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+  MT_TRY((launch_gemm<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
                                  EpMasked{dflat, flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1, s)));
   float *slab = ws + L.wslab;
   if constexpr (Ar::NCONV == 3) {

@@ -55,10 +55,13 @@ class PAACLearner(ActorLearner):
         dev = self.dev
         self.states = torch.zeros(T + 1, E, 84, 84, C, dtype=torch.uint8, device=dev)
         self.values = torch.zeros(T, E, dtype=torch.float32, device=dev)
-        self.a_idx = torch.zeros(T, E, dtype=torch.int32, device=dev)
-        self.r_idx = torch.zeros(T, E, dtype=torch.int32, device=dev)
-        self.rewards_d = torch.zeros(T, E, dtype=torch.float32, device=dev)
-        self.masks_d = torch.zeros(T, E, dtype=torch.float32, device=dev)
+        # [t][0] = action index, [t][1] = repetition index: one D2H copy per macro-step
+        self.idx = torch.zeros(T, 2, E, dtype=torch.int32, device=dev)
+        self.a_idx = self.idx[:, 0]
+        self.r_idx = self.idx[:, 1]
+        self.rm_d = torch.zeros(2, T, E, dtype=torch.float32, device=dev)  # rewards; masks
+        self.rewards_d = self.rm_d[0]
+        self.masks_d = self.rm_d[1]
         self.y = torch.zeros(T, E, dtype=torch.float32, device=dev)
         self.adv = torch.zeros(T, E, dtype=torch.float32, device=dev)
         self.pi_roll = torch.zeros(E, self.num_actions, dtype=torch.float32, device=dev)
@@ -66,11 +69,15 @@ class PAACLearner(ActorLearner):
         self.v_boot = torch.zeros(E, dtype=torch.float32, device=dev)
         self.loss_terms = torch.zeros(T * E, 4, dtype=torch.float32, device=dev)
         self.counters = torch.zeros(E, dtype=torch.int64, device=dev)
+        self.a_flat = torch.zeros(T * E, dtype=torch.int32, device=dev)  # row t*E+e (paac.py:239)
+        self.r_flat = torch.zeros(T * E, dtype=torch.int32, device=dev)
         pin = dict(pin_memory=True)
-        self.rewards_h = torch.zeros(T, E, dtype=torch.float32, **pin)
-        self.masks_h = torch.zeros(T, E, dtype=torch.float32, **pin)
-        self.a_h = torch.zeros(T, E, dtype=torch.int32, **pin)
-        self.r_h = torch.zeros(T, E, dtype=torch.int32, **pin)
+        self.rm_h = torch.zeros(2, T, E, dtype=torch.float32, **pin)
+        self.rewards_h = self.rm_h[0]
+        self.masks_h = self.rm_h[1]
+        self.idx_h = torch.zeros(T, 2, E, dtype=torch.int32, **pin)
+        self.a_h = self.idx_h[:, 0]
+        self.r_h = self.idx_h[:, 1]
         self.pi_h = torch.zeros(E, self.num_actions, dtype=torch.float32, **pin)
         self.rep_h = torch.zeros(E, self.total_repetitions, dtype=torch.float32, **pin)
         self.row_lut = torch.from_numpy(ROW_LUT.astype(np.int32)).to(dev)
@@ -88,8 +95,9 @@ class PAACLearner(ActorLearner):
             bank = self.environment_creator.create_bank(0, E)
             self.runners = NativeRunners(bank, self.workers, self.tab_rep)
             self.raw_d = torch.zeros(4 * E, 2, bank.frame_bytes, dtype=torch.uint8, device=self.dev)
-            self.off_d = torch.zeros(E, dtype=torch.int32, device=self.dev)
-            self.cnt_d = torch.zeros(E, dtype=torch.int32, device=self.dev)
+            self.meta_d = torch.zeros(2, E, dtype=torch.int32, device=self.dev)
+            self.off_d = self.meta_d[0]
+            self.cnt_d = self.meta_d[1]
             total = self.runners.reset()
             self._upload_pushes(total, self.states[0], self.states[0].clone())
         else:
@@ -108,8 +116,7 @@ class PAACLearner(ActorLearner):
         """H2D of the compact staging (only the pushed screens), then mt_preprocess."""
         r = self.runners
         self.raw_d[:total].copy_(r.staging[:total], non_blocking=True)
-        self.off_d.copy_(r.push_offset, non_blocking=True)
-        self.cnt_d.copy_(r.push_count, non_blocking=True)
+        self.meta_d.copy_(r.push_meta, non_blocking=True)
         devnet.preprocess(self.raw_d, self.off_d, self.cnt_d, self.emulator_counts, self.depth,
                           self.row_lut, self.col_lut, prev, out)
 
@@ -133,8 +140,7 @@ class PAACLearner(ActorLearner):
             end.record()
         if self.sampling == 'device':
             devnet.sample(pi, rep, self.sample_seed, self.counters, self.a_idx[t], self.r_idx[t])
-            self.a_h[t].copy_(self.a_idx[t], non_blocking=True)
-            self.r_h[t].copy_(self.r_idx[t], non_blocking=True)
+            self.idx_h[t].copy_(self.idx[t], non_blocking=True)
             self.event.record()
             self.event.synchronize()
             a = self.a_h[t].numpy()
@@ -147,8 +153,7 @@ class PAACLearner(ActorLearner):
             a, r = self.explo_policy.choose_indices(self.pi_h.numpy(), self.rep_h.numpy())
             self.a_h[t].numpy()[...] = a
             self.r_h[t].numpy()[...] = r
-            self.a_idx[t].copy_(self.a_h[t], non_blocking=True)
-            self.r_idx[t].copy_(self.r_h[t], non_blocking=True)
+            self.idx[t].copy_(self.idx_h[t], non_blocking=True)
         if self.runner_kind == 'native':
             total = self.runners.step(self.a_h[t], self.r_h[t])
             reward = self.runners.reward.numpy()
@@ -173,15 +178,16 @@ class PAACLearner(ActorLearner):
         E, T = self.emulator_counts, self.max_local_steps
         N = E * T
         net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout')
-        self.rewards_d.copy_(self.rewards_h, non_blocking=True)
-        self.masks_d.copy_(self.masks_h, non_blocking=True)
+        self.rm_d.copy_(self.rm_h, non_blocking=True)
         devnet.returns(self.rewards_d, self.masks_d, self.values, self.v_boot, self.gamma, self.y, self.adv)
         lr = self.get_lr()
         net.set_lr(lr)
         obs = self.states[:T].reshape(N, 84, 84, self.C)
+        self.a_flat.view(T, E).copy_(self.a_idx)
+        self.r_flat.view(T, E).copy_(self.r_idx)
         end = self._mark('train_pass')
         v, pi, rep = net.forward(obs, N, ws_key='train')
-        net.loss_backward(obs, N, v, pi, rep, self.a_idx.view(N), self.r_idx.view(N), self.y.view(N),
+        net.loss_backward(obs, N, v, pi, rep, self.a_flat, self.r_flat, self.y.view(N),
                           self.adv.view(N), loss_terms=self.loss_terms, ws_key='train')
         if end is not None:
             end.record()

@@ -39,8 +39,9 @@ class NativeRunners(object):
         pin = torch.cuda.is_available()
         mk = lambda *shape, dtype: torch.zeros(*shape, dtype=dtype, pin_memory=pin)
         self.staging = mk(4 * self.E, 2, self.frame_bytes, dtype=torch.uint8)
-        self.push_offset = mk(self.E, dtype=torch.int32)
-        self.push_count = mk(self.E, dtype=torch.int32)
+        self.push_meta = mk(2, self.E, dtype=torch.int32)  # [offset; count]: one H2D copy
+        self.push_offset = self.push_meta[0]
+        self.push_count = self.push_meta[1]
         self.reward = mk(self.E, dtype=torch.float32)
         self.over = mk(self.E, dtype=torch.float32)
         self.total = 0

@@ -18,5 +18,6 @@ for step in ${STEPS:-smoke tests bench}; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run tests 900 python -m pytest tests -q -m gpu ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    prof) run prof 600 bash tools/prof.sh ${PROF_NAME:-prof} ;;
   esac
 done
