@@ -191,6 +191,18 @@ def main():
         elapsed = float(e.item())
     prof = {k: [s.elapsed_time(e) for (s, e) in v] for k, v in learner.profile.items()}
     learner.profile = None
+    # rollout-batch forward (E rows), timed with HIP events on its stream, back to back
+    E = cfg['ec']
+    fw = []
+    for _ in range(30):
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_ev.record()
+        learner.network.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
+                                ws_key='rollout')
+        e_ev.record()
+        fw.append((s_ev, e_ev))
+    torch.cuda.synchronize()
+    prof['rollout_forward'] = [s_ev.elapsed_time(e_ev) for (s_ev, e_ev) in fw[5:]]
     ec = cfg['ec']
     value = world * ec * T * a.steps / elapsed
 

@@ -75,6 +75,7 @@ int mt_net_num_vars(const mt_net *net, int *n);
 int mt_net_var_info(const mt_net *net, int i, char *name, int name_len, int64_t *shape4,
                     int *ndim, size_t *offset, float *init_bound);
 int mt_net_feature_dim(const mt_net *net, int *f); /* width of the trunk output (256/512/...) */
+int mt_net_get_config(const mt_net *net, mt_net_config *cfg);
 /* Bytes of device workspace a forward/backward on `batch` rows needs. */
 int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes);
 
@@ -145,6 +146,38 @@ int mt_clip_rmsprop(float *w, float *ms, float *mom, const float *g, size_t n,
 int mt_preprocess(const uint8_t *raw, const int32_t *push_offset, const int32_t *push_count,
                   int E, int depth, const int32_t *row_lut, const int32_t *col_lut,
                   const uint8_t *prev, uint8_t *out, mt_stream_t stream);
+
+/* ---- native rollout macro-step (orchestrates A1-A3, A8; paac.py:140-205) -------------------
+ * One call = one macro-step t of every env: mt_forward on state slot t -> mt_sample into
+ * idx[0][t], idx[1][t] -> async D2H of the indices -> one event wait -> mh_runner_step (native
+ * emulator threads, libmanette_host.so) -> mh_book_step (bookkeeping into rm_host[.][t]) ->
+ * async H2D of the pushed screens + push metadata -> mt_preprocess into state slot t+1.
+ * All buffers are caller-owned; `runner` / `book` are mh_runner* / mh_book* handles. */
+typedef struct mt_rollout mt_rollout;
+typedef struct mt_rollout_buffers {
+  /* device */
+  uint8_t *states;             /* [T+1][E][84][84][4*depth] */
+  float *values;               /* [T][E] */
+  int32_t *idx;                /* [2][T][E]: action indices, then repetition indices */
+  float *pi, *rep;             /* [E][A], [E][R] */
+  void *ws;                    /* forward workspace for E rows */
+  size_t ws_bytes;
+  uint64_t *counters;          /* [E] sampling counters */
+  uint8_t *raw;                /* [4E][2][210*160*depth] screen staging */
+  int32_t *meta;               /* [2][E] push offsets; push counts */
+  const int32_t *row_lut, *col_lut;
+  /* pinned host */
+  int32_t *idx_host;           /* [2][T][E] */
+  uint8_t *staging_host;       /* [4E][2][210*160*depth] */
+  int32_t *meta_host;          /* [2][E] */
+  float *reward_host, *over_host; /* [E] */
+  float *rm_host;              /* [2][T][E]: clipped rewards; masks */
+} mt_rollout_buffers;
+int mt_rollout_create(const mt_net *net, int E, int T, void *runner, void *book,
+                      const mt_rollout_buffers *buffers, uint64_t seed, mt_rollout **out);
+void mt_rollout_destroy(mt_rollout *ro);
+int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64_t *global_step,
+                    mt_stream_t stream);
 
 /* ---- small helpers ----------------------------------------------------------------------- */
 /* out[i] = sum_z parts[z*n + i] (deterministic order); used for split reductions. */

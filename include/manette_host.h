@@ -53,6 +53,25 @@ int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx, uin
 /* Per-env counters (for tests): k (next() calls incl. reset pushes) and steps in episode. */
 int mh_runner_env_state(const mh_runner *r, int e, int64_t *k, int32_t *steps);
 
+/* ---- rollout bookkeeping (A8): paac.py:154-205, vectorised over envs -----------------------
+ * Per macro-step: masks = 1 - over; rewards = clip(reward, +-1) (actor_learner.py:108-114);
+ * per env, in env order: total episode reward += reward (float32, the shared array's type),
+ * emulator_steps += tab_rep[r] + 1 (planned repeats, :183), global_step += 1 (:184),
+ * histogram[a][r] += 1 and nb_actions += r + 1 (:157, :187-189); on `over` an episode record
+ * (global_step at that env, total reward, emulator_steps) is queued and both counters reset. */
+typedef struct mh_book mh_book;
+int mh_book_create(int n_envs, int num_actions, const int32_t *tab_rep, int n_reps, mh_book **out);
+void mh_book_destroy(mh_book *b);
+int mh_book_step(mh_book *b, int64_t *global_step, const int32_t *a_idx, const int32_t *r_idx,
+                 const float *reward, const float *over, float *rewards_out, float *masks_out);
+/* Start a new update: clears the action/repetition histogram and nb_actions (paac.py:135-136). */
+int mh_book_new_update(mh_book *b);
+/* hist [A][R] int64 of the current update, nb_actions (may be NULL). */
+int mh_book_histogram(const mh_book *b, int64_t *hist, int64_t *nb_actions);
+/* Pop up to max queued episodes (oldest first); *n receives the count popped. */
+int mh_book_pop_episodes(mh_book *b, int64_t *global_step, float *reward, int64_t *length, int max,
+                         int *n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,14 @@ class MTError(RuntimeError):
     pass
 
 
+class mt_rollout_buffers(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ('states', 'values', 'idx', 'pi', 'rep', 'ws')] + \
+               [('ws_bytes', C.c_size_t)] + \
+               [(n, C.c_void_p) for n in ('counters', 'raw', 'meta', 'row_lut', 'col_lut', 'idx_host',
+                                          'staging_host', 'meta_host', 'reward_host', 'over_host',
+                                          'rm_host')]
+
+
 class mt_net_config(C.Structure):
     _fields_ = [('arch', C.c_int32), ('depth', C.c_int32), ('num_actions', C.c_int32),
                 ('num_reps', C.c_int32), ('activation', C.c_int32), ('alpha_leaky', C.c_float),
@@ -50,6 +58,10 @@ _HIP_SIGS = {
     'mt_clip_rmsprop': (_I, [_P, _P, _P, _P, _SZ, _P, _P, _F, _F, _F, _F, _I, _F, _P, _P]),
     'mt_preprocess': (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     'mt_sum_slabs': (_I, [_P, _I, _SZ, _P, _P]),
+    'mt_net_get_config': (_I, [_P, C.POINTER(mt_net_config)]),
+    'mt_rollout_create': (_I, [_P, _I, _I, _P, _P, C.POINTER(mt_rollout_buffers), C.c_uint64, C.POINTER(_P)]),
+    'mt_rollout_destroy': (None, [_P]),
+    'mt_rollout_step': (_I, [_P, _P, _I, C.POINTER(C.c_int64), _P]),
     'mt_graph_begin': (_I, [_P]),
     'mt_graph_end': (_I, [_P, C.POINTER(_P)]),
     'mt_graph_launch': (_I, [_P, _P]),
@@ -63,6 +75,12 @@ _HOST_SIGS = {
     'mh_runner_reset': (_I, [_P, _P, _P, _P, C.POINTER(_I)]),
     'mh_runner_step': (_I, [_P, _P, _P, _P, _P, _P, _P, _P, C.POINTER(_I)]),
     'mh_runner_env_state': (_I, [_P, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    'mh_book_create': (_I, [_I, _I, _P, _I, C.POINTER(_P)]),
+    'mh_book_destroy': (None, [_P]),
+    'mh_book_step': (_I, [_P, C.POINTER(C.c_int64), _P, _P, _P, _P, _P, _P]),
+    'mh_book_new_update': (_I, [_P]),
+    'mh_book_histogram': (_I, [_P, _P, C.POINTER(C.c_int64)]),
+    'mh_book_pop_episodes': (_I, [_P, _P, _P, _P, _I, C.POINTER(_I)]),
 }
 
 _hip = None
@@ -84,6 +102,7 @@ def _load(path, sigs):
 def hip():
     global _hip
     if _hip is None:
+        host()  # libmanette_hip.so links libmanette_host.so (rpath $ORIGIN)
         _hip = _load(HIP_LIB, _HIP_SIGS)
     return _hip
 

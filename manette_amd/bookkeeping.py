@@ -58,3 +58,74 @@ class Bookkeeper(object):
         histo_a = np.repeat(np.arange(self.A), nb_a)
         histo_r = np.repeat(self.tab + 1, nb_r)
         return histo_a, histo_r
+
+
+class NativeBook(object):
+    """The same bookkeeping in libmanette_host.so (mh_book_*), used by the learner so a native
+    macro-step needs no Python; interface of Bookkeeper (tests pin one against the other)."""
+
+    def __init__(self, n_envs, num_actions, tab_rep):
+        import ctypes as C
+        from . import _lib
+        self._C = C
+        self._lib = _lib
+        self.E = n_envs
+        self.A = num_actions
+        self.tab = np.ascontiguousarray(np.asarray(tab_rep, dtype=np.int32))
+        self.R = len(self.tab)
+        h = C.c_void_p()
+        _lib.check_host(_lib.host().mh_book_create(n_envs, num_actions, self.tab.ctypes.data_as(C.c_void_p),
+                                                   self.R, C.byref(h)), 'mh_book_create')
+        self._h = h
+        self.total_rewards = []
+        self.total_steps = []
+        self.episodes = []
+
+    @property
+    def handle(self):
+        return self._h
+
+    def step(self, global_step, a_idx, r_idx, reward, over, rewards_out, masks_out):
+        C = self._C
+        gs = C.c_int64(global_step)
+        arrs = [np.ascontiguousarray(a_idx, np.int32), np.ascontiguousarray(r_idx, np.int32),
+                np.ascontiguousarray(reward, np.float32), np.ascontiguousarray(over, np.float32)]
+        assert rewards_out.flags.c_contiguous and masks_out.flags.c_contiguous
+        self._lib.check_host(self._lib.host().mh_book_step(
+            self._h, C.byref(gs), *[a.ctypes.data_as(C.c_void_p) for a in arrs],
+            rewards_out.ctypes.data_as(C.c_void_p), masks_out.ctypes.data_as(C.c_void_p)), 'mh_book_step')
+        self.drain()
+        return gs.value
+
+    def drain(self):
+        C = self._C
+        n = C.c_int(1)
+        while n.value:
+            st = np.zeros(256, np.int64)
+            rw = np.zeros(256, np.float32)
+            ln = np.zeros(256, np.int64)
+            self._lib.check_host(self._lib.host().mh_book_pop_episodes(
+                self._h, st.ctypes.data_as(C.c_void_p), rw.ctypes.data_as(C.c_void_p),
+                ln.ctypes.data_as(C.c_void_p), 256, C.byref(n)))
+            for i in range(n.value):
+                self.total_rewards.append(float(rw[i]))
+                self.total_steps.append(int(ln[i]))
+                self.episodes.append((int(st[i]), float(rw[i]), int(ln[i])))
+
+    def new_update(self):
+        self._lib.check_host(self._lib.host().mh_book_new_update(self._h))
+
+    def histograms(self):
+        C = self._C
+        hist = np.zeros((self.A, self.R), np.int64)
+        nb = C.c_int64()
+        self._lib.check_host(self._lib.host().mh_book_histogram(self._h, hist.ctypes.data_as(C.c_void_p),
+                                                                C.byref(nb)))
+        self.nb_actions = nb.value
+        return np.repeat(np.arange(self.A), hist.sum(1)), np.repeat(self.tab.astype(np.int64) + 1, hist.sum(0))
+
+    def __del__(self):
+        h = getattr(self, '_h', None)
+        if h:
+            self._lib.host().mh_book_destroy(h)
+            self._h = None

@@ -10,7 +10,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
-HIP_SOURCES = ['net.hip', 'misc.hip']
+HIP_SOURCES = ['net.hip', 'misc.hip', 'rollout.hip']
 HIP_HEADERS = ['common.h', 'gemm.h']
 HOST_SOURCES = ['runner.cpp']
 HIP_LIB = os.path.join(HERE, 'libmanette_hip.so')
@@ -34,12 +34,14 @@ def _stale(target, deps):
 
 def build_hip(force=False, verbose=False):
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [os.path.join(INCLUDE, 'manette_hip.h')]
+    deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [os.path.join(INCLUDE, 'manette_hip.h'),
+                                                                  os.path.join(INCLUDE, 'manette_host.h'), HOST_LIB]
     if not force and not _stale(HIP_LIB, deps):
         return HIP_LIB
     tmp = HIP_LIB + '.tmp'
     cmd = [_hipcc(), '--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
-           '-Wno-unused-result', '-o', tmp] + srcs
+           '-Wno-unused-result', '-o', tmp] + srcs + [
+               '-L' + HERE, '-lmanette_host', '-Wl,-rpath,$ORIGIN']
     if verbose:
         print(' '.join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)

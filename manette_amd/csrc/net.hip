@@ -675,6 +675,12 @@ extern "C" int mt_net_var_info(const mt_net *net, int i, char *name, int name_le
   return MT_OK;
 }
 
+extern "C" int mt_net_get_config(const mt_net *net, mt_net_config *cfg) {
+  MT_CHECK_ARG(net && cfg, "null argument");
+  *cfg = net->cfg;
+  return MT_OK;
+}
+
 extern "C" int mt_net_feature_dim(const mt_net *net, int *f) {
   MT_CHECK_ARG(net && f, "null argument");
   *f = net->F;

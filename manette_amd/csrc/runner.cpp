@@ -266,3 +266,119 @@ extern "C" int mh_runner_env_state(const mh_runner *r, int e, int64_t *k, int32_
   if (steps) *steps = r->env[e].steps;
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Rollout bookkeeping (A8) — same semantics as manette_amd/bookkeeping.py (pinned to the
+// reference's golden host-loop vectors), kept native so a macro-step needs no Python.
+// ---------------------------------------------------------------------------------------------
+struct mh_book {
+  int E = 0, A = 0, R = 0;
+  std::vector<int32_t> tab;
+  std::vector<int64_t> emulator_steps;
+  std::vector<float> total_reward;
+  std::vector<int64_t> hist;  // [A][R]
+  int64_t nb_actions = 0;
+  struct Episode {
+    int64_t step;
+    float reward;
+    int64_t length;
+  };
+  std::vector<Episode> episodes;  // FIFO
+  size_t head = 0;
+};
+
+extern "C" int mh_book_create(int n_envs, int num_actions, const int32_t *tab_rep, int n_reps,
+                              mh_book **out) {
+  if (!out || !tab_rep || n_envs < 1 || num_actions < 1 || n_reps < 1) {
+    set_error("bad argument");
+    return 1;
+  }
+  mh_book *b = new mh_book();
+  b->E = n_envs;
+  b->A = num_actions;
+  b->R = n_reps;
+  b->tab.assign(tab_rep, tab_rep + n_reps);
+  b->emulator_steps.assign(n_envs, 0);
+  b->total_reward.assign(n_envs, 0.f);
+  b->hist.assign((size_t)num_actions * n_reps, 0);
+  *out = b;
+  return 0;
+}
+
+extern "C" void mh_book_destroy(mh_book *b) { delete b; }
+
+extern "C" int mh_book_step(mh_book *b, int64_t *global_step, const int32_t *a_idx,
+                            const int32_t *r_idx, const float *reward, const float *over,
+                            float *rewards_out, float *masks_out) {
+  if (!b || !global_step || !a_idx || !r_idx || !reward || !over || !rewards_out || !masks_out) {
+    set_error("null argument");
+    return 1;
+  }
+  for (int e = 0; e < b->E; ++e) {
+    const int a = a_idx[e], r = r_idx[e];
+    if (a < 0 || a >= b->A || r < 0 || r >= b->R) {
+      set_error("index out of range at env %d (a=%d, r=%d)", e, a, r);
+      return 1;
+    }
+  }
+  const int64_t gs0 = *global_step;
+  for (int e = 0; e < b->E; ++e) {
+    const float rw = reward[e];
+    masks_out[e] = 1.0f - over[e];
+    b->total_reward[e] += rw;
+    rewards_out[e] = rw > 1.0f ? 1.0f : (rw < -1.0f ? -1.0f : rw);
+    const int a = a_idx[e], r = r_idx[e];
+    b->emulator_steps[e] += b->tab[r] + 1;
+    b->hist[(size_t)a * b->R + r] += 1;
+    b->nb_actions += r + 1;
+    if (over[e] != 0.f) {
+      b->episodes.push_back({gs0 + e + 1, b->total_reward[e], b->emulator_steps[e]});
+      b->total_reward[e] = 0.f;
+      b->emulator_steps[e] = 0;
+    }
+  }
+  *global_step = gs0 + b->E;
+  return 0;
+}
+
+extern "C" int mh_book_new_update(mh_book *b) {
+  if (!b) {
+    set_error("null argument");
+    return 1;
+  }
+  std::fill(b->hist.begin(), b->hist.end(), 0);
+  b->nb_actions = 0;
+  return 0;
+}
+
+extern "C" int mh_book_histogram(const mh_book *b, int64_t *hist, int64_t *nb_actions) {
+  if (!b) {
+    set_error("null argument");
+    return 1;
+  }
+  if (hist) std::copy(b->hist.begin(), b->hist.end(), hist);
+  if (nb_actions) *nb_actions = b->nb_actions;
+  return 0;
+}
+
+extern "C" int mh_book_pop_episodes(mh_book *b, int64_t *global_step, float *reward,
+                                    int64_t *length, int max, int *n) {
+  if (!b || !n) {
+    set_error("null argument");
+    return 1;
+  }
+  int k = 0;
+  while (k < max && b->head < b->episodes.size()) {
+    const auto &ep = b->episodes[b->head++];
+    if (global_step) global_step[k] = ep.step;
+    if (reward) reward[k] = ep.reward;
+    if (length) length[k] = ep.length;
+    ++k;
+  }
+  if (b->head == b->episodes.size()) {
+    b->episodes.clear();
+    b->head = 0;
+  }
+  *n = k;
+  return 0;
+}

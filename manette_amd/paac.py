@@ -26,7 +26,7 @@ import torch
 
 from . import network as devnet
 from .actor_learner import ActorLearner
-from .bookkeeping import Bookkeeper
+from .bookkeeping import NativeBook
 from .environment import COL_LUT, ROW_LUT
 from .runners import NativeRunners, Runners
 from .emulator_runner import EmulatorRunner
@@ -55,10 +55,10 @@ class PAACLearner(ActorLearner):
         dev = self.dev
         self.states = torch.zeros(T + 1, E, 84, 84, C, dtype=torch.uint8, device=dev)
         self.values = torch.zeros(T, E, dtype=torch.float32, device=dev)
-        # [t][0] = action index, [t][1] = repetition index: one D2H copy per macro-step
-        self.idx = torch.zeros(T, 2, E, dtype=torch.int32, device=dev)
-        self.a_idx = self.idx[:, 0]
-        self.r_idx = self.idx[:, 1]
+        # [0] = action indices, [1] = repetition indices, each [T][E] (row t*E+e, paac.py:239)
+        self.idx = torch.zeros(2, T, E, dtype=torch.int32, device=dev)
+        self.a_idx = self.idx[0]
+        self.r_idx = self.idx[1]
         self.rm_d = torch.zeros(2, T, E, dtype=torch.float32, device=dev)  # rewards; masks
         self.rewards_d = self.rm_d[0]
         self.masks_d = self.rm_d[1]
@@ -69,21 +69,20 @@ class PAACLearner(ActorLearner):
         self.v_boot = torch.zeros(E, dtype=torch.float32, device=dev)
         self.loss_terms = torch.zeros(T * E, 4, dtype=torch.float32, device=dev)
         self.counters = torch.zeros(E, dtype=torch.int64, device=dev)
-        self.a_flat = torch.zeros(T * E, dtype=torch.int32, device=dev)  # row t*E+e (paac.py:239)
-        self.r_flat = torch.zeros(T * E, dtype=torch.int32, device=dev)
         pin = dict(pin_memory=True)
         self.rm_h = torch.zeros(2, T, E, dtype=torch.float32, **pin)
         self.rewards_h = self.rm_h[0]
         self.masks_h = self.rm_h[1]
-        self.idx_h = torch.zeros(T, 2, E, dtype=torch.int32, **pin)
-        self.a_h = self.idx_h[:, 0]
-        self.r_h = self.idx_h[:, 1]
+        self.idx_h = torch.zeros(2, T, E, dtype=torch.int32, **pin)
+        self.a_h = self.idx_h[0]
+        self.r_h = self.idx_h[1]
         self.pi_h = torch.zeros(E, self.num_actions, dtype=torch.float32, **pin)
         self.rep_h = torch.zeros(E, self.total_repetitions, dtype=torch.float32, **pin)
         self.row_lut = torch.from_numpy(ROW_LUT.astype(np.int32)).to(dev)
         self.col_lut = torch.from_numpy(COL_LUT.astype(np.int32)).to(dev)
         self.event = torch.cuda.Event()
-        self.book = Bookkeeper(E, self.num_actions, self.tab_rep)
+        self.book = NativeBook(E, self.num_actions, self.tab_rep)
+        self.native_step = None  # mt_rollout handle (native runner + device sampling)
         self.runners = None
         self.profile = None      # name -> [(start_event, end_event)] when profiling (bench.py)
         self.sample_seed = (self.seed * 1000003 + self.rank * 7919 + 1) & 0xffffffffffff
@@ -100,6 +99,8 @@ class PAACLearner(ActorLearner):
             self.cnt_d = self.meta_d[1]
             total = self.runners.reset()
             self._upload_pushes(total, self.states[0], self.states[0].clone())
+            if self.sampling == 'device':
+                self._make_native_step()
         else:
             emus = [self.environment_creator.create_environment(i) for i in range(E)]
             s0 = np.asarray([e.get_initial_state() for e in emus], dtype=np.uint8)
@@ -112,6 +113,23 @@ class PAACLearner(ActorLearner):
             self.obs_h.numpy()[...] = self.shared[0]
             self.states[0].copy_(self.obs_h, non_blocking=True)
 
+    def _make_native_step(self):
+        import ctypes as C
+        from . import _lib
+        net, r = self.network, self.runners
+        ws = net.workspace(self.emulator_counts, 'rollout')
+        p = lambda t: C.c_void_p(t.data_ptr())
+        self._bufs = _lib.mt_rollout_buffers(
+            p(self.states), p(self.values), p(self.idx), p(self.pi_roll), p(self.rep_roll), p(ws), ws.numel(),
+            p(self.counters), p(self.raw_d), p(self.meta_d), p(self.row_lut), p(self.col_lut), p(self.idx_h),
+            p(r.staging), p(r.push_meta), p(r.reward), p(r.over), p(self.rm_h))
+        h = C.c_void_p()
+        _lib.check(_lib.hip().mt_rollout_create(net._h, self.emulator_counts, self.max_local_steps, r._h,
+                                                self.book.handle, C.byref(self._bufs),
+                                                C.c_uint64(self.sample_seed), C.byref(h)), 'mt_rollout_create')
+        self.native_step = h
+        self._gs = C.c_int64(0)
+
     def _upload_pushes(self, total, out, prev):
         """H2D of the compact staging (only the pushed screens), then mt_preprocess."""
         r = self.runners
@@ -119,6 +137,11 @@ class PAACLearner(ActorLearner):
         self.meta_d.copy_(r.push_meta, non_blocking=True)
         devnet.preprocess(self.raw_d, self.off_d, self.cnt_d, self.emulator_counts, self.depth,
                           self.row_lut, self.col_lut, prev, out)
+
+    @staticmethod
+    def _lib_ref(x):
+        import ctypes as C
+        return C.byref(x)
 
     def _mark(self, name):
         if self.profile is None:
@@ -133,6 +156,14 @@ class PAACLearner(ActorLearner):
         """One rollout macro-step (paac.py:140-205)."""
         net = self.network
         E = self.emulator_counts
+        if self.native_step is not None:
+            from . import _lib
+            self._gs.value = self.global_step
+            _lib.check(_lib.hip().mt_rollout_step(self.native_step, devnet._ptr(net.params), t,
+                                                  self._lib_ref(self._gs), devnet._stream()), 'mt_rollout_step')
+            self.global_step = self._gs.value
+            self.book.drain()
+            return
         end = self._mark('rollout_forward')
         v, pi, rep = net.forward(self.states[t], E, out=(self.values[t], self.pi_roll, self.rep_roll),
                                  ws_key='rollout')
@@ -183,11 +214,9 @@ class PAACLearner(ActorLearner):
         lr = self.get_lr()
         net.set_lr(lr)
         obs = self.states[:T].reshape(N, 84, 84, self.C)
-        self.a_flat.view(T, E).copy_(self.a_idx)
-        self.r_flat.view(T, E).copy_(self.r_idx)
         end = self._mark('train_pass')
         v, pi, rep = net.forward(obs, N, ws_key='train')
-        net.loss_backward(obs, N, v, pi, rep, self.a_flat, self.r_flat, self.y.view(N),
+        net.loss_backward(obs, N, v, pi, rep, self.idx[0].view(N), self.idx[1].view(N), self.y.view(N),
                           self.adv.view(N), loss_terms=self.loss_terms, ws_key='train')
         if end is not None:
             end.record()
@@ -247,6 +276,10 @@ class PAACLearner(ActorLearner):
             torch.cuda.synchronize()
             super(PAACLearner, self).cleanup()
         finally:
+            if self.native_step is not None:
+                from . import _lib
+                _lib.hip().mt_rollout_destroy(self.native_step)
+                self.native_step = None
             if self.runners is not None:
                 self.runners.stop()
                 self.runners = None

@@ -1,0 +1,140 @@
+"""End-to-end learner parity on the GPU box: every path through PAACLearner that should produce
+identical trajectories does, bit for bit, and the CLI trains / checkpoints / resumes."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _learner(tmp, runner, sampling, arch='NIPS', ec=8, game='pong', max_rep=0, nb=1, workers=2, seed=0):
+    sys.path.insert(0, ROOT)
+    import train as cli
+    from manette_amd.exploration_policy import ExplorationPolicy
+    from manette_amd.paac import PAACLearner
+    a = cli.get_arg_parser().parse_args([])
+    a.game, a.arch, a.emulator_counts, a.emulator_workers = game, arch, ec, workers
+    a.max_repetition, a.nb_choices = max_rep, nb
+    a.runner, a.sampling, a.seed = runner, sampling, seed
+    a.debugging_folder = str(tmp) + '/'
+    a.max_global_steps = 1 << 40
+    a.checkpoint_interval = 1 << 40
+    a.lr_annealing_steps = 100000
+    np.random.seed(1234)
+    explo = ExplorationPolicy(a)
+    nc, ec_ = cli.get_network_and_environment_creator(a, explo)
+    L = PAACLearner(nc, ec_, explo, a)
+    L.start()
+    return L
+
+
+def _run(L, updates):
+    for _ in range(updates):
+        L.book.new_update()
+        for t in range(L.max_local_steps):
+            L.step(t)
+        L.update()
+    torch.cuda.synchronize()
+
+
+def _state(L):
+    return dict(params=L.network.params.cpu().numpy().copy(), ms=L.network.ms.cpu().numpy().copy(),
+                states=L.states.cpu().numpy().copy(), gs=L.global_step, episodes=list(L.book.episodes))
+
+
+@pytest.mark.parametrize('max_rep,nb', [(0, 1), (10, 11)])
+def test_native_step_equals_python_step(tmp_path, max_rep, nb):
+    """mt_rollout_step (C++ orchestration) == the Python step() on the same kernels."""
+    A = _learner(tmp_path / 'a', 'native', 'device', max_rep=max_rep, nb=nb)
+    assert A.native_step is not None
+    _run(A, 6)
+    sa = _state(A)
+    A.cleanup()
+    B = _learner(tmp_path / 'b', 'native', 'device', max_rep=max_rep, nb=nb)
+    from manette_amd import _lib
+    _lib.hip().mt_rollout_destroy(B.native_step)
+    B.native_step = None
+    _run(B, 6)
+    sb = _state(B)
+    B.cleanup()
+    for k in ('params', 'ms', 'states'):
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    assert sa['gs'] == sb['gs'] == 6 * 5 * 8
+
+
+def test_native_runner_equals_reference_contract_runner(tmp_path):
+    """Native emulator threads + GPU preprocess == reference-contract Python emulators with CPU
+    preprocess (same seeds, host numpy sampling): identical trajectories and updates."""
+    A = _learner(tmp_path / 'a', 'native', 'host', max_rep=10, nb=11)
+    _run(A, 5)
+    sa = _state(A)
+    A.cleanup()
+    B = _learner(tmp_path / 'b', 'python', 'host', max_rep=10, nb=11, workers=0)
+    _run(B, 5)
+    sb = _state(B)
+    B.cleanup()
+    for k in ('params', 'ms', 'states'):
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    assert sa['gs'] == sb['gs']
+
+
+def test_python_runner_processes(tmp_path):
+    A = _learner(tmp_path / 'a', 'python', 'host', workers=0)
+    _run(A, 3)
+    sa = _state(A)
+    A.cleanup()
+    B = _learner(tmp_path / 'b', 'python', 'host', workers=2)
+    _run(B, 3)
+    sb = _state(B)
+    B.cleanup()
+    np.testing.assert_array_equal(sa['params'], sb['params'])
+
+
+def test_train_cli_checkpoint_resume(tmp_path):
+    df = str(tmp_path / 'run') + '/'
+    cmd = [sys.executable, os.path.join(ROOT, 'train.py'), '-g', 'breakout', '--arch', 'NATURE', '-ec', '8',
+           '-ew', '2', '--max_repetition', '10', '--nb_choices', '11', '--max_global_steps', '200',
+           '--checkpoint_interval', '80', '-df', df]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    args = json.load(open(df + 'args.json'))
+    assert args['arch'] == 'NATURE' and args['nb_choices'] == 11
+    ck = sorted(os.listdir(df + 'checkpoints'))
+    assert 'checkpoint' in ck and '-200.npz' in ck
+    assert os.listdir(df + 'optimizer_checkpoints') == ['-200.npz', 'checkpoint'] or \
+        sorted(os.listdir(df + 'optimizer_checkpoints')) == ['-200.npz', 'checkpoint']
+    with np.load(df + 'checkpoints/-200.npz') as z:
+        assert z['Network/conv3/conv3_weights'].shape == (3, 3, 64, 64)
+        assert z['Training/Repetition/repetition_output/repetition_output_weights'].shape == (512, 11)
+    with np.load(df + 'optimizer_checkpoints/-200.npz') as z:
+        assert 'Network/fc4/fc4_weights/OptimizerVariables' in z.files
+    # resume: starts from step 200 and continues to 280
+    cmd[cmd.index('--max_global_steps') + 1] = '280'
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert 'Restoring network variables' in out.stdout + out.stderr
+    assert '-280.npz' in os.listdir(df + 'checkpoints')
+
+
+def test_dp_two_ranks_gloo_on_one_gpu(tmp_path):
+    """world_size 2 (gloo over the same GPU): the flat gradient is all-reduced once per update
+    and both replicas stay bit-identical."""
+    script = os.path.join(ROOT, 'tests', 'dp_worker.py')
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT='29533', WORLD_SIZE='2')
+    procs = []
+    for r in range(2):
+        e = dict(env, RANK=str(r), LOCAL_RANK='0')
+        procs.append(subprocess.Popen([sys.executable, script, str(tmp_path), 'gpu'], env=e,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, o[-2000:] + e[-3000:]
+    p0 = np.load(os.path.join(str(tmp_path), 'rank0.npy'))
+    p1 = np.load(os.path.join(str(tmp_path), 'rank1.npy'))
+    np.testing.assert_array_equal(p0, p1)
