@@ -30,6 +30,9 @@ CONFIGS = {
                                   nb_choices=11, rgb=False),
     'seaquest-nature': dict(game='seaquest', arch='NATURE', ec=32, ew=8, max_repetition=0, nb_choices=1,
                             rgb=False),
+    # the CLI's default arch and the arch of every FiGAR checkpoint
+    'breakout-pwyx-figar-rgb': dict(game='breakout', arch='PWYX', ec=32, ew=8, max_repetition=10,
+                                    nb_choices=11, rgb=True),
 }
 MI355X_FP32_TFLOPS = 157.3   # dense fp32 (vector = MFMA), MI355X_MICROARCH.md
 MI355X_HBM_GBS = 8000.0      # HBM3E peak, MI355X_MICROARCH.md
@@ -40,19 +43,26 @@ def conv_out(h, k, s):
 
 
 def arch_flops(arch, depth, A, R):
-    """Forward FLOPs per sample per layer (2*MACs) for NIPS/NATURE, and weights (floats)."""
+    """Per sample per layer: (kind, forward FLOPs = 2*MACs, weight floats, output floats) for
+    NIPS / NATURE / PWYX (networks.py:178-278)."""
     C = 4 * depth
     if arch == 'NIPS':
-        convs = [(8, 4, C, 16), (4, 2, 16, 32)]
+        convs = [(8, 4, C, 16, 'VALID', False), (4, 2, 16, 32, 'VALID', False)]
         F = 256
+    elif arch == 'NATURE':
+        convs = [(8, 4, C, 32, 'VALID', False), (4, 2, 32, 64, 'VALID', False), (3, 1, 64, 64, 'VALID', False)]
+        F = 512
     else:
-        convs = [(8, 4, C, 32), (4, 2, 32, 64), (3, 1, 64, 64)]
+        convs = [(5, 1, C, 32, 'SAME', True), (5, 1, 32, 32, 'SAME', True), (4, 1, 32, 64, 'SAME', True),
+                 (3, 1, 64, 64, 'SAME', False)]
         F = 512
     h = 84
     layers = []
-    for (k, s, cin, cout) in convs:
-        h = conv_out(h, k, s)
+    for (k, s, cin, cout, pad, pool) in convs:
+        h = conv_out(h, k, s) if pad == 'VALID' else -(-h // s)
         layers.append(('conv', 2.0 * h * h * cout * k * k * cin, k * k * cin * cout + cout, h * h * cout))
+        if pool:
+            h //= 2
     flat = h * h * convs[-1][3]
     layers.append(('fc', 2.0 * flat * F, flat * F + F, F))
     layers.append(('heads', 2.0 * F * (1 + A + R), F * (1 + A + R) + 1 + A + R, 1 + A + R))
@@ -141,6 +151,8 @@ def main():
     ap.add_argument('--cpu_seconds', type=float, default=15.0)
     ap.add_argument('--no_cpu_baseline', action='store_true')
     ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--step_impl', default='native', choices=['native', 'python'],
+                    help='macro-step orchestration: native (mt_rollout_step) or Python')
     a = ap.parse_args()
 
     import torch
@@ -165,6 +177,10 @@ def main():
     learner = PAACLearner(net_creator, env_creator, explo, args)
     learner.is_chief = False  # no checkpoint writes from the benchmark
     learner.start()
+    if a.step_impl == 'python' and learner.native_step is not None:
+        from manette_amd import _lib
+        _lib.hip().mt_rollout_destroy(learner.native_step)
+        learner.native_step = None
 
     def one_update():
         learner.book.new_update()
@@ -178,6 +194,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     learner.profile = {}
+    stats = None
+    if learner.native_step is not None:
+        import ctypes as C
+        from manette_amd import _lib
+        stats = (C.c_double * 5)()
+        _lib.hip().mt_rollout_stats(learner.native_step, stats, 1)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         one_update()
@@ -185,6 +207,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if stats is not None:
+        _lib.hip().mt_rollout_stats(learner.native_step, stats, 0)
+        n = max(stats[4], 1)
+        step_phases = {k: round(stats[i] / n, 2) for i, k in enumerate(
+            ['launch_and_wait_us', 'emulators_us', 'bookkeeping_us', 'upload_enqueue_us'])}
+    else:
+        step_phases = None
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -230,8 +259,8 @@ def main():
             'vs_baseline': None,
             'dtype': 'fp32',
             'data': 'synthetic (seeded 210x160 screens, native emulator threads, GPU preprocess)',
-            'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling' % (
-                a.config, ec, cfg['ew'], T, a.sampling), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
+            'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step' % (
+                a.config, ec, cfg['ew'], T, a.sampling, a.step_impl), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
                 'global_emulators': ec * world, 'parallelism': 'dp%d' % world},
             'roofline': {'bound': 'mfma', 'kernel': 'train pass (fwd+bwd, %d rows)' % N,
                          'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',
@@ -241,6 +270,8 @@ def main():
                                 'hbm_gbs': round(fwd_bytes / (rf_ms * 1e-3) / 1e9, 1),
                                 'hbm_frac': round(fwd_bytes / (rf_ms * 1e-3) / 1e9 / MI355X_HBM_GBS, 4)},
         }
+        if step_phases:
+            line['macro_step_host_us'] = step_phases
         if world == 1 and not a.no_cpu_baseline:
             learner.cleanup()
             learner = None

@@ -178,6 +178,10 @@ int mt_rollout_create(const mt_net *net, int E, int T, void *runner, void *book,
 void mt_rollout_destroy(mt_rollout *ro);
 int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64_t *global_step,
                     mt_stream_t stream);
+/* Host wall-clock microseconds accumulated by mt_rollout_step, per phase: [0] launch + wait
+ * for the sampled indices, [1] emulator step, [2] bookkeeping, [3] upload + preprocess
+ * enqueue, [4] number of steps. reset != 0 zeroes the counters. */
+int mt_rollout_stats(mt_rollout *ro, double *out5, int reset);
 
 /* ---- small helpers ----------------------------------------------------------------------- */
 /* out[i] = sum_z parts[z*n + i] (deterministic order); used for split reductions. */

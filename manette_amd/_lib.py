@@ -62,6 +62,7 @@ _HIP_SIGS = {
     'mt_rollout_create': (_I, [_P, _I, _I, _P, _P, C.POINTER(mt_rollout_buffers), C.c_uint64, C.POINTER(_P)]),
     'mt_rollout_destroy': (None, [_P]),
     'mt_rollout_step': (_I, [_P, _P, _I, C.POINTER(C.c_int64), _P]),
+    'mt_rollout_stats': (_I, [_P, C.POINTER(C.c_double), _I]),
     'mt_graph_begin': (_I, [_P]),
     'mt_graph_end': (_I, [_P, C.POINTER(_P)]),
     'mt_graph_launch': (_I, [_P, _P]),

@@ -344,11 +344,14 @@ template <class G, bool U8>
 struct LdIm2col {
   static constexpr bool KMAJOR = true;
   const typename InElem<U8>::T *X;
+  // k >= KK (a BK that does not divide KK) is zeroed inside fetch_fast, so only the rows decide.
   __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
-    return row0 + rows <= nrows && k0 + bk <= ke;
+    return row0 + rows <= nrows && (k0 + bk <= ke || ke == G::KK);
   }
-  // Padding (SAME) handled branch-free: clamped address, zero by select.
+  // Padding (SAME) and the k tail handled branch-free: clamped address, zero by select.
   __device__ __forceinline__ f32x4 fetch_fast(int m, int k) const {
+    const bool kok = k < G::KK;
+    k = kok ? k : 0;
     const int b = m / (G::OH * G::OW);
     const int rem = m - b * (G::OH * G::OW);
     const int oy = rem / G::OW, ox = rem - oy * G::OW;
@@ -357,12 +360,13 @@ struct LdIm2col {
     const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
     const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
     if constexpr (G::SAME) {
-      const bool ok = iy >= 0 && iy < G::H && ix >= 0 && ix < G::W;
+      const bool ok = kok && iy >= 0 && iy < G::H && ix >= 0 && ix < G::W;
       const int iyc = min(max(iy, 0), G::H - 1), ixc = min(max(ix, 0), G::W - 1);
       const f32x4 v = InElem<U8>::load4(X + (((size_t)b * G::H + iyc) * G::W + ixc) * G::CIN + ci);
       return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     } else {
-      return InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
+      const f32x4 v = InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
+      return kok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {

@@ -8,34 +8,58 @@
 #include <vector>
 #include <cmath>
 #include <algorithm>
+#include <tuple>
 
 #include "gemm.h"
 
 namespace mt {
 
 // ---------------------------------------------------------------------------------------------
-// Architectures (compile-time geometry). C = 4*depth input channels.
+// Architectures (compile-time geometry). C = 4*depth input channels. Layers = tuple of conv
+// geometries; POOL bitmask = layers followed by a 2x2/2 VALID max pool (networks.py:108-110).
 // ---------------------------------------------------------------------------------------------
 template <int C>
 struct NipsArch {  // networks.py:178-192
-  using G1 = ConvGeom<C, 16, 8, 4, 84, 84, false>;
-  using G2 = ConvGeom<16, 32, 4, 2, 20, 20, false>;
-  using G3 = G2;  // unused
+  using Layers = std::tuple<ConvGeom<C, 16, 8, 4, 84, 84, false>, ConvGeom<16, 32, 4, 2, 20, 20, false>>;
   static constexpr int NCONV = 2;
-  static constexpr int FLAT = G2::OH * G2::OW * G2::COUT;  // 2592
+  static constexpr unsigned POOL = 0;
+  static constexpr int FLAT = 9 * 9 * 32;  // 2592
   static constexpr int F = 256;
   static constexpr const char *FC = "fc3";
 };
 template <int C>
 struct NatureArch {  // networks.py:261-278
-  using G1 = ConvGeom<C, 32, 8, 4, 84, 84, false>;
-  using G2 = ConvGeom<32, 64, 4, 2, 20, 20, false>;
-  using G3 = ConvGeom<64, 64, 3, 1, 9, 9, false>;
+  using Layers = std::tuple<ConvGeom<C, 32, 8, 4, 84, 84, false>, ConvGeom<32, 64, 4, 2, 20, 20, false>,
+                            ConvGeom<64, 64, 3, 1, 9, 9, false>>;
   static constexpr int NCONV = 3;
-  static constexpr int FLAT = G3::OH * G3::OW * G3::COUT;  // 3136
+  static constexpr unsigned POOL = 0;
+  static constexpr int FLAT = 7 * 7 * 64;  // 3136
   static constexpr int F = 512;
   static constexpr const char *FC = "fc4";
 };
+template <int C>
+struct PwyxArch {  // networks.py:206-225: SAME convs, 2x2 pools after conv1-3
+  using Layers = std::tuple<ConvGeom<C, 32, 5, 1, 84, 84, true>, ConvGeom<32, 32, 5, 1, 42, 42, true>,
+                            ConvGeom<32, 64, 4, 1, 21, 21, true>, ConvGeom<64, 64, 3, 1, 10, 10, true>>;
+  static constexpr int NCONV = 4;
+  static constexpr unsigned POOL = 0x7;
+  static constexpr int FLAT = 10 * 10 * 64;  // 6400
+  static constexpr int F = 512;
+  static constexpr const char *FC = "fc5";
+};
+
+template <class Ar, int I>
+using LayerG = std::tuple_element_t<I, typename Ar::Layers>;
+template <class Ar, int I>
+constexpr bool pooled() {
+  return (Ar::POOL >> I) & 1u;
+}
+// spatial size of layer I's output after its (optional) pool
+template <class Ar, int I>
+constexpr int out_hw() {
+  using G = LayerG<Ar, I>;
+  return pooled<Ar, I>() ? G::OH / 2 : G::OH;
+}
 
 }  // namespace mt
 
@@ -56,7 +80,7 @@ struct mt_net {
   int flat;
   std::vector<VarInfo> vars;
   size_t nparams;
-  size_t off_conv[3];  // weights offset of each conv (biases follow)
+  size_t off_conv[4];  // weights offset of each conv (biases follow)
   size_t off_fc, off_critic, off_actor, off_rep;
 };
 
@@ -100,12 +124,20 @@ static void add_conv(mt_net *n, size_t &off, int idx) {
            &n->off_conv[idx]);
 }
 
+template <class Ar, int I = 0>
+static void add_convs(mt_net *n, size_t &off) {
+  if constexpr (I < Ar::NCONV) {
+    add_conv<LayerG<Ar, I>>(n, off, I);
+    add_convs<Ar, I + 1>(n, off);
+  }
+}
+
 template <class Ar>
 static void build_layout(mt_net *n) {
+  static_assert(out_hw<Ar, Ar::NCONV - 1>() * out_hw<Ar, Ar::NCONV - 1>() *
+                    LayerG<Ar, Ar::NCONV - 1>::COUT == Ar::FLAT, "flatten width");
   size_t off = 0;
-  add_conv<typename Ar::G1>(n, off, 0);
-  add_conv<typename Ar::G2>(n, off, 1);
-  if constexpr (Ar::NCONV == 3) add_conv<typename Ar::G3>(n, off, 2);
+  add_convs<Ar>(n, off);
   const float bf = (float)(1.0 / std::sqrt((double)Ar::FLAT));  // networks.py:72-89
   add_pair(n, off, "Network", Ar::FC, {Ar::FLAT, Ar::F}, Ar::F, bf, bf, &n->off_fc);
   const float bh = (float)(1.0 / std::sqrt((double)Ar::F));
@@ -124,11 +156,12 @@ static void build_layout(mt_net *n) {
 // Workspace layout (floats), a pure function of (net, batch).
 // ---------------------------------------------------------------------------------------------
 struct WsLayout {
-  size_t act[3], dact[3], fcslab, H, dz, dH, wslab, total;
+  // per conv layer: act = post-activation conv output, pool = pooled output (if pooled),
+  // dact = its gradient (pre-activation after masking), dpool = gradient w.r.t. the pooled output
+  size_t act[4], pool[4], dact[4], dpool[4], fcslab, H, dz, dH, wslab, total;
   int fc_splits;
 };
 
-// Tile by output width N (16 / 32 / >= 64 columns) and K-chunk depth BK.
 template <int N, int BK>
 struct TileFor {
   using T = Tile<64, 64, 2, 2, BK>;
@@ -189,6 +222,26 @@ static int fc_splits(int B, int F) {
   return gemm_splits<TileFc>(Ar::FLAT, s);
 }
 
+template <class Ar, int I = 0>
+static void ws_layers(WsLayout &L, size_t &off, int B, size_t &wslab) {
+  if constexpr (I < Ar::NCONV) {
+    using G = LayerG<Ar, I>;
+    auto take = [&](size_t nf) {
+      size_t o = off;
+      off = align64(off + nf);
+      return o;
+    };
+    const size_t a = (size_t)B * G::OH * G::OW * G::COUT;
+    const size_t p = pooled<Ar, I>() ? (size_t)B * (G::OH / 2) * (G::OW / 2) * G::COUT : 0;
+    L.act[I] = take(a);
+    L.dact[I] = take(a);
+    L.pool[I] = take(p);
+    L.dpool[I] = take(p);
+    wslab = std::max(wslab, conv_wgrad_slab<G>(B));
+    ws_layers<Ar, I + 1>(L, off, B, wslab);
+  }
+}
+
 template <class Ar>
 static WsLayout ws_layout(const mt_net *n, int B) {
   WsLayout L{};
@@ -198,27 +251,14 @@ static WsLayout ws_layout(const mt_net *n, int B) {
     off = align64(off + nf);
     return o;
   };
-  using G1 = typename Ar::G1;
-  using G2 = typename Ar::G2;
-  using G3 = typename Ar::G3;
-  const size_t a1 = (size_t)B * G1::OH * G1::OW * G1::COUT;
-  const size_t a2 = (size_t)B * G2::OH * G2::OW * G2::COUT;
-  const size_t a3 = Ar::NCONV == 3 ? (size_t)B * G3::OH * G3::OW * G3::COUT : 0;
-  L.act[0] = take(a1);
-  L.act[1] = take(a2);
-  L.act[2] = take(a3);
-  L.dact[0] = take(a1);
-  L.dact[1] = take(a2);
-  L.dact[2] = take(a3);
+  size_t wslab = 0;
+  ws_layers<Ar>(L, off, B, wslab);
   L.fc_splits = fc_splits<Ar>(B, Ar::F);
   L.fcslab = take((size_t)L.fc_splits * B * Ar::F);
   L.H = take((size_t)B * Ar::F);
   L.dz = take((size_t)B * n->O);
   L.dH = take((size_t)B * Ar::F);
-  size_t ws = conv_wgrad_slab<G1>(B);
-  ws = std::max(ws, conv_wgrad_slab<G2>(B));
-  if constexpr (Ar::NCONV == 3) ws = std::max(ws, conv_wgrad_slab<G3>(B));
-  L.wslab = take(ws);
+  L.wslab = take(wslab);
   L.total = off;
   return L;
 }
@@ -511,34 +551,139 @@ static int conv_dgrad(const float *dY, const float *Wt, const float *Xact, float
     if (rc_ != MT_OK) return rc_; \
   } while (0)
 
+// 2x2/2 VALID max pool over NHWC (networks.py:108-110): one thread per output float4 of channels.
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float *__restrict__ X, int B, int H, int W,
+                                                          int C, float *__restrict__ Y) {
+  const int OH = H / 2, OW = W / 2, C4 = C / 4;
+  const size_t total = (size_t)B * OH * OW * C4;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    size_t r = i / C4;
+    const int ox = (int)(r % OW);
+    r /= OW;
+    const int oy = (int)(r % OH);
+    const int b = (int)(r / OH);
+    const f32x4 *x = reinterpret_cast<const f32x4 *>(X) + (((size_t)b * H + 2 * oy) * W + 2 * ox) * C4 + c4;
+    const f32x4 a = x[0], bq = x[C4], c = x[(size_t)W * C4], d = x[(size_t)W * C4 + C4];
+    f32x4 m;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = fmaxf(fmaxf(a[e], bq[e]), fmaxf(c[e], d[e]));
+    reinterpret_cast<f32x4 *>(Y)[i] = m;
+  }
+}
+
+// MaxPoolGrad: the pooled gradient goes to the first maximum of the window in (row, col) order;
+// every other input position (and the dropped odd row/col) gets 0. dP is already masked by the
+// activation derivative (act'(P) == act'(X[argmax])).
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float *__restrict__ X,
+                                                          const float *__restrict__ P,
+                                                          const float *__restrict__ dP, int B, int H,
+                                                          int W, int C, float *__restrict__ dX) {
+  const int OH = H / 2, OW = W / 2, C4 = C / 4;
+  const size_t total = (size_t)B * H * W * C4;  // one thread per input float4
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    size_t r = i / C4;
+    const int x = (int)(r % W);
+    r /= W;
+    const int y = (int)(r % H);
+    const int b = (int)(r / H);
+    const int oy = y / 2, ox = x / 2;
+    f32x4 g = {0.f, 0.f, 0.f, 0.f};
+    if (oy < OH && ox < OW) {
+      const size_t pi = (((size_t)b * OH + oy) * OW + ox) * C4 + c4;
+      const f32x4 p = reinterpret_cast<const f32x4 *>(P)[pi];
+      const f32x4 dp = reinterpret_cast<const f32x4 *>(dP)[pi];
+      const f32x4 *xw = reinterpret_cast<const f32x4 *>(X) + (((size_t)b * H + 2 * oy) * W + 2 * ox) * C4 + c4;
+      const f32x4 w0 = xw[0], w1 = xw[C4], w2 = xw[(size_t)W * C4], w3 = xw[(size_t)W * C4 + C4];
+      const int pos = (y - 2 * oy) * 2 + (x - 2 * ox);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int first = w0[e] == p[e] ? 0 : (w1[e] == p[e] ? 1 : (w2[e] == p[e] ? 2 : 3));
+        g[e] = first == pos ? dp[e] : 0.f;
+      }
+    }
+    reinterpret_cast<f32x4 *>(dX)[i] = g;
+  }
+}
+
+static int maxpool_fwd(const float *X, int B, int H, int W, int C, float *Y, hipStream_t s) {
+  const size_t total = (size_t)B * (H / 2) * (W / 2) * (C / 4);
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks), dim3(256), 0, s, X, B, H, W, C, Y);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+static int maxpool_bwd(const float *X, const float *P, const float *dP, int B, int H, int W, int C,
+                       float *dX, hipStream_t s) {
+  const size_t total = (size_t)B * H * W * (C / 4);
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks), dim3(256), 0, s, X, P, dP, B, H, W, C, dX);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+template <class Ar, int I>
+static const float *layer_out(float *ws, const WsLayout &L) {
+  return ws + (pooled<Ar, I>() ? L.pool[I] : L.act[I]);
+}
+
+template <class Ar, int I = 0>
+static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, float *ws,
+                         const WsLayout &L, hipStream_t s) {
+  if constexpr (I < Ar::NCONV) {
+    using G = LayerG<Ar, I>;
+    const float *W = P + n->off_conv[I];
+    MT_TRY((conv_forward<G, I == 0>(x, W, W + G::KK * G::COUT, ws + L.act[I], B, n->cfg.activation,
+                                    n->cfg.alpha_leaky, s)));
+    if constexpr (pooled<Ar, I>())
+      MT_TRY(maxpool_fwd(ws + L.act[I], B, G::OH, G::OW, G::COUT, ws + L.pool[I], s));
+    return trunk_forward<Ar, I + 1>(n, P, layer_out<Ar, I>(ws, L), B, ws, L, s);
+  }
+  return MT_OK;
+}
+
+// Backward through conv layer I given the gradient w.r.t. its post-activation output, already
+// masked (ws + L.dact[I]): weight gradient, then (I > 0) the masked gradient of its input,
+// routed through the previous layer's pool when there is one.
+template <class Ar, int I>
+static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
+                          const WsLayout &L, float *grad, hipStream_t s) {
+  using G = LayerG<Ar, I>;
+  const int act = n->cfg.activation;
+  const float al = n->cfg.alpha_leaky;
+  const void *x = I == 0 ? (const void *)obs : (const void *)layer_out<Ar, (I > 0 ? I - 1 : 0)>(ws, L);
+  MT_TRY((conv_wgrad<G, I == 0>(x, ws + L.dact[I], ws + L.wslab, grad + n->off_conv[I], B, s)));
+  if constexpr (I > 0) {
+    constexpr int J = I - 1;
+    using GJ = LayerG<Ar, J>;
+    if constexpr (pooled<Ar, J>()) {
+      MT_TRY((conv_dgrad<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J], ws + L.dpool[J], B, act, al, s)));
+      MT_TRY(maxpool_bwd(ws + L.act[J], ws + L.pool[J], ws + L.dpool[J], B, GJ::OH, GJ::OW, GJ::COUT,
+                         ws + L.dact[J], s));
+    } else {
+      MT_TRY((conv_dgrad<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B, act, al, s)));
+    }
+    return trunk_backward<Ar, J>(n, P, obs, B, ws, L, grad, s);
+  }
+  return MT_OK;
+}
+
 template <class Ar>
 static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
                         float *v, float *pi, float *rep, hipStream_t s) {
   const WsLayout L = ws_layout<Ar>(n, B);
-  const int act = n->cfg.activation;
-  const float al = n->cfg.alpha_leaky;
-  using G1 = typename Ar::G1;
-  using G2 = typename Ar::G2;
-  using G3 = typename Ar::G3;
-  float *a1 = ws + L.act[0], *a2 = ws + L.act[1], *a3 = ws + L.act[2];
-  MT_TRY((conv_forward<G1, true>(obs, P + n->off_conv[0], P + n->off_conv[0] + G1::KK * G1::COUT,
-                                 a1, B, act, al, s)));
-  MT_TRY((conv_forward<G2, false>(a1, P + n->off_conv[1], P + n->off_conv[1] + G2::KK * G2::COUT,
-                                  a2, B, act, al, s)));
-  const float *flat = a2;
-  if constexpr (Ar::NCONV == 3) {
-    MT_TRY((conv_forward<G3, false>(a2, P + n->off_conv[2], P + n->off_conv[2] + G3::KK * G3::COUT,
-                                    a3, B, act, al, s)));
-    flat = a3;
-  }
+  MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s)));
+  const float *flat = layer_out<Ar, Ar::NCONV - 1>(ws, L);
   // dense layer (networks.py:57-70), split-K partial slabs; heads kernel finishes bias + act.
   const float *Wfc = P + n->off_fc;
   MT_TRY((launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1},
                               EpSlab{ws + L.fcslab, B, Ar::F}, B, Ar::F, Ar::FLAT, L.fc_splits, s)));
   HeadParams hp = head_params(n, P);
   hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, L.fc_splits, B,
-                     Wfc + (size_t)Ar::FLAT * Ar::F, act, al, hp, n->cfg.softmax_temp, ws + L.H, v,
-                     pi, rep);
+                     Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp,
+                     n->cfg.softmax_temp, ws + L.H, v, pi, rep);
   MT_LAUNCHED();
   return MT_OK;
 }
@@ -551,11 +696,6 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
   const WsLayout L = ws_layout<Ar>(n, B);
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
-  using G1 = typename Ar::G1;
-  using G2 = typename Ar::G2;
-  using G3 = typename Ar::G3;
-  float *a1 = ws + L.act[0], *a2 = ws + L.act[1], *a3 = ws + L.act[2];
-  float *d1 = ws + L.dact[0], *d2 = ws + L.dact[1], *d3 = ws + L.dact[2];
   MT_HIP(hipMemsetAsync(grad, 0, n->nparams * sizeof(float), s));
 
   // loss scaling 5.0 and the batch mean (policy_v_network.py:70-74): scale = 5/B.
@@ -577,29 +717,29 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
       return MT_ERR_ARG;
     }
     hipLaunchKernelGGL(head_wgrad_kernel, dim3(cdiv(Ar::F + 1, 64)), dim3(256),
-                       sizeof(float) * (size_t)B * n->O, s, ws + L.H,
-                       ws + L.dz, B, Ar::F, n->cfg.num_actions, n->cfg.num_reps,
-                       grad + n->off_critic, grad + n->off_actor, grad + n->off_rep);
+                       sizeof(float) * (size_t)B * n->O, s, ws + L.H, ws + L.dz, B, Ar::F,
+                       n->cfg.num_actions, n->cfg.num_reps, grad + n->off_critic, grad + n->off_actor,
+                       grad + n->off_rep);
     MT_LAUNCHED();
   }
-  const float *flat = Ar::NCONV == 3 ? a3 : a2;
-  float *dflat = Ar::NCONV == 3 ? d3 : d2;
+  constexpr int K = Ar::NCONV - 1;
+  const float *flat = layer_out<Ar, K>(ws, L);
   const float *Wfc = P + n->off_fc;
   // dense dW, db: [flat, 1]^T . dH -> grad[(FLAT+1) x F]
   MT_TRY((launch_gemm<TileDenseW>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
-                                 EpStore{grad + n->off_fc, Ar::F}, Ar::FLAT + 1, Ar::F, B, 1, s)));
-  // dense dX: dH . W^T, masked by the last conv's activation
-  MT_TRY((launch_gemm<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
-                                 EpMasked{dflat, flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1, s)));
-  float *slab = ws + L.wslab;
-  if constexpr (Ar::NCONV == 3) {
-    MT_TRY((conv_wgrad<G3, false>(a2, d3, slab, grad + n->off_conv[2], B, s)));
-    MT_TRY((conv_dgrad<G3>(d3, P + n->off_conv[2], a2, d2, B, act, al, s)));
+                                  EpStore{grad + n->off_fc, Ar::F}, Ar::FLAT + 1, Ar::F, B, 1, s)));
+  // dense dX: dH . W^T, masked by the last conv's (pooled) activation, then through its pool
+  if constexpr (pooled<Ar, K>()) {
+    using GK = LayerG<Ar, K>;
+    MT_TRY((launch_gemm<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+                                    EpMasked{ws + L.dpool[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1, s)));
+    MT_TRY(maxpool_bwd(ws + L.act[K], ws + L.pool[K], ws + L.dpool[K], B, GK::OH, GK::OW, GK::COUT,
+                       ws + L.dact[K], s));
+  } else {
+    MT_TRY((launch_gemm<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+                                    EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1, s)));
   }
-  MT_TRY((conv_wgrad<G2, false>(a1, d2, slab, grad + n->off_conv[1], B, s)));
-  MT_TRY((conv_dgrad<G2>(d2, P + n->off_conv[1], a1, d1, B, act, al, s)));
-  MT_TRY((conv_wgrad<G1, true>(obs, d1, slab, grad + n->off_conv[0], B, s)));
-  return MT_OK;
+  return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s);
 }
 
 }  // namespace mt
@@ -616,6 +756,8 @@ using namespace mt;
     else if (arch_ == MT_ARCH_NIPS && d_ == 3) { using Ar = NipsArch<12>; __VA_ARGS__; }   \
     else if (arch_ == MT_ARCH_NATURE && d_ == 1) { using Ar = NatureArch<4>; __VA_ARGS__; } \
     else if (arch_ == MT_ARCH_NATURE && d_ == 3) { using Ar = NatureArch<12>; __VA_ARGS__; } \
+    else if (arch_ == MT_ARCH_PWYX && d_ == 1) { using Ar = PwyxArch<4>; __VA_ARGS__; }     \
+    else if (arch_ == MT_ARCH_PWYX && d_ == 3) { using Ar = PwyxArch<12>; __VA_ARGS__; }    \
     else { set_error("arch %d depth %d not built", arch_, d_); return MT_ERR_UNSUPPORTED; } \
   } while (0)
 
@@ -635,6 +777,8 @@ extern "C" int mt_net_create(const mt_net_config *cfg, mt_net **out) {
   else if (arch == MT_ARCH_NIPS && d == 3) build_layout<NipsArch<12>>(n);
   else if (arch == MT_ARCH_NATURE && d == 1) build_layout<NatureArch<4>>(n);
   else if (arch == MT_ARCH_NATURE && d == 3) build_layout<NatureArch<12>>(n);
+  else if (arch == MT_ARCH_PWYX && d == 1) build_layout<PwyxArch<4>>(n);
+  else if (arch == MT_ARCH_PWYX && d == 3) build_layout<PwyxArch<12>>(n);
   else {
     delete n;
     set_error("arch %d not built into this library", arch);

@@ -1,8 +1,14 @@
 // Native rollout macro-step: the per-step orchestration of paac.py:140-205 without Python.
 // See include/manette_hip.h (mt_rollout_*). Host code + HIP runtime calls; the emulator threads
 // and the bookkeeping live in libmanette_host.so (include/manette_host.h).
+#include <chrono>
+
 #include "common.h"
 #include "../../include/manette_host.h"
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 struct mt_rollout {
   const mt_net *net;
@@ -13,6 +19,7 @@ struct mt_rollout {
   mt_rollout_buffers b;
   uint64_t seed;
   hipEvent_t ev;
+  double acc[5];  // host wall us: launch+wait for indices, runner, book, upload+preprocess enqueue; steps
 };
 
 using namespace mt;
@@ -76,6 +83,7 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   const mt_rollout_buffers &b = ro->b;
   hipStream_t s = (hipStream_t)stream;
   const int E = ro->E, T = ro->T;
+  const double t0 = now_us();
   const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
   uint8_t *cur = b.states + (size_t)t * slot;
   uint8_t *nxt = cur + slot;
@@ -88,6 +96,7 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   MT_HIP(hipMemcpyAsync(r_h, r_d, sizeof(int32_t) * E, hipMemcpyDeviceToHost, s));
   MT_HIP(hipEventRecord(ro->ev, s));
   MT_HIP(hipEventSynchronize(ro->ev));
+  const double t1 = now_us();
   // 2. emulators (runners.py:44-50 / emulator_runner.py:24-41) + bookkeeping (paac.py:176-205)
   int total = 0;
   if (mh_runner_step(ro->runner, a_h, r_h, b.staging_host, b.meta_host, b.meta_host + E,
@@ -95,14 +104,31 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
     set_error("mh_runner_step: %s", mh_last_error());
     return MT_ERR_ARG;
   }
+  const double t2 = now_us();
   if (mh_book_step(ro->book, global_step, a_h, r_h, b.reward_host, b.over_host,
                    b.rm_host + (size_t)t * E, b.rm_host + (size_t)T * E + (size_t)t * E) != 0) {
     set_error("mh_book_step: %s", mh_last_error());
     return MT_ERR_ARG;
   }
+  const double t3 = now_us();
   // 3. screens -> HBM, preprocess into slot t+1 (atari_emulator.py:79-124)
   MT_HIP(hipMemcpyAsync(b.raw, b.staging_host, (size_t)total * 2 * ro->frame_bytes,
                         hipMemcpyHostToDevice, s));
   MT_HIP(hipMemcpyAsync(b.meta, b.meta_host, sizeof(int32_t) * 2 * E, hipMemcpyHostToDevice, s));
-  return mt_preprocess(b.raw, b.meta, b.meta + E, E, ro->depth, b.row_lut, b.col_lut, cur, nxt, stream);
+  const int rc = mt_preprocess(b.raw, b.meta, b.meta + E, E, ro->depth, b.row_lut, b.col_lut, cur, nxt, stream);
+  const double t4 = now_us();
+  ro->acc[0] += t1 - t0;
+  ro->acc[1] += t2 - t1;
+  ro->acc[2] += t3 - t2;
+  ro->acc[3] += t4 - t3;
+  ro->acc[4] += 1;
+  return rc;
+}
+
+extern "C" int mt_rollout_stats(mt_rollout *ro, double *out5, int reset) {
+  MT_CHECK_ARG(ro && out5, "null argument");
+  for (int i = 0; i < 5; ++i) out5[i] = ro->acc[i];
+  if (reset)
+    for (int i = 0; i < 5; ++i) ro->acc[i] = 0;
+  return MT_OK;
 }

@@ -162,7 +162,6 @@ class PAACLearner(ActorLearner):
             _lib.check(_lib.hip().mt_rollout_step(self.native_step, devnet._ptr(net.params), t,
                                                   self._lib_ref(self._gs), devnet._stream()), 'mt_rollout_step')
             self.global_step = self._gs.value
-            self.book.drain()
             return
         end = self._mark('rollout_forward')
         v, pi, rep = net.forward(self.states[t], E, out=(self.values[t], self.pi_roll, self.rep_roll),
@@ -171,7 +170,8 @@ class PAACLearner(ActorLearner):
             end.record()
         if self.sampling == 'device':
             devnet.sample(pi, rep, self.sample_seed, self.counters, self.a_idx[t], self.r_idx[t])
-            self.idx_h[t].copy_(self.idx[t], non_blocking=True)
+            self.a_h[t].copy_(self.a_idx[t], non_blocking=True)
+            self.r_h[t].copy_(self.r_idx[t], non_blocking=True)
             self.event.record()
             self.event.synchronize()
             a = self.a_h[t].numpy()
@@ -184,7 +184,8 @@ class PAACLearner(ActorLearner):
             a, r = self.explo_policy.choose_indices(self.pi_h.numpy(), self.rep_h.numpy())
             self.a_h[t].numpy()[...] = a
             self.r_h[t].numpy()[...] = r
-            self.idx[t].copy_(self.idx_h[t], non_blocking=True)
+            self.a_idx[t].copy_(self.a_h[t], non_blocking=True)
+            self.r_idx[t].copy_(self.r_h[t], non_blocking=True)
         if self.runner_kind == 'native':
             total = self.runners.step(self.a_h[t], self.r_h[t])
             reward = self.runners.reward.numpy()
@@ -206,6 +207,7 @@ class PAACLearner(ActorLearner):
         """Bootstrap, n-step returns, fused loss backward, [all-reduce], clip + RMSProp
         (paac.py:219-256)."""
         net = self.network
+        self.book.drain()
         E, T = self.emulator_counts, self.max_local_steps
         N = E * T
         net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout')

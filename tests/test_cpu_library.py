@@ -34,7 +34,7 @@ def test_libraries_export_every_symbol():
 
 
 @pytest.mark.parametrize('arch,depth,A,R', [('NIPS', 1, 6, 1), ('NIPS', 3, 3, 11), ('NATURE', 1, 4, 11),
-                                            ('NATURE', 3, 18, 1)])
+                                            ('NATURE', 3, 18, 1), ('PWYX', 1, 9, 11), ('PWYX', 3, 4, 11)])
 def test_layout_matches_oracle(arch, depth, A, R):
     import ctypes as C
     from manette_amd import _lib

@@ -12,7 +12,8 @@ from oracle import nets, optim, preprocess, returns
 
 pytestmark = pytest.mark.gpu
 
-CONFIGS = [('NIPS', 1, 6, 1), ('NIPS', 3, 4, 11), ('NATURE', 1, 4, 11), ('NATURE', 3, 18, 1)]
+CONFIGS = [('NIPS', 1, 6, 1), ('NIPS', 3, 4, 11), ('NATURE', 1, 4, 11), ('NATURE', 3, 18, 1),
+           ('PWYX', 1, 4, 11), ('PWYX', 3, 6, 1)]
 
 
 def _net(arch, depth, A, R, seed=0, act='relu'):
