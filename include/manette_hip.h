@@ -94,9 +94,10 @@ int mt_forward(const mt_net *net, const float *params, const uint8_t *obs, int b
  * distribution numpy's multinomial(1, p - epsneg) draws from. Uniforms come from a
  * counter-based hash of (seed, row, counters[row]); counters (device, one uint64 per row) are
  * incremented by the call, so a captured graph draws fresh numbers on every replay.
- * Writes int32 indices a_idx [batch], r_idx [batch]. */
+ * Writes int32 indices a_idx [batch], r_idx [batch], and (if pair != NULL) both again into
+ * pair [2][batch] so one copy moves them to the host. */
 int mt_sample(const float *pi, const float *rep, int batch, int num_actions, int num_reps,
-              uint64_t seed, uint64_t *counters, int32_t *a_idx, int32_t *r_idx,
+              uint64_t seed, uint64_t *counters, int32_t *a_idx, int32_t *r_idx, int32_t *pair,
               mt_stream_t stream);
 
 /* ---- n-step return / advantage scan (A9) ---------------------------------------------------
@@ -140,11 +141,13 @@ int mt_clip_rmsprop(float *w, float *ms, float *mom, const float *g, size_t n,
  * emulator.next() (atari_emulator.py:90-100): pooled = max(f0, f1) (np.amax), resized to 84x84
  * with the nearest LUT (row_lut[84], col_lut[84] = source row/col), appended to the 4-deep
  * observation stack. Per env e: push_offset[e], push_count[e] (1..4) index the pushes (oldest
- * first) in `raw` = [total_pushes][2][210][160][depth] uint8. prev/out: [E][84][84][4*depth];
+ * first) in `raw` = [total_pushes][2][src_rows][160][depth] uint8: whole screens (src_rows 210,
+ * row_lut = the resize LUT) or the 84 rows the resize reads, staged by the runner (src_rows 84,
+ * row_lut = identity). prev/out: [E][84][84][4*depth];
  * out[c] = prev[c+p] for c < 4-p, else the (c-(4-p))-th new push; RGB interleaves channels as
  * [R_t0..R_t3, G_t0..G_t3, B_t0..B_t3] (environment.py:75). out may not alias prev. */
 int mt_preprocess(const uint8_t *raw, const int32_t *push_offset, const int32_t *push_count,
-                  int E, int depth, const int32_t *row_lut, const int32_t *col_lut,
+                  int E, int depth, int src_rows, const int32_t *row_lut, const int32_t *col_lut,
                   const uint8_t *prev, uint8_t *out, mt_stream_t stream);
 
 /* ---- native rollout macro-step (orchestrates A1-A3, A8; paac.py:140-205) -------------------
@@ -163,12 +166,15 @@ typedef struct mt_rollout_buffers {
   void *ws;                    /* forward workspace for E rows */
   size_t ws_bytes;
   uint64_t *counters;          /* [E] sampling counters */
-  uint8_t *raw;                /* [4E][2][210*160*depth] screen staging */
+  uint8_t *raw;                /* [4E][2][src_rows*160*depth] screen staging */
+  int32_t src_rows;            /* staged screen rows: 210, or 84 when the runner selects rows */
+  int32_t *pair;               /* [2][E] device scratch: this step's indices for one D2H copy */
+  int32_t *pair_host;          /* [2][E] pinned */
   int32_t *meta;               /* [2][E] push offsets; push counts */
   const int32_t *row_lut, *col_lut;
   /* pinned host */
   int32_t *idx_host;           /* [2][T][E] */
-  uint8_t *staging_host;       /* [4E][2][210*160*depth] */
+  uint8_t *staging_host;       /* [4E][2][src_rows*160*depth] */
   int32_t *meta_host;          /* [2][E] */
   float *reward_host, *over_host; /* [E] */
   float *rm_host;              /* [2][T][E]: clipped rewards; masks */

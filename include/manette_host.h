@@ -27,11 +27,15 @@ typedef struct mh_runner mh_runner;
 
 const char *mh_last_error(void);
 
-/* screens: [n_envs][ring][frame_bytes] uint8, rewards: [n_envs][reward_len] float32 (caller
- * keeps both alive). tab_rep: FiGAR repetition table (exploration_policy.py:56-62). */
+/* screens: [n_envs][ring][frame_bytes] uint8 (frame_bytes = 210 rows x row_bytes), rewards:
+ * [n_envs][reward_len] float32 (caller keeps both alive). tab_rep: FiGAR repetition table
+ * (exploration_policy.py:56-62). row_select [n_rows] (or NULL / 0 for whole screens): stage only
+ * these screen rows — the rows the 84x84 nearest resize reads (atari_emulator.py:85) — so a
+ * push is n_rows*row_bytes per screen on PCIe instead of 210 rows. */
 int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_rep, int n_reps,
                      const uint8_t *screens, int ring, size_t frame_bytes, const float *rewards,
-                     int reward_len, int episode_len, mh_runner **out);
+                     int reward_len, int episode_len, const int32_t *row_select, int n_rows,
+                     mh_runner **out);
 void mh_runner_destroy(mh_runner *r);
 
 /* get_initial_state() of every env: 4 pushes each. Outputs as mh_runner_step. */
@@ -40,7 +44,7 @@ int mh_runner_reset(mh_runner *r, uint8_t *staging, int32_t *push_offset, int32_
 
 /* One macro-step (emulator_runner.py:24-41) of every env with action a_idx[e] repeated
  * tab_rep[r_idx[e]] more times unless the episode ends. Outputs:
- *   staging      [total_pushes][2][frame_bytes]: screens of the last <=4 pushes of each env,
+ *   staging      [total_pushes][2][staged frame]: screens of the last <=4 pushes of each env,
  *                env-major, oldest first (a terminal's reset pushes included);
  *   push_offset  [E] first staging slot of env e; push_count [E] in 1..4;
  *   reward       [E] float32 sum over the repeats (shared float32 array semantics);

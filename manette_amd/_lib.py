@@ -23,7 +23,8 @@ class MTError(RuntimeError):
 class mt_rollout_buffers(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ('states', 'values', 'idx', 'pi', 'rep', 'ws')] + \
                [('ws_bytes', C.c_size_t)] + \
-               [(n, C.c_void_p) for n in ('counters', 'raw', 'meta', 'row_lut', 'col_lut', 'idx_host',
+               [(n, C.c_void_p) for n in ('counters', 'raw')] + [('src_rows', C.c_int32)] + \
+               [(n, C.c_void_p) for n in ('pair', 'pair_host', 'meta', 'row_lut', 'col_lut', 'idx_host',
                                           'staging_host', 'meta_host', 'reward_host', 'over_host',
                                           'rm_host')]
 
@@ -51,12 +52,12 @@ _HIP_SIGS = {
     'mt_net_feature_dim': (_I, [_P, C.POINTER(_I)]),
     'mt_net_workspace_bytes': (_I, [_P, _I, C.POINTER(_SZ)]),
     'mt_forward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P]),
-    'mt_sample': (_I, [_P, _P, _I, _I, _I, C.c_uint64, _P, _P, _P, _P]),
+    'mt_sample': (_I, [_P, _P, _I, _I, _I, C.c_uint64, _P, _P, _P, _P, _P]),
     'mt_returns': (_I, [_P, _P, _P, _P, C.c_double, _I, _I, _P, _P, _P]),
     'mt_loss_backward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
     'mt_grad_sumsq': (_I, [_P, _SZ, _F, _P, _P]),
     'mt_clip_rmsprop': (_I, [_P, _P, _P, _P, _SZ, _P, _P, _F, _F, _F, _F, _I, _F, _P, _P]),
-    'mt_preprocess': (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    'mt_preprocess': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
     'mt_sum_slabs': (_I, [_P, _I, _SZ, _P, _P]),
     'mt_net_get_config': (_I, [_P, C.POINTER(mt_net_config)]),
     'mt_rollout_create': (_I, [_P, _I, _I, _P, _P, C.POINTER(mt_rollout_buffers), C.c_uint64, C.POINTER(_P)]),
@@ -71,7 +72,7 @@ _HIP_SIGS = {
 
 _HOST_SIGS = {
     'mh_last_error': (C.c_char_p, []),
-    'mh_runner_create': (_I, [_I, _I, _P, _I, _P, _I, _SZ, _P, _I, _I, C.POINTER(_P)]),
+    'mh_runner_create': (_I, [_I, _I, _P, _I, _P, _I, _SZ, _P, _I, _I, _P, _I, C.POINTER(_P)]),
     'mh_runner_destroy': (None, [_P]),
     'mh_runner_reset': (_I, [_P, _P, _P, _P, C.POINTER(_I)]),
     'mh_runner_step': (_I, [_P, _P, _P, _P, _P, _P, _P, _P, C.POINTER(_I)]),

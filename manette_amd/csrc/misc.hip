@@ -122,9 +122,10 @@ __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
 template <int DEPTH>
 __global__ __launch_bounds__(256) void preprocess_kernel(
     const uint8_t *__restrict__ raw, const int32_t *__restrict__ push_offset,
-    const int32_t *__restrict__ push_count, int E, const int32_t *__restrict__ row_lut,
+    const int32_t *__restrict__ push_count, int E, int SH, const int32_t *__restrict__ row_lut,
     const int32_t *__restrict__ col_lut, const uint8_t *__restrict__ prev, uint8_t *__restrict__ out) {
-  constexpr int SH = 210, SW = 160, FR = SH * SW * DEPTH;  // one ALE screen
+  constexpr int SW = 160;
+  const int FR = SH * SW * DEPTH;  // one staged ALE screen
   constexpr int C = 4 * DEPTH;
   __shared__ int rl[84], cl[84];
   if (threadIdx.x < 84) {
@@ -181,7 +182,8 @@ __device__ __forceinline__ int draw_index(const float *p, int n, double u) {
 
 __global__ void sample_kernel(const float *__restrict__ pi, const float *__restrict__ rep, int B,
                               int A, int R, uint64_t seed, uint64_t *__restrict__ counters,
-                              int32_t *__restrict__ a_idx, int32_t *__restrict__ r_idx) {
+                              int32_t *__restrict__ a_idx, int32_t *__restrict__ r_idx,
+                              int32_t *__restrict__ pair) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const uint64_t c = counters[b];
@@ -190,8 +192,14 @@ __global__ void sample_kernel(const float *__restrict__ pi, const float *__restr
   const uint64_t h2 = mix64(h ^ 0x9e3779b97f4a7c15ULL);
   const double ua = (double)(h >> 11) * (1.0 / 9007199254740992.0);
   const double ur = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
-  a_idx[b] = draw_index(pi + (size_t)b * A, A, ua);
-  r_idx[b] = draw_index(rep + (size_t)b * R, R, ur);
+  const int a = draw_index(pi + (size_t)b * A, A, ua);
+  const int r = draw_index(rep + (size_t)b * R, R, ur);
+  a_idx[b] = a;
+  r_idx[b] = r;
+  if (pair) {
+    pair[b] = a;
+    pair[B + b] = r;
+  }
 }
 
 }  // namespace mt
@@ -241,22 +249,23 @@ extern "C" int mt_clip_rmsprop(float *w, float *ms, float *mom, const float *g, 
 }
 
 extern "C" int mt_preprocess(const uint8_t *raw, const int32_t *push_offset,
-                             const int32_t *push_count, int E, int depth, const int32_t *row_lut,
-                             const int32_t *col_lut, const uint8_t *prev, uint8_t *out,
-                             mt_stream_t stream) {
+                             const int32_t *push_count, int E, int depth, int src_rows,
+                             const int32_t *row_lut, const int32_t *col_lut, const uint8_t *prev,
+                             uint8_t *out, mt_stream_t stream) {
   MT_CHECK_ARG(raw && push_offset && push_count && row_lut && col_lut && prev && out,
                "null argument");
   MT_CHECK_ARG(E >= 1, "E must be >= 1");
+  MT_CHECK_ARG(src_rows >= 84 && src_rows <= 210, "src_rows must be in [84, 210]");
   MT_CHECK_ARG(prev != out, "out may not alias prev");
   const int total = E * 84 * 84;
   if (depth == 1) {
     hipLaunchKernelGGL(preprocess_kernel<1>, dim3(cdiv(total, 256)), dim3(256), 0,
-                       (hipStream_t)stream, raw, push_offset, push_count, E, row_lut, col_lut, prev,
-                       out);
+                       (hipStream_t)stream, raw, push_offset, push_count, E, src_rows, row_lut, col_lut,
+                       prev, out);
   } else if (depth == 3) {
     hipLaunchKernelGGL(preprocess_kernel<3>, dim3(cdiv(total, 256)), dim3(256), 0,
-                       (hipStream_t)stream, raw, push_offset, push_count, E, row_lut, col_lut, prev,
-                       out);
+                       (hipStream_t)stream, raw, push_offset, push_count, E, src_rows, row_lut, col_lut,
+                       prev, out);
   } else {
     set_error("depth must be 1 or 3");
     return MT_ERR_ARG;
@@ -267,11 +276,11 @@ extern "C" int mt_preprocess(const uint8_t *raw, const int32_t *push_offset,
 
 extern "C" int mt_sample(const float *pi, const float *rep, int batch, int num_actions,
                          int num_reps, uint64_t seed, uint64_t *counters, int32_t *a_idx,
-                         int32_t *r_idx, mt_stream_t stream) {
+                         int32_t *r_idx, int32_t *pair, mt_stream_t stream) {
   MT_CHECK_ARG(pi && rep && counters && a_idx && r_idx, "null argument");
   MT_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_reps >= 1, "bad sizes");
   hipLaunchKernelGGL(sample_kernel, dim3(cdiv(batch, 64)), dim3(64), 0, (hipStream_t)stream, pi,
-                     rep, batch, num_actions, num_reps, seed, counters, a_idx, r_idx);
+                     rep, batch, num_actions, num_reps, seed, counters, a_idx, r_idx, pair);
   MT_LAUNCHED();
   return MT_OK;
 }

@@ -31,7 +31,8 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
   const mt_rollout_buffers &b = *buffers;
   MT_CHECK_ARG(b.states && b.values && b.idx && b.pi && b.rep && b.ws && b.counters && b.raw &&
-                   b.meta && b.row_lut && b.col_lut && b.idx_host && b.staging_host &&
+                   b.meta && b.row_lut && b.col_lut && b.idx_host && b.staging_host && b.pair &&
+                   b.pair_host && b.src_rows >= 84 && b.src_rows <= 210 &&
                    b.meta_host && b.reward_host && b.over_host && b.rm_host,
                "null buffer");
   mt_net_config cfg;
@@ -49,7 +50,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->A = cfg.num_actions;
   ro->R = cfg.num_reps;
   ro->depth = cfg.depth;
-  ro->frame_bytes = (size_t)210 * 160 * cfg.depth;
+  ro->frame_bytes = (size_t)b.src_rows * 160 * cfg.depth;
   ro->runner = (mh_runner *)runner;
   ro->book = (mh_book *)book;
   ro->b = b;
@@ -91,11 +92,12 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   int32_t *a_h = b.idx_host + (size_t)t * E, *r_h = b.idx_host + (size_t)T * E + (size_t)t * E;
   // 1. policy/value forward + device sampling (paac.py:144-147)
   MT_TRY_(mt_forward(ro->net, params, cur, E, b.ws, b.ws_bytes, b.values + (size_t)t * E, b.pi, b.rep, stream));
-  MT_TRY_(mt_sample(b.pi, b.rep, E, ro->A, ro->R, ro->seed, b.counters, a_d, r_d, stream));
-  MT_HIP(hipMemcpyAsync(a_h, a_d, sizeof(int32_t) * E, hipMemcpyDeviceToHost, s));
-  MT_HIP(hipMemcpyAsync(r_h, r_d, sizeof(int32_t) * E, hipMemcpyDeviceToHost, s));
+  MT_TRY_(mt_sample(b.pi, b.rep, E, ro->A, ro->R, ro->seed, b.counters, a_d, r_d, b.pair, stream));
+  MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
   MT_HIP(hipEventRecord(ro->ev, s));
   MT_HIP(hipEventSynchronize(ro->ev));
+  std::memcpy(a_h, b.pair_host, sizeof(int32_t) * E);
+  std::memcpy(r_h, b.pair_host + E, sizeof(int32_t) * E);
   const double t1 = now_us();
   // 2. emulators (runners.py:44-50 / emulator_runner.py:24-41) + bookkeeping (paac.py:176-205)
   int total = 0;
@@ -115,7 +117,8 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   MT_HIP(hipMemcpyAsync(b.raw, b.staging_host, (size_t)total * 2 * ro->frame_bytes,
                         hipMemcpyHostToDevice, s));
   MT_HIP(hipMemcpyAsync(b.meta, b.meta_host, sizeof(int32_t) * 2 * E, hipMemcpyHostToDevice, s));
-  const int rc = mt_preprocess(b.raw, b.meta, b.meta + E, E, ro->depth, b.row_lut, b.col_lut, cur, nxt, stream);
+  const int rc = mt_preprocess(b.raw, b.meta, b.meta + E, E, ro->depth, b.src_rows, b.row_lut,
+                               b.col_lut, cur, nxt, stream);
   const double t4 = now_us();
   ro->acc[0] += t1 - t0;
   ro->acc[1] += t2 - t1;

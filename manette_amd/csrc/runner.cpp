@@ -46,7 +46,10 @@ struct mh_runner {
   int E = 0, W = 0;
   std::vector<int32_t> tab;
   int ring = 0;
-  size_t fb = 0;
+  size_t fb = 0;        // bytes of one emulator screen (210 rows)
+  size_t row_bytes = 0;
+  std::vector<int32_t> rows;  // staged rows (empty = whole screen)
+  size_t sfb = 0;       // bytes of one staged screen
   int reward_len = 0, episode_len = 0;
   std::vector<Env> env;
   std::vector<std::thread> threads;
@@ -111,9 +114,17 @@ struct mh_runner {
         const int n = std::min(e.npush, 4);
         for (int j = 0; j < n; ++j) {
           const int64_t kk = e.last[(e.npush - n + j) & 3];
-          uint8_t *dst = staging + (size_t)(push_offset[i] + j) * 2 * fb;
-          std::memcpy(dst, e.screens + (size_t)((2 * kk) % ring) * fb, fb);
-          std::memcpy(dst + fb, e.screens + (size_t)((2 * kk + 1) % ring) * fb, fb);
+          uint8_t *dst = staging + (size_t)(push_offset[i] + j) * 2 * sfb;
+          for (int f = 0; f < 2; ++f) {
+            const uint8_t *src = e.screens + (size_t)((2 * kk + f) % ring) * fb;
+            uint8_t *d = dst + f * sfb;
+            if (rows.empty()) {
+              std::memcpy(d, src, fb);
+            } else {
+              for (size_t q = 0; q < rows.size(); ++q)
+                std::memcpy(d + q * row_bytes, src + (size_t)rows[q] * row_bytes, row_bytes);
+            }
+          }
         }
       }
     }
@@ -170,16 +181,21 @@ extern "C" const char *mh_last_error(void) { return g_err; }
 extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_rep, int n_reps,
                                 const uint8_t *screens, int ring, size_t frame_bytes,
                                 const float *rewards, int reward_len, int episode_len,
-                                mh_runner **out) {
+                                const int32_t *row_select, int n_rows, mh_runner **out) {
   if (!out || !tab_rep || !screens || !rewards) {
     set_error("null argument");
     return 1;
   }
   if (n_envs < 1 || n_workers < 1 || n_reps < 1 || ring < 2 || frame_bytes == 0 ||
-      reward_len < 1 || episode_len < 1) {
+      reward_len < 1 || episode_len < 1 || frame_bytes % 210 != 0 || n_rows < 0) {
     set_error("bad sizes");
     return 1;
   }
+  for (int q = 0; q < n_rows; ++q)
+    if (!row_select || row_select[q] < 0 || row_select[q] >= 210) {
+      set_error("row_select[%d] out of [0,210)", q);
+      return 1;
+    }
   for (int i = 0; i < n_reps; ++i)
     if (tab_rep[i] < 0) {
       set_error("negative repetition");
@@ -191,6 +207,9 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
   r->tab.assign(tab_rep, tab_rep + n_reps);
   r->ring = ring;
   r->fb = frame_bytes;
+  r->row_bytes = frame_bytes / 210;
+  if (n_rows > 0) r->rows.assign(row_select, row_select + n_rows);
+  r->sfb = n_rows > 0 ? (size_t)n_rows * r->row_bytes : frame_bytes;
   r->reward_len = reward_len;
   r->episode_len = episode_len;
   r->env.resize(n_envs);

@@ -177,12 +177,12 @@ class DeviceNetwork(object):
                                   _ptr(self.norm_dev), s), 'mt_clip_rmsprop')
 
 
-def sample(pi, rep, seed, counters, a_idx, r_idx):
+def sample(pi, rep, seed, counters, a_idx, r_idx, pair=None):
     """Device multinomial draw (perf mode of exploration_policy.py:108-116)."""
     B, A = pi.shape
     R = rep.shape[1]
     check(_lib.hip().mt_sample(_ptr(pi), _ptr(rep), B, A, R, C.c_uint64(seed), _ptr(counters),
-                               _ptr(a_idx), _ptr(r_idx), _stream()), 'mt_sample')
+                               _ptr(a_idx), _ptr(r_idx), _ptr(pair), _stream()), 'mt_sample')
 
 
 def returns(rewards, masks, values, v_boot, gamma, y, adv):
@@ -192,8 +192,9 @@ def returns(rewards, masks, values, v_boot, gamma, y, adv):
                                 T, E, _ptr(y), _ptr(adv), _stream()), 'mt_returns')
 
 
-def preprocess(raw, push_offset, push_count, E, depth, row_lut, col_lut, prev, out):
-    """atari_emulator.py:79-124 frame pool + resize + stack on device."""
-    check(_lib.hip().mt_preprocess(_ptr(raw), _ptr(push_offset), _ptr(push_count), E, depth,
+def preprocess(raw, push_offset, push_count, E, depth, row_lut, col_lut, prev, out, src_rows=210):
+    """atari_emulator.py:79-124 frame pool + resize + stack on device (raw screens of src_rows
+    rows: 210 = whole screens with the resize LUT, 84 = runner-selected rows, identity LUT)."""
+    check(_lib.hip().mt_preprocess(_ptr(raw), _ptr(push_offset), _ptr(push_count), E, depth, int(src_rows),
                                    _ptr(row_lut), _ptr(col_lut), _ptr(prev), _ptr(out), _stream()),
           'mt_preprocess')

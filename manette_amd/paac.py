@@ -92,8 +92,12 @@ class PAACLearner(ActorLearner):
         E, C = self.emulator_counts, self.C
         if self.runner_kind == 'native':
             bank = self.environment_creator.create_bank(0, E)
-            self.runners = NativeRunners(bank, self.workers, self.tab_rep)
-            self.raw_d = torch.zeros(4 * E, 2, bank.frame_bytes, dtype=torch.uint8, device=self.dev)
+            # only the 84 screen rows the nearest resize reads are staged and copied (PCIe)
+            self.runners = NativeRunners(bank, self.workers, self.tab_rep, row_select=ROW_LUT)
+            self.stage_row_lut = torch.arange(84, dtype=torch.int32, device=self.dev)
+            self.raw_d = torch.zeros(4 * E, 2, self.runners.frame_bytes, dtype=torch.uint8, device=self.dev)
+            self.pair_d = torch.zeros(2, E, dtype=torch.int32, device=self.dev)
+            self.pair_h = torch.zeros(2, E, dtype=torch.int32, pin_memory=True)
             self.meta_d = torch.zeros(2, E, dtype=torch.int32, device=self.dev)
             self.off_d = self.meta_d[0]
             self.cnt_d = self.meta_d[1]
@@ -121,8 +125,9 @@ class PAACLearner(ActorLearner):
         p = lambda t: C.c_void_p(t.data_ptr())
         self._bufs = _lib.mt_rollout_buffers(
             p(self.states), p(self.values), p(self.idx), p(self.pi_roll), p(self.rep_roll), p(ws), ws.numel(),
-            p(self.counters), p(self.raw_d), p(self.meta_d), p(self.row_lut), p(self.col_lut), p(self.idx_h),
-            p(r.staging), p(r.push_meta), p(r.reward), p(r.over), p(self.rm_h))
+            p(self.counters), p(self.raw_d), r.src_rows, p(self.pair_d), p(self.pair_h), p(self.meta_d),
+            p(self.stage_row_lut), p(self.col_lut), p(self.idx_h), p(r.staging), p(r.push_meta), p(r.reward),
+            p(r.over), p(self.rm_h))
         h = C.c_void_p()
         _lib.check(_lib.hip().mt_rollout_create(net._h, self.emulator_counts, self.max_local_steps, r._h,
                                                 self.book.handle, C.byref(self._bufs),
@@ -136,7 +141,7 @@ class PAACLearner(ActorLearner):
         self.raw_d[:total].copy_(r.staging[:total], non_blocking=True)
         self.meta_d.copy_(r.push_meta, non_blocking=True)
         devnet.preprocess(self.raw_d, self.off_d, self.cnt_d, self.emulator_counts, self.depth,
-                          self.row_lut, self.col_lut, prev, out)
+                          self.stage_row_lut, self.col_lut, prev, out, src_rows=r.src_rows)
 
     @staticmethod
     def _lib_ref(x):

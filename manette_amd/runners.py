@@ -23,18 +23,24 @@ def _np(t):
 
 
 class NativeRunners(object):
-    def __init__(self, bank, n_workers, tab_rep):
+    """row_select: screen rows to stage (None = whole 210-row screens). The learner passes the
+    84 rows the nearest resize reads, so only those cross PCIe."""
+
+    def __init__(self, bank, n_workers, tab_rep, row_select=None):
         self.bank = bank
         self.E = bank.screens.shape[0]
         self.tab = np.ascontiguousarray(np.asarray(tab_rep, dtype=np.int32))
-        self.frame_bytes = bank.frame_bytes
+        self.rows = None if row_select is None else np.ascontiguousarray(np.asarray(row_select, np.int32))
+        self.src_rows = 210 if self.rows is None else len(self.rows)
+        self.frame_bytes = bank.frame_bytes // 210 * self.src_rows  # one staged screen
         h = C.c_void_p()
         lib = _lib.host()
         _lib.check_host(lib.mh_runner_create(
             self.E, int(n_workers), self.tab.ctypes.data_as(C.c_void_p), len(self.tab),
-            bank.screens.ctypes.data_as(C.c_void_p), bank.screens.shape[1], self.frame_bytes,
+            bank.screens.ctypes.data_as(C.c_void_p), bank.screens.shape[1], bank.frame_bytes,
             bank.rewards.ctypes.data_as(C.c_void_p), bank.rewards.shape[1], bank.episode_len,
-            C.byref(h)), 'mh_runner_create')
+            None if self.rows is None else self.rows.ctypes.data_as(C.c_void_p),
+            0 if self.rows is None else len(self.rows), C.byref(h)), 'mh_runner_create')
         self._h = h
         pin = torch.cuda.is_available()
         mk = lambda *shape, dtype: torch.zeros(*shape, dtype=dtype, pin_memory=pin)

@@ -179,3 +179,31 @@ def test_lut_product_matches_pil_fixture():
     p = np.load(os.path.join(GOLDEN, 'preprocess.npz'))
     np.testing.assert_array_equal(ROW_LUT, p['row_lut'])
     np.testing.assert_array_equal(COL_LUT, p['col_lut'])
+
+
+def test_native_runner_row_selected_staging():
+    """Staging only the resize's 84 rows carries exactly those rows of the whole screens."""
+    from manette_amd.environment import ROW_LUT
+    from manette_amd.runners import NativeRunners
+    from manette_amd.synthetic import SyntheticBank
+    tab = opol.tab_repetitions(10, 11)
+    bank = SyntheticBank(3, 6, episode_len=9)
+    full = NativeRunners(bank, 2, tab)
+    rows = NativeRunners(bank, 3, tab, row_select=ROW_LUT)
+    try:
+        assert rows.src_rows == 84 and rows.frame_bytes == 84 * 160
+        n1, n2 = full.reset(), rows.reset()
+        rs = np.random.RandomState(0)
+        for step in range(12):
+            assert n1 == n2
+            np.testing.assert_array_equal(full.push_meta.numpy(), rows.push_meta.numpy())
+            a = full.staging.numpy()[:n1].reshape(n1, 2, 210, 160)[:, :, ROW_LUT]
+            b = rows.staging.numpy()[:n2 * 2 * 84 * 160].reshape(n2, 2, 84, 160)
+            np.testing.assert_array_equal(a, b)
+            act = rs.randint(0, 6, 6).astype(np.int32)
+            rep = rs.randint(0, 11, 6).astype(np.int32)
+            n1, n2 = full.step(act, rep), rows.step(act, rep)
+            np.testing.assert_array_equal(full.reward.numpy(), rows.reward.numpy())
+    finally:
+        full.stop()
+        rows.stop()

@@ -143,8 +143,9 @@ def test_clip_rmsprop(clip_type, gscale):
     np.testing.assert_array_equal(net.params.cpu().numpy(), w)
 
 
+@pytest.mark.parametrize('rows_only', [False, True])
 @pytest.mark.parametrize('depth', [1, 3])
-def test_preprocess_bit_exact(depth):
+def test_preprocess_bit_exact(depth, rows_only):
     from manette_amd.network import preprocess as dev_pre
     rs = np.random.RandomState(depth)
     E = 7
@@ -154,8 +155,12 @@ def test_preprocess_bit_exact(depth):
     prev = rs.randint(0, 256, size=(E, 84, 84, 4 * depth)).astype(np.uint8)
     d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
     out = torch.empty(E, 84, 84, 4 * depth, dtype=torch.uint8, device='cuda')
-    dev_pre(d(raw), d(offs), d(counts), E, depth, d(preprocess.ROW_LUT.astype(np.int32)),
-            d(preprocess.COL_LUT.astype(np.int32)), d(prev), out)
+    if rows_only:  # runner-staged rows (the 84 the resize reads) + identity row LUT
+        dev_pre(d(raw[:, :, preprocess.ROW_LUT]), d(offs), d(counts), E, depth, d(np.arange(84, dtype=np.int32)),
+                d(preprocess.COL_LUT.astype(np.int32)), d(prev), out, src_rows=84)
+    else:
+        dev_pre(d(raw), d(offs), d(counts), E, depth, d(preprocess.ROW_LUT.astype(np.int32)),
+                d(preprocess.COL_LUT.astype(np.int32)), d(prev), out)
     got = out.cpu().numpy()
     for e in range(E):
         pushes = [preprocess.pool_and_resize(raw[offs[e] + j, 0], raw[offs[e] + j, 1]) for j in range(counts[e])]
