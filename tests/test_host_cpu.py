@@ -198,7 +198,7 @@ def test_native_runner_row_selected_staging():
             assert n1 == n2
             np.testing.assert_array_equal(full.push_meta.numpy(), rows.push_meta.numpy())
             a = full.staging.numpy()[:n1].reshape(n1, 2, 210, 160)[:, :, ROW_LUT]
-            b = rows.staging.numpy()[:n2 * 2 * 84 * 160].reshape(n2, 2, 84, 160)
+            b = rows.staging.numpy()[:n2].reshape(n2, 2, 84, 160)
             np.testing.assert_array_equal(a, b)
             act = rs.randint(0, 6, 6).astype(np.int32)
             rep = rs.randint(0, 11, 6).astype(np.int32)
