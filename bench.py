@@ -153,6 +153,7 @@ def main():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--step_impl', default='native', choices=['native', 'python'],
                     help='macro-step orchestration: native (mt_rollout_step) or Python')
+    ap.add_argument('--staging', default='zero_copy', choices=['zero_copy', 'copy'])
     a = ap.parse_args()
 
     import torch
@@ -167,6 +168,7 @@ def main():
     T = a.t_max
     args = build_args(cfg, T, a.sampling, a.seed)
     args.env_id_offset = rank * cfg['ec']
+    args.staging = a.staging
 
     from manette_amd.exploration_policy import ExplorationPolicy
     from manette_amd.paac import PAACLearner
@@ -259,8 +261,8 @@ def main():
             'vs_baseline': None,
             'dtype': 'fp32',
             'data': 'synthetic (seeded 210x160 screens, native emulator threads, GPU preprocess)',
-            'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step' % (
-                a.config, ec, cfg['ew'], T, a.sampling, a.step_impl), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
+            'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step, %s staging' % (
+                a.config, ec, cfg['ew'], T, a.sampling, a.step_impl, a.staging), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
                 'global_emulators': ec * world, 'parallelism': 'dp%d' % world},
             'roofline': {'bound': 'mfma', 'kernel': 'train pass (fwd+bwd, %d rows)' % N,
                          'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',

@@ -151,11 +151,17 @@ int mt_preprocess(const uint8_t *raw, const int32_t *push_offset, const int32_t 
                   const uint8_t *prev, uint8_t *out, mt_stream_t stream);
 
 /* ---- native rollout macro-step (orchestrates A1-A3, A8; paac.py:140-205) -------------------
- * One call = one macro-step t of every env: mt_forward on state slot t -> mt_sample into
- * idx[0][t], idx[1][t] -> async D2H of the indices -> one event wait -> mh_runner_step (native
- * emulator threads, libmanette_host.so) -> mh_book_step (bookkeeping into rm_host[.][t]) ->
- * async H2D of the pushed screens + push metadata -> mt_preprocess into state slot t+1.
- * All buffers are caller-owned; `runner` / `book` are mh_runner* / mh_book* handles. */
+ * One call = one macro-step t of every env: mt_forward on state slot t with the A3 draw fused
+ * into its heads kernel (indices into idx[0][t], idx[1][t] and the [2][E] pair) -> wait for the
+ * pair (spin on the stream's event) -> mh_runner_step (native emulator threads,
+ * libmanette_host.so) -> mh_book_step (bookkeeping into rm_host[.][t]) -> mt_preprocess of the
+ * pushed screens into state slot t+1.
+ * flags = 0: the pair is copied D2H and the screens + push metadata H2D (hipMemcpyAsync).
+ * flags & MT_ROLLOUT_ZERO_COPY: the heads kernel writes the pair into pair_host and the
+ * preprocess kernel reads staging_host / meta_host in place (host-mapped pinned memory): no
+ * copy engine and no cross-engine wait on the per-step critical path; raw / meta / pair may then
+ * be null. All buffers are caller-owned; `runner` / `book` are mh_runner* / mh_book* handles. */
+#define MT_ROLLOUT_ZERO_COPY 1
 typedef struct mt_rollout mt_rollout;
 typedef struct mt_rollout_buffers {
   /* device */
@@ -178,6 +184,7 @@ typedef struct mt_rollout_buffers {
   int32_t *meta_host;          /* [2][E] */
   float *reward_host, *over_host; /* [E] */
   float *rm_host;              /* [2][T][E]: clipped rewards; masks */
+  int32_t flags;               /* MT_ROLLOUT_* */
 } mt_rollout_buffers;
 int mt_rollout_create(const mt_net *net, int E, int T, void *runner, void *book,
                       const mt_rollout_buffers *buffers, uint64_t seed, mt_rollout **out);

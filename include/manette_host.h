@@ -31,11 +31,17 @@ const char *mh_last_error(void);
  * [n_envs][reward_len] float32 (caller keeps both alive). tab_rep: FiGAR repetition table
  * (exploration_policy.py:56-62). row_select [n_rows] (or NULL / 0 for whole screens): stage only
  * these screen rows — the rows the 84x84 nearest resize reads (atari_emulator.py:85) — so a
- * push is n_rows*row_bytes per screen on PCIe instead of 210 rows. */
+ * push is n_rows*row_bytes per screen on PCIe instead of 210 rows.
+ * flags & MH_RUNNER_FIXED_SLOTS: env e's pushes always go to staging slots [4e, 4e+count)
+ * (push_offset[e] = 4e, *total_pushes = 4E) and each worker stages its envs while it steps them
+ * (one worker release per macro-step) — for consumers that read the staging in place
+ * (MT_ROLLOUT_ZERO_COPY). Otherwise the slots are compacted env-major (a prefix sum between
+ * two worker phases) so a copy engine moves only the pushed screens. */
+#define MH_RUNNER_FIXED_SLOTS 1
 int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_rep, int n_reps,
                      const uint8_t *screens, int ring, size_t frame_bytes, const float *rewards,
                      int reward_len, int episode_len, const int32_t *row_select, int n_rows,
-                     mh_runner **out);
+                     int flags, mh_runner **out);
 void mh_runner_destroy(mh_runner *r);
 
 /* get_initial_state() of every env: 4 pushes each. Outputs as mh_runner_step. */

@@ -26,7 +26,10 @@ class mt_rollout_buffers(C.Structure):
                [(n, C.c_void_p) for n in ('counters', 'raw')] + [('src_rows', C.c_int32)] + \
                [(n, C.c_void_p) for n in ('pair', 'pair_host', 'meta', 'row_lut', 'col_lut', 'idx_host',
                                           'staging_host', 'meta_host', 'reward_host', 'over_host',
-                                          'rm_host')]
+                                          'rm_host')] + [('flags', C.c_int32)]
+
+
+MT_ROLLOUT_ZERO_COPY = 1
 
 
 class mt_net_config(C.Structure):
@@ -72,7 +75,7 @@ _HIP_SIGS = {
 
 _HOST_SIGS = {
     'mh_last_error': (C.c_char_p, []),
-    'mh_runner_create': (_I, [_I, _I, _P, _I, _P, _I, _SZ, _P, _I, _I, _P, _I, C.POINTER(_P)]),
+    'mh_runner_create': (_I, [_I, _I, _P, _I, _P, _I, _SZ, _P, _I, _I, _P, _I, _I, C.POINTER(_P)]),
     'mh_runner_destroy': (None, [_P]),
     'mh_runner_reset': (_I, [_P, _P, _P, _P, C.POINTER(_I)]),
     'mh_runner_step': (_I, [_P, _P, _P, _P, _P, _P, _P, _P, C.POINTER(_I)]),

@@ -54,4 +54,56 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// A3 perf mode sampler: counter-based uniforms (splitmix64 of seed, row, per-row counter),
+// inverse CDF over (p - epsneg(float32)) accumulated in double — the standalone sample kernel
+// and the fused rollout heads kernel share it so both draw identical indices.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ void row_uniforms(uint64_t seed, int b, uint64_t c, double *ua, double *ur) {
+  const uint64_t h = mix64(seed ^ mix64(((uint64_t)b << 40) ^ c));
+  const uint64_t h2 = mix64(h ^ 0x9e3779b97f4a7c15ULL);
+  *ua = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+  *ur = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+}
+
+__device__ __forceinline__ int draw_index(const float *p, int n, double u) {
+  const double epsneg = 5.9604644775390625e-08;  // np.finfo(np.float32).epsneg
+  double cum = 0.0;
+  for (int j = 0; j < n - 1; ++j) {
+    cum += (double)(p[j] - (float)epsneg);
+    if (u < cum) return j;
+  }
+  return n - 1;
+}
+
+__device__ __forceinline__ void sample_row(const float *pa, int A, const float *pr, int R, uint64_t seed,
+                                           int b, uint64_t *counters, int *a, int *r) {
+  const uint64_t c = counters[b];
+  counters[b] = c + 1;
+  double ua, ur;
+  row_uniforms(seed, b, c, &ua, &ur);
+  *a = draw_index(pa, A, ua);
+  *r = draw_index(pr, R, ur);
+}
+
+// Rollout-path sampling fused into the heads kernel (mt_rollout_step): indices to device
+// buffers and, when pair != null, to a host-mapped [2][B] pair.
+struct SampleArgs {
+  uint64_t seed;
+  uint64_t *counters;
+  int32_t *a_idx, *r_idx, *pair;
+};
+
+}  // namespace mt
+
+struct mt_net;
+namespace mt {
+// forward (mt_forward) with the A3 draw fused into the heads kernel; smp may be null.
+int forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
+                   size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp,
+                   hipStream_t stream);
 }  // namespace mt

@@ -117,83 +117,67 @@ __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// A2: one thread per (env, y, x) output pixel; writes the 4*depth stacked channels.
+// A2: block = (12 output rows, env). Phase 1 streams the source rows those output rows read
+// (row_lut) of both frames of each of the env's p pushes with 16-byte loads — HBM, or host
+// memory over PCIe when the staging is read in place — and keeps max(f0, f1) in LDS. Phase 2
+// gathers the resize columns (col_lut) from LDS and writes each pixel's 4*depth stacked
+// channels: the p new pooled frames after the prev channels they push out.
 // ---------------------------------------------------------------------------------------------
+constexpr int kPreRows = 12;  // 84 = 7 x 12
+
+typedef unsigned char u8x16 __attribute__((ext_vector_type(16)));
+
 template <int DEPTH>
 __global__ __launch_bounds__(256) void preprocess_kernel(
     const uint8_t *__restrict__ raw, const int32_t *__restrict__ push_offset,
-    const int32_t *__restrict__ push_count, int E, int SH, const int32_t *__restrict__ row_lut,
+    const int32_t *__restrict__ push_count, int SH, const int32_t *__restrict__ row_lut,
     const int32_t *__restrict__ col_lut, const uint8_t *__restrict__ prev, uint8_t *__restrict__ out) {
-  constexpr int SW = 160;
-  const int FR = SH * SW * DEPTH;  // one staged ALE screen
+  constexpr int ROWB = 160 * DEPTH;  // bytes of one screen row
+  constexpr int Q = ROWB / 16;
   constexpr int C = 4 * DEPTH;
-  __shared__ int rl[84], cl[84];
-  if (threadIdx.x < 84) {
-    rl[threadIdx.x] = row_lut[threadIdx.x];
-    cl[threadIdx.x] = col_lut[threadIdx.x];
+  __shared__ u8x16 pooled[4][kPreRows][Q];
+  __shared__ int rl[kPreRows], cl[84];
+  const int e = blockIdx.y, y0 = blockIdx.x * kPreRows;
+  const int p = min(max(push_count[e], 1), 4);
+  const size_t FR = (size_t)SH * ROWB;  // one staged screen
+  const uint8_t *base = raw + (size_t)push_offset[e] * 2 * FR;
+  if (threadIdx.x < kPreRows) rl[threadIdx.x] = row_lut[y0 + threadIdx.x];
+  if (threadIdx.x < 84) cl[threadIdx.x] = col_lut[threadIdx.x];
+  __syncthreads();
+  for (int i = threadIdx.x; i < p * kPreRows * Q; i += 256) {
+    const int j = i / (kPreRows * Q), rem = i - j * (kPreRows * Q);
+    const int r = rem / Q, q = rem - r * Q;
+    const u8x16 *f0 = reinterpret_cast<const u8x16 *>(base + j * 2 * FR + (size_t)rl[r] * ROWB) + q;
+    const u8x16 a = f0[0], b = f0[FR / 16];
+    pooled[j][r][q] = __builtin_elementwise_max(a, b);  // np.amax over the 2-frame pool
   }
   __syncthreads();
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= E * 84 * 84) return;
-  const int e = idx / (84 * 84);
-  const int pix = idx - e * (84 * 84);
-  const int yy = pix / 84, xx = pix - yy * 84;
-  const int p = push_count[e];
-  const int off = push_offset[e];
-  const uint8_t *pv = prev + (size_t)idx * C;
-  uint8_t *po = out + (size_t)idx * C;
-  const size_t src = ((size_t)rl[yy] * SW + cl[xx]) * DEPTH;
+  const uint8_t *pl = reinterpret_cast<const uint8_t *>(&pooled[0][0][0]);
+  for (int i = threadIdx.x; i < kPreRows * 84; i += 256) {
+    const int r = i / 84, x = i - r * 84;
+    const size_t o = (((size_t)e * 84 + y0 + r) * 84 + x) * C;
+    const int src = cl[x] * DEPTH;
 #pragma unroll
-  for (int col = 0; col < DEPTH; ++col) {
-    uint8_t v[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (c < 4 - p) {
-        v[c] = pv[col * 4 + c + p];
-      } else {
-        const uint8_t *f = raw + (size_t)(off + c - (4 - p)) * 2 * FR;
-        const uint8_t a = f[src + col], b = f[FR + src + col];
-        v[c] = a > b ? a : b;  // np.amax over the 2-frame pool
-      }
+    for (int col = 0; col < DEPTH; ++col) {
+      uint32_t v = p < 4 ? *reinterpret_cast<const uint32_t *>(prev + o + col * 4) >> (8 * p) : 0u;
+      for (int j = 0; j < p; ++j)
+        v |= (uint32_t)pl[(j * kPreRows + r) * ROWB + src + col] << (8 * (4 - p + j));
+      *reinterpret_cast<uint32_t *>(out + o + col * 4) = v;
     }
-    *reinterpret_cast<uint32_t *>(po + col * 4) =
-        (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // A3 perf mode: counter-based uniforms, inverse CDF over (p - epsneg(float32)).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
-  return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ int draw_index(const float *p, int n, double u) {
-  const double epsneg = 5.9604644775390625e-08;  // np.finfo(np.float32).epsneg
-  double cum = 0.0;
-  for (int j = 0; j < n - 1; ++j) {
-    cum += (double)(p[j] - (float)epsneg);
-    if (u < cum) return j;
-  }
-  return n - 1;
-}
-
 __global__ void sample_kernel(const float *__restrict__ pi, const float *__restrict__ rep, int B,
                               int A, int R, uint64_t seed, uint64_t *__restrict__ counters,
                               int32_t *__restrict__ a_idx, int32_t *__restrict__ r_idx,
                               int32_t *__restrict__ pair) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const uint64_t c = counters[b];
-  counters[b] = c + 1;
-  const uint64_t h = mix64(seed ^ mix64(((uint64_t)b << 40) ^ c));
-  const uint64_t h2 = mix64(h ^ 0x9e3779b97f4a7c15ULL);
-  const double ua = (double)(h >> 11) * (1.0 / 9007199254740992.0);
-  const double ur = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
-  const int a = draw_index(pi + (size_t)b * A, A, ua);
-  const int r = draw_index(rep + (size_t)b * R, R, ur);
+  int a, r;
+  sample_row(pi + (size_t)b * A, A, rep + (size_t)b * R, R, seed, b, counters, &a, &r);
   a_idx[b] = a;
   r_idx[b] = r;
   if (pair) {
@@ -257,15 +241,14 @@ extern "C" int mt_preprocess(const uint8_t *raw, const int32_t *push_offset,
   MT_CHECK_ARG(E >= 1, "E must be >= 1");
   MT_CHECK_ARG(src_rows >= 84 && src_rows <= 210, "src_rows must be in [84, 210]");
   MT_CHECK_ARG(prev != out, "out may not alias prev");
-  const int total = E * 84 * 84;
+  MT_CHECK_ARG(((uintptr_t)raw & 15) == 0, "raw must be 16-byte aligned");
+  const dim3 grid(84 / kPreRows, E);
   if (depth == 1) {
-    hipLaunchKernelGGL(preprocess_kernel<1>, dim3(cdiv(total, 256)), dim3(256), 0,
-                       (hipStream_t)stream, raw, push_offset, push_count, E, src_rows, row_lut, col_lut,
-                       prev, out);
+    hipLaunchKernelGGL(preprocess_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, raw, push_offset,
+                       push_count, src_rows, row_lut, col_lut, prev, out);
   } else if (depth == 3) {
-    hipLaunchKernelGGL(preprocess_kernel<3>, dim3(cdiv(total, 256)), dim3(256), 0,
-                       (hipStream_t)stream, raw, push_offset, push_count, E, src_rows, row_lut, col_lut,
-                       prev, out);
+    hipLaunchKernelGGL(preprocess_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, raw, push_offset,
+                       push_count, src_rows, row_lut, col_lut, prev, out);
   } else {
     set_error("depth must be 1 or 3");
     return MT_ERR_ARG;

@@ -351,19 +351,33 @@ __device__ __forceinline__ float wave_softmax(float x, int lane, int n) {
 
 constexpr int kMaxHeads = 64;  // 1 + A + R <= 64
 
+// draw_index (common.h) over probabilities held in lanes [0, n): same order and rounding.
+__device__ __forceinline__ int wave_draw(float p, int n, double u) {
+  const double epsneg = 5.9604644775390625e-08;
+  double cum = 0.0;
+  int res = n - 1;
+  for (int j = 0; j < n - 1; ++j) {
+    const float pj = __shfl(p, j, 64);
+    cum += (double)(pj - (float)epsneg);
+    if (res == n - 1 && u < cum) res = j;
+  }
+  return res;
+}
+
 // One workgroup per row b (4 waves):
 //  1. h = act(sum_z slabs[z][b] + b_fc) — the split-K dense layer finished here
 //     (networks.py:57-70); every thread owns F/256 features, the slab loads of a feature are
 //     issued 8 at a time;
 //  2. logits_o = [h, 1] . W_o for the 1+A+R head outputs (policy_v_network.py:22, :31, :47):
 //     wave w takes outputs o = w, w+4, ...; lanes split F and reduce with shuffles;
-//  3. wave 0: v = logit_0, pi = softmax(logits_A / temp), rep = softmax(logits_R / temp).
+//  3. wave 0: v = logit_0, pi = softmax(logits_A / temp), rep = softmax(logits_R / temp);
+//  4. rollout path (smp.counters != null): wave 0 draws (a, r) for the row (A3, common.h).
 __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict__ slabs, int S, int B,
                                                         const float *__restrict__ fc_b, int act,
                                                         float alpha, HeadParams hp, float temp,
                                                         float *__restrict__ H, float *__restrict__ v,
                                                         float *__restrict__ pi,
-                                                        float *__restrict__ rep) {
+                                                        float *__restrict__ rep, SampleArgs smp) {
   __shared__ float hs[512];
   __shared__ float zs[64];
   const int b = blockIdx.x;
@@ -404,6 +418,21 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict_
   const float zr = __shfl(z, (lane + 1 + hp.A) & 63, 64) / temp;
   const float pr = wave_softmax(zr, lane, hp.R);
   if (lane < hp.R) rep[(size_t)b * hp.R + lane] = pr;
+  if (smp.counters) {
+    const uint64_t c = smp.counters[b];
+    double ua, ur;
+    row_uniforms(smp.seed, b, c, &ua, &ur);
+    const int a = wave_draw(pa, hp.A, ua), r = wave_draw(pr, hp.R, ur);
+    if (lane == 0) {
+      smp.counters[b] = c + 1;
+      smp.a_idx[b] = a;
+      smp.r_idx[b] = r;
+      if (smp.pair) {
+        smp.pair[b] = a;
+        smp.pair[B + b] = r;
+      }
+    }
+  }
 }
 
 // dL/dlogit for one softmax head (policy_v_network.py:29-57, :59-74), one wave, lanes [0, n):
@@ -672,7 +701,7 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
 
 template <class Ar>
 static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
-                        float *v, float *pi, float *rep, hipStream_t s) {
+                        float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s) {
   const WsLayout L = ws_layout<Ar>(n, B);
   MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s)));
   const float *flat = layer_out<Ar, Ar::NCONV - 1>(ws, L);
@@ -683,7 +712,7 @@ static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int
   HeadParams hp = head_params(n, P);
   hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, L.fc_splits, B,
                      Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp,
-                     n->cfg.softmax_temp, ws + L.H, v, pi, rep);
+                     n->cfg.softmax_temp, ws + L.H, v, pi, rep, smp ? *smp : SampleArgs{});
   MT_LAUNCHED();
   return MT_OK;
 }
@@ -841,7 +870,15 @@ extern "C" int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *byte
 extern "C" int mt_forward(const mt_net *net, const float *params, const uint8_t *obs, int batch,
                           void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
                           mt_stream_t stream) {
+  return mt::forward_sample(net, params, obs, batch, ws, ws_bytes, v, pi, rep, nullptr,
+                            (hipStream_t)stream);
+}
+
+int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch,
+                       void *ws, size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp,
+                       hipStream_t stream) {
   MT_CHECK_ARG(net && params && obs && ws && v && pi && rep, "null argument");
+  MT_CHECK_ARG(!smp || (smp->counters && smp->a_idx && smp->r_idx), "null sample buffer");
   MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
   MT_ARCH_SWITCH(net, {
     const WsLayout L = ws_layout<Ar>(net, batch);
@@ -849,7 +886,7 @@ extern "C" int mt_forward(const mt_net *net, const float *params, const uint8_t 
       set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
       return MT_ERR_WORKSPACE;
     }
-    return forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, (hipStream_t)stream);
+    return forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
   });
   return MT_OK;
 }

@@ -19,6 +19,9 @@ struct mt_rollout {
   mt_rollout_buffers b;
   uint64_t seed;
   hipEvent_t ev;
+  bool zero_copy;
+  uint8_t *staging_dev;  // device addresses of the host-mapped buffers (zero-copy mode)
+  int32_t *meta_dev, *pair_dev;
   double acc[5];  // host wall us: launch+wait for indices, runner, book, upload+preprocess enqueue; steps
 };
 
@@ -30,11 +33,19 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   MT_CHECK_ARG(net && runner && book && buffers && out, "null argument");
   MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
   const mt_rollout_buffers &b = *buffers;
-  MT_CHECK_ARG(b.states && b.values && b.idx && b.pi && b.rep && b.ws && b.counters && b.raw &&
-                   b.meta && b.row_lut && b.col_lut && b.idx_host && b.staging_host && b.pair &&
-                   b.pair_host && b.src_rows >= 84 && b.src_rows <= 210 &&
+  const bool zc = (b.flags & MT_ROLLOUT_ZERO_COPY) != 0;
+  MT_CHECK_ARG((b.flags & ~MT_ROLLOUT_ZERO_COPY) == 0, "unknown rollout flags %d", b.flags);
+  MT_CHECK_ARG(b.states && b.values && b.idx && b.pi && b.rep && b.ws && b.counters &&
+                   (zc || (b.raw && b.meta && b.pair)) && b.row_lut && b.col_lut && b.idx_host &&
+                   b.staging_host && b.pair_host && b.src_rows >= 84 && b.src_rows <= 210 &&
                    b.meta_host && b.reward_host && b.over_host && b.rm_host,
                "null buffer");
+  void *staging_dev = nullptr, *meta_dev = nullptr, *pair_dev = nullptr;
+  if (zc) {  // the three buffers must be pinned + mapped (hipHostMalloc / torch pin_memory)
+    MT_HIP(hipHostGetDevicePointer(&staging_dev, b.staging_host, 0));
+    MT_HIP(hipHostGetDevicePointer(&meta_dev, b.meta_host, 0));
+    MT_HIP(hipHostGetDevicePointer(&pair_dev, b.pair_host, 0));
+  }
   mt_net_config cfg;
   MT_CHECK_ARG(mt_net_get_config(net, &cfg) == MT_OK, "bad net");
   size_t need = 0;
@@ -55,6 +66,10 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->book = (mh_book *)book;
   ro->b = b;
   ro->seed = seed;
+  ro->zero_copy = zc;
+  ro->staging_dev = (uint8_t *)staging_dev;
+  ro->meta_dev = (int32_t *)meta_dev;
+  ro->pair_dev = (int32_t *)pair_dev;
   hipError_t e = hipEventCreateWithFlags(&ro->ev, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete ro;
@@ -90,12 +105,17 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   uint8_t *nxt = cur + slot;
   int32_t *a_d = b.idx + (size_t)t * E, *r_d = b.idx + (size_t)T * E + (size_t)t * E;
   int32_t *a_h = b.idx_host + (size_t)t * E, *r_h = b.idx_host + (size_t)T * E + (size_t)t * E;
-  // 1. policy/value forward + device sampling (paac.py:144-147)
-  MT_TRY_(mt_forward(ro->net, params, cur, E, b.ws, b.ws_bytes, b.values + (size_t)t * E, b.pi, b.rep, stream));
-  MT_TRY_(mt_sample(b.pi, b.rep, E, ro->A, ro->R, ro->seed, b.counters, a_d, r_d, b.pair, stream));
-  MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
+  // 1. policy/value forward + device sampling fused in its heads kernel (paac.py:144-147)
+  const SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
+  MT_TRY_(forward_sample(ro->net, params, cur, E, b.ws, b.ws_bytes, b.values + (size_t)t * E, b.pi,
+                         b.rep, &smp, s));
+  if (!ro->zero_copy)
+    MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
   MT_HIP(hipEventRecord(ro->ev, s));
-  MT_HIP(hipEventSynchronize(ro->ev));
+  // spin: a blocking wait sleeps past the ~50 us the chain takes and pays the wake-up latency
+  hipError_t q;
+  while ((q = hipEventQuery(ro->ev)) == hipErrorNotReady) __builtin_ia32_pause();
+  MT_HIP(q);
   std::memcpy(a_h, b.pair_host, sizeof(int32_t) * E);
   std::memcpy(r_h, b.pair_host + E, sizeof(int32_t) * E);
   const double t1 = now_us();
@@ -113,12 +133,18 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
     return MT_ERR_ARG;
   }
   const double t3 = now_us();
-  // 3. screens -> HBM, preprocess into slot t+1 (atari_emulator.py:79-124)
-  MT_HIP(hipMemcpyAsync(b.raw, b.staging_host, (size_t)total * 2 * ro->frame_bytes,
-                        hipMemcpyHostToDevice, s));
-  MT_HIP(hipMemcpyAsync(b.meta, b.meta_host, sizeof(int32_t) * 2 * E, hipMemcpyHostToDevice, s));
-  const int rc = mt_preprocess(b.raw, b.meta, b.meta + E, E, ro->depth, b.src_rows, b.row_lut,
-                               b.col_lut, cur, nxt, stream);
+  // 3. screens -> preprocess into slot t+1 (atari_emulator.py:79-124)
+  const uint8_t *raw = ro->staging_dev;
+  const int32_t *meta = ro->meta_dev;
+  if (!ro->zero_copy) {
+    MT_HIP(hipMemcpyAsync(b.raw, b.staging_host, (size_t)total * 2 * ro->frame_bytes,
+                          hipMemcpyHostToDevice, s));
+    MT_HIP(hipMemcpyAsync(b.meta, b.meta_host, sizeof(int32_t) * 2 * E, hipMemcpyHostToDevice, s));
+    raw = b.raw;
+    meta = b.meta;
+  }
+  const int rc = mt_preprocess(raw, meta, meta + E, E, ro->depth, b.src_rows, b.row_lut, b.col_lut,
+                               cur, nxt, stream);
   const double t4 = now_us();
   ro->acc[0] += t1 - t0;
   ro->acc[1] += t2 - t1;

@@ -5,10 +5,12 @@
 // while not terminal, reward sum, reset on terminal). Here the workers are persistent threads
 // released by a generation counter and joined by an arrival counter (spin, then futex wait via
 // std::atomic::wait), so a macro-step costs a few microseconds of synchronisation instead of
-// 2*ew Queue round trips. A step runs in two phases:
+// 2*ew Queue round trips. Compact staging runs a step in two phases:
 //   A: each worker steps its envs and records which screens each env pushed (last <= 4);
 //   main: prefix sum of push counts -> compact staging offsets;
 //   B: each worker copies its envs' screens into the staging buffer (pinned, H2D'd whole).
+// Fixed-slot staging (MH_RUNNER_FIXED_SLOTS) does A and B in one phase: env e's screens go to
+// slots [4e, 4e+n), read in place by the GPU.
 #include <algorithm>
 #include <atomic>
 #include <cstdarg>
@@ -57,7 +59,8 @@ struct mh_runner {
   std::atomic<uint32_t> gen{0};
   std::atomic<int> arrived{0};
   std::atomic<bool> quit{false};
-  int phase = 0;  // 0 = reset, 1 = step A, 2 = copy B
+  bool fixed = false;
+  int phase = 0;  // 0 = reset, 1 = step A (+ B when fixed), 2 = copy B
   const int32_t *a_idx = nullptr, *r_idx = nullptr;
   uint8_t *staging = nullptr;
   int32_t *push_offset = nullptr, *push_count = nullptr;
@@ -106,9 +109,13 @@ struct mh_runner {
         }
         reward[i] = rs;
         over[i] = term ? 1.f : 0.f;
+        if (fixed) {
+          push_offset[i] = 4 * i;
+          push_count[i] = std::min(e.npush, 4);
+        }
       }
     }
-    if (phase == 0 || phase == 2) {
+    if (phase == 0 || phase == 2 || fixed) {
       for (int i = b0; i < b1; ++i) {
         const Env &e = env[i];
         const int n = std::min(e.npush, 4);
@@ -181,13 +188,14 @@ extern "C" const char *mh_last_error(void) { return g_err; }
 extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_rep, int n_reps,
                                 const uint8_t *screens, int ring, size_t frame_bytes,
                                 const float *rewards, int reward_len, int episode_len,
-                                const int32_t *row_select, int n_rows, mh_runner **out) {
+                                const int32_t *row_select, int n_rows, int flags, mh_runner **out) {
   if (!out || !tab_rep || !screens || !rewards) {
     set_error("null argument");
     return 1;
   }
   if (n_envs < 1 || n_workers < 1 || n_reps < 1 || ring < 2 || frame_bytes == 0 ||
-      reward_len < 1 || episode_len < 1 || frame_bytes % 210 != 0 || n_rows < 0) {
+      reward_len < 1 || episode_len < 1 || frame_bytes % 210 != 0 || n_rows < 0 ||
+      (flags & ~MH_RUNNER_FIXED_SLOTS) != 0) {
     set_error("bad sizes");
     return 1;
   }
@@ -204,6 +212,7 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
   mh_runner *r = new mh_runner();
   r->E = n_envs;
   r->W = std::min(n_workers, n_envs);
+  r->fixed = (flags & MH_RUNNER_FIXED_SLOTS) != 0;
   r->tab.assign(tab_rep, tab_rep + n_reps);
   r->ring = ring;
   r->fb = frame_bytes;
@@ -271,6 +280,10 @@ extern "C" int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t 
   r->reward = reward;
   r->over = over;
   r->dispatch(1);
+  if (r->fixed) {
+    *total_pushes = 4 * r->E;
+    return 0;
+  }
   r->compact(total_pushes);
   r->dispatch(2);
   return 0;

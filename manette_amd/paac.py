@@ -44,6 +44,9 @@ class PAACLearner(ActorLearner):
         self.tab_rep = explo_policy.tab_rep
         self.runner_kind = getattr(args, 'runner', 'native')
         self.sampling = getattr(args, 'sampling', 'host')
+        # native step: kernels read the pinned staging / write the sampled pair in place (zero_copy)
+        # or go through hipMemcpyAsync (copy)
+        self.staging = getattr(args, 'staging', 'zero_copy')
         self.depth = 3 if getattr(args, 'rgb', False) else 1
         self.C = 4 * self.depth
         self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
@@ -93,7 +96,9 @@ class PAACLearner(ActorLearner):
         if self.runner_kind == 'native':
             bank = self.environment_creator.create_bank(0, E)
             # only the 84 screen rows the nearest resize reads are staged and copied (PCIe)
-            self.runners = NativeRunners(bank, self.workers, self.tab_rep, row_select=ROW_LUT)
+            # zero-copy native step: kernels read env e's pushes in place at slots 4e..
+            fixed = self.sampling == 'device' and self.staging == 'zero_copy'
+            self.runners = NativeRunners(bank, self.workers, self.tab_rep, row_select=ROW_LUT, fixed_slots=fixed)
             self.stage_row_lut = torch.arange(84, dtype=torch.int32, device=self.dev)
             self.raw_d = torch.zeros(4 * E, 2, self.runners.frame_bytes, dtype=torch.uint8, device=self.dev)
             self.pair_d = torch.zeros(2, E, dtype=torch.int32, device=self.dev)
@@ -127,7 +132,7 @@ class PAACLearner(ActorLearner):
             p(self.states), p(self.values), p(self.idx), p(self.pi_roll), p(self.rep_roll), p(ws), ws.numel(),
             p(self.counters), p(self.raw_d), r.src_rows, p(self.pair_d), p(self.pair_h), p(self.meta_d),
             p(self.stage_row_lut), p(self.col_lut), p(self.idx_h), p(r.staging), p(r.push_meta), p(r.reward),
-            p(r.over), p(self.rm_h))
+            p(r.over), p(self.rm_h), _lib.MT_ROLLOUT_ZERO_COPY if self.staging == 'zero_copy' else 0)
         h = C.c_void_p()
         _lib.check(_lib.hip().mt_rollout_create(net._h, self.emulator_counts, self.max_local_steps, r._h,
                                                 self.book.handle, C.byref(self._bufs),

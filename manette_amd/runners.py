@@ -1,8 +1,9 @@
 """Host-side emulator runners (A1): runners.py:7-50 + emulator_runner.py:19-42.
 
 NativeRunners  — the hot path: a libmanette_host.so thread pool steps a native emulator bank
-                 and writes every env's pushed screens into ONE compact pinned staging buffer,
-                 which the learner copies to HBM on its stream for mt_preprocess.
+                 and writes every env's pushed screens into ONE pinned staging buffer: compact
+                 (copied to HBM on the learner's stream for mt_preprocess) or, with
+                 fixed_slots, at slots [4e, 4e+n) for kernels that read it in place.
 Runners        — the reference interface for Python emulators (BaseEnvironment objects,
                  e.g. an ALE wrapper): `ew` worker processes over shared memory, a go-queue per
                  worker and a barrier queue; workers=0 runs the same loop in process.
@@ -24,9 +25,10 @@ def _np(t):
 
 class NativeRunners(object):
     """row_select: screen rows to stage (None = whole 210-row screens). The learner passes the
-    84 rows the nearest resize reads, so only those cross PCIe."""
+    84 rows the nearest resize reads, so only those cross PCIe. fixed_slots: MH_RUNNER_FIXED_SLOTS
+    (env e's pushes at staging slots 4e.., one worker phase per step)."""
 
-    def __init__(self, bank, n_workers, tab_rep, row_select=None):
+    def __init__(self, bank, n_workers, tab_rep, row_select=None, fixed_slots=False):
         self.bank = bank
         self.E = bank.screens.shape[0]
         self.tab = np.ascontiguousarray(np.asarray(tab_rep, dtype=np.int32))
@@ -40,7 +42,8 @@ class NativeRunners(object):
             bank.screens.ctypes.data_as(C.c_void_p), bank.screens.shape[1], bank.frame_bytes,
             bank.rewards.ctypes.data_as(C.c_void_p), bank.rewards.shape[1], bank.episode_len,
             None if self.rows is None else self.rows.ctypes.data_as(C.c_void_p),
-            0 if self.rows is None else len(self.rows), C.byref(h)), 'mh_runner_create')
+            0 if self.rows is None else len(self.rows), 1 if fixed_slots else 0, C.byref(h)), 'mh_runner_create')
+        self.fixed_slots = bool(fixed_slots)
         self._h = h
         pin = torch.cuda.is_available()
         mk = lambda *shape, dtype: torch.zeros(*shape, dtype=dtype, pin_memory=pin)

@@ -207,3 +207,33 @@ def test_native_runner_row_selected_staging():
     finally:
         full.stop()
         rows.stop()
+
+
+def test_native_runner_fixed_slots_match_compact():
+    """MH_RUNNER_FIXED_SLOTS stages env e's pushes at slots 4e.. with the same bytes, counts,
+    rewards and terminals as the compact layout."""
+    from manette_amd.environment import ROW_LUT
+    from manette_amd.runners import NativeRunners
+    from manette_amd.synthetic import SyntheticBank
+    tab = opol.tab_repetitions(10, 11)
+    bank = SyntheticBank(5, 7, episode_len=6)
+    comp = NativeRunners(bank, 2, tab, row_select=ROW_LUT)
+    fix = NativeRunners(bank, 3, tab, row_select=ROW_LUT, fixed_slots=True)
+    try:
+        n1, n2 = comp.reset(), fix.reset()
+        rs = np.random.RandomState(1)
+        for step in range(15):
+            assert n2 == 4 * 7
+            np.testing.assert_array_equal(fix.push_offset.numpy(), 4 * np.arange(7))
+            np.testing.assert_array_equal(comp.push_count.numpy(), fix.push_count.numpy())
+            for e in range(7):
+                o1, o2, c = int(comp.push_offset[e]), 4 * e, int(comp.push_count[e])
+                np.testing.assert_array_equal(comp.staging.numpy()[o1:o1 + c], fix.staging.numpy()[o2:o2 + c])
+            act = rs.randint(0, 6, 7).astype(np.int32)
+            rep = rs.randint(0, 11, 7).astype(np.int32)
+            n1, n2 = comp.step(act, rep), fix.step(act, rep)
+            np.testing.assert_array_equal(comp.reward.numpy(), fix.reward.numpy())
+            np.testing.assert_array_equal(comp.over.numpy(), fix.over.numpy())
+    finally:
+        comp.stop()
+        fix.stop()

@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _learner(tmp, runner, sampling, arch='NIPS', ec=8, game='pong', max_rep=0, nb=1, workers=2, seed=0):
+def _learner(tmp, runner, sampling, arch='NIPS', ec=8, game='pong', max_rep=0, nb=1, workers=2, seed=0,
+             staging='zero_copy'):
     sys.path.insert(0, ROOT)
     import train as cli
     from manette_amd.exploration_policy import ExplorationPolicy
@@ -21,7 +22,7 @@ def _learner(tmp, runner, sampling, arch='NIPS', ec=8, game='pong', max_rep=0, n
     a = cli.get_arg_parser().parse_args([])
     a.game, a.arch, a.emulator_counts, a.emulator_workers = game, arch, ec, workers
     a.max_repetition, a.nb_choices = max_rep, nb
-    a.runner, a.sampling, a.seed = runner, sampling, seed
+    a.runner, a.sampling, a.seed, a.staging = runner, sampling, seed, staging
     a.debugging_folder = str(tmp) + '/'
     a.max_global_steps = 1 << 40
     a.checkpoint_interval = 1 << 40
@@ -48,10 +49,12 @@ def _state(L):
                 states=L.states.cpu().numpy().copy(), gs=L.global_step, episodes=list(L.book.episodes))
 
 
-@pytest.mark.parametrize('max_rep,nb', [(0, 1), (10, 11)])
-def test_native_step_equals_python_step(tmp_path, max_rep, nb):
-    """mt_rollout_step (C++ orchestration) == the Python step() on the same kernels."""
-    A = _learner(tmp_path / 'a', 'native', 'device', max_rep=max_rep, nb=nb)
+@pytest.mark.parametrize('max_rep,nb,staging', [(0, 1, 'zero_copy'), (10, 11, 'zero_copy'), (10, 11, 'copy')])
+def test_native_step_equals_python_step(tmp_path, max_rep, nb, staging):
+    """mt_rollout_step (C++ orchestration, sampling fused in the heads kernel, zero-copy or
+    copied staging) == the Python step() on the standalone kernels (mt_forward, mt_sample,
+    hipMemcpy + mt_preprocess)."""
+    A = _learner(tmp_path / 'a', 'native', 'device', max_rep=max_rep, nb=nb, staging=staging)
     assert A.native_step is not None
     _run(A, 6)
     sa = _state(A)

@@ -1,7 +1,8 @@
 """Training CLI: the flags, defaults, args.json and signal handling of the reference's train.py
 (train.py:1-130), driving the MI355X learner (manette_amd.paac.PAACLearner).
 
-Extra flags (this build only): --runner {native,python}, --sampling {host,device}, --seed.
+Extra flags (this build only): --runner {native,python}, --sampling {host,device},
+--staging {zero_copy,copy}, --seed.
 Multi-GPU: launch one process per GPU with torch.distributed.run; each rank trains
 -ec emulators of its own (global env ids offset by rank) and gradients are all-reduced.
 """
@@ -128,6 +129,7 @@ def get_arg_parser():
     parser.add_argument('--alpha_leaky_relu', default=0.1, type=float, help="coef for leaky relu", dest="alpha_leaky_relu")
     # this build
     parser.add_argument('--runner', default='native', choices=['native', 'python'], help='native: C++ emulator threads + GPU preprocess; python: reference-contract emulator processes', dest='runner')
+    parser.add_argument('--staging', default='zero_copy', choices=['zero_copy', 'copy'], help='native device-sampling step: kernels read pinned screens in place (zero_copy) or via hipMemcpyAsync (copy)', dest='staging')
     parser.add_argument('--sampling', default='host', choices=['host', 'device'], help='host: numpy multinomial (reference stream); device: mt_sample', dest='sampling')
     parser.add_argument('--seed', default=0, type=int, help='parameter init / device sampling seed', dest='seed')
     return parser
