@@ -16,7 +16,7 @@ run() {  # name seconds cmd...
 for step in ${STEPS:-smoke tests bench}; do
   case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 900 python -m pytest tests -q -m gpu ;;
+    tests) run tests 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof) run prof 600 bash tools/prof.sh ${PROF_NAME:-prof} ;;
   esac
