@@ -153,7 +153,8 @@ def main():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--step_impl', default='native', choices=['native', 'python'],
                     help='macro-step orchestration: native (mt_rollout_step) or Python')
-    ap.add_argument('--staging', default='zero_copy', choices=['zero_copy', 'copy'])
+    ap.add_argument('--staging', default='in_place', choices=['in_place', 'zero_copy', 'copy', 'pooled'])
+    ap.add_argument('--pipeline', action='store_true', help='MT_ROLLOUT_PIPELINED native step')
     a = ap.parse_args()
 
     import torch
@@ -169,6 +170,7 @@ def main():
     args = build_args(cfg, T, a.sampling, a.seed)
     args.env_id_offset = rank * cfg['ec']
     args.staging = a.staging
+    args.pipeline = a.pipeline
 
     from manette_amd.exploration_policy import ExplorationPolicy
     from manette_amd.paac import PAACLearner
@@ -229,7 +231,7 @@ def main():
         s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s_ev.record()
         learner.network.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
-                                ws_key='rollout')
+                                ws_key='rollout', infer=True)
         e_ev.record()
         fw.append((s_ev, e_ev))
     torch.cuda.synchronize()
@@ -261,8 +263,8 @@ def main():
             'vs_baseline': None,
             'dtype': 'fp32',
             'data': 'synthetic (seeded 210x160 screens, native emulator threads, GPU preprocess)',
-            'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step, %s staging' % (
-                a.config, ec, cfg['ew'], T, a.sampling, a.step_impl, a.staging), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
+            'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step, %s staging%s' % (
+                a.config, ec, cfg['ew'], T, a.sampling, a.step_impl, a.staging, ', pipelined' if a.pipeline else ''), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
                 'global_emulators': ec * world, 'parallelism': 'dp%d' % world},
             'roofline': {'bound': 'mfma', 'kernel': 'train pass (fwd+bwd, %d rows)' % N,
                          'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',

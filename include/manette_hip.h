@@ -88,6 +88,14 @@ int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes);
 int mt_forward(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                size_t ws_bytes, float *v, float *pi, float *rep, mt_stream_t stream);
 
+/* ---- inference forward (rollout steps, bootstrap V(s_T)) -----------------------------------
+ * Same outputs as mt_forward (paac.py:144-146, :219-224) but keeps no activations for a backward
+ * pass, so the NIPS arch runs its fused trunk (conv1 -> conv2 -> dense partials in one launch,
+ * manette_amd/csrc/trunk_fused.h) followed by the heads kernel; other arches take mt_forward's
+ * layered path. Same workspace size as mt_forward. */
+int mt_forward_infer(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
+                     size_t ws_bytes, float *v, float *pi, float *rep, mt_stream_t stream);
+
 /* ---- device multinomial sampling (perf mode of A3) -----------------------------------------
  * Replaces ExplorationPolicy.multinomial_choose (exploration_policy.py:108-116) with an
  * inverse-CDF draw on (p - float32 epsneg), the last category taking the remainder — the
@@ -150,6 +158,24 @@ int mt_preprocess(const uint8_t *raw, const int32_t *push_offset, const int32_t 
                   int E, int depth, int src_rows, const int32_t *row_lut, const int32_t *col_lut,
                   const uint8_t *prev, uint8_t *out, mt_stream_t stream);
 
+/* Pooled variant: each staging slot holds ONE screen per push, max(f0, f1) already taken on the
+ * host by the emulator's frame pool (mh_runner MH_RUNNER_POOLED): raw = [slots][src_rows][160][depth]. */
+int mt_preprocess_pooled(const uint8_t *raw, const int32_t *push_offset, const int32_t *push_count,
+                         int E, int depth, int src_rows, const int32_t *row_lut, const int32_t *col_lut,
+                         const uint8_t *prev, uint8_t *out, mt_stream_t stream);
+
+/* In-place variant (MT_ROLLOUT_IN_PLACE): the pushes' screens are read where the emulators left
+ * them. screens = a bank of whole 210-row screens [..][210][160][depth] (pinned + device-mapped
+ * host memory, or device memory); push j's frame f of env e is screen frame_idx[e*8 + 2j + f]
+ * (j < push_count[e]), as mh_runner_step_frames writes them (include/manette_host.h). Only the
+ * 84 rows row_lut names are read. */
+int mt_preprocess_frames(const uint8_t *screens, const int32_t *frame_idx, const int32_t *push_count,
+                         int E, int depth, const int32_t *row_lut, const int32_t *col_lut,
+                         const uint8_t *prev, uint8_t *out, mt_stream_t stream);
+
+/* Device address of pinned (page-locked, mapped) host memory, e.g. an emulator screen bank. */
+int mt_host_device_pointer(void *host, void **dev);
+
 /* ---- native rollout macro-step (orchestrates A1-A3, A8; paac.py:140-205) -------------------
  * One call = one macro-step t of every env: mt_forward on state slot t with the A3 draw fused
  * into its heads kernel (indices into idx[0][t], idx[1][t] and the [2][E] pair) -> wait for the
@@ -157,11 +183,24 @@ int mt_preprocess(const uint8_t *raw, const int32_t *push_offset, const int32_t 
  * libmanette_host.so) -> mh_book_step (bookkeeping into rm_host[.][t]) -> mt_preprocess of the
  * pushed screens into state slot t+1.
  * flags = 0: the pair is copied D2H and the screens + push metadata H2D (hipMemcpyAsync).
+ * flags & MT_ROLLOUT_IN_PLACE (implies ZERO_COPY): no screen is staged at all — the emulators run
+ * mh_runner_step_frames and mt_preprocess_frames reads their screens in place: staging_host is
+ * then the emulators' screen bank (pinned, device-mapped), frames_host [E][8] the frame indices
+ * and meta_host[E..2E) the push counts.
  * flags & MT_ROLLOUT_ZERO_COPY: the heads kernel writes the pair into pair_host and the
  * preprocess kernel reads staging_host / meta_host in place (host-mapped pinned memory): no
  * copy engine and no cross-engine wait on the per-step critical path; raw / meta / pair may then
  * be null. All buffers are caller-owned; `runner` / `book` are mh_runner* / mh_book* handles. */
 #define MT_ROLLOUT_ZERO_COPY 1
+#define MT_ROLLOUT_IN_PLACE 2
+/* flags & MT_ROLLOUT_POOLED: the runner stages ONE pooled screen per push (MH_RUNNER_POOLED) and the
+ * preprocess is mt_preprocess_pooled. */
+#define MT_ROLLOUT_POOLED 4
+/* flags & MT_ROLLOUT_PIPELINED (needs ZERO_COPY or IN_PLACE): each call enqueues step t+1's chain
+ * (a bounded device wait on sync_host[0], preprocess, forward + draw) before it waits for step t's
+ * indices, and after the emulators only stores the step word — no launch on the critical path.
+ * sync_host = [2] uint32 pinned + mapped: [0] host step word, [1] device wait timeout status. */
+#define MT_ROLLOUT_PIPELINED 8
 typedef struct mt_rollout mt_rollout;
 typedef struct mt_rollout_buffers {
   /* device */
@@ -184,6 +223,8 @@ typedef struct mt_rollout_buffers {
   int32_t *meta_host;          /* [2][E] */
   float *reward_host, *over_host; /* [E] */
   float *rm_host;              /* [2][T][E]: clipped rewards; masks */
+  int32_t *frames_host;        /* [E][8] in-place frame indices (MT_ROLLOUT_IN_PLACE), else NULL */
+  uint32_t *sync_host;         /* [2] pipelined step word + wait status (MT_ROLLOUT_PIPELINED), else NULL */
   int32_t flags;               /* MT_ROLLOUT_* */
 } mt_rollout_buffers;
 int mt_rollout_create(const mt_net *net, int E, int T, void *runner, void *book,

@@ -38,6 +38,10 @@ const char *mh_last_error(void);
  * (MT_ROLLOUT_ZERO_COPY). Otherwise the slots are compacted env-major (a prefix sum between
  * two worker phases) so a copy engine moves only the pushed screens. */
 #define MH_RUNNER_FIXED_SLOTS 1
+/* flags & MH_RUNNER_POOLED: each staging slot holds ONE screen per push, max(f0, f1) of its two
+ * screens (the emulator's FramePool, atari_emulator.py:79-88), so half the bytes cross PCIe;
+ * staging must hold 4*E slots of one staged screen. */
+#define MH_RUNNER_POOLED 2
 int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_rep, int n_reps,
                      const uint8_t *screens, int ring, size_t frame_bytes, const float *rewards,
                      int reward_len, int episode_len, const int32_t *row_select, int n_rows,
@@ -50,7 +54,8 @@ int mh_runner_reset(mh_runner *r, uint8_t *staging, int32_t *push_offset, int32_
 
 /* One macro-step (emulator_runner.py:24-41) of every env with action a_idx[e] repeated
  * tab_rep[r_idx[e]] more times unless the episode ends. Outputs:
- *   staging      [total_pushes][2][staged frame]: screens of the last <=4 pushes of each env,
+ *   staging      [total_pushes][2][staged frame] ([total_pushes][staged frame] pooled): screens
+ *                of the last <=4 pushes of each env,
  *                env-major, oldest first (a terminal's reset pushes included);
  *   push_offset  [E] first staging slot of env e; push_count [E] in 1..4;
  *   reward       [E] float32 sum over the repeats (shared float32 array semantics);
@@ -59,6 +64,16 @@ int mh_runner_reset(mh_runner *r, uint8_t *staging, int32_t *push_offset, int32_
 int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx, uint8_t *staging,
                    int32_t *push_offset, int32_t *push_count, float *reward, float *over,
                    int *total_pushes);
+
+/* In-place frames: the same macro-step (and reset), but no screen is copied. Per env e,
+ * push_count[e] in 1..4 and frame_idx[e*8 + 2j + f] (j < push_count[e], f = 0, 1) = index of the
+ * f-th pooled screen of push j (oldest first) in the `screens` bank given to mh_runner_create,
+ * i.e. the screen starts at screens + frame_idx * frame_bytes. A consumer that reads the bank in
+ * place (mt_preprocess_frames on a pinned, device-mapped bank) must finish before the emulators
+ * overwrite those ring slots; the synchronous PAAC step guarantees it for ring >= 16. */
+int mh_runner_reset_frames(mh_runner *r, int32_t *frame_idx, int32_t *push_count);
+int mh_runner_step_frames(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx, int32_t *frame_idx,
+                          int32_t *push_count, float *reward, float *over);
 
 /* Per-env counters (for tests): k (next() calls incl. reset pushes) and steps in episode. */
 int mh_runner_env_state(const mh_runner *r, int e, int64_t *k, int32_t *steps);

@@ -26,10 +26,15 @@ class mt_rollout_buffers(C.Structure):
                [(n, C.c_void_p) for n in ('counters', 'raw')] + [('src_rows', C.c_int32)] + \
                [(n, C.c_void_p) for n in ('pair', 'pair_host', 'meta', 'row_lut', 'col_lut', 'idx_host',
                                           'staging_host', 'meta_host', 'reward_host', 'over_host',
-                                          'rm_host')] + [('flags', C.c_int32)]
+                                          'rm_host', 'frames_host', 'sync_host')] + [('flags', C.c_int32)]
 
 
 MT_ROLLOUT_ZERO_COPY = 1
+MT_ROLLOUT_IN_PLACE = 2
+MT_ROLLOUT_POOLED = 4
+MT_ROLLOUT_PIPELINED = 8
+MH_RUNNER_FIXED_SLOTS = 1
+MH_RUNNER_POOLED = 2
 
 
 class mt_net_config(C.Structure):
@@ -55,12 +60,16 @@ _HIP_SIGS = {
     'mt_net_feature_dim': (_I, [_P, C.POINTER(_I)]),
     'mt_net_workspace_bytes': (_I, [_P, _I, C.POINTER(_SZ)]),
     'mt_forward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P]),
+    'mt_forward_infer': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P]),
     'mt_sample': (_I, [_P, _P, _I, _I, _I, C.c_uint64, _P, _P, _P, _P, _P]),
     'mt_returns': (_I, [_P, _P, _P, _P, C.c_double, _I, _I, _P, _P, _P]),
     'mt_loss_backward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
     'mt_grad_sumsq': (_I, [_P, _SZ, _F, _P, _P]),
     'mt_clip_rmsprop': (_I, [_P, _P, _P, _P, _SZ, _P, _P, _F, _F, _F, _F, _I, _F, _P, _P]),
     'mt_preprocess': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
+    'mt_preprocess_pooled': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
+    'mt_preprocess_frames': (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    'mt_host_device_pointer': (_I, [_P, C.POINTER(_P)]),
     'mt_sum_slabs': (_I, [_P, _I, _SZ, _P, _P]),
     'mt_net_get_config': (_I, [_P, C.POINTER(mt_net_config)]),
     'mt_rollout_create': (_I, [_P, _I, _I, _P, _P, C.POINTER(mt_rollout_buffers), C.c_uint64, C.POINTER(_P)]),
@@ -79,6 +88,8 @@ _HOST_SIGS = {
     'mh_runner_destroy': (None, [_P]),
     'mh_runner_reset': (_I, [_P, _P, _P, _P, C.POINTER(_I)]),
     'mh_runner_step': (_I, [_P, _P, _P, _P, _P, _P, _P, _P, C.POINTER(_I)]),
+    'mh_runner_reset_frames': (_I, [_P, _P, _P]),
+    'mh_runner_step_frames': (_I, [_P, _P, _P, _P, _P, _P, _P]),
     'mh_runner_env_state': (_I, [_P, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     'mh_book_create': (_I, [_I, _I, _P, _I, C.POINTER(_P)]),
     'mh_book_destroy': (None, [_P]),

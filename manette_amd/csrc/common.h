@@ -104,6 +104,6 @@ struct mt_net;
 namespace mt {
 // forward (mt_forward) with the A3 draw fused into the heads kernel; smp may be null.
 int forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
-                   size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp,
+                   size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp, bool infer,
                    hipStream_t stream);
 }  // namespace mt

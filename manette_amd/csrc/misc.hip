@@ -127,7 +127,14 @@ constexpr int kPreRows = 12;  // 84 = 7 x 12
 
 typedef unsigned char u8x16 __attribute__((ext_vector_type(16)));
 
-template <int DEPTH>
+// Source of push j of env e, by mode:
+//   kSrcPairs   staging slot push_offset[e] + j holds the push's two SH-row screens;
+//   kSrcPooled  staging slot push_offset[e] + j holds ONE SH-row screen, max(f0, f1) already
+//               taken by the emulator's frame pool on the host (mt_preprocess_pooled);
+//   kSrcBank    frames read where the emulators left them: frame f is screen frame_idx[e*8+2j+f]
+//               of a bank of whole 210-row screens (mt_preprocess_frames).
+enum { kSrcPairs = 0, kSrcPooled = 1, kSrcBank = 2 };
+template <int DEPTH, int SRC>
 __global__ __launch_bounds__(256) void preprocess_kernel(
     const uint8_t *__restrict__ raw, const int32_t *__restrict__ push_offset,
     const int32_t *__restrict__ push_count, int SH, const int32_t *__restrict__ row_lut,
@@ -137,19 +144,33 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
   constexpr int C = 4 * DEPTH;
   __shared__ u8x16 pooled[4][kPreRows][Q];
   __shared__ int rl[kPreRows], cl[84];
+  __shared__ size_t foff[8];  // byte offset of (push j, frame f) = foff[2j + f]
   const int e = blockIdx.y, y0 = blockIdx.x * kPreRows;
   const int p = min(max(push_count[e], 1), 4);
-  const size_t FR = (size_t)SH * ROWB;  // one staged screen
-  const uint8_t *base = raw + (size_t)push_offset[e] * 2 * FR;
+  const size_t FR = (size_t)SH * ROWB;  // one screen
   if (threadIdx.x < kPreRows) rl[threadIdx.x] = row_lut[y0 + threadIdx.x];
   if (threadIdx.x < 84) cl[threadIdx.x] = col_lut[threadIdx.x];
+  if (threadIdx.x < 8) {
+    const int j = threadIdx.x >> 1, f = threadIdx.x & 1;
+    if constexpr (SRC == kSrcBank)
+      foff[threadIdx.x] = j < p ? (size_t)push_offset[e * 8 + threadIdx.x] * FR : 0;
+    else if constexpr (SRC == kSrcPooled)
+      foff[threadIdx.x] = ((size_t)push_offset[e] + j) * FR;
+    else
+      foff[threadIdx.x] = ((size_t)push_offset[e] + j) * 2 * FR + f * FR;
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < p * kPreRows * Q; i += 256) {
     const int j = i / (kPreRows * Q), rem = i - j * (kPreRows * Q);
     const int r = rem / Q, q = rem - r * Q;
-    const u8x16 *f0 = reinterpret_cast<const u8x16 *>(base + j * 2 * FR + (size_t)rl[r] * ROWB) + q;
-    const u8x16 a = f0[0], b = f0[FR / 16];
-    pooled[j][r][q] = __builtin_elementwise_max(a, b);  // np.amax over the 2-frame pool
+    const size_t ro = (size_t)rl[r] * ROWB;
+    const u8x16 a = reinterpret_cast<const u8x16 *>(raw + foff[2 * j] + ro)[q];
+    if constexpr (SRC == kSrcPooled) {
+      pooled[j][r][q] = a;
+    } else {
+      const u8x16 b = reinterpret_cast<const u8x16 *>(raw + foff[2 * j + 1] + ro)[q];
+      pooled[j][r][q] = __builtin_elementwise_max(a, b);  // np.amax over the 2-frame pool
+    }
   }
   __syncthreads();
   const uint8_t *pl = reinterpret_cast<const uint8_t *>(&pooled[0][0][0]);
@@ -244,16 +265,69 @@ extern "C" int mt_preprocess(const uint8_t *raw, const int32_t *push_offset,
   MT_CHECK_ARG(((uintptr_t)raw & 15) == 0, "raw must be 16-byte aligned");
   const dim3 grid(84 / kPreRows, E);
   if (depth == 1) {
-    hipLaunchKernelGGL(preprocess_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, raw, push_offset,
+    hipLaunchKernelGGL((preprocess_kernel<1, kSrcPairs>), grid, dim3(256), 0, (hipStream_t)stream, raw, push_offset,
                        push_count, src_rows, row_lut, col_lut, prev, out);
   } else if (depth == 3) {
-    hipLaunchKernelGGL(preprocess_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, raw, push_offset,
+    hipLaunchKernelGGL((preprocess_kernel<3, kSrcPairs>), grid, dim3(256), 0, (hipStream_t)stream, raw, push_offset,
                        push_count, src_rows, row_lut, col_lut, prev, out);
   } else {
     set_error("depth must be 1 or 3");
     return MT_ERR_ARG;
   }
   MT_LAUNCHED();
+  return MT_OK;
+}
+
+extern "C" int mt_preprocess_pooled(const uint8_t *raw, const int32_t *push_offset,
+                                    const int32_t *push_count, int E, int depth, int src_rows,
+                                    const int32_t *row_lut, const int32_t *col_lut, const uint8_t *prev,
+                                    uint8_t *out, mt_stream_t stream) {
+  MT_CHECK_ARG(raw && push_offset && push_count && row_lut && col_lut && prev && out, "null argument");
+  MT_CHECK_ARG(E >= 1, "E must be >= 1");
+  MT_CHECK_ARG(src_rows >= 84 && src_rows <= 210, "src_rows must be in [84, 210]");
+  MT_CHECK_ARG(prev != out, "out may not alias prev");
+  MT_CHECK_ARG(((uintptr_t)raw & 15) == 0, "raw must be 16-byte aligned");
+  const dim3 grid(84 / kPreRows, E);
+  if (depth == 1) {
+    hipLaunchKernelGGL((preprocess_kernel<1, kSrcPooled>), grid, dim3(256), 0, (hipStream_t)stream, raw, push_offset,
+                       push_count, src_rows, row_lut, col_lut, prev, out);
+  } else if (depth == 3) {
+    hipLaunchKernelGGL((preprocess_kernel<3, kSrcPooled>), grid, dim3(256), 0, (hipStream_t)stream, raw, push_offset,
+                       push_count, src_rows, row_lut, col_lut, prev, out);
+  } else {
+    set_error("depth must be 1 or 3");
+    return MT_ERR_ARG;
+  }
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+extern "C" int mt_preprocess_frames(const uint8_t *screens, const int32_t *frame_idx,
+                                    const int32_t *push_count, int E, int depth, const int32_t *row_lut,
+                                    const int32_t *col_lut, const uint8_t *prev, uint8_t *out,
+                                    mt_stream_t stream) {
+  MT_CHECK_ARG(screens && frame_idx && push_count && row_lut && col_lut && prev && out, "null argument");
+  MT_CHECK_ARG(E >= 1, "E must be >= 1");
+  MT_CHECK_ARG(prev != out, "out may not alias prev");
+  MT_CHECK_ARG(((uintptr_t)screens & 15) == 0, "screens must be 16-byte aligned");
+  const dim3 grid(84 / kPreRows, E);
+  if (depth == 1) {
+    hipLaunchKernelGGL((preprocess_kernel<1, kSrcBank>), grid, dim3(256), 0, (hipStream_t)stream, screens, frame_idx,
+                       push_count, 210, row_lut, col_lut, prev, out);
+  } else if (depth == 3) {
+    hipLaunchKernelGGL((preprocess_kernel<3, kSrcBank>), grid, dim3(256), 0, (hipStream_t)stream, screens, frame_idx,
+                       push_count, 210, row_lut, col_lut, prev, out);
+  } else {
+    set_error("depth must be 1 or 3");
+    return MT_ERR_ARG;
+  }
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+extern "C" int mt_host_device_pointer(void *host, void **dev) {
+  MT_CHECK_ARG(host && dev, "null argument");
+  MT_HIP(hipHostGetDevicePointer(dev, host, 0));
   return MT_OK;
 }
 

@@ -11,6 +11,7 @@
 #include <tuple>
 
 #include "gemm.h"
+#include "trunk_fused.h"
 
 namespace mt {
 
@@ -26,6 +27,7 @@ struct NipsArch {  // networks.py:178-192
   static constexpr int FLAT = 9 * 9 * 32;  // 2592
   static constexpr int F = 256;
   static constexpr const char *FC = "fc3";
+  static constexpr int FUSED_SLABS = FusedNips<C>::ROWS2;  // inference forward: trunk_fused.h
 };
 template <int C>
 struct NatureArch {  // networks.py:261-278
@@ -36,6 +38,7 @@ struct NatureArch {  // networks.py:261-278
   static constexpr int FLAT = 7 * 7 * 64;  // 3136
   static constexpr int F = 512;
   static constexpr const char *FC = "fc4";
+  static constexpr int FUSED_SLABS = 0;  // no fused inference trunk: layered path
 };
 template <int C>
 struct PwyxArch {  // networks.py:206-225: SAME convs, 2x2 pools after conv1-3
@@ -46,6 +49,7 @@ struct PwyxArch {  // networks.py:206-225: SAME convs, 2x2 pools after conv1-3
   static constexpr int FLAT = 10 * 10 * 64;  // 6400
   static constexpr int F = 512;
   static constexpr const char *FC = "fc5";
+  static constexpr int FUSED_SLABS = 0;
 };
 
 template <class Ar, int I>
@@ -254,7 +258,7 @@ static WsLayout ws_layout(const mt_net *n, int B) {
   size_t wslab = 0;
   ws_layers<Ar>(L, off, B, wslab);
   L.fc_splits = fc_splits<Ar>(B, Ar::F);
-  L.fcslab = take((size_t)L.fc_splits * B * Ar::F);
+  L.fcslab = take((size_t)std::max(L.fc_splits, Ar::FUSED_SLABS) * B * Ar::F);
   L.H = take((size_t)B * Ar::F);
   L.dz = take((size_t)B * n->O);
   L.dH = take((size_t)B * Ar::F);
@@ -717,6 +721,31 @@ static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int
   return MT_OK;
 }
 
+// Inference forward (rollout steps, bootstrap): the fused trunk where the arch has one
+// (trunk_fused.h), whose 9 conv2-row slabs heads_fwd_kernel finishes; else the layered forward.
+template <class Ar>
+static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
+                              float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s) {
+  if constexpr (Ar::FUSED_SLABS > 0) {
+    constexpr int C = LayerG<Ar, 0>::CIN;
+    using Fz = FusedNips<C>;
+    const WsLayout L = ws_layout<Ar>(n, B);
+    const float *Wfc = P + n->off_fc;
+    hipLaunchKernelGGL(nips_fused_trunk_kernel<C>, dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, obs, B,
+                       P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation, n->cfg.alpha_leaky,
+                       ws + L.fcslab);
+    MT_LAUNCHED();
+    HeadParams hp = head_params(n, P);
+    hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, Fz::ROWS2, B,
+                       Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp,
+                       n->cfg.softmax_temp, ws + L.H, v, pi, rep, smp ? *smp : SampleArgs{});
+    MT_LAUNCHED();
+    return MT_OK;
+  } else {
+    return forward_impl<Ar>(n, P, obs, B, ws, v, pi, rep, smp, s);
+  }
+}
+
 template <class Ar>
 static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
                          const float *pi, const float *rep, const float *v, const int32_t *a_idx,
@@ -870,13 +899,20 @@ extern "C" int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *byte
 extern "C" int mt_forward(const mt_net *net, const float *params, const uint8_t *obs, int batch,
                           void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
                           mt_stream_t stream) {
-  return mt::forward_sample(net, params, obs, batch, ws, ws_bytes, v, pi, rep, nullptr,
+  return mt::forward_sample(net, params, obs, batch, ws, ws_bytes, v, pi, rep, nullptr, false,
+                            (hipStream_t)stream);
+}
+
+extern "C" int mt_forward_infer(const mt_net *net, const float *params, const uint8_t *obs, int batch,
+                                void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
+                                mt_stream_t stream) {
+  return mt::forward_sample(net, params, obs, batch, ws, ws_bytes, v, pi, rep, nullptr, true,
                             (hipStream_t)stream);
 }
 
 int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch,
                        void *ws, size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp,
-                       hipStream_t stream) {
+                       bool infer, hipStream_t stream) {
   MT_CHECK_ARG(net && params && obs && ws && v && pi && rep, "null argument");
   MT_CHECK_ARG(!smp || (smp->counters && smp->a_idx && smp->r_idx), "null sample buffer");
   MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
@@ -886,7 +922,8 @@ int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *ob
       set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
       return MT_ERR_WORKSPACE;
     }
-    return forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
+    return infer ? forward_infer_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream)
+                 : forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
   });
   return MT_OK;
 }

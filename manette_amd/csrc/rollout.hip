@@ -18,10 +18,13 @@ struct mt_rollout {
   mh_book *book;
   mt_rollout_buffers b;
   uint64_t seed;
-  hipEvent_t ev;
-  bool zero_copy;
+  hipEvent_t ev2[2];  // pair of step t ready: ev2[t & 1]
+  bool zero_copy, in_place, pooled, pipelined;
+  int armed = -1;     // step whose forward is already enqueued (pipelined), else -1
+  uint32_t seq = 0;   // host step sequence word value last stored
   uint8_t *staging_dev;  // device addresses of the host-mapped buffers (zero-copy mode)
-  int32_t *meta_dev, *pair_dev;
+  int32_t *meta_dev, *pair_dev, *frames_dev;
+  uint32_t *seq_dev, *status_dev;
   double acc[5];  // host wall us: launch+wait for indices, runner, book, upload+preprocess enqueue; steps
 };
 
@@ -33,18 +36,32 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   MT_CHECK_ARG(net && runner && book && buffers && out, "null argument");
   MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
   const mt_rollout_buffers &b = *buffers;
-  const bool zc = (b.flags & MT_ROLLOUT_ZERO_COPY) != 0;
-  MT_CHECK_ARG((b.flags & ~MT_ROLLOUT_ZERO_COPY) == 0, "unknown rollout flags %d", b.flags);
+  const bool ip = (b.flags & MT_ROLLOUT_IN_PLACE) != 0;
+  const bool zc = ip || (b.flags & MT_ROLLOUT_ZERO_COPY) != 0;
+  const bool pl = (b.flags & MT_ROLLOUT_PIPELINED) != 0;
+  const bool po = (b.flags & MT_ROLLOUT_POOLED) != 0;
+  MT_CHECK_ARG((b.flags & ~(MT_ROLLOUT_ZERO_COPY | MT_ROLLOUT_IN_PLACE | MT_ROLLOUT_POOLED | MT_ROLLOUT_PIPELINED)) == 0,
+               "unknown rollout flags %d", b.flags);
+  MT_CHECK_ARG(!ip || b.frames_host, "in-place rollout needs frames_host");
+  MT_CHECK_ARG(!ip || !po, "in-place and pooled staging are exclusive");
+  MT_CHECK_ARG(!pl || (zc && b.sync_host), "pipelined rollout needs zero-copy or in-place screens and sync_host");
   MT_CHECK_ARG(b.states && b.values && b.idx && b.pi && b.rep && b.ws && b.counters &&
                    (zc || (b.raw && b.meta && b.pair)) && b.row_lut && b.col_lut && b.idx_host &&
                    b.staging_host && b.pair_host && b.src_rows >= 84 && b.src_rows <= 210 &&
                    b.meta_host && b.reward_host && b.over_host && b.rm_host,
                "null buffer");
-  void *staging_dev = nullptr, *meta_dev = nullptr, *pair_dev = nullptr;
-  if (zc) {  // the three buffers must be pinned + mapped (hipHostMalloc / torch pin_memory)
+  void *staging_dev = nullptr, *meta_dev = nullptr, *pair_dev = nullptr, *frames_dev = nullptr;
+  if (zc) {  // these buffers must be pinned + mapped (hipHostMalloc / torch pin_memory)
     MT_HIP(hipHostGetDevicePointer(&staging_dev, b.staging_host, 0));
     MT_HIP(hipHostGetDevicePointer(&meta_dev, b.meta_host, 0));
     MT_HIP(hipHostGetDevicePointer(&pair_dev, b.pair_host, 0));
+    if (ip) MT_HIP(hipHostGetDevicePointer(&frames_dev, b.frames_host, 0));
+  }
+  void *sync_dev = nullptr;
+  if (pl) {
+    MT_HIP(hipHostGetDevicePointer(&sync_dev, b.sync_host, 0));
+    b.sync_host[0] = 0;
+    b.sync_host[1] = 0;
   }
   mt_net_config cfg;
   MT_CHECK_ARG(mt_net_get_config(net, &cfg) == MT_OK, "bad net");
@@ -67,14 +84,23 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->b = b;
   ro->seed = seed;
   ro->zero_copy = zc;
+  ro->in_place = ip;
+  ro->pooled = po;
+  ro->pipelined = pl;
+  ro->frames_dev = (int32_t *)frames_dev;
+  ro->seq_dev = (uint32_t *)sync_dev;
+  ro->status_dev = sync_dev ? (uint32_t *)sync_dev + 1 : nullptr;
   ro->staging_dev = (uint8_t *)staging_dev;
   ro->meta_dev = (int32_t *)meta_dev;
   ro->pair_dev = (int32_t *)pair_dev;
-  hipError_t e = hipEventCreateWithFlags(&ro->ev, hipEventDisableTiming);
-  if (e != hipSuccess) {
-    delete ro;
-    set_error("hipEventCreate: %s", hipGetErrorString(e));
-    return MT_ERR_HIP;
+  for (int i = 0; i < 2; ++i) {
+    hipError_t e = hipEventCreateWithFlags(&ro->ev2[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+      if (i) (void)hipEventDestroy(ro->ev2[0]);
+      delete ro;
+      set_error("hipEventCreate: %s", hipGetErrorString(e));
+      return MT_ERR_HIP;
+    }
   }
   *out = ro;
   return MT_OK;
@@ -82,7 +108,8 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
 
 extern "C" void mt_rollout_destroy(mt_rollout *ro) {
   if (!ro) return;
-  (void)hipEventDestroy(ro->ev);
+  (void)hipEventDestroy(ro->ev2[0]);
+  (void)hipEventDestroy(ro->ev2[1]);
   delete ro;
 }
 
@@ -92,6 +119,73 @@ extern "C" void mt_rollout_destroy(mt_rollout *ro) {
     if (rc_ != MT_OK) return rc_;  \
   } while (0)
 
+// Device-side wait for the host's step sequence word (pipelined mode): one lane polls the
+// host-mapped word with system-scope vector loads (never the scalar cache) until it equals seq.
+// Bounded: after ~2 s (s_memrealtime, 100 MHz) it gives up, records the failure in status (the
+// host turns it into an error at its next wait for the indices) and lets the stream drain.
+__global__ void wait_seq_kernel(const uint32_t *seq_word, uint32_t seq, uint32_t *status) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(seq_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+      __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
+}
+
+namespace {
+// forward of state slot t with the A3 draw fused into its heads kernel (paac.py:144-147); the
+// indices land in idx[.][t] and the [2][E] pair; ev[t & 1] marks the pair ready.
+int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s) {
+  const mt_rollout_buffers &b = ro->b;
+  const int E = ro->E, T = ro->T;
+  const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
+  int32_t *a_d = b.idx + (size_t)t * E, *r_d = b.idx + (size_t)T * E + (size_t)t * E;
+  const SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
+  MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)t * slot, E, b.ws, b.ws_bytes,
+                         b.values + (size_t)t * E, b.pi, b.rep, &smp, true, s));
+  if (!ro->zero_copy)
+    MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
+  MT_HIP(hipEventRecord(ro->ev2[t & 1], s));
+  return MT_OK;
+}
+
+// preprocess of the pushes of macro-step t into state slot t+1 (atari_emulator.py:79-124)
+int enqueue_preprocess(mt_rollout *ro, int t, int total, hipStream_t s) {
+  const mt_rollout_buffers &b = ro->b;
+  const int E = ro->E;
+  const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
+  const uint8_t *cur = b.states + (size_t)t * slot;
+  uint8_t *nxt = b.states + (size_t)(t + 1) * slot;
+  mt_stream_t st = (mt_stream_t)s;
+  if (ro->in_place)
+    return mt_preprocess_frames(ro->staging_dev, ro->frames_dev, ro->meta_dev + E, E, ro->depth, b.row_lut,
+                                b.col_lut, cur, nxt, st);
+  const uint8_t *raw = ro->staging_dev;
+  const int32_t *meta = ro->meta_dev;
+  if (!ro->zero_copy) {
+    const size_t per_push = (ro->pooled ? 1 : 2) * ro->frame_bytes;
+    MT_HIP(hipMemcpyAsync(b.raw, b.staging_host, (size_t)total * per_push, hipMemcpyHostToDevice, s));
+    MT_HIP(hipMemcpyAsync(b.meta, b.meta_host, sizeof(int32_t) * 2 * E, hipMemcpyHostToDevice, s));
+    raw = b.raw;
+    meta = b.meta;
+  }
+  return ro->pooled ? mt_preprocess_pooled(raw, meta, meta + E, E, ro->depth, b.src_rows, b.row_lut, b.col_lut,
+                                           cur, nxt, st)
+                    : mt_preprocess(raw, meta, meta + E, E, ro->depth, b.src_rows, b.row_lut, b.col_lut, cur,
+                                    nxt, st);
+}
+}  // namespace
+
+// One macro-step t (paac.py:140-205). Pipelined mode keeps the GPU one step ahead of the host's
+// launch calls: before waiting for step t's indices it enqueues step t+1's chain behind a
+// device-side wait on the host sequence word — wait_seq -> preprocess(t -> t+1) -> forward(t+1)
+// — so when the emulators finish, the host only stores the word and the GPU runs the whole
+// chain without a launch on the critical path. Stream order keeps every buffer hand-off safe:
+// the staging of step t is read by preprocess(t) only after the word, and rewritten by the
+// emulators of step t+1 only after forward(t+1)'s indices (which follow preprocess(t)) arrived.
 extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64_t *global_step,
                                mt_stream_t stream) {
   MT_CHECK_ARG(ro && params && global_step, "null argument");
@@ -100,29 +194,40 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   hipStream_t s = (hipStream_t)stream;
   const int E = ro->E, T = ro->T;
   const double t0 = now_us();
-  const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
-  uint8_t *cur = b.states + (size_t)t * slot;
-  uint8_t *nxt = cur + slot;
-  int32_t *a_d = b.idx + (size_t)t * E, *r_d = b.idx + (size_t)T * E + (size_t)t * E;
   int32_t *a_h = b.idx_host + (size_t)t * E, *r_h = b.idx_host + (size_t)T * E + (size_t)t * E;
-  // 1. policy/value forward + device sampling fused in its heads kernel (paac.py:144-147)
-  const SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
-  MT_TRY_(forward_sample(ro->net, params, cur, E, b.ws, b.ws_bytes, b.values + (size_t)t * E, b.pi,
-                         b.rep, &smp, s));
-  if (!ro->zero_copy)
-    MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
-  MT_HIP(hipEventRecord(ro->ev, s));
-  // spin: a blocking wait sleeps past the ~50 us the chain takes and pays the wake-up latency
+  // 1. forward + draw of step t, unless the previous call already enqueued it
+  if (ro->armed != t) MT_TRY_(enqueue_forward(ro, params, t, s));
+  ro->armed = -1;
+  // 2. pipelined: arm step t+1 while the GPU works on step t
+  if (ro->pipelined) {
+    hipLaunchKernelGGL(wait_seq_kernel, dim3(1), dim3(64), 0, s, ro->seq_dev, ro->seq + 1, ro->status_dev);
+    MT_LAUNCHED();
+    MT_TRY_(enqueue_preprocess(ro, t, 4 * E, s));
+    if (t + 1 < T) {
+      MT_TRY_(enqueue_forward(ro, params, t + 1, s));
+      ro->armed = t + 1;
+    }
+  }
+  // 3. wait for the indices of step t (spin: a blocking wait sleeps past the chain and pays the
+  //    wake-up latency)
   hipError_t q;
-  while ((q = hipEventQuery(ro->ev)) == hipErrorNotReady) __builtin_ia32_pause();
+  while ((q = hipEventQuery(ro->ev2[t & 1])) == hipErrorNotReady) __builtin_ia32_pause();
   MT_HIP(q);
+  if (ro->pipelined && __atomic_load_n(&b.sync_host[1], __ATOMIC_ACQUIRE) != 0) {
+    set_error("device wait for the host step word timed out (host stalled > 2 s); rollout state is invalid");
+    return MT_ERR_HIP;
+  }
   std::memcpy(a_h, b.pair_host, sizeof(int32_t) * E);
   std::memcpy(r_h, b.pair_host + E, sizeof(int32_t) * E);
   const double t1 = now_us();
-  // 2. emulators (runners.py:44-50 / emulator_runner.py:24-41) + bookkeeping (paac.py:176-205)
+  // 4. emulators (runners.py:44-50 / emulator_runner.py:24-41) + bookkeeping (paac.py:176-205)
   int total = 0;
-  if (mh_runner_step(ro->runner, a_h, r_h, b.staging_host, b.meta_host, b.meta_host + E,
-                     b.reward_host, b.over_host, &total) != 0) {
+  const int rs = ro->in_place
+                     ? mh_runner_step_frames(ro->runner, a_h, r_h, b.frames_host, b.meta_host + E, b.reward_host,
+                                             b.over_host)
+                     : mh_runner_step(ro->runner, a_h, r_h, b.staging_host, b.meta_host, b.meta_host + E,
+                                      b.reward_host, b.over_host, &total);
+  if (rs != 0) {
     set_error("mh_runner_step: %s", mh_last_error());
     return MT_ERR_ARG;
   }
@@ -133,18 +238,14 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
     return MT_ERR_ARG;
   }
   const double t3 = now_us();
-  // 3. screens -> preprocess into slot t+1 (atari_emulator.py:79-124)
-  const uint8_t *raw = ro->staging_dev;
-  const int32_t *meta = ro->meta_dev;
-  if (!ro->zero_copy) {
-    MT_HIP(hipMemcpyAsync(b.raw, b.staging_host, (size_t)total * 2 * ro->frame_bytes,
-                          hipMemcpyHostToDevice, s));
-    MT_HIP(hipMemcpyAsync(b.meta, b.meta_host, sizeof(int32_t) * 2 * E, hipMemcpyHostToDevice, s));
-    raw = b.raw;
-    meta = b.meta;
+  // 5. release the armed chain (pipelined), or enqueue the preprocess now
+  int rc = MT_OK;
+  if (ro->pipelined) {
+    ro->seq += 1;
+    __atomic_store_n(&b.sync_host[0], ro->seq, __ATOMIC_RELEASE);
+  } else {
+    rc = enqueue_preprocess(ro, t, total, s);
   }
-  const int rc = mt_preprocess(raw, meta, meta + E, E, ro->depth, b.src_rows, b.row_lut, b.col_lut,
-                               cur, nxt, stream);
   const double t4 = now_us();
   ro->acc[0] += t1 - t0;
   ro->acc[1] += t2 - t1;

@@ -9,9 +9,15 @@
 //   A: each worker steps its envs and records which screens each env pushed (last <= 4);
 //   main: prefix sum of push counts -> compact staging offsets;
 //   B: each worker copies its envs' screens into the staging buffer (pinned, H2D'd whole).
+// Pooled staging (MH_RUNNER_POOLED) stages max(f0, f1) of a push's two screens — the emulator's
+// frame pool — so one screen per push crosses PCIe.
 // Fixed-slot staging (MH_RUNNER_FIXED_SLOTS) does A and B in one phase: env e's screens go to
 // slots [4e, 4e+n), read in place by the GPU.
+// In-place frames (mh_runner_step_frames) copies nothing: each worker writes, per env, the bank
+// indices of the screens its pushes produced, and the GPU reads those screens where the
+// emulators left them (a pinned, device-mapped bank).
 #include <algorithm>
+#include <climits>
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
@@ -60,10 +66,12 @@ struct mh_runner {
   std::atomic<int> arrived{0};
   std::atomic<bool> quit{false};
   bool fixed = false;
+  bool pooled = false;  // stage max(f0, f1) of each push (one screen per slot)
   int phase = 0;  // 0 = reset, 1 = step A (+ B when fixed), 2 = copy B
   const int32_t *a_idx = nullptr, *r_idx = nullptr;
   uint8_t *staging = nullptr;
   int32_t *push_offset = nullptr, *push_count = nullptr;
+  int32_t *frame_idx = nullptr;  // in-place mode: [E][8] bank frame indices (else null)
   float *reward = nullptr, *over = nullptr;
 
   int block_begin(int w) const { return (int)((int64_t)E * w / W); }
@@ -115,12 +123,36 @@ struct mh_runner {
         }
       }
     }
+    if (frame_idx) {  // in place: record where the pushed screens are, oldest first
+      for (int i = b0; i < b1; ++i) {
+        const Env &e = env[i];
+        const int n = std::min(e.npush, 4);
+        push_count[i] = n;
+        for (int j = 0; j < n; ++j) {
+          const int64_t kk = e.last[(e.npush - n + j) & 3];
+          for (int f = 0; f < 2; ++f) frame_idx[i * 8 + 2 * j + f] = (int32_t)(i * ring + (2 * kk + f) % ring);
+        }
+      }
+      return;
+    }
     if (phase == 0 || phase == 2 || fixed) {
       for (int i = b0; i < b1; ++i) {
         const Env &e = env[i];
         const int n = std::min(e.npush, 4);
         for (int j = 0; j < n; ++j) {
           const int64_t kk = e.last[(e.npush - n + j) & 3];
+          if (pooled) {  // FramePool max (atari_emulator.py:79-88) of the staged rows, on the host
+            uint8_t *d = staging + (size_t)(push_offset[i] + j) * sfb;
+            const uint8_t *s0 = e.screens + (size_t)((2 * kk) % ring) * fb;
+            const uint8_t *s1 = e.screens + (size_t)((2 * kk + 1) % ring) * fb;
+            const size_t nr = rows.empty() ? 210 : rows.size();
+            for (size_t q = 0; q < nr; ++q) {
+              const size_t so = (rows.empty() ? q : (size_t)rows[q]) * row_bytes;
+              uint8_t *dq = d + q * row_bytes;
+              for (size_t x = 0; x < row_bytes; ++x) dq[x] = std::max(s0[so + x], s1[so + x]);
+            }
+            continue;
+          }
           uint8_t *dst = staging + (size_t)(push_offset[i] + j) * 2 * sfb;
           for (int f = 0; f < 2; ++f) {
             const uint8_t *src = e.screens + (size_t)((2 * kk + f) % ring) * fb;
@@ -195,7 +227,7 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
   }
   if (n_envs < 1 || n_workers < 1 || n_reps < 1 || ring < 2 || frame_bytes == 0 ||
       reward_len < 1 || episode_len < 1 || frame_bytes % 210 != 0 || n_rows < 0 ||
-      (flags & ~MH_RUNNER_FIXED_SLOTS) != 0) {
+      (flags & ~(MH_RUNNER_FIXED_SLOTS | MH_RUNNER_POOLED)) != 0) {
     set_error("bad sizes");
     return 1;
   }
@@ -213,6 +245,7 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
   r->E = n_envs;
   r->W = std::min(n_workers, n_envs);
   r->fixed = (flags & MH_RUNNER_FIXED_SLOTS) != 0;
+  r->pooled = (flags & MH_RUNNER_POOLED) != 0;
   r->tab.assign(tab_rep, tab_rep + n_reps);
   r->ring = ring;
   r->fb = frame_bytes;
@@ -286,6 +319,52 @@ extern "C" int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t 
   }
   r->compact(total_pushes);
   r->dispatch(2);
+  return 0;
+}
+
+extern "C" int mh_runner_reset_frames(mh_runner *r, int32_t *frame_idx, int32_t *push_count) {
+  if (!r || !frame_idx || !push_count) {
+    set_error("null argument");
+    return 1;
+  }
+  if ((int64_t)r->E * r->ring > INT32_MAX) {
+    set_error("bank too large for int32 frame indices");
+    return 1;
+  }
+  r->frame_idx = frame_idx;
+  r->push_count = push_count;
+  r->dispatch(0);
+  r->frame_idx = nullptr;
+  return 0;
+}
+
+extern "C" int mh_runner_step_frames(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx,
+                                     int32_t *frame_idx, int32_t *push_count, float *reward, float *over) {
+  if (!r || !a_idx || !r_idx || !frame_idx || !push_count || !reward || !over) {
+    set_error("null argument");
+    return 1;
+  }
+  if ((int64_t)r->E * r->ring > INT32_MAX) {
+    set_error("bank too large for int32 frame indices");
+    return 1;
+  }
+  const int nr = (int)r->tab.size();
+  for (int i = 0; i < r->E; ++i)
+    if (r_idx[i] < 0 || r_idx[i] >= nr) {
+      set_error("r_idx[%d] = %d out of range [0,%d)", i, r_idx[i], nr);
+      return 1;
+    }
+  r->a_idx = a_idx;
+  r->r_idx = r_idx;
+  r->frame_idx = frame_idx;
+  r->push_count = push_count;
+  r->reward = reward;
+  r->over = over;
+  const bool fixed = r->fixed;
+  r->fixed = false;  // no staging slots in this mode
+  r->dispatch(1);
+  r->fixed = fixed;
+  r->frame_idx = nullptr;
   return 0;
 }
 

@@ -136,16 +136,18 @@ class DeviceNetwork(object):
         return o
 
     # ---- compute -----------------------------------------------------------------------------
-    def forward(self, obs, batch=None, out=None, ws_key=None):
+    def forward(self, obs, batch=None, out=None, ws_key=None, infer=False):
         """obs: uint8 cuda tensor [B,84,84,4*depth]. Returns (v, pi, rep) device tensors.
-        The activations stay in the workspace of `ws_key or batch` for loss_backward."""
+        The activations stay in the workspace of `ws_key or batch` for loss_backward, unless
+        infer=True (mt_forward_infer: fused trunk where built, nothing kept for a backward)."""
         B = int(batch if batch is not None else obs.shape[0])
         assert obs.dtype == torch.uint8 and obs.is_cuda and obs.is_contiguous()
         assert obs.numel() >= B * 84 * 84 * 4 * self.depth
         ws = self.workspace(B, ws_key)
         v, pi, rep = out if out is not None else self.outputs(B)
-        check(_lib.hip().mt_forward(self._h, _ptr(self.params), _ptr(obs), B, _ptr(ws), ws.numel(),
-                                    _ptr(v), _ptr(pi), _ptr(rep), _stream()), 'mt_forward')
+        fn = _lib.hip().mt_forward_infer if infer else _lib.hip().mt_forward
+        check(fn(self._h, _ptr(self.params), _ptr(obs), B, _ptr(ws), ws.numel(), _ptr(v), _ptr(pi), _ptr(rep),
+                 _stream()), 'mt_forward_infer' if infer else 'mt_forward')
         return v, pi, rep
 
     def loss_backward(self, obs, B, v, pi, rep, a_idx, r_idx, y, adv, loss_terms=None, ws_key=None):
@@ -185,6 +187,22 @@ def sample(pi, rep, seed, counters, a_idx, r_idx, pair=None):
                                _ptr(a_idx), _ptr(r_idx), _ptr(pair), _stream()), 'mt_sample')
 
 
+def host_device_pointer(t):
+    """Device address of a pinned host tensor (hipHostGetDevicePointer)."""
+    assert t.is_pinned()
+    d = C.c_void_p()
+    check(_lib.hip().mt_host_device_pointer(C.c_void_p(t.data_ptr()), C.byref(d)), 'mt_host_device_pointer')
+    return d.value
+
+
+def preprocess_frames(screens_dev, frame_idx, push_count, E, depth, row_lut, col_lut, prev, out):
+    """atari_emulator.py:79-124 on device, reading each push's two screens where the emulators
+    left them (screens_dev: device address of the bank, frame_idx [E][8], push_count [E])."""
+    check(_lib.hip().mt_preprocess_frames(C.c_void_p(screens_dev), _ptr(frame_idx), _ptr(push_count), E, depth,
+                                          _ptr(row_lut), _ptr(col_lut), _ptr(prev), _ptr(out), _stream()),
+          'mt_preprocess_frames')
+
+
 def returns(rewards, masks, values, v_boot, gamma, y, adv):
     """paac.py:219-231 on device."""
     T, E = rewards.shape
@@ -192,9 +210,10 @@ def returns(rewards, masks, values, v_boot, gamma, y, adv):
                                 T, E, _ptr(y), _ptr(adv), _stream()), 'mt_returns')
 
 
-def preprocess(raw, push_offset, push_count, E, depth, row_lut, col_lut, prev, out, src_rows=210):
+def preprocess(raw, push_offset, push_count, E, depth, row_lut, col_lut, prev, out, src_rows=210, pooled=False):
     """atari_emulator.py:79-124 frame pool + resize + stack on device (raw screens of src_rows
-    rows: 210 = whole screens with the resize LUT, 84 = runner-selected rows, identity LUT)."""
-    check(_lib.hip().mt_preprocess(_ptr(raw), _ptr(push_offset), _ptr(push_count), E, depth, int(src_rows),
-                                   _ptr(row_lut), _ptr(col_lut), _ptr(prev), _ptr(out), _stream()),
-          'mt_preprocess')
+    rows: 210 = whole screens with the resize LUT, 84 = runner-selected rows, identity LUT).
+    pooled: raw holds one screen per push, the frame-pool max already taken (mt_preprocess_pooled)."""
+    name = 'mt_preprocess_pooled' if pooled else 'mt_preprocess'
+    check(getattr(_lib.hip(), name)(_ptr(raw), _ptr(push_offset), _ptr(push_count), E, depth, int(src_rows),
+                                    _ptr(row_lut), _ptr(col_lut), _ptr(prev), _ptr(out), _stream()), name)

@@ -44,9 +44,15 @@ class PAACLearner(ActorLearner):
         self.tab_rep = explo_policy.tab_rep
         self.runner_kind = getattr(args, 'runner', 'native')
         self.sampling = getattr(args, 'sampling', 'host')
-        # native step: kernels read the pinned staging / write the sampled pair in place (zero_copy)
-        # or go through hipMemcpyAsync (copy)
-        self.staging = getattr(args, 'staging', 'zero_copy')
+        # native runner screens: 'in_place' = the GPU reads them in the emulators' pinned bank (no
+        # host copy); 'zero_copy' = staged rows read in place from pinned staging; 'copy' = staged
+        # rows hipMemcpyAsync'd to HBM; 'pooled' = zero_copy with the frame-pool max taken by the
+        # emulator threads (one staged screen per push)
+        self.staging = getattr(args, 'staging', 'in_place')
+        if self.staging not in ('in_place', 'zero_copy', 'copy', 'pooled'):
+            raise ValueError('staging must be in_place, zero_copy, copy or pooled')
+        # native step only: keep the GPU one macro-step ahead (MT_ROLLOUT_PIPELINED)
+        self.pipeline = bool(getattr(args, 'pipeline', False))
         self.depth = 3 if getattr(args, 'rgb', False) else 1
         self.C = 4 * self.depth
         self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
@@ -95,19 +101,31 @@ class PAACLearner(ActorLearner):
         E, C = self.emulator_counts, self.C
         if self.runner_kind == 'native':
             bank = self.environment_creator.create_bank(0, E)
-            # only the 84 screen rows the nearest resize reads are staged and copied (PCIe)
-            # zero-copy native step: kernels read env e's pushes in place at slots 4e..
-            fixed = self.sampling == 'device' and self.staging == 'zero_copy'
-            self.runners = NativeRunners(bank, self.workers, self.tab_rep, row_select=ROW_LUT, fixed_slots=fixed)
-            self.stage_row_lut = torch.arange(84, dtype=torch.int32, device=self.dev)
-            self.raw_d = torch.zeros(4 * E, 2, self.runners.frame_bytes, dtype=torch.uint8, device=self.dev)
+            self.bank = bank
+            self.in_place = self.staging == 'in_place'
             self.pair_d = torch.zeros(2, E, dtype=torch.int32, device=self.dev)
             self.pair_h = torch.zeros(2, E, dtype=torch.int32, pin_memory=True)
             self.meta_d = torch.zeros(2, E, dtype=torch.int32, device=self.dev)
             self.off_d = self.meta_d[0]
             self.cnt_d = self.meta_d[1]
-            total = self.runners.reset()
-            self._upload_pushes(total, self.states[0], self.states[0].clone())
+            if self.in_place:
+                self.runners = NativeRunners(bank, self.workers, self.tab_rep)
+                self.raw_d = None
+                self.frames_d = torch.zeros(E, 8, dtype=torch.int32, device=self.dev)
+                self.screens_dev = devnet.host_device_pointer(bank.screens_t)
+                self.runners.reset_frames()
+                self._upload_frames(self.states[0], self.states[0].clone())
+            else:
+                # only the 84 screen rows the nearest resize reads are staged (PCIe); zero_copy:
+                # kernels read env e's pushes in place at staging slots 4e..
+                fixed = self.sampling == 'device' and self.staging in ('zero_copy', 'pooled')
+                self.runners = NativeRunners(bank, self.workers, self.tab_rep, row_select=ROW_LUT,
+                                             fixed_slots=fixed, pooled=self.staging == 'pooled')
+                self.stage_row_lut = torch.arange(84, dtype=torch.int32, device=self.dev)
+                self.raw_d = torch.zeros(4 * E, self.runners.staging.shape[1], self.runners.frame_bytes,
+                                         dtype=torch.uint8, device=self.dev)
+                total = self.runners.reset()
+                self._upload_pushes(total, self.states[0], self.states[0].clone())
             if self.sampling == 'device':
                 self._make_native_step()
         else:
@@ -127,12 +145,26 @@ class PAACLearner(ActorLearner):
         from . import _lib
         net, r = self.network, self.runners
         ws = net.workspace(self.emulator_counts, 'rollout')
-        p = lambda t: C.c_void_p(t.data_ptr())
+        p = lambda t: C.c_void_p(None if t is None else t.data_ptr())
+        if self.in_place:
+            flags, staging, frames, src_rows, rows = (_lib.MT_ROLLOUT_IN_PLACE, self.bank.screens_t, r.frames, 210,
+                                                      self.row_lut)
+        else:
+            flags = _lib.MT_ROLLOUT_ZERO_COPY if self.staging in ('zero_copy', 'pooled') else 0
+            if self.staging == 'pooled':
+                flags |= _lib.MT_ROLLOUT_POOLED
+            staging, frames, src_rows, rows = r.staging, None, r.src_rows, self.stage_row_lut
+        self.sync_h = None
+        if self.pipeline:
+            if flags & (_lib.MT_ROLLOUT_ZERO_COPY | _lib.MT_ROLLOUT_IN_PLACE) == 0:
+                raise ValueError('pipeline needs in_place, zero_copy or pooled staging')
+            flags |= _lib.MT_ROLLOUT_PIPELINED
+            self.sync_h = torch.zeros(2, dtype=torch.int32, pin_memory=True)
         self._bufs = _lib.mt_rollout_buffers(
             p(self.states), p(self.values), p(self.idx), p(self.pi_roll), p(self.rep_roll), p(ws), ws.numel(),
-            p(self.counters), p(self.raw_d), r.src_rows, p(self.pair_d), p(self.pair_h), p(self.meta_d),
-            p(self.stage_row_lut), p(self.col_lut), p(self.idx_h), p(r.staging), p(r.push_meta), p(r.reward),
-            p(r.over), p(self.rm_h), _lib.MT_ROLLOUT_ZERO_COPY if self.staging == 'zero_copy' else 0)
+            p(self.counters), p(self.raw_d), src_rows, p(self.pair_d), p(self.pair_h), p(self.meta_d),
+            p(rows), p(self.col_lut), p(self.idx_h), p(staging), p(r.push_meta), p(r.reward),
+            p(r.over), p(self.rm_h), p(frames), p(self.sync_h), flags)
         h = C.c_void_p()
         _lib.check(_lib.hip().mt_rollout_create(net._h, self.emulator_counts, self.max_local_steps, r._h,
                                                 self.book.handle, C.byref(self._bufs),
@@ -146,7 +178,16 @@ class PAACLearner(ActorLearner):
         self.raw_d[:total].copy_(r.staging[:total], non_blocking=True)
         self.meta_d.copy_(r.push_meta, non_blocking=True)
         devnet.preprocess(self.raw_d, self.off_d, self.cnt_d, self.emulator_counts, self.depth,
-                          self.stage_row_lut, self.col_lut, prev, out, src_rows=r.src_rows)
+                          self.stage_row_lut, self.col_lut, prev, out, src_rows=r.src_rows, pooled=r.pooled)
+
+    def _upload_frames(self, out, prev):
+        """In-place mode: H2D of the frame indices + push counts (a few hundred bytes), then
+        mt_preprocess_frames reads the screens in the pinned bank."""
+        r = self.runners
+        self.frames_d.copy_(r.frames, non_blocking=True)
+        self.meta_d.copy_(r.push_meta, non_blocking=True)
+        devnet.preprocess_frames(self.screens_dev, self.frames_d, self.cnt_d, self.emulator_counts, self.depth,
+                                 self.row_lut, self.col_lut, prev, out)
 
     @staticmethod
     def _lib_ref(x):
@@ -175,7 +216,7 @@ class PAACLearner(ActorLearner):
             return
         end = self._mark('rollout_forward')
         v, pi, rep = net.forward(self.states[t], E, out=(self.values[t], self.pi_roll, self.rep_roll),
-                                 ws_key='rollout')
+                                 ws_key='rollout', infer=True)
         if end is not None:
             end.record()
         if self.sampling == 'device':
@@ -197,10 +238,14 @@ class PAACLearner(ActorLearner):
             self.a_idx[t].copy_(self.a_h[t], non_blocking=True)
             self.r_idx[t].copy_(self.r_h[t], non_blocking=True)
         if self.runner_kind == 'native':
-            total = self.runners.step(self.a_h[t], self.r_h[t])
+            if self.in_place:
+                self.runners.step_frames(self.a_h[t], self.r_h[t])
+                self._upload_frames(self.states[t + 1], self.states[t])
+            else:
+                total = self.runners.step(self.a_h[t], self.r_h[t])
+                self._upload_pushes(total, self.states[t + 1], self.states[t])
             reward = self.runners.reward.numpy()
             over = self.runners.over.numpy()
-            self._upload_pushes(total, self.states[t + 1], self.states[t])
         else:
             sh = self.shared
             sh[3][...] = a
@@ -220,7 +265,7 @@ class PAACLearner(ActorLearner):
         self.book.drain()
         E, T = self.emulator_counts, self.max_local_steps
         N = E * T
-        net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout')
+        net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout', infer=True)
         self.rm_d.copy_(self.rm_h, non_blocking=True)
         devnet.returns(self.rewards_d, self.masks_d, self.values, self.v_boot, self.gamma, self.y, self.adv)
         lr = self.get_lr()

@@ -26,9 +26,12 @@ def _np(t):
 class NativeRunners(object):
     """row_select: screen rows to stage (None = whole 210-row screens). The learner passes the
     84 rows the nearest resize reads, so only those cross PCIe. fixed_slots: MH_RUNNER_FIXED_SLOTS
-    (env e's pushes at staging slots 4e.., one worker phase per step)."""
+    (env e's pushes at staging slots 4e.., one worker phase per step). pooled: MH_RUNNER_POOLED
+    (one staged screen per push, max of its two frames, atari_emulator.py:79-88)."""
 
-    def __init__(self, bank, n_workers, tab_rep, row_select=None, fixed_slots=False):
+    def __init__(self, bank, n_workers, tab_rep, row_select=None, fixed_slots=False, pooled=False):
+        """in-place frame mode (reset_frames / step_frames) needs no row_select: the screens stay
+        in the bank, only their indices are written (frames [E][8] + push_count)."""
         self.bank = bank
         self.E = bank.screens.shape[0]
         self.tab = np.ascontiguousarray(np.asarray(tab_rep, dtype=np.int32))
@@ -42,17 +45,21 @@ class NativeRunners(object):
             bank.screens.ctypes.data_as(C.c_void_p), bank.screens.shape[1], bank.frame_bytes,
             bank.rewards.ctypes.data_as(C.c_void_p), bank.rewards.shape[1], bank.episode_len,
             None if self.rows is None else self.rows.ctypes.data_as(C.c_void_p),
-            0 if self.rows is None else len(self.rows), 1 if fixed_slots else 0, C.byref(h)), 'mh_runner_create')
+            0 if self.rows is None else len(self.rows),
+            (_lib.MH_RUNNER_FIXED_SLOTS if fixed_slots else 0) | (_lib.MH_RUNNER_POOLED if pooled else 0),
+            C.byref(h)), 'mh_runner_create')
         self.fixed_slots = bool(fixed_slots)
+        self.pooled = bool(pooled)
         self._h = h
         pin = torch.cuda.is_available()
         mk = lambda *shape, dtype: torch.zeros(*shape, dtype=dtype, pin_memory=pin)
-        self.staging = mk(4 * self.E, 2, self.frame_bytes, dtype=torch.uint8)
+        self.staging = mk(4 * self.E, 1 if pooled else 2, self.frame_bytes, dtype=torch.uint8)
         self.push_meta = mk(2, self.E, dtype=torch.int32)  # [offset; count]: one H2D copy
         self.push_offset = self.push_meta[0]
         self.push_count = self.push_meta[1]
         self.reward = mk(self.E, dtype=torch.float32)
         self.over = mk(self.E, dtype=torch.float32)
+        self.frames = mk(self.E, 8, dtype=torch.int32)  # in-place mode: bank frame indices
         self.total = 0
 
     def _ptr(self, t):
@@ -77,6 +84,19 @@ class NativeRunners(object):
             'mh_runner_step')
         self.total = tot.value
         return self.total
+
+    def reset_frames(self):
+        """get_initial_state() of every env, in-place mode: frames/push_count name the screens."""
+        _lib.check_host(_lib.host().mh_runner_reset_frames(self._h, self._ptr(self.frames),
+                                                           self._ptr(self.push_count)), 'mh_runner_reset_frames')
+
+    def step_frames(self, a_idx, r_idx):
+        """One macro-step, in-place mode (no screen copied): fills frames, push_count, reward, over."""
+        a = a_idx if isinstance(a_idx, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a_idx, np.int32))
+        r = r_idx if isinstance(r_idx, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(r_idx, np.int32))
+        _lib.check_host(_lib.host().mh_runner_step_frames(
+            self._h, self._ptr(a), self._ptr(r), self._ptr(self.frames), self._ptr(self.push_count),
+            self._ptr(self.reward), self._ptr(self.over)), 'mh_runner_step_frames')
 
     def env_state(self, e):
         k = C.c_int64()

@@ -65,12 +65,18 @@ class SyntheticEmulator(BaseEnvironment):
 
 
 class SyntheticBank(object):
-    """Streams of envs [first, first+n) in the layout mh_runner_create takes."""
+    """Streams of envs [first, first+n) in the layout mh_runner_create takes. The screen ring
+    lives in pinned (page-locked, device-mapped) host memory when a GPU is present, as an ALE
+    worker's frame buffers would, so the GPU can read screens where the emulators left them
+    (mh_runner_step_frames + mt_preprocess_frames)."""
 
-    def __init__(self, first_env_id, n_envs, rgb=False, episode_len=EPISODE_LEN):
+    def __init__(self, first_env_id, n_envs, rgb=False, episode_len=EPISODE_LEN, pinned=None):
+        import torch
         depth = 3 if rgb else 1
         self.depth = depth
-        self.screens = np.empty((n_envs, RING, 210, 160, depth), dtype=np.uint8)
+        pinned = torch.cuda.is_available() if pinned is None else pinned
+        self.screens_t = torch.empty((n_envs, RING, 210, 160, depth), dtype=torch.uint8, pin_memory=pinned)
+        self.screens = self.screens_t.numpy()
         self.rewards = np.empty((n_envs, REWARD_LEN), dtype=np.float32)
         for i in range(n_envs):
             self.screens[i], self.rewards[i] = env_streams(first_env_id + i, depth)

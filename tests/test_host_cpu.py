@@ -237,3 +237,69 @@ def test_native_runner_fixed_slots_match_compact():
     finally:
         comp.stop()
         fix.stop()
+
+
+def test_native_runner_in_place_frames_match_staging():
+    """In-place frame mode (mh_runner_step_frames) names, per env and push, the bank screens whose
+    bytes the staged mode copies: same counts, rewards and terminals, and bank[frame_idx] equals
+    the staged screens byte for byte (oldest push first)."""
+    from manette_amd.runners import NativeRunners
+    from manette_amd.synthetic import SyntheticBank
+    tab = opol.tab_repetitions(10, 11)
+    E = 7
+    bank = SyntheticBank(9, E, episode_len=5)
+    comp = NativeRunners(bank, 2, tab)
+    ip = NativeRunners(bank, 3, tab)
+    flat = bank.screens.reshape(-1, 210 * 160)
+    try:
+        n1 = comp.reset()
+        ip.reset_frames()
+        rs = np.random.RandomState(2)
+        for step in range(15):
+            np.testing.assert_array_equal(comp.push_count.numpy(), ip.push_count.numpy())
+            fr = ip.frames.numpy()
+            for e in range(E):
+                o, c = int(comp.push_offset[e]), int(comp.push_count[e])
+                staged = comp.staging.numpy()[o:o + c].reshape(c, 2, 210 * 160)
+                np.testing.assert_array_equal(flat[fr[e, :2 * c]].reshape(c, 2, -1), staged)
+                assert (fr[e, :2 * c] // 64 == e).all()  # env e's own ring
+            act = rs.randint(0, 6, E).astype(np.int32)
+            rep = rs.randint(0, 11, E).astype(np.int32)
+            n1 = comp.step(act, rep)
+            ip.step_frames(act, rep)
+            np.testing.assert_array_equal(comp.reward.numpy(), ip.reward.numpy())
+            np.testing.assert_array_equal(comp.over.numpy(), ip.over.numpy())
+    finally:
+        comp.stop()
+        ip.stop()
+
+
+def test_native_runner_pooled_staging_is_frame_pool_max():
+    """MH_RUNNER_POOLED stages one screen per push: the elementwise max of the two screens the
+    unpooled layout stages (FramePool, atari_emulator.py:79-88), same slots, counts, rewards."""
+    from manette_amd.environment import ROW_LUT
+    from manette_amd.runners import NativeRunners
+    from manette_amd.synthetic import SyntheticBank
+    tab = opol.tab_repetitions(10, 11)
+    E = 6
+    bank = SyntheticBank(3, E, episode_len=7)
+    two = NativeRunners(bank, 2, tab, row_select=ROW_LUT, fixed_slots=True)
+    one = NativeRunners(bank, 3, tab, row_select=ROW_LUT, fixed_slots=True, pooled=True)
+    assert one.staging.shape[1] == 1 and two.staging.shape[1] == 2
+    try:
+        two.reset(), one.reset()
+        rs = np.random.RandomState(4)
+        for step in range(12):
+            np.testing.assert_array_equal(two.push_count.numpy(), one.push_count.numpy())
+            for e in range(E):
+                c = int(two.push_count[e])
+                s2 = two.staging.numpy()[4 * e:4 * e + c]
+                np.testing.assert_array_equal(one.staging.numpy()[4 * e:4 * e + c, 0], np.maximum(s2[:, 0], s2[:, 1]))
+            act = rs.randint(0, 6, E).astype(np.int32)
+            rep = rs.randint(0, 11, E).astype(np.int32)
+            two.step(act, rep), one.step(act, rep)
+            np.testing.assert_array_equal(two.reward.numpy(), one.reward.numpy())
+            np.testing.assert_array_equal(two.over.numpy(), one.over.numpy())
+    finally:
+        two.stop()
+        one.stop()

@@ -46,6 +46,28 @@ def test_forward_parity(arch, depth, A, R, B):
     np.testing.assert_allclose(rep.cpu().numpy(), rep0, rtol=2e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize('arch,depth,A,R,act', [('NIPS', 1, 6, 1, 'relu'), ('NIPS', 3, 4, 11, 'relu'),
+                                                 ('NIPS', 1, 9, 11, 'leaky_relu'), ('NATURE', 1, 4, 11, 'relu')])
+@pytest.mark.parametrize('B', [1, 7, 32, 33])
+def test_forward_infer_parity(arch, depth, A, R, act, B):
+    """mt_forward_infer (NIPS: the fused trunk, trunk_fused.h) vs the oracle, and vs mt_forward
+    (the layered GEMM path) on the same rows. B = 32 takes the XCD-aware block mapping, 7/33 not."""
+    net = _net(arch, depth, A, R, seed=11 + B, act=act)
+    rs = np.random.RandomState(1000 + B)
+    obs = rs.randint(0, 256, size=(B, 84, 84, 4 * depth)).astype(np.uint8)
+    obs_d = torch.from_numpy(obs).cuda()
+    v, pi, rep = [t.clone() for t in net.forward(obs_d, infer=True, ws_key='infer')]
+    v1, pi1, rep1 = net.forward(obs_d)
+    torch.cuda.synchronize()
+    spec = nets.arch_spec(arch, depth, A, R)
+    v0, pi0, rep0, _ = nets.forward(spec, net.get_variables(), obs, act=act, alpha=0.1)
+    np.testing.assert_allclose(v.cpu().numpy(), v0, rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(pi.cpu().numpy(), pi0, rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(rep.cpu().numpy(), rep0, rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(v.cpu().numpy(), v1.cpu().numpy(), rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(pi.cpu().numpy(), pi1.cpu().numpy(), rtol=2e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize('arch,depth,A,R', CONFIGS)
 @pytest.mark.parametrize('B', [5, 40])
 def test_loss_backward_parity(arch, depth, A, R, B):
@@ -164,6 +186,29 @@ def test_preprocess_bit_exact(depth, rows_only):
     got = out.cpu().numpy()
     for e in range(E):
         pushes = [preprocess.pool_and_resize(raw[offs[e] + j, 0], raw[offs[e] + j, 1]) for j in range(counts[e])]
+        np.testing.assert_array_equal(got[e], preprocess.stack_update(prev[e], pushes, depth))
+
+
+@pytest.mark.parametrize('depth', [1, 3])
+def test_preprocess_pooled_bit_exact(depth):
+    """mt_preprocess_pooled: one staged screen per push, max(f0, f1) taken on the host."""
+    from manette_amd.network import preprocess as dev_pre
+    rs = np.random.RandomState(10 + depth)
+    E = 6
+    counts = np.array([4, 1, 3, 2, 4, 1], np.int32)
+    offs = (4 * np.arange(E)).astype(np.int32)
+    raw = rs.randint(0, 256, size=(4 * E, 2, 84, 160, depth)).astype(np.uint8)
+    pooled = np.maximum(raw[:, 0], raw[:, 1])[:, None]
+    prev = rs.randint(0, 256, size=(E, 84, 84, 4 * depth)).astype(np.uint8)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    out = torch.empty(E, 84, 84, 4 * depth, dtype=torch.uint8, device='cuda')
+    dev_pre(d(pooled), d(offs), d(counts), E, depth, d(np.arange(84, dtype=np.int32)),
+            d(preprocess.COL_LUT.astype(np.int32)), d(prev), out, src_rows=84, pooled=True)
+    got = out.cpu().numpy()
+    full = np.zeros((4 * E, 2, 210, 160, depth), np.uint8)
+    full[:, :, preprocess.ROW_LUT] = raw
+    for e in range(E):
+        pushes = [preprocess.pool_and_resize(full[offs[e] + j, 0], full[offs[e] + j, 1]) for j in range(counts[e])]
         np.testing.assert_array_equal(got[e], preprocess.stack_update(prev[e], pushes, depth))
 
 

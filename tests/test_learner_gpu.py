@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _learner(tmp, runner, sampling, arch='NIPS', ec=8, game='pong', max_rep=0, nb=1, workers=2, seed=0,
-             staging='zero_copy'):
+             staging='in_place', pipeline=False):
     sys.path.insert(0, ROOT)
     import train as cli
     from manette_amd.exploration_policy import ExplorationPolicy
@@ -22,7 +22,7 @@ def _learner(tmp, runner, sampling, arch='NIPS', ec=8, game='pong', max_rep=0, n
     a = cli.get_arg_parser().parse_args([])
     a.game, a.arch, a.emulator_counts, a.emulator_workers = game, arch, ec, workers
     a.max_repetition, a.nb_choices = max_rep, nb
-    a.runner, a.sampling, a.seed, a.staging = runner, sampling, seed, staging
+    a.runner, a.sampling, a.seed, a.staging, a.pipeline = runner, sampling, seed, staging, pipeline
     a.debugging_folder = str(tmp) + '/'
     a.max_global_steps = 1 << 40
     a.checkpoint_interval = 1 << 40
@@ -49,17 +49,20 @@ def _state(L):
                 states=L.states.cpu().numpy().copy(), gs=L.global_step, episodes=list(L.book.episodes))
 
 
-@pytest.mark.parametrize('max_rep,nb,staging', [(0, 1, 'zero_copy'), (10, 11, 'zero_copy'), (10, 11, 'copy')])
-def test_native_step_equals_python_step(tmp_path, max_rep, nb, staging):
-    """mt_rollout_step (C++ orchestration, sampling fused in the heads kernel, zero-copy or
-    copied staging) == the Python step() on the standalone kernels (mt_forward, mt_sample,
-    hipMemcpy + mt_preprocess)."""
-    A = _learner(tmp_path / 'a', 'native', 'device', max_rep=max_rep, nb=nb, staging=staging)
+@pytest.mark.parametrize('max_rep,nb,staging,pipeline', [(0, 1, 'in_place', False), (10, 11, 'in_place', False),
+                                                         (10, 11, 'zero_copy', False), (10, 11, 'copy', False),
+                                                         (10, 11, 'pooled', False), (0, 1, 'in_place', True),
+                                                         (10, 11, 'in_place', True), (10, 11, 'pooled', True)])
+def test_native_step_equals_python_step(tmp_path, max_rep, nb, staging, pipeline):
+    """mt_rollout_step (C++ orchestration, sampling fused in the heads kernel; in-place, zero-copy,
+    pooled or copied staging; optionally pipelined one step ahead behind a device wait) == the
+    Python step() on the standalone kernels (mt_forward, mt_sample, hipMemcpy + mt_preprocess)."""
+    A = _learner(tmp_path / 'a', 'native', 'device', max_rep=max_rep, nb=nb, staging=staging, pipeline=pipeline)
     assert A.native_step is not None
     _run(A, 6)
     sa = _state(A)
     A.cleanup()
-    B = _learner(tmp_path / 'b', 'native', 'device', max_rep=max_rep, nb=nb)
+    B = _learner(tmp_path / 'b', 'native', 'device', max_rep=max_rep, nb=nb, staging='copy')
     from manette_amd import _lib
     _lib.hip().mt_rollout_destroy(B.native_step)
     B.native_step = None
