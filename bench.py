@@ -33,6 +33,9 @@ CONFIGS = {
     # the CLI's default arch and the arch of every FiGAR checkpoint
     'breakout-pwyx-figar-rgb': dict(game='breakout', arch='PWYX', ec=32, ew=8, max_repetition=10,
                                     nb_choices=11, rgb=True),
+    # BASELINE.json configs[4]: MsPacman LSTM + FiGAR10, ec=256 over 8 GPUs = 32 per GPU
+    'mspacman-lstm-figar': dict(game='ms_pacman', arch='LSTM', ec=32, ew=8, max_repetition=10, nb_choices=11,
+                                rgb=False),
 }
 MI355X_FP32_TFLOPS = 157.3   # dense fp32 (vector = MFMA), MI355X_MICROARCH.md
 MI355X_HBM_GBS = 8000.0      # HBM3E peak, MI355X_MICROARCH.md
@@ -44,7 +47,8 @@ def conv_out(h, k, s):
 
 def arch_flops(arch, depth, A, R):
     """Per sample per layer: (kind, forward FLOPs = 2*MACs, weight floats, output floats) for
-    NIPS / NATURE / PWYX (networks.py:178-278)."""
+    NIPS / NATURE / PWYX / LSTM (networks.py:178-278). An LSTM sample is a 5-frame window: its
+    trunk layers count 5 frames, then the cell (x and h products), projection and fc6."""
     C = 4 * depth
     if arch == 'NIPS':
         convs = [(8, 4, C, 16, 'VALID', False), (4, 2, 16, 32, 'VALID', False)]
@@ -55,15 +59,22 @@ def arch_flops(arch, depth, A, R):
     else:
         convs = [(5, 1, C, 32, 'SAME', True), (5, 1, 32, 32, 'SAME', True), (4, 1, 32, 64, 'SAME', True),
                  (3, 1, 64, 64, 'SAME', False)]
-        F = 512
+        F = 128 if arch == 'LSTM' else 512
+    frames = 5 if arch == 'LSTM' else 1
     h = 84
     layers = []
     for (k, s, cin, cout, pad, pool) in convs:
         h = conv_out(h, k, s) if pad == 'VALID' else -(-h // s)
-        layers.append(('conv', 2.0 * h * h * cout * k * k * cin, k * k * cin * cout + cout, h * h * cout))
+        layers.append(('conv', frames * 2.0 * h * h * cout * k * k * cin, k * k * cin * cout + cout,
+                       frames * h * h * cout))
         if pool:
             h //= 2
     flat = h * h * convs[-1][3]
+    if arch == 'LSTM':
+        nh = 32
+        layers.append(('lstm', frames * 2.0 * (flat + nh) * 4 * nh, (flat + nh + 1) * 4 * nh, frames * 4 * nh))
+        layers.append(('proj', 2.0 * nh * nh, nh * nh + nh, nh))
+        flat = nh
     layers.append(('fc', 2.0 * flat * F, flat * F + F, F))
     layers.append(('heads', 2.0 * F * (1 + A + R), F * (1 + A + R) + 1 + A + R, 1 + A + R))
     return layers
@@ -117,7 +128,7 @@ def cpu_baseline(cfg, T, seconds, rank):
     class Timed(host_loop.HostLoop):
         pass
 
-    loop = Timed(emus, net, tab, A, max_local_steps=T, workers=ew, record=False)
+    loop = Timed(emus, net, tab, A, max_local_steps=T, workers=ew, record=False, lstm=cfg['arch'] == 'LSTM')
     # warm up one update, then time whole updates until `seconds` elapse (at most 200)
     steps_per_update = ec * T
     t_start = [None]
@@ -230,8 +241,8 @@ def main():
     for _ in range(30):
         s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s_ev.record()
-        learner.network.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
-                                ws_key='rollout', infer=True)
+        learner.network.forward(learner.memory if learner.lstm_bool else learner.states[0], E,
+                                out=(learner.v_boot, learner.pi_roll, learner.rep_roll), ws_key='rollout', infer=True)
         e_ev.record()
         fw.append((s_ev, e_ev))
     torch.cuda.synchronize()
@@ -248,7 +259,9 @@ def main():
         tp_flops = train_pass_flops(layers, N)
         rf_ms = float(np.mean(prof['rollout_forward']))
         fwd_flops = ec * sum(l[1] for l in layers)
-        fwd_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in layers) + 4 * ec * sum(l[3] for l in layers)
+        frames = 5 if cfg['arch'] == 'LSTM' else 1
+        fwd_bytes = (ec * frames * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in layers) +
+                     4 * ec * sum(l[3] for l in layers))
         achieved = tp_flops / (tp_ms * 1e-3) / 1e12
         line = {
             'metric': 'env-steps/sec (ec x t_max frames per update)',

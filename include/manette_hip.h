@@ -176,6 +176,14 @@ int mt_preprocess_frames(const uint8_t *screens, const int32_t *frame_idx, const
 /* Device address of pinned (page-locked, mapped) host memory, e.g. an emulator screen bank. */
 int mt_host_device_pointer(void *host, void **dev);
 
+/* ---- LSTM memory window (paac.py:79-83 update_memory + :202-203 episode-end reset) --------
+ * memory [E][5][frame] (the window each env's forward reads), whole_t [E][5][frame] = row t of
+ * whole_memory, fresh [E][frame] = the new states, masks [E] = 1 - episode_over (float32).
+ * whole_t <- memory; memory <- shift left + fresh; memory[e] <- 0 where masks[e] == 0.
+ * frame = 84*84*4*depth bytes. */
+int mt_memory_push(uint8_t *memory, uint8_t *whole_t, const uint8_t *fresh, const float *masks, int E,
+                   size_t frame_bytes, mt_stream_t stream);
+
 /* ---- native rollout macro-step (orchestrates A1-A3, A8; paac.py:140-205) -------------------
  * One call = one macro-step t of every env: mt_forward on state slot t with the A3 draw fused
  * into its heads kernel (indices into idx[0][t], idx[1][t] and the [2][E] pair) -> wait for the

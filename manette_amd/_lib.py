@@ -69,6 +69,7 @@ _HIP_SIGS = {
     'mt_preprocess': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
     'mt_preprocess_pooled': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
     'mt_preprocess_frames': (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    'mt_memory_push': (_I, [_P, _P, _P, _P, _I, _SZ, _P]),
     'mt_host_device_pointer': (_I, [_P, C.POINTER(_P)]),
     'mt_sum_slabs': (_I, [_P, _I, _SZ, _P, _P]),
     'mt_net_get_config': (_I, [_P, C.POINTER(mt_net_config)]),

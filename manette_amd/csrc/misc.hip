@@ -4,6 +4,7 @@
 //   A9  n-step return / advantage scan         (paac.py:219-231)
 //   A11 global-norm clip + TF1 ApplyRMSProp    (actor_learner.py:47-74)
 // plus error reporting and hipGraph capture helpers of the C ABI.
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 
@@ -371,5 +372,44 @@ extern "C" int mt_graph_launch(void *graph_exec, mt_stream_t stream) {
 
 extern "C" int mt_graph_destroy(void *graph_exec) {
   if (graph_exec) MT_HIP(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
+  return MT_OK;
+}
+
+// ---- LSTM memory window (paac.py:79-83, :191-203) --------------------------------------------
+// One thread per 16-byte column of a frame of env e: reads that column of the 5 window frames
+// and of the new state, writes the window to whole_t (whole_memory[t] = memory), then the
+// shifted window (memory[:, :-1] = memory[:, 1:]; memory[:, -1] = new state), or zeros when the
+// episode ended (mask == 0, paac.py:202-203). Each thread touches only its own column: no race.
+__global__ __launch_bounds__(256) void memory_push_kernel(uint4 *__restrict__ memory, uint4 *__restrict__ whole_t,
+                                                          const uint4 *__restrict__ fresh,
+                                                          const float *__restrict__ masks, int E, int n16) {
+  const int e = blockIdx.y;
+  const bool keep = masks[e] != 0.f;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) {
+    uint4 m[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) m[k] = memory[((size_t)e * 5 + k) * n16 + i];
+    const uint4 f = fresh[(size_t)e * n16 + i];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) whole_t[((size_t)e * 5 + k) * n16 + i] = m[k];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) memory[((size_t)e * 5 + k) * n16 + i] = keep ? (k < 4 ? m[k + 1] : f) : z;
+  }
+}
+
+extern "C" int mt_memory_push(uint8_t *memory, uint8_t *whole_t, const uint8_t *fresh, const float *masks, int E,
+                              size_t frame_bytes, mt_stream_t stream) {
+  MT_CHECK_ARG(memory && whole_t && fresh && masks, "null argument");
+  MT_CHECK_ARG(E >= 1, "E must be >= 1");
+  MT_CHECK_ARG(frame_bytes % 16 == 0, "frame_bytes must be a multiple of 16");
+  MT_CHECK_ARG((((uintptr_t)memory | (uintptr_t)fresh | (uintptr_t)whole_t) & 15) == 0,
+               "buffers must be 16-byte aligned");
+  MT_CHECK_ARG(whole_t != memory, "whole_t may not alias memory");
+  const int n16 = (int)(frame_bytes / 16);
+  const dim3 grid((unsigned)std::min(cdiv(n16, 256), 64), (unsigned)E);
+  hipLaunchKernelGGL(memory_push_kernel, grid, dim3(256), 0, (hipStream_t)stream, reinterpret_cast<uint4 *>(memory),
+                     reinterpret_cast<uint4 *>(whole_t), reinterpret_cast<const uint4 *>(fresh), masks, E, n16);
+  MT_LAUNCHED();
   return MT_OK;
 }

@@ -28,6 +28,7 @@ struct NipsArch {  // networks.py:178-192
   static constexpr int F = 256;
   static constexpr const char *FC = "fc3";
   static constexpr int FUSED_SLABS = FusedNips<C>::ROWS2;  // inference forward: trunk_fused.h
+  static constexpr bool LSTM = false;
 };
 template <int C>
 struct NatureArch {  // networks.py:261-278
@@ -39,6 +40,7 @@ struct NatureArch {  // networks.py:261-278
   static constexpr int F = 512;
   static constexpr const char *FC = "fc4";
   static constexpr int FUSED_SLABS = 0;  // no fused inference trunk: layered path
+  static constexpr bool LSTM = false;
 };
 template <int C>
 struct PwyxArch {  // networks.py:206-225: SAME convs, 2x2 pools after conv1-3
@@ -50,6 +52,7 @@ struct PwyxArch {  // networks.py:206-225: SAME convs, 2x2 pools after conv1-3
   static constexpr int F = 512;
   static constexpr const char *FC = "fc5";
   static constexpr int FUSED_SLABS = 0;
+  static constexpr bool LSTM = false;
 };
 
 template <class Ar, int I>
@@ -86,17 +89,18 @@ struct mt_net {
   size_t nparams;
   size_t off_conv[4];  // weights offset of each conv (biases follow)
   size_t off_fc, off_critic, off_actor, off_rep;
+  size_t off_lstm = 0, off_proj = 0;  // LSTM arch: cell kernel (+bias), projection w (+b)
 };
 
 namespace mt {
 
 static size_t align64(size_t x) { return (x + 63) & ~size_t(63); }
 
-static void add_pair(mt_net *n, size_t &off, const std::string &scope, const std::string &nm,
-                     std::vector<int64_t> wshape, int64_t nb, float bw, float bb, size_t *woff) {
+static void add_named_pair(mt_net *n, size_t &off, const std::string &wname, const std::string &bname,
+                           std::vector<int64_t> wshape, int64_t nb, float bw, float bb, size_t *woff) {
   off = align64(off);
   VarInfo w{};
-  w.name = scope + "/" + nm + "/" + nm + "_weights";
+  w.name = wname;
   w.ndim = (int)wshape.size();
   size_t ws = 1;
   for (int i = 0; i < w.ndim; ++i) {
@@ -106,7 +110,7 @@ static void add_pair(mt_net *n, size_t &off, const std::string &scope, const std
   w.offset = off;
   w.bound = bw;
   VarInfo b{};
-  b.name = scope + "/" + nm + "/" + nm + "_biases";
+  b.name = bname;
   b.ndim = 1;
   b.shape[0] = nb;
   b.offset = off + ws;
@@ -115,6 +119,12 @@ static void add_pair(mt_net *n, size_t &off, const std::string &scope, const std
   n->vars.push_back(w);
   n->vars.push_back(b);
   off = off + ws + (size_t)nb;
+}
+
+static void add_pair(mt_net *n, size_t &off, const std::string &scope, const std::string &nm,
+                     std::vector<int64_t> wshape, int64_t nb, float bw, float bb, size_t *woff) {
+  add_named_pair(n, off, scope + "/" + nm + "/" + nm + "_weights", scope + "/" + nm + "/" + nm + "_biases",
+                 std::move(wshape), nb, bw, bb, woff);
 }
 
 template <class G>
@@ -137,6 +147,16 @@ static void add_convs(mt_net *n, size_t &off) {
 }
 
 template <class Ar>
+static void add_heads(mt_net *n, size_t &off) {
+  const float bh = (float)(1.0 / std::sqrt((double)Ar::F));
+  const int A = n->cfg.num_actions, R = n->cfg.num_reps;
+  // policy_v_network.py:22 (critic), :31 (actor), :47 (repetition) — TF creation order.
+  add_pair(n, off, "Training/Critic", "critic_output", {Ar::F, 1}, 1, bh, bh, &n->off_critic);
+  add_pair(n, off, "Training/Actor", "actor_output", {Ar::F, A}, A, bh, bh, &n->off_actor);
+  add_pair(n, off, "Training/Repetition", "repetition_output", {Ar::F, R}, R, bh, bh, &n->off_rep);
+}
+
+template <class Ar>
 static void build_layout(mt_net *n) {
   static_assert(out_hw<Ar, Ar::NCONV - 1>() * out_hw<Ar, Ar::NCONV - 1>() *
                     LayerG<Ar, Ar::NCONV - 1>::COUT == Ar::FLAT, "flatten width");
@@ -144,12 +164,7 @@ static void build_layout(mt_net *n) {
   add_convs<Ar>(n, off);
   const float bf = (float)(1.0 / std::sqrt((double)Ar::FLAT));  // networks.py:72-89
   add_pair(n, off, "Network", Ar::FC, {Ar::FLAT, Ar::F}, Ar::F, bf, bf, &n->off_fc);
-  const float bh = (float)(1.0 / std::sqrt((double)Ar::F));
-  const int A = n->cfg.num_actions, R = n->cfg.num_reps;
-  // policy_v_network.py:22 (critic), :31 (actor), :47 (repetition) — TF creation order.
-  add_pair(n, off, "Training/Critic", "critic_output", {Ar::F, 1}, 1, bh, bh, &n->off_critic);
-  add_pair(n, off, "Training/Actor", "actor_output", {Ar::F, A}, A, bh, bh, &n->off_actor);
-  add_pair(n, off, "Training/Repetition", "repetition_output", {Ar::F, R}, R, bh, bh, &n->off_rep);
+  add_heads<Ar>(n, off);
   n->nparams = align64(off);
   n->F = Ar::F;
   n->flat = Ar::FLAT;
@@ -246,8 +261,13 @@ static void ws_layers(WsLayout &L, size_t &off, int B, size_t &wslab) {
   }
 }
 
+struct LstmWs;
+template <class Ar>
+static WsLayout lstm_ws_layout(const mt_net *n, int B, LstmWs *X);  // lstm.h
+
 template <class Ar>
 static WsLayout ws_layout(const mt_net *n, int B) {
+  if constexpr (Ar::LSTM) return lstm_ws_layout<Ar>(n, B, nullptr);
   WsLayout L{};
   size_t off = 0;
   auto take = [&](size_t nf) {
@@ -746,16 +766,16 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
   }
 }
 
+// Loss + head gradients (policy_v_network.py:25-74): zeroes grad, writes dz, dH (masked by the
+// trunk output's activation derivative) and the three head (w, b) gradients.
 template <class Ar>
-static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
-                         const float *pi, const float *rep, const float *v, const int32_t *a_idx,
-                         const int32_t *r_idx, const float *y, const float *adv, float beta,
-                         float *grad, float *loss_terms, hipStream_t s) {
-  const WsLayout L = ws_layout<Ar>(n, B);
+static int heads_backward(const mt_net *n, const float *P, int B, float *ws, const WsLayout &L, const float *pi,
+                          const float *rep, const float *v, const int32_t *a_idx, const int32_t *r_idx,
+                          const float *y, const float *adv, float beta, float *grad, float *loss_terms,
+                          hipStream_t s) {
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
   MT_HIP(hipMemsetAsync(grad, 0, n->nparams * sizeof(float), s));
-
   // loss scaling 5.0 and the batch mean (policy_v_network.py:70-74): scale = 5/B.
   const float scale = 5.0f / (float)B;
   HeadParams hp = head_params(n, P);
@@ -780,6 +800,18 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
                        grad + n->off_rep);
     MT_LAUNCHED();
   }
+  return MT_OK;
+}
+
+template <class Ar>
+static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
+                         const float *pi, const float *rep, const float *v, const int32_t *a_idx,
+                         const int32_t *r_idx, const float *y, const float *adv, float beta,
+                         float *grad, float *loss_terms, hipStream_t s) {
+  const WsLayout L = ws_layout<Ar>(n, B);
+  const int act = n->cfg.activation;
+  const float al = n->cfg.alpha_leaky;
+  MT_TRY(heads_backward<Ar>(n, P, B, ws, L, pi, rep, v, a_idx, r_idx, y, adv, beta, grad, loss_terms, s));
   constexpr int K = Ar::NCONV - 1;
   const float *flat = layer_out<Ar, K>(ws, L);
   const float *Wfc = P + n->off_fc;
@@ -802,6 +834,8 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
 
 }  // namespace mt
 
+#include "lstm.h"
+
 // ---------------------------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------------------------
@@ -816,6 +850,8 @@ using namespace mt;
     else if (arch_ == MT_ARCH_NATURE && d_ == 3) { using Ar = NatureArch<12>; __VA_ARGS__; } \
     else if (arch_ == MT_ARCH_PWYX && d_ == 1) { using Ar = PwyxArch<4>; __VA_ARGS__; }     \
     else if (arch_ == MT_ARCH_PWYX && d_ == 3) { using Ar = PwyxArch<12>; __VA_ARGS__; }    \
+    else if (arch_ == MT_ARCH_LSTM && d_ == 1) { using Ar = LstmArch<4>; __VA_ARGS__; }     \
+    else if (arch_ == MT_ARCH_LSTM && d_ == 3) { using Ar = LstmArch<12>; __VA_ARGS__; }    \
     else { set_error("arch %d depth %d not built", arch_, d_); return MT_ERR_UNSUPPORTED; } \
   } while (0)
 
@@ -837,6 +873,8 @@ extern "C" int mt_net_create(const mt_net_config *cfg, mt_net **out) {
   else if (arch == MT_ARCH_NATURE && d == 3) build_layout<NatureArch<12>>(n);
   else if (arch == MT_ARCH_PWYX && d == 1) build_layout<PwyxArch<4>>(n);
   else if (arch == MT_ARCH_PWYX && d == 3) build_layout<PwyxArch<12>>(n);
+  else if (arch == MT_ARCH_LSTM && d == 1) build_layout_lstm<LstmArch<4>>(n);
+  else if (arch == MT_ARCH_LSTM && d == 3) build_layout_lstm<LstmArch<12>>(n);
   else {
     delete n;
     set_error("arch %d not built into this library", arch);
@@ -922,8 +960,11 @@ int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *ob
       set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
       return MT_ERR_WORKSPACE;
     }
-    return infer ? forward_infer_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream)
-                 : forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
+    if constexpr (Ar::LSTM)
+      return lstm_forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
+    else
+      return infer ? forward_infer_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream)
+                   : forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
   });
   return MT_OK;
 }
@@ -943,8 +984,12 @@ extern "C" int mt_loss_backward(const mt_net *net, const float *params, const ui
       set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
       return MT_ERR_WORKSPACE;
     }
-    return backward_impl<Ar>(net, params, obs, batch, (float *)ws, pi, rep, v, a_idx, r_idx, y, adv,
-                             entropy_beta, grad, loss_terms, (hipStream_t)stream);
+    if constexpr (Ar::LSTM)
+      return lstm_backward_impl<Ar>(net, params, obs, batch, (float *)ws, pi, rep, v, a_idx, r_idx, y, adv,
+                                    entropy_beta, grad, loss_terms, (hipStream_t)stream);
+    else
+      return backward_impl<Ar>(net, params, obs, batch, (float *)ws, pi, rep, v, a_idx, r_idx, y, adv,
+                               entropy_beta, grad, loss_terms, (hipStream_t)stream);
   });
   return MT_OK;
 }

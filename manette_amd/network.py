@@ -88,12 +88,13 @@ class DeviceNetwork(object):
 
     # ---- parameters ------------------------------------------------------------------------
     def init_params(self, seed=0):
-        """U(-d, d) per variable with the reference init bounds (networks.py:34-89)."""
+        """U(-d, d) per variable with the reference init bounds (networks.py:34-89); d < 0 is
+        N(0, 1) (the LSTM projection, networks.py:124-125)."""
         rs = np.random.RandomState(seed)
         flat = np.zeros(self.nparams, dtype=np.float32)
         for name, shape, off, d in self.vars:
             n = int(np.prod(shape))
-            flat[off:off + n] = rs.uniform(-d, d, size=n).astype(np.float32)
+            flat[off:off + n] = (rs.uniform(-d, d, size=n) if d >= 0 else rs.standard_normal(size=n)).astype(np.float32)
         self.params.copy_(torch.from_numpy(flat))
         self.ms.fill_(1.0)
         self.mom.zero_()
@@ -201,6 +202,14 @@ def preprocess_frames(screens_dev, frame_idx, push_count, E, depth, row_lut, col
     check(_lib.hip().mt_preprocess_frames(C.c_void_p(screens_dev), _ptr(frame_idx), _ptr(push_count), E, depth,
                                           _ptr(row_lut), _ptr(col_lut), _ptr(prev), _ptr(out), _stream()),
           'mt_preprocess_frames')
+
+
+def memory_push(memory, whole_t, fresh, masks):
+    """paac.py:79-83 + :202-203 on device: whole_t <- memory, shift + fresh, zero ended episodes."""
+    E = memory.shape[0]
+    frame = memory[0, 0].numel()
+    check(_lib.hip().mt_memory_push(_ptr(memory), _ptr(whole_t), _ptr(fresh), _ptr(masks), E, frame, _stream()),
+          'mt_memory_push')
 
 
 def returns(rewards, masks, values, v_boot, gamma, y, adv):

@@ -39,8 +39,6 @@ class PAACLearner(ActorLearner):
         self.workers = args.emulator_workers
         self.total_repetitions = args.nb_choices
         self.lstm_bool = (args.arch == 'LSTM')
-        if self.lstm_bool:
-            raise NotImplementedError('LSTM arch: device kernels not built yet (DESIGN.md §next)')
         self.tab_rep = explo_policy.tab_rep
         self.runner_kind = getattr(args, 'runner', 'native')
         self.sampling = getattr(args, 'sampling', 'host')
@@ -63,6 +61,10 @@ class PAACLearner(ActorLearner):
         E, T, C = self.emulator_counts, self.max_local_steps, self.C
         dev = self.dev
         self.states = torch.zeros(T + 1, E, 84, 84, C, dtype=torch.uint8, device=dev)
+        if self.lstm_bool:  # paac.py:107-112: the window each forward reads + its per-step record
+            self.n_steps = 5
+            self.memory = torch.zeros(E, self.n_steps, 84, 84, C, dtype=torch.uint8, device=dev)
+            self.whole_memory = torch.zeros(T, E, self.n_steps, 84, 84, C, dtype=torch.uint8, device=dev)
         self.values = torch.zeros(T, E, dtype=torch.float32, device=dev)
         # [0] = action indices, [1] = repetition indices, each [T][E] (row t*E+e, paac.py:239)
         self.idx = torch.zeros(2, T, E, dtype=torch.int32, device=dev)
@@ -126,7 +128,7 @@ class PAACLearner(ActorLearner):
                                          dtype=torch.uint8, device=self.dev)
                 total = self.runners.reset()
                 self._upload_pushes(total, self.states[0], self.states[0].clone())
-            if self.sampling == 'device':
+            if self.sampling == 'device' and not self.lstm_bool:
                 self._make_native_step()
         else:
             emus = [self.environment_creator.create_environment(i) for i in range(E)]
@@ -215,8 +217,8 @@ class PAACLearner(ActorLearner):
             self.global_step = self._gs.value
             return
         end = self._mark('rollout_forward')
-        v, pi, rep = net.forward(self.states[t], E, out=(self.values[t], self.pi_roll, self.rep_roll),
-                                 ws_key='rollout', infer=True)
+        v, pi, rep = net.forward(self.memory if self.lstm_bool else self.states[t], E,
+                                 out=(self.values[t], self.pi_roll, self.rep_roll), ws_key='rollout', infer=True)
         if end is not None:
             end.record()
         if self.sampling == 'device':
@@ -257,6 +259,9 @@ class PAACLearner(ActorLearner):
             reward, over = sh[1], sh[2]
         self.global_step = self.book.step(self.global_step, a, r, reward, over,
                                           self.rewards_h[t].numpy(), self.masks_h[t].numpy())
+        if self.lstm_bool:  # update_memory + episode-end reset (paac.py:173-174, :202-203)
+            self.masks_d[t].copy_(self.masks_h[t], non_blocking=True)
+            devnet.memory_push(self.memory, self.whole_memory[t], self.states[t + 1], self.masks_d[t])
 
     def update(self):
         """Bootstrap, n-step returns, fused loss backward, [all-reduce], clip + RMSProp
@@ -265,12 +270,16 @@ class PAACLearner(ActorLearner):
         self.book.drain()
         E, T = self.emulator_counts, self.max_local_steps
         N = E * T
-        net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout', infer=True)
+        net.forward(self.memory if self.lstm_bool else self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll),
+                    ws_key='rollout', infer=True)
         self.rm_d.copy_(self.rm_h, non_blocking=True)
         devnet.returns(self.rewards_d, self.masks_d, self.values, self.v_boot, self.gamma, self.y, self.adv)
         lr = self.get_lr()
         net.set_lr(lr)
-        obs = self.states[:T].reshape(N, 84, 84, self.C)
+        if self.lstm_bool:  # flat whole_memory (paac.py:233-234)
+            obs = self.whole_memory.reshape(N, self.n_steps, 84, 84, self.C)
+        else:
+            obs = self.states[:T].reshape(N, 84, 84, self.C)
         end = self._mark('train_pass')
         v, pi, rep = net.forward(obs, N, ws_key='train')
         net.loss_backward(obs, N, v, pi, rep, self.idx[0].view(N), self.idx[1].view(N), self.y.view(N),
@@ -300,6 +309,9 @@ class PAACLearner(ActorLearner):
             torch.distributed.broadcast(self.network.mom, 0)
         self.global_step_start = self.global_step
         self._start_runners()
+        if self.lstm_bool:  # memory[e, -1] = initial state (paac.py:109-112)
+            self.memory.zero_()
+            self.memory[:, -1].copy_(self.states[0])
 
     def train(self):
         """Main actor learner loop (paac.py:86-297)."""

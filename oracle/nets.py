@@ -1,7 +1,7 @@
 """numpy restatement of the policy/value networks, heads, loss and backward (oracle).
 
 networks.py:14-127 (Operations), :152-155 (input scale), :178-192 (NIPS), :206-225 (PWYX),
-:261-278 (NATURE); policy_v_network.py:19-74 (heads + loss). NHWC activations, HWIO conv
+:227-258 (LSTM), :261-278 (NATURE); policy_v_network.py:19-74 (heads + loss). NHWC activations, HWIO conv
 weights, (in, out) dense weights, TF VALID/SAME padding, flatten in NHWC order.
 Backward is the hand-derived gradient of the same graph (TF's ops: Conv2DBackprop*, MatMul
 grads, ReluGrad on the activation output, Softmax/Log grads).
@@ -20,10 +20,11 @@ def arch_spec(arch, depth, num_actions, num_reps):
         convs = [('conv1', 8, 4, C, 32, 'VALID', False), ('conv2', 4, 2, 32, 64, 'VALID', False),
                  ('conv3', 3, 1, 64, 64, 'VALID', False)]
         fc = ('fc4', 512)
-    elif arch == 'PWYX':
+    elif arch in ('PWYX', 'LSTM'):
+        # LSTM (networks.py:227-258) runs the PWYX trunk on each of its 5 window frames
         convs = [('conv1', 5, 1, C, 32, 'SAME', True), ('conv2', 5, 1, 32, 32, 'SAME', True),
                  ('conv3', 4, 1, 32, 64, 'SAME', True), ('conv4', 3, 1, 64, 64, 'SAME', False)]
-        fc = ('fc5', 512)
+        fc = ('fc5', 512) if arch == 'PWYX' else ('fc6', 128)
     else:
         raise ValueError(arch)
     H = 84
@@ -37,13 +38,30 @@ def arch_spec(arch, depth, num_actions, num_reps):
     for (name, k, s, cin, cout, pad, pool) in convs:
         vars_.append(('Network/%s/%s_weights' % (name, name), (k, k, cin, cout), 1.0 / np.sqrt(cout * k * k)))
         vars_.append(('Network/%s/%s_biases' % (name, name), (cout,), 1.0 / np.sqrt(cin * k * k)))
-    vars_.append(('Network/%s/%s_weights' % (fc[0], fc[0]), (flat, F), 1.0 / np.sqrt(flat)))
-    vars_.append(('Network/%s/%s_biases' % (fc[0], fc[0]), (F,), 1.0 / np.sqrt(flat)))
+    lstm = None
+    fc_in = flat
+    if arch == 'LSTM':
+        # Operations.rnn (networks.py:112-127): static_rnn of BasicLSTMCell(32, forget_bias=1) over
+        # 5 steps of 6400 features, then matmul(h_5, w) + b. TF 1.3 names the cell variables
+        # rnn/basic_lstm_cell/{kernel,bias} (get_variable ignores name_scope; kernel = [x, h] x 4
+        # gates i, j, f, o; glorot-uniform kernel, zero bias); w, b are unnamed tf.Variables under
+        # the Network/lstm name scope with N(0, 1) init (bound < 0 below means N(0, 1)). No LSTM
+        # checkpoint exists: names and gate order follow TF 1.3 semantics, parity unpinned.
+        n_hidden, n_steps = 32, 5
+        lstm = dict(hidden=n_hidden, steps=n_steps, forget_bias=1.0)
+        kin = flat + n_hidden
+        vars_.append(('rnn/basic_lstm_cell/kernel', (kin, 4 * n_hidden), np.sqrt(6.0 / (kin + 4 * n_hidden))))
+        vars_.append(('rnn/basic_lstm_cell/bias', (4 * n_hidden,), 0.0))
+        vars_.append(('Network/lstm/Variable', (n_hidden, n_hidden), -1.0))
+        vars_.append(('Network/lstm/Variable_1', (n_hidden,), -1.0))
+        fc_in = n_hidden
+    vars_.append(('Network/%s/%s_weights' % (fc[0], fc[0]), (fc_in, F), 1.0 / np.sqrt(fc_in)))
+    vars_.append(('Network/%s/%s_biases' % (fc[0], fc[0]), (F,), 1.0 / np.sqrt(fc_in)))
     for scope, nm, n in [('Training/Critic', 'critic_output', 1), ('Training/Actor', 'actor_output', num_actions),
                          ('Training/Repetition', 'repetition_output', num_reps)]:
         vars_.append(('%s/%s/%s_weights' % (scope, nm, nm), (F, n), 1.0 / np.sqrt(F)))
         vars_.append(('%s/%s/%s_biases' % (scope, nm, nm), (n,), 1.0 / np.sqrt(F)))
-    return dict(convs=convs, fc=fc, flat=flat, F=F, vars=vars_, A=num_actions, R=num_reps)
+    return dict(convs=convs, fc=fc, flat=flat, F=F, vars=vars_, A=num_actions, R=num_reps, lstm=lstm)
 
 
 def _pads(H, k, s, padding):
@@ -120,8 +138,78 @@ def softmax(z):
     return e / e.sum(axis=1, keepdims=True)
 
 
+def sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def lstm_forward(spec, P, flat, dtype):
+    """Operations.rnn (networks.py:112-127): flat [B*5, 6400] frame features (window-major) ->
+    h = matmul(h_5, w) + b [B, 32]. BasicLSTMCell: z = [x_t, h_{t-1}] K + bias, gates (i, j, f, o),
+    c_t = c_{t-1} sigmoid(f + 1) + sigmoid(i) tanh(j), h_t = tanh(c_t) sigmoid(o); zero state."""
+    L = spec['lstm']
+    nh, T = L['hidden'], L['steps']
+    B = flat.shape[0] // T
+    X = flat.reshape(B, T, -1)
+    K = P['rnn/basic_lstm_cell/kernel'].astype(dtype)
+    kb = P['rnn/basic_lstm_cell/bias'].astype(dtype)
+    c = np.zeros((B, nh), dtype)
+    h = np.zeros((B, nh), dtype)
+    steps = []
+    for t in range(T):
+        xh = np.concatenate([X[:, t], h], axis=1)
+        z = xh @ K + kb
+        i, j, f, o = (z[:, g * nh:(g + 1) * nh] for g in range(4))
+        si, tj, sf, so = sigmoid(i), np.tanh(j), sigmoid(f + L['forget_bias']), sigmoid(o)
+        c_prev = c
+        c = c_prev * sf + si * tj
+        tc = np.tanh(c)
+        h = tc * so
+        steps.append(dict(xh=xh, si=si, tj=tj, sf=sf, so=so, c_prev=c_prev, tc=tc))
+    w = P['Network/lstm/Variable'].astype(dtype)
+    b = P['Network/lstm/Variable_1'].astype(dtype)
+    return h @ w + b, dict(steps=steps, h5=h)
+
+
+def lstm_backward(spec, P, lc, dout, dtype, G):
+    """Gradient of lstm_forward: fills G for the cell and projection variables, returns dflat
+    [B*5, 6400] (TF SigmoidGrad / TanhGrad: y(1-y), 1-y^2 on the forward outputs)."""
+    L = spec['lstm']
+    nh, T = L['hidden'], L['steps']
+    w = P['Network/lstm/Variable'].astype(dtype)
+    K = P['rnn/basic_lstm_cell/kernel'].astype(dtype)
+    G['Network/lstm/Variable'] = lc['h5'].T @ dout
+    G['Network/lstm/Variable_1'] = dout.sum(0)
+    dh = dout @ w.T
+    B = dh.shape[0]
+    dc = np.zeros_like(dh)
+    dK = np.zeros_like(K)
+    dkb = np.zeros(K.shape[1], dtype)
+    nin = K.shape[0] - nh
+    dX = np.zeros((B, T, nin), dtype)
+    for t in range(T - 1, -1, -1):
+        st = lc['steps'][t]
+        dzo = dh * st['tc'] * st['so'] * (1 - st['so'])
+        dc = dc + dh * st['so'] * (1 - st['tc'] ** 2)
+        dzi = dc * st['tj'] * st['si'] * (1 - st['si'])
+        dzj = dc * st['si'] * (1 - st['tj'] ** 2)
+        dzf = dc * st['c_prev'] * st['sf'] * (1 - st['sf'])
+        dc = dc * st['sf']
+        dz = np.concatenate([dzi, dzj, dzf, dzo], axis=1)
+        dK += st['xh'].T @ dz
+        dkb += dz.sum(0)
+        dxh = dz @ K.T
+        dX[:, t] = dxh[:, :nin]
+        dh = dxh[:, nin:]
+    G['rnn/basic_lstm_cell/kernel'] = dK
+    G['rnn/basic_lstm_cell/bias'] = dkb
+    return dX.reshape(B * T, nin)
+
+
 def forward(spec, P, obs, act='relu', alpha=0.1, temp=1.0, dtype=np.float64):
-    """P: dict name -> array. obs uint8 [B,84,84,C]. Returns (v, pi, rep, cache)."""
+    """P: dict name -> array. obs uint8 [B,84,84,C] (LSTM: [B,5,84,84,C], the memory window of
+    paac.py:79-83). Returns (v, pi, rep, cache)."""
+    if spec.get('lstm'):
+        obs = obs.reshape((-1,) + obs.shape[2:])
     x = obs.astype(dtype) * dtype(1.0 / 255.0)  # networks.py:155
     cache = dict(layers=[])
     for (name, k, s, cin, cout, pad, pool) in spec['convs']:
@@ -138,11 +226,15 @@ def forward(spec, P, obs, act='relu', alpha=0.1, temp=1.0, dtype=np.float64):
         x = y
     B = x.shape[0]
     flat = x.reshape(B, -1)
+    cache.update(flat=flat)
+    fc_in = flat
+    if spec.get('lstm'):
+        fc_in, cache['lstm'] = lstm_forward(spec, P, flat, dtype)
     fc = spec['fc'][0]
     Wf = P['Network/%s/%s_weights' % (fc, fc)].astype(dtype)
     bf = P['Network/%s/%s_biases' % (fc, fc)].astype(dtype)
-    h = act_fwd(flat @ Wf + bf, act, alpha)
-    cache.update(flat=flat, h=h)
+    h = act_fwd(fc_in @ Wf + bf, act, alpha)
+    cache.update(fc_in=fc_in, h=h)
     Wc = P['Training/Critic/critic_output/critic_output_weights'].astype(dtype)
     bc = P['Training/Critic/critic_output/critic_output_biases'].astype(dtype)
     Wa = P['Training/Actor/actor_output/actor_output_weights'].astype(dtype)
@@ -200,9 +292,11 @@ def loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0
     dh = (dv[:, None] @ Wc.T + dza @ Wa.T + dzr @ Wr.T) * act_bwd(h, act, alpha)
     fc = spec['fc'][0]
     Wf = P['Network/%s/%s_weights' % (fc, fc)].astype(dtype)
-    G['Network/%s/%s_weights' % (fc, fc)] = c['flat'].T @ dh
+    G['Network/%s/%s_weights' % (fc, fc)] = c['fc_in'].T @ dh
     G['Network/%s/%s_biases' % (fc, fc)] = dh.sum(0)
     dflat = dh @ Wf.T
+    if spec.get('lstm'):
+        dflat = lstm_backward(spec, P, c['lstm'], dflat, dtype, G)
     layers = c['layers']
     last = layers[-1]
     dx = dflat.reshape(last['yp'].shape if last['pool'] else last['y'].shape)
@@ -225,7 +319,9 @@ def loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0
 
 
 def init_params(spec, seed):
-    """U(-d, d) with the TF init bounds of networks.py:34-89 (the TF RNG stream itself is not
-    reproducible without TF; parity is on the bounds)."""
+    """U(-d, d) with the TF init bounds of networks.py:34-89, N(0, 1) where d < 0
+    (networks.py:124-125) (the TF RNG stream itself is not reproducible without TF; parity is
+    on the bounds)."""
     rs = np.random.RandomState(seed)
-    return {n: rs.uniform(-d, d, size=shape).astype(np.float32) for (n, shape, d) in spec['vars']}
+    return {n: (rs.uniform(-d, d, size=shape) if d >= 0 else rs.standard_normal(size=shape)).astype(np.float32)
+            for (n, shape, d) in spec['vars']}

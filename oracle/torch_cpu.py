@@ -28,6 +28,9 @@ class TorchCPUNetwork(object):
 
     def _forward(self, states):
         P = self.P
+        lstm = self.spec.get('lstm')
+        if lstm:  # memory windows [B, 5, 84, 84, C] -> 5B frames (networks.py:239-241)
+            states = np.ascontiguousarray(states).reshape((-1,) + states.shape[2:])
         x = torch.from_numpy(np.ascontiguousarray(states)).permute(0, 3, 1, 2).float() * (1.0 / 255.0)
         for (name, k, s, cin, cout, pad, pool) in self.spec['convs']:
             W = P['Network/%s/%s_weights' % (name, name)].permute(3, 2, 0, 1)
@@ -40,6 +43,18 @@ class TorchCPUNetwork(object):
             if pool:
                 x = Fn.max_pool2d(x, 2, 2)
         flat = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+        if lstm:  # BasicLSTMCell(32, forget_bias=1) x 5 + linear projection (networks.py:112-127)
+            nh, S = lstm['hidden'], lstm['steps']
+            X = flat.reshape(-1, S, flat.shape[1])
+            K, kb = P['rnn/basic_lstm_cell/kernel'], P['rnn/basic_lstm_cell/bias']
+            h = torch.zeros(X.shape[0], nh)
+            c = torch.zeros(X.shape[0], nh)
+            for t in range(S):
+                z = torch.cat([X[:, t], h], 1) @ K + kb
+                i, j, f, o = z.split(nh, 1)
+                c = c * torch.sigmoid(f + lstm['forget_bias']) + torch.sigmoid(i) * torch.tanh(j)
+                h = torch.tanh(c) * torch.sigmoid(o)
+            flat = h @ P['Network/lstm/Variable'] + P['Network/lstm/Variable_1']
         fc = self.spec['fc'][0]
         h = torch.relu(flat @ P['Network/%s/%s_weights' % (fc, fc)] + P['Network/%s/%s_biases' % (fc, fc)])
         v = (h @ P['Training/Critic/critic_output/critic_output_weights'] +

@@ -34,7 +34,8 @@ def test_libraries_export_every_symbol():
 
 
 @pytest.mark.parametrize('arch,depth,A,R', [('NIPS', 1, 6, 1), ('NIPS', 3, 3, 11), ('NATURE', 1, 4, 11),
-                                            ('NATURE', 3, 18, 1), ('PWYX', 1, 9, 11), ('PWYX', 3, 4, 11)])
+                                            ('NATURE', 3, 18, 1), ('PWYX', 1, 9, 11), ('PWYX', 3, 4, 11),
+                                            ('LSTM', 1, 9, 11), ('LSTM', 3, 6, 1)])
 def test_layout_matches_oracle(arch, depth, A, R):
     import ctypes as C
     from manette_amd import _lib
@@ -60,7 +61,7 @@ def test_layout_matches_oracle(arch, depth, A, R):
             assert tuple(sh[k] for k in range(nd.value)) == tuple(shape)
             assert np.float32(b.value) == np.float32(bound)
             assert off.value >= prev_end
-            if name.endswith('_biases'):
+            if i % 2 == 1:
                 assert off.value == prev_end  # (weights, biases) contiguous
             else:
                 assert off.value % 64 == 0
@@ -68,6 +69,11 @@ def test_layout_matches_oracle(arch, depth, A, R):
         n = C.c_size_t()
         lib.mt_net_num_params(h, C.byref(n))
         assert n.value >= prev_end
+        # SURVEY §8 parameter totals (checkpoint-consistent where a checkpoint exists)
+        total = sum(int(np.prod(sh)) for _, sh, _ in spec['vars'])
+        known = {('NIPS', 1, 6, 1): 678200, ('LSTM', 1, 9, 11): 930037}
+        if (arch, depth, A, R) in known:
+            assert total == known[(arch, depth, A, R)]
         ws = C.c_size_t()
         _lib.check(lib.mt_net_workspace_bytes(h, 160, C.byref(ws)))
         assert ws.value > 0

@@ -1,0 +1,201 @@
+"""LSTM arch (networks.py:227-258) on the device vs the float64 oracle, through the C ABI.
+
+obs are memory windows [B][5][84][84][4*depth] (paac.py:79-83). Tolerances as the other
+arches: forward 2e-5 relative, gradients 2e-4 relative L2 per variable (the cell kernel's
+dot products run over K = 6432). With tens of frames the fp64 oracle finds a few max-pool
+windows whose top two values differ by < 1e-6 relative; fp32 rounding may route such a
+window's gradient to the other position (MaxPoolGrad is discontinuous there), which moves the
+weight gradients of the pooled convs (conv1-3) by ~1e-3 relative L2 per flip. Those variables
+are checked at 5e-3 when the oracle counts such near-ties (still far below any indexing or
+layout error, which is O(1)); every other variable, and every variable when there is no
+near-tie, at 2e-4.
+The LSTM's TF1 kernel arithmetic is parity-unpinned (no LSTM checkpoint, TF absent): the
+oracle restates BasicLSTMCell and is itself checked against torch's LSTM cell in
+tests/test_oracle_torch.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nets
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(depth, A, R, seed, act='relu'):
+    from manette_amd.network import DeviceNetwork
+    conf = dict(arch='LSTM', rgb=depth == 3, num_actions=A, nb_choices=R, softmax_temp=1.0,
+                entropy_regularisation_strength=0.02, clip_norm=3.0, clip_norm_type='global',
+                activation=act, alpha_leaky_relu=0.1)
+    net = DeviceNetwork(conf)
+    net.init_params(seed)
+    # non-zero cell bias so every gate term is exercised (TF initialises it to zero)
+    P = net.get_variables()
+    P['rnn/basic_lstm_cell/bias'] = np.random.RandomState(seed).uniform(-0.5, 0.5, 128).astype(np.float32)
+    net.set_variables(P)
+    return net
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(np.asarray(a, np.float64) - b) / max(np.linalg.norm(b), 1e-12))
+
+
+def _near_tie_layers(spec, P, obs, act):
+    """Names of pooled convs at or below a max-pool window with a near-tie (< 1e-5 relative)."""
+    _, _, _, cache = nets.forward(spec, P, obs, act=act, alpha=0.1)
+    hit = []
+    for L in cache['layers']:
+        if not L['pool']:
+            continue
+        y = L['y']
+        B, H, W, C = y.shape
+        w = y[:, :H // 2 * 2, :W // 2 * 2].reshape(B, H // 2, 2, W // 2, 2, C).transpose(0, 1, 3, 5, 2, 4)
+        s = np.sort(w.reshape(-1, 4), axis=1)
+        gap = (s[:, 3] - s[:, 2]) / np.maximum(np.abs(s[:, 3]), 1e-30)
+        if ((gap > 0) & (gap < 1e-5)).any():
+            hit.append(L['name'])
+    if not hit:
+        return set()
+    last = max(int(n[4:]) for n in hit)
+    return {'Network/conv%d/conv%d_%s' % (i, i, k) for i in range(1, last + 1) for k in ('weights', 'biases')}
+
+
+def _windows(rs, B, depth, zero_frac=0.3):
+    obs = rs.randint(0, 256, size=(B, 5, 84, 84, 4 * depth)).astype(np.uint8)
+    # zeroed leading frames, as after an episode end (paac.py:202-203)
+    for b in range(B):
+        k = rs.randint(0, 5) if rs.rand() < zero_frac else 0
+        obs[b, :k] = 0
+    return obs
+
+
+@pytest.mark.parametrize('depth,A,R,act', [(1, 9, 11, 'relu'), (3, 4, 1, 'relu'), (1, 6, 3, 'leaky_relu')])
+@pytest.mark.parametrize('B', [1, 6, 33])
+def test_lstm_forward_parity(depth, A, R, act, B):
+    net = _net(depth, A, R, seed=B, act=act)
+    rs = np.random.RandomState(B)
+    obs = _windows(rs, B, depth)
+    v, pi, rep = net.forward(torch.from_numpy(obs).cuda())
+    v2, pi2, rep2 = [t.clone() for t in net.forward(torch.from_numpy(obs).cuda(), infer=True, ws_key='i')]
+    torch.cuda.synchronize()
+    spec = nets.arch_spec('LSTM', depth, A, R)
+    v0, pi0, rep0, _ = nets.forward(spec, net.get_variables(), obs, act=act, alpha=0.1)
+    np.testing.assert_allclose(v.cpu().numpy(), v0, rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(pi.cpu().numpy(), pi0, rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(rep.cpu().numpy(), rep0, rtol=2e-5, atol=1e-6)
+    np.testing.assert_array_equal(v2.cpu().numpy(), v.cpu().numpy())
+    np.testing.assert_array_equal(pi2.cpu().numpy(), pi.cpu().numpy())
+
+
+@pytest.mark.parametrize('depth,A,R,act', [(1, 9, 11, 'relu'), (3, 4, 1, 'relu'), (1, 6, 3, 'leaky_relu')])
+@pytest.mark.parametrize('B', [4, 9, 32])
+def test_lstm_loss_backward_parity(depth, A, R, act, B):
+    net = _net(depth, A, R, seed=7 + B, act=act)
+    rs = np.random.RandomState(100 + B)
+    obs = _windows(rs, B, depth)
+    a_idx = rs.randint(0, A, size=B).astype(np.int32)
+    r_idx = rs.randint(0, R, size=B).astype(np.int32)
+    y = rs.randn(B).astype(np.float32)
+    adv = rs.randn(B).astype(np.float32)
+    d = lambda x: torch.from_numpy(x).cuda()
+    obs_d = d(obs)
+    v, pi, rep = net.forward(obs_d)
+    terms = torch.zeros(B, 4, device='cuda')
+    net.loss_backward(obs_d, B, v, pi, rep, d(a_idx), d(r_idx), d(y), d(adv), loss_terms=terms)
+    torch.cuda.synchronize()
+    spec = nets.arch_spec('LSTM', depth, A, R)
+    loss, G, aux = nets.loss_and_grads(spec, net.get_variables(), obs, a_idx, r_idx, y, adv, 0.02, act=act,
+                                       alpha=0.1)
+    got = net.get_variables('grad')
+    loose = _near_tie_layers(spec, net.get_variables(), obs, act)
+    errs = {name: _rel(got[name], G[name]) for name, _, _ in spec['vars']}
+    bad = {n: e for n, e in errs.items() if e >= (5e-3 if n in loose else 2e-4)}
+    assert not bad, (bad, sorted(loose))
+    np.testing.assert_allclose(terms.cpu().numpy(), aux['terms'], rtol=1e-4, atol=1e-5)
+    flat = net.grad.cpu().numpy()
+    mask = np.ones(net.nparams, bool)
+    for _, shape, off, _ in net.vars:
+        mask[off:off + int(np.prod(shape))] = False
+    assert not flat[mask].any()
+
+
+def _np_memory_push(memory, fresh, masks):
+    """paac.py:79-83 update_memory, then :202-203 memory[e] = 0 for ended episodes."""
+    whole = memory.copy()
+    memory[:, :-1] = memory[:, 1:]
+    memory[:, -1] = fresh
+    memory[masks == 0] = 0
+    return whole
+
+
+@pytest.mark.parametrize('E,depth', [(1, 1), (7, 1), (32, 3)])
+def test_memory_push_bit_exact(E, depth):
+    from manette_amd.network import memory_push
+    rs = np.random.RandomState(E)
+    mem = rs.randint(0, 256, size=(E, 5, 84, 84, 4 * depth)).astype(np.uint8)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    mem_d = d(mem)
+    whole_d = torch.zeros_like(mem_d)
+    for step in range(4):
+        fresh = rs.randint(0, 256, size=(E, 84, 84, 4 * depth)).astype(np.uint8)
+        masks = (rs.rand(E) > 0.3).astype(np.float32)
+        memory_push(mem_d, whole_d, d(fresh), d(masks))
+        whole = _np_memory_push(mem, fresh, masks)
+        np.testing.assert_array_equal(whole_d.cpu().numpy(), whole)
+        np.testing.assert_array_equal(mem_d.cpu().numpy(), mem)
+
+
+def test_lstm_learner_memory_windows(tmp_path):
+    """The learner's device memory windows (forward input at every step and the flat train
+    batch, paac.py:107-112, :173-174, :202-203, :233-234) equal a numpy replay of the reference
+    bookkeeping over the recorded states and episode-end masks, with resets inside the rollout;
+    the LSTM update runs and changes the parameters."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import train as cli
+    from manette_amd.exploration_policy import ExplorationPolicy
+    from manette_amd.paac import PAACLearner
+    from manette_amd.synthetic import SyntheticBank
+    a = cli.get_arg_parser().parse_args([])
+    a.game, a.arch, a.emulator_counts, a.emulator_workers = 'ms_pacman', 'LSTM', 6, 2
+    a.max_repetition, a.nb_choices = 10, 11
+    a.runner, a.sampling, a.seed = 'native', 'device', 0
+    a.debugging_folder = str(tmp_path) + '/'
+    a.max_global_steps = 1 << 40
+    a.checkpoint_interval = 1 << 40
+    np.random.seed(1234)
+    explo = ExplorationPolicy(a)
+    nc, ec = cli.get_network_and_environment_creator(a, explo)
+    ec.create_bank = lambda first, n: SyntheticBank(first, n, episode_len=9)
+    L = PAACLearner(nc, ec, explo, a)
+    L.start()
+    assert L.native_step is None  # LSTM takes the Python step
+    try:
+        E, T = 6, L.max_local_steps
+        mem = L.memory.cpu().numpy()
+        s0 = L.states[0].cpu().numpy()
+        assert (mem[:, :-1] == 0).all() and (mem[:, -1] == s0).all()
+        p0 = L.network.params.cpu().numpy().copy()
+        resets = 0
+        for u in range(3):
+            L.book.new_update()
+            for t in range(T):
+                L.step(t)
+            torch.cuda.synchronize()
+            states = L.states.cpu().numpy()
+            masks = L.masks_h.numpy().copy()
+            resets += int((masks == 0).sum())
+            whole = np.zeros((T,) + mem.shape, np.uint8)
+            for t in range(T):
+                whole[t] = _np_memory_push(mem, states[t + 1], masks[t])
+            np.testing.assert_array_equal(L.whole_memory.cpu().numpy(), whole)
+            np.testing.assert_array_equal(L.memory.cpu().numpy(), mem)
+            L.update()
+        torch.cuda.synchronize()
+        assert resets > 0
+        p1 = L.network.params.cpu().numpy()
+        assert np.isfinite(p1).all() and not np.array_equal(p0, p1)
+    finally:
+        L.cleanup()

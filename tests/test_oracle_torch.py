@@ -10,6 +10,9 @@ from oracle import nets
 
 def torch_loss(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1):
     T = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in P.items()}
+    lstm = spec.get('lstm')
+    if lstm:  # [B, 5, 84, 84, C] memory windows -> 5B frames
+        obs = obs.reshape((-1,) + obs.shape[2:])
     x = torch.tensor(obs, dtype=torch.float64) / 255.0
     x = x.permute(0, 3, 1, 2)
     for (name, k, s, cin, cout, pad, pool) in spec['convs']:
@@ -25,6 +28,24 @@ def torch_loss(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1):
         if pool:
             x = Fn.max_pool2d(x, 2, 2)
     flat = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # NHWC flatten (networks.py:14-17)
+    if lstm:
+        # torch.nn.LSTMCell (gate order i, f, g, o) with the TF kernel (i, j, f, o) mapped onto it
+        # and forget_bias folded into b_ih: an independent restatement of BasicLSTMCell.
+        nh, S = lstm['hidden'], lstm['steps']
+        K, kb = T['rnn/basic_lstm_cell/kernel'], T['rnn/basic_lstm_cell/bias']
+        nin = K.shape[0] - nh
+        perm = torch.cat([torch.arange(0, nh), torch.arange(2 * nh, 3 * nh), torch.arange(nh, 2 * nh),
+                          torch.arange(3 * nh, 4 * nh)])
+        fb = torch.zeros(4 * nh, dtype=torch.float64)
+        fb[nh:2 * nh] = lstm['forget_bias']
+        X = flat.reshape(-1, S, nin)
+        Bw = X.shape[0]
+        h5 = torch.zeros(Bw, nh, dtype=torch.float64)
+        c5 = torch.zeros(Bw, nh, dtype=torch.float64)
+        for t in range(S):
+            h5, c5 = torch._VF.lstm_cell(X[:, t], (h5, c5), K[:nin, perm].T, K[nin:, perm].T, kb[perm] + fb,
+                                         torch.zeros(4 * nh, dtype=torch.float64))
+        flat = h5 @ T['Network/lstm/Variable'] + T['Network/lstm/Variable_1']
     fc = spec['fc'][0]
     h = flat @ T['Network/%s/%s_weights' % (fc, fc)] + T['Network/%s/%s_biases' % (fc, fc)]
     h = torch.relu(h) if act == 'relu' else torch.maximum(h, alpha * h)
@@ -47,13 +68,17 @@ def torch_loss(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1):
 
 
 @pytest.mark.parametrize('arch,depth,A,R,act', [('NIPS', 1, 6, 1, 'relu'), ('NATURE', 1, 4, 11, 'relu'),
-                                                ('NIPS', 3, 5, 3, 'leaky_relu'), ('PWYX', 1, 4, 11, 'relu')])
+                                                ('NIPS', 3, 5, 3, 'leaky_relu'), ('PWYX', 1, 4, 11, 'relu'),
+                                                ('LSTM', 1, 9, 11, 'relu'), ('LSTM', 1, 4, 1, 'leaky_relu')])
 def test_oracle_backward_vs_autograd(arch, depth, A, R, act):
     spec = nets.arch_spec(arch, depth, A, R)
     P = {k: v.astype(np.float64) for k, v in nets.init_params(spec, 1).items()}
+    if arch == 'LSTM':  # non-zero cell bias so every gate term is exercised
+        P['rnn/basic_lstm_cell/bias'] = np.random.RandomState(3).uniform(-0.5, 0.5, 128)
     rs = np.random.RandomState(2)
     B = 3
-    obs = rs.randint(0, 256, size=(B, 84, 84, 4 * depth)).astype(np.uint8)
+    shape = (B, 5, 84, 84, 4 * depth) if arch == 'LSTM' else (B, 84, 84, 4 * depth)
+    obs = rs.randint(0, 256, size=shape).astype(np.uint8)
     a_idx = rs.randint(0, A, B)
     r_idx = rs.randint(0, R, B)
     y = rs.randn(B)
@@ -63,3 +88,19 @@ def test_oracle_backward_vs_autograd(arch, depth, A, R, act):
     assert abs(loss - tl) < 1e-10 * max(1, abs(tl))
     for k in TG:
         np.testing.assert_allclose(G[k].reshape(TG[k].shape), TG[k], rtol=1e-8, atol=1e-12, err_msg=k)
+
+
+@pytest.mark.parametrize('arch,A,R', [('NIPS', 6, 1), ('NATURE', 4, 11), ('LSTM', 9, 11)])
+def test_cpu_baseline_network_matches_oracle(arch, A, R):
+    """The timed CPU baseline's torch network (oracle/torch_cpu.py) computes the oracle's graph."""
+    from oracle.torch_cpu import TorchCPUNetwork
+    net = TorchCPUNetwork(arch, 1, A, R, seed=4, threads=2)
+    rs = np.random.RandomState(5)
+    shape = (2, 5, 84, 84, 4) if arch == 'LSTM' else (2, 84, 84, 4)
+    obs = rs.randint(0, 256, size=shape).astype(np.uint8)
+    v, pi, rep = net.forward(obs)
+    P = {k: t.detach().numpy() for k, t in net.P.items()}
+    v0, pi0, rep0, _ = nets.forward(net.spec, P, obs)
+    np.testing.assert_allclose(v, v0, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(pi, pi0, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(rep, rep0, rtol=1e-4, atol=1e-6)
