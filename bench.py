@@ -39,6 +39,23 @@ CONFIGS = {
 }
 MI355X_FP32_TFLOPS = 157.3   # dense fp32 (vector = MFMA), MI355X_MICROARCH.md
 MI355X_HBM_GBS = 8000.0      # HBM3E peak, MI355X_MICROARCH.md
+# the one kernel mt_forward_trunk launches (its rocprof name), per arch where it is a single kernel
+TRUNK_KERNEL = {'NIPS': 'nips_fused_trunk_kernel'}
+
+
+def load_pmc(config, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
+    (profiles/pmc_<config>.json, written by tools/pmc.sh + tools/pmc_summary.py), or None."""
+    if not kernel:
+        return None
+    path = os.path.join(ROOT, 'profiles', 'pmc_%s.json' % config)
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    for k, v in d.items():
+        if k.split('<')[0].endswith(kernel):
+            return dict(hbm_bytes=v['hbm_bytes'], source='profiles/pmc_%s.json' % config)
+    return None
 
 
 def conv_out(h, k, s):
@@ -164,8 +181,9 @@ def main():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--step_impl', default='native', choices=['native', 'python'],
                     help='macro-step orchestration: native (mt_rollout_step) or Python')
-    ap.add_argument('--staging', default='in_place', choices=['in_place', 'zero_copy', 'copy', 'pooled'])
-    ap.add_argument('--pipeline', action='store_true', help='MT_ROLLOUT_PIPELINED native step')
+    ap.add_argument('--staging', default='zero_copy', choices=['in_place', 'zero_copy', 'copy', 'pooled'])
+    ap.add_argument('--no_pipeline', dest='pipeline', action='store_false',
+                    help='disable MT_ROLLOUT_PIPELINED (on by default)')
     a = ap.parse_args()
 
     import torch
@@ -235,18 +253,31 @@ def main():
         elapsed = float(e.item())
     prof = {k: [s.elapsed_time(e) for (s, e) in v] for k, v in learner.profile.items()}
     learner.profile = None
-    # rollout-batch forward (E rows), timed with HIP events on its stream, back to back
+    # rollout-batch forward (E rows) and its trunk half alone (the roofline kernel: mt_forward_trunk,
+    # one launch of the fused NIPS trunk), each timed with HIP events on the stream they are
+    # launched on (torch's current stream, passed to every C-ABI call), back to back
     E = cfg['ec']
+    x_roll = learner.memory if learner.lstm_bool else learner.states[0]
     fw = []
-    for _ in range(30):
+    for it in range(30):
         s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s_ev.record()
-        learner.network.forward(learner.memory if learner.lstm_bool else learner.states[0], E,
-                                out=(learner.v_boot, learner.pi_roll, learner.rep_roll), ws_key='rollout', infer=True)
+        learner.network.forward(x_roll, E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
+                                ws_key='rollout', infer=True)
         e_ev.record()
         fw.append((s_ev, e_ev))
+    # trunk: 5 warm launches, then 40 launches back to back between one event pair (the GPU
+    # stays busy, so the per-launch average is the kernel's duration, as rocprof reports it)
+    for _ in range(5):
+        learner.network.forward_trunk(x_roll, E, ws_key='rollout')
+    s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_ev.record()
+    for _ in range(40):
+        learner.network.forward_trunk(x_roll, E, ws_key='rollout')
+    e_ev.record()
     torch.cuda.synchronize()
-    prof['rollout_forward'] = [s_ev.elapsed_time(e_ev) for (s_ev, e_ev) in fw[5:]]
+    prof['rollout_forward'] = [s_ev_.elapsed_time(e_ev_) for (s_ev_, e_ev_) in fw[5:]]
+    prof['rollout_trunk'] = [s_ev.elapsed_time(e_ev) / 40.0]
     ec = cfg['ec']
     value = world * ec * T * a.steps / elapsed
 
@@ -258,10 +289,21 @@ def main():
         tp_ms = float(np.mean(prof['train_pass']))
         tp_flops = train_pass_flops(layers, N)
         rf_ms = float(np.mean(prof['rollout_forward']))
+        tk_ms = float(np.mean(prof['rollout_trunk']))
         fwd_flops = ec * sum(l[1] for l in layers)
         frames = 5 if cfg['arch'] == 'LSTM' else 1
         fwd_bytes = (ec * frames * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in layers) +
                      4 * ec * sum(l[3] for l in layers))
+        # trunk (roofline kernel): algorithmic bytes = the frames read once + the trunk weights
+        # read once + the dense layer's pre-activation output written once
+        trunk = [l for l in layers if l[0] in ('conv', 'fc', 'lstm')]
+        if cfg['arch'] == 'LSTM':
+            trunk = [l for l in layers if l[0] in ('conv', 'lstm')]
+        out_floats = (4 * 32 * frames) if cfg['arch'] == 'LSTM' else trunk[-1][3]
+        tk_bytes = ec * frames * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in trunk) + 4 * ec * out_floats
+        tk_flops = ec * sum(l[1] for l in trunk)
+        tk_gbs = tk_bytes / (tk_ms * 1e-3) / 1e9
+        pmc = load_pmc(a.config, TRUNK_KERNEL.get(cfg['arch']))
         achieved = tp_flops / (tp_ms * 1e-3) / 1e12
         line = {
             'metric': 'env-steps/sec (ec x t_max frames per update)',
@@ -279,10 +321,17 @@ def main():
             'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step, %s staging%s' % (
                 a.config, ec, cfg['ew'], T, a.sampling, a.step_impl, a.staging, ', pipelined' if a.pipeline else ''), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
                 'global_emulators': ec * world, 'parallelism': 'dp%d' % world},
-            'roofline': {'bound': 'mfma', 'kernel': 'train pass (fwd+bwd, %d rows)' % N,
-                         'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',
-                         'frac': round(achieved / MI355X_FP32_TFLOPS, 4), 'traffic': None,
-                         'ms_per_launch': round(tp_ms, 4), 'flop_per_launch': tp_flops},
+            'roofline': {'bound': 'hbm', 'kernel': TRUNK_KERNEL.get(cfg['arch'], 'mt_forward_trunk (layered)'),
+                         'achieved': round(tk_gbs, 1), 'peak': MI355X_HBM_GBS, 'unit': 'GB/s',
+                         'frac': round(tk_gbs / MI355X_HBM_GBS, 4),
+                         'traffic': pmc['hbm_bytes'] if pmc else None,
+                         'algorithmic_bytes_per_launch': tk_bytes, 'us_per_launch': round(tk_ms * 1e3, 2),
+                         'tflops': round(tk_flops / (tk_ms * 1e-3) / 1e12, 3),
+                         'traffic_source': pmc['source'] if pmc else None},
+            'train_pass': {'bound': 'mfma', 'kernels': 'forward + fused loss backward, %d rows' % N,
+                           'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',
+                           'frac': round(achieved / MI355X_FP32_TFLOPS, 4),
+                           'ms_per_launch': round(tp_ms, 4), 'flop_per_launch': tp_flops},
             'rollout_forward': {'ms': round(rf_ms, 4), 'tflops': round(fwd_flops / (rf_ms * 1e-3) / 1e12, 3),
                                 'hbm_gbs': round(fwd_bytes / (rf_ms * 1e-3) / 1e9, 1),
                                 'hbm_frac': round(fwd_bytes / (rf_ms * 1e-3) / 1e9 / MI355X_HBM_GBS, 4)},

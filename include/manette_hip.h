@@ -96,6 +96,11 @@ int mt_forward(const mt_net *net, const float *params, const uint8_t *obs, int b
 int mt_forward_infer(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                      size_t ws_bytes, float *v, float *pi, float *rep, mt_stream_t stream);
 
+/* Trunk half of mt_forward_infer alone (roofline timing / diagnostics): the convs and the dense
+ * layer's partial products, left in `ws` (NIPS: the one fused-trunk launch). */
+int mt_forward_trunk(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
+                     size_t ws_bytes, mt_stream_t stream);
+
 /* ---- device multinomial sampling (perf mode of A3) -----------------------------------------
  * Replaces ExplorationPolicy.multinomial_choose (exploration_policy.py:108-116) with an
  * inverse-CDF draw on (p - float32 epsneg), the last category taking the remainder — the

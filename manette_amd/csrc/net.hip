@@ -941,6 +941,54 @@ extern "C" int mt_forward(const mt_net *net, const float *params, const uint8_t 
                             (hipStream_t)stream);
 }
 
+// Trunk half of the inference forward (diagnostics / roofline timing): everything up to the
+// dense layer's partial slabs that heads_fwd_kernel finishes — the fused NIPS trunk, else the
+// layered convs + split-K fc (LSTM: the 5B-frame trunk + the cell's x-product slabs).
+template <class Ar>
+static int trunk_infer_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws, hipStream_t s) {
+  if constexpr (Ar::LSTM) {
+    LstmWs X;
+    const WsLayout L = lstm_ws_layout<Ar>(n, B, &X);
+    const int rows = B * Ar::STEPS;
+    MT_TRY((trunk_forward<Ar>(n, P, obs, rows, ws, L, s)));
+    return launch_gemm<TileFc>(LdRowMajor{layer_out<Ar, Ar::NCONV - 1>(ws, L), Ar::FLAT},
+                               LdColMajor{P + n->off_lstm, Ar::G4, -1}, EpSlab{ws + X.xg, rows, Ar::G4}, rows,
+                               Ar::G4, Ar::FLAT, X.xg_splits, s);
+  } else {
+    const WsLayout L = ws_layout<Ar>(n, B);
+    const float *Wfc = P + n->off_fc;
+    if constexpr (Ar::FUSED_SLABS > 0) {
+      constexpr int C = LayerG<Ar, 0>::CIN;
+      using Fz = FusedNips<C>;
+      hipLaunchKernelGGL(nips_fused_trunk_kernel<C>, dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, obs, B,
+                         P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation, n->cfg.alpha_leaky,
+                         ws + L.fcslab);
+      MT_LAUNCHED();
+      return MT_OK;
+    } else {
+      MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s)));
+      return launch_gemm<TileFc>(LdRowMajor{layer_out<Ar, Ar::NCONV - 1>(ws, L), Ar::FLAT},
+                                 LdColMajor{Wfc, Ar::F, -1}, EpSlab{ws + L.fcslab, B, Ar::F}, B, Ar::F, Ar::FLAT,
+                                 L.fc_splits, s);
+    }
+  }
+}
+
+extern "C" int mt_forward_trunk(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
+                                size_t ws_bytes, mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && obs && ws, "null argument");
+  MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
+  MT_ARCH_SWITCH(net, {
+    const WsLayout L = ws_layout<Ar>(net, batch);
+    if (ws_bytes < L.total * sizeof(float)) {
+      set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
+      return MT_ERR_WORKSPACE;
+    }
+    return trunk_infer_impl<Ar>(net, params, obs, batch, (float *)ws, (hipStream_t)stream);
+  });
+  return MT_OK;
+}
+
 extern "C" int mt_forward_infer(const mt_net *net, const float *params, const uint8_t *obs, int batch,
                                 void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
                                 mt_stream_t stream) {

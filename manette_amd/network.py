@@ -151,6 +151,12 @@ class DeviceNetwork(object):
                  _stream()), 'mt_forward_infer' if infer else 'mt_forward')
         return v, pi, rep
 
+    def forward_trunk(self, obs, batch, ws_key=None):
+        """mt_forward_trunk: the trunk half of the inference forward only (roofline timing)."""
+        ws = self.workspace(batch, ws_key)
+        check(_lib.hip().mt_forward_trunk(self._h, _ptr(self.params), _ptr(obs), int(batch), _ptr(ws), ws.numel(),
+                                          _stream()), 'mt_forward_trunk')
+
     def loss_backward(self, obs, B, v, pi, rep, a_idx, r_idx, y, adv, loss_terms=None, ws_key=None):
         """Gradient of policy_v_network.py:25-74 into self.grad (needs forward() on obs first)."""
         ws = self.workspace(B, ws_key)
