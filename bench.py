@@ -63,9 +63,10 @@ def conv_out(h, k, s):
 
 
 def arch_flops(arch, depth, A, R):
-    """Per sample per layer: (kind, forward FLOPs = 2*MACs, weight floats, output floats) for
-    NIPS / NATURE / PWYX / LSTM (networks.py:178-278). An LSTM sample is a 5-frame window: its
-    trunk layers count 5 frames, then the cell (x and h products), projection and fc6."""
+    """Per layer: (kind, forward FLOPs = 2*MACs, weight floats, output floats) for NIPS / NATURE /
+    PWYX / LSTM (networks.py:178-278), per frame for the trunk ('conv', LSTM 'lstm_x') and per
+    sample for the rest. The LSTM build computes each distinct frame once (frame store), so its
+    per-frame and per-window costs are counted separately (train_pass_flops)."""
     C = 4 * depth
     if arch == 'NIPS':
         convs = [(8, 4, C, 16, 'VALID', False), (4, 2, 16, 32, 'VALID', False)]
@@ -77,19 +78,18 @@ def arch_flops(arch, depth, A, R):
         convs = [(5, 1, C, 32, 'SAME', True), (5, 1, 32, 32, 'SAME', True), (4, 1, 32, 64, 'SAME', True),
                  (3, 1, 64, 64, 'SAME', False)]
         F = 128 if arch == 'LSTM' else 512
-    frames = 5 if arch == 'LSTM' else 1
     h = 84
     layers = []
     for (k, s, cin, cout, pad, pool) in convs:
         h = conv_out(h, k, s) if pad == 'VALID' else -(-h // s)
-        layers.append(('conv', frames * 2.0 * h * h * cout * k * k * cin, k * k * cin * cout + cout,
-                       frames * h * h * cout))
+        layers.append(('conv', 2.0 * h * h * cout * k * k * cin, k * k * cin * cout + cout, h * h * cout))
         if pool:
             h //= 2
     flat = h * h * convs[-1][3]
     if arch == 'LSTM':
         nh = 32
-        layers.append(('lstm', frames * 2.0 * (flat + nh) * 4 * nh, (flat + nh + 1) * 4 * nh, frames * 4 * nh))
+        layers.append(('lstm_x', 2.0 * flat * 4 * nh, flat * 4 * nh, 4 * nh))
+        layers.append(('lstm_h', 5 * 2.0 * nh * 4 * nh, (nh + 1) * 4 * nh, 5 * 4 * nh))
         layers.append(('proj', 2.0 * nh * nh, nh * nh + nh, nh))
         flat = nh
     layers.append(('fc', 2.0 * flat * F, flat * F + F, F))
@@ -97,10 +97,19 @@ def arch_flops(arch, depth, A, R):
     return layers
 
 
-def train_pass_flops(layers, N):
-    """forward + backward (dW everywhere, dX everywhere except the input conv)."""
-    fwd = sum(l[1] for l in layers)
-    return N * (3 * fwd - layers[0][1])
+FRAME_LAYERS = ('conv', 'lstm_x')
+
+
+def train_pass_flops(layers, N, frame_rows=None):
+    """forward + backward (dW everywhere, dX everywhere except the input conv). LSTM frame
+    store: the rollout already ran the forward, so the train pass is the backward of the
+    frame_rows distinct frames (2x their forward, minus conv1's dX) + that of the N windows."""
+    if frame_rows is None:
+        fwd = sum(l[1] for l in layers)
+        return N * (3 * fwd - layers[0][1])
+    per_frame = sum(l[1] for l in layers if l[0] in FRAME_LAYERS)
+    per_win = sum(l[1] for l in layers if l[0] not in FRAME_LAYERS)
+    return frame_rows * (2 * per_frame - layers[0][1]) + N * 2 * per_win
 
 
 def build_args(cfg, T, sampling, seed):
@@ -257,23 +266,29 @@ def main():
     # one launch of the fused NIPS trunk), each timed with HIP events on the stream they are
     # launched on (torch's current stream, passed to every C-ABI call), back to back
     E = cfg['ec']
-    x_roll = learner.memory if learner.lstm_bool else learner.states[0]
+    net = learner.network
+    if learner.lstm_bool:  # a step's new frames (trunk + cell x-product), + its E windows
+        roll_fwd = lambda: learner._lstm_forward(1, learner.v_boot)
+        roll_trunk = lambda: net.lstm_frames_forward(learner.fstore, 1 + 5 * E, E, E, T)
+    else:
+        roll_fwd = lambda: net.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
+                                       ws_key='rollout', infer=True)
+        roll_trunk = lambda: net.forward_trunk(learner.states[0], E, ws_key='rollout')
     fw = []
     for it in range(30):
         s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s_ev.record()
-        learner.network.forward(x_roll, E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
-                                ws_key='rollout', infer=True)
+        roll_fwd()
         e_ev.record()
         fw.append((s_ev, e_ev))
     # trunk: 5 warm launches, then 40 launches back to back between one event pair (the GPU
     # stays busy, so the per-launch average is the kernel's duration, as rocprof reports it)
     for _ in range(5):
-        learner.network.forward_trunk(x_roll, E, ws_key='rollout')
+        roll_trunk()
     s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s_ev.record()
     for _ in range(40):
-        learner.network.forward_trunk(x_roll, E, ws_key='rollout')
+        roll_trunk()
     e_ev.record()
     torch.cuda.synchronize()
     prof['rollout_forward'] = [s_ev_.elapsed_time(e_ev_) for (s_ev_, e_ev_) in fw[5:]]
@@ -286,21 +301,19 @@ def main():
         A = args.num_actions
         layers = arch_flops(cfg['arch'], depth, A, cfg['nb_choices'])
         N = ec * T
+        lstm = cfg['arch'] == 'LSTM'
         tp_ms = float(np.mean(prof['train_pass']))
-        tp_flops = train_pass_flops(layers, N)
+        tp_flops = train_pass_flops(layers, N, 1 + (T + 4) * ec if lstm else None)
         rf_ms = float(np.mean(prof['rollout_forward']))
         tk_ms = float(np.mean(prof['rollout_trunk']))
+        # one rollout step: E new frames (trunk) + E windows (LSTM) / E states
         fwd_flops = ec * sum(l[1] for l in layers)
-        frames = 5 if cfg['arch'] == 'LSTM' else 1
-        fwd_bytes = (ec * frames * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in layers) +
-                     4 * ec * sum(l[3] for l in layers))
+        fwd_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in layers) + 4 * ec * sum(l[3] for l in layers)
         # trunk (roofline kernel): algorithmic bytes = the frames read once + the trunk weights
         # read once + the dense layer's pre-activation output written once
-        trunk = [l for l in layers if l[0] in ('conv', 'fc', 'lstm')]
-        if cfg['arch'] == 'LSTM':
-            trunk = [l for l in layers if l[0] in ('conv', 'lstm')]
-        out_floats = (4 * 32 * frames) if cfg['arch'] == 'LSTM' else trunk[-1][3]
-        tk_bytes = ec * frames * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in trunk) + 4 * ec * out_floats
+        trunk = [l for l in layers if l[0] in ('conv', 'fc', 'lstm_x')]
+        out_floats = trunk[-1][3]
+        tk_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in trunk) + 4 * ec * out_floats
         tk_flops = ec * sum(l[1] for l in trunk)
         tk_gbs = tk_bytes / (tk_ms * 1e-3) / 1e9
         pmc = load_pmc(a.config, TRUNK_KERNEL.get(cfg['arch']))
@@ -328,7 +341,7 @@ def main():
                          'algorithmic_bytes_per_launch': tk_bytes, 'us_per_launch': round(tk_ms * 1e3, 2),
                          'tflops': round(tk_flops / (tk_ms * 1e-3) / 1e12, 3),
                          'traffic_source': pmc['source'] if pmc else None},
-            'train_pass': {'bound': 'mfma', 'kernels': 'forward + fused loss backward, %d rows' % N,
+            'train_pass': {'bound': 'mfma', 'kernels': ('backward of %d windows over %d distinct frames (forward reused from the rollout)' % (N, 1 + (T + 4) * ec)) if lstm else 'forward + fused loss backward, %d rows' % N,
                            'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',
                            'frac': round(achieved / MI355X_FP32_TFLOPS, 4),
                            'ms_per_launch': round(tp_ms, 4), 'flop_per_launch': tp_flops},

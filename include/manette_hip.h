@@ -101,6 +101,32 @@ int mt_forward_infer(const mt_net *net, const float *params, const uint8_t *obs,
 int mt_forward_trunk(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                      size_t ws_bytes, mt_stream_t stream);
 
+/* ---- LSTM frame-store mode (the learner's LSTM path; manette_amd/csrc/lstm.h) -------------
+ * The reference feeds each step's memory window [E][5][84][84][C] (paac.py:79-83) and the train
+ * step the T*E windows of whole_memory (paac.py:233-234); consecutive windows share 4 frames.
+ * Here the caller keeps ONE frame store fstore [1 + (T+5)*E][84][84][C] uint8: row 0 = zeros,
+ * row 1 + slot*E + e = env e's state in slot `slot` (slots 0..3 = the previous rollout's last 4
+ * states, slot 4 + t = the state before step t), and per window only nz = its number of leading
+ * zero frames (reference memory[e] = 0 at an episode end, then shifted). Window (t, e) reads
+ * zero frames at positions k < nz[t][e] and slot t + k otherwise.
+ *  - mt_lstm_frames_forward: trunk + the cell's x-product of frame rows [row0, row0+nrows),
+ *    kept in ws (step 0: rows [0, 1+5E) — zero frame + slots 0..4; step t: slot 4+t's E rows);
+ *  - mt_lstm_windows_forward: the E windows of step t (t == T: the bootstrap windows) ->
+ *    v [E], pi [E][A], rep [E][R] (paac.py:144-152, :219-224), nz_t = nz[t][0..E);
+ *  - mt_lstm_frames_backward: loss + gradient of the T*E windows of steps 0..T-1 (the train
+ *    step of paac.py:254-256) from the rollout's activations (unchanged parameters), with pi,
+ *    rep, v [T*E] the rollout outputs; back-propagates through each distinct frame once. */
+int mt_lstm_frames_workspace_bytes(const mt_net *net, int E, int T, size_t *bytes);
+int mt_lstm_frames_forward(const mt_net *net, const float *params, const uint8_t *fstore, int row0, int nrows,
+                           int E, int T, void *ws, size_t ws_bytes, mt_stream_t stream);
+int mt_lstm_windows_forward(const mt_net *net, const float *params, const int32_t *nz_t, int t, int E, int T,
+                            void *ws, size_t ws_bytes, float *v, float *pi, float *rep, mt_stream_t stream);
+int mt_lstm_frames_backward(const mt_net *net, const float *params, const uint8_t *fstore, const int32_t *nz,
+                            int E, int T, void *ws, size_t ws_bytes, const float *pi, const float *rep,
+                            const float *v, const int32_t *a_idx, const int32_t *r_idx, const float *y,
+                            const float *adv, float entropy_beta, float *grad, float *loss_terms,
+                            mt_stream_t stream);
+
 /* ---- device multinomial sampling (perf mode of A3) -----------------------------------------
  * Replaces ExplorationPolicy.multinomial_choose (exploration_policy.py:108-116) with an
  * inverse-CDF draw on (p - float32 epsneg), the last category taking the remainder — the

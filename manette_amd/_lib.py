@@ -60,6 +60,10 @@ _HIP_SIGS = {
     'mt_net_feature_dim': (_I, [_P, C.POINTER(_I)]),
     'mt_net_workspace_bytes': (_I, [_P, _I, C.POINTER(_SZ)]),
     'mt_forward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P]),
+    'mt_lstm_frames_workspace_bytes': (_I, [_P, _I, _I, C.POINTER(_SZ)]),
+    'mt_lstm_frames_forward': (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),
+    'mt_lstm_windows_forward': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P, _P, _P, _P]),
+    'mt_lstm_frames_backward': (_I, [_P, _P, _P, _P, _I, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
     'mt_forward_trunk': (_I, [_P, _P, _P, _I, _P, _SZ, _P]),
     'mt_forward_infer': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P]),
     'mt_sample': (_I, [_P, _P, _I, _I, _I, C.c_uint64, _P, _P, _P, _P, _P]),

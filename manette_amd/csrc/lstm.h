@@ -99,9 +99,24 @@ static void build_layout_lstm(mt_net *n) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 
-// One workgroup (128 threads) per window b. xg: split-K slabs of x_t K_x, [S][5B][128].
+// Row of the x-product slabs that position k of window b reads.
+//  window layout (nz == null): the caller's [B][5] frames, row b*5 + k;
+//  frame-store layout: row 0 is the zero frame, row 1 + slot*E + e is env e's state of frame
+//  slot `slot`; window b = (step t0 + b / E, env b % E) holds nz[b] leading zero frames, then
+//  slots t..t+4 (paac.py:79-83: the window of step t is s_{t-4} .. s_t).
+struct XgRows {
+  const int32_t *nz;
+  int t0, E;
+  __device__ __forceinline__ int operator()(int b, int k) const {
+    if (!nz) return b * 5 + k;
+    if (k < nz[b]) return 0;
+    return 1 + (t0 + b / E + k) * E + b % E;
+  }
+};
+
+// One workgroup (128 threads) per window b. xg: split-K slabs of x_t K_x, [S][rows][128].
 template <int NH, int STEPS>
-__global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__ xg, int S, int rows,
+__global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__ xg, int S, int rows, XgRows map,
                                                        const float *__restrict__ Kh, const float *__restrict__ kb,
                                                        const float *__restrict__ Wp, const float *__restrict__ bp,
                                                        const float *__restrict__ W6, int F, float forget_bias,
@@ -121,8 +136,9 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
   __syncthreads();
   for (int t = 0; t < STEPS; ++t) {
     const int row = b * STEPS + t;
+    const int xr = map(b, t);
     float z = 0.f;
-    for (int s = 0; s < S; ++s) z += xg[((size_t)s * rows + row) * G4 + g];
+    for (int s = 0; s < S; ++s) z += xg[((size_t)s * rows + xr) * G4 + g];
     float hz = 0.f;
 #pragma unroll
     for (int k = 0; k < NH; ++k) hz += hs[k] * wcol[k];
@@ -231,7 +247,7 @@ static int lstm_forward_impl(const mt_net *n, const float *P, const uint8_t *obs
   const float *Wp = P + n->off_proj;
   const float *W6 = P + n->off_fc;
   hipLaunchKernelGGL((lstm_fwd_kernel<Ar::NH, Ar::STEPS>), dim3(B), dim3(Ar::G4), 0, s, ws + X.xg, X.xg_splits,
-                     rows, Kh, kb, Wp, Wp + Ar::NH * Ar::NH, W6, Ar::F, 1.0f, ws + X.gates, ws + X.cst,
+                     rows, XgRows{nullptr, 0, 0}, Kh, kb, Wp, Wp + Ar::NH * Ar::NH, W6, Ar::F, 1.0f, ws + X.gates, ws + X.cst,
                      ws + X.hprev, ws + X.h5, ws + X.out32, ws + X.slab6);
   MT_LAUNCHED();
   HeadParams hp = head_params(n, P);
@@ -280,6 +296,204 @@ static int lstm_backward_impl(const mt_net *n, const float *P, const uint8_t *ob
                                   EpMasked{ws + L.dact[K], layer_out<Ar, K>(ws, L), Ar::FLAT, act, al}, rows,
                                   Ar::FLAT, Ar::G4, 1, s)));
   return trunk_backward<Ar, K>(n, P, obs, rows, ws, L, grad, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Frame-store mode (the learner's path). A window of step t is frames s_{t-4} .. s_t of one env
+// with nz leading zero frames (paac.py:79-83, :202-203), so consecutive windows share 4 of their
+// 5 frames and the trunk + x-product of every distinct frame is computed ONCE per parameter
+// version: the frame store holds row 0 = the zero frame and rows 1 + slot*E + e (slot 0..3 = the
+// previous rollout's last 4 states, slot 4 + t = s_t), and the workspace keeps every row's
+// trunk activations and x-product slabs. The rollout computes the new rows of each step and the
+// recurrence of its E windows (window t*E + e); the train pass reuses all of it (the parameters
+// have not changed since the rollout) and back-propagates through each distinct frame once,
+// with the gate gradients of the windows that read it summed per frame first (exact by
+// linearity; fixed summation order).
+// ---------------------------------------------------------------------------------------------
+struct LstmFrameWs {
+  WsLayout L;
+  size_t xg, dxg, zpart, slab6, gates, cst, hprev, h5, out32, dout32, dgates;
+  int S, R_max, R_bwd, W;
+};
+
+constexpr int kZeroParts = 64;  // partial sums of the zero frame's gate gradients
+
+template <class Ar, int I = 0>
+static size_t max_wgrad_slab(int B) {
+  if constexpr (I < Ar::NCONV) return std::max(conv_wgrad_slab<LayerG<Ar, I>>(B), max_wgrad_slab<Ar, I + 1>(B));
+  return 0;
+}
+
+template <class Ar, int I = 0>
+static void shift_rows(WsLayout &L, size_t row0) {
+  if constexpr (I < Ar::NCONV) {
+    using G = LayerG<Ar, I>;
+    const size_t a = row0 * G::OH * G::OW * G::COUT;
+    L.act[I] += a;
+    L.dact[I] += a;
+    if constexpr (pooled<Ar, I>()) {
+      const size_t p = row0 * (G::OH / 2) * (G::OW / 2) * G::COUT;
+      L.pool[I] += p;
+      L.dpool[I] += p;
+    }
+    shift_rows<Ar, I + 1>(L, row0);
+  }
+}
+
+template <class Ar>
+static LstmFrameWs lstm_frame_layout(const mt_net *n, int E, int T) {
+  LstmFrameWs X{};
+  X.R_max = 1 + (T + 5) * E;
+  X.R_bwd = 1 + (T + 4) * E;  // slot 4 + T (s_T) is read by the bootstrap only
+  X.W = (T + 1) * E;          // windows of steps 0..T (T = bootstrap)
+  size_t off = 0;
+  auto take = [&](size_t nf) {
+    size_t o = off;
+    off = align64(off + nf);
+    return o;
+  };
+  size_t wslab = 0;
+  ws_layers<Ar>(X.L, off, X.R_max, wslab);
+  wslab = std::max(wslab, max_wgrad_slab<Ar>(X.R_bwd));
+  const int s = pick_splits(cdiv(E, TileFc::BM) * cdiv(Ar::G4, TileFc::BN), Ar::FLAT, TileFc::BK, 128);
+  X.S = gemm_splits<TileFc>(Ar::FLAT, s);
+  const size_t W = X.W, WT = (size_t)T * E;
+  X.xg = take((size_t)X.S * X.R_max * Ar::G4);
+  X.dxg = take((size_t)X.R_max * Ar::G4);
+  X.zpart = take((size_t)kZeroParts * Ar::G4);
+  X.slab6 = take(W * Ar::F);
+  X.gates = take(W * Ar::STEPS * Ar::G4);
+  X.cst = take(W * Ar::STEPS * Ar::NH);
+  X.hprev = take(W * Ar::STEPS * Ar::NH);
+  X.h5 = take(W * Ar::NH);
+  X.out32 = take(W * Ar::NH);
+  X.dout32 = take(WT * Ar::NH);
+  X.dgates = take(WT * Ar::STEPS * Ar::G4);
+  X.L.fc_splits = 1;
+  X.L.fcslab = X.slab6;
+  X.L.H = take(W * Ar::F);
+  X.L.dz = take(WT * n->O);
+  X.L.dH = take(WT * Ar::F);
+  X.L.wslab = take(wslab);
+  X.L.total = off;
+  return X;
+}
+
+// Zero frame (row 0): partial sums over window chunks of the gate gradients of the positions
+// that read it (k < nz), 128 threads = gate columns; summed in chunk order by the gather kernel.
+__global__ __launch_bounds__(128) void lstm_zero_partials_kernel(const float *__restrict__ dgates,
+                                                                 const int32_t *__restrict__ nz, int W,
+                                                                 float *__restrict__ part) {
+  const int g = threadIdx.x, c = blockIdx.x;
+  const int per = cdiv(W, gridDim.x);
+  float acc = 0.f;
+  for (int w = c * per; w < min(W, (c + 1) * per); ++w) {
+    const int z = nz[w];
+    for (int k = 0; k < z; ++k) acc += dgates[((size_t)w * 5 + k) * 128 + g];
+  }
+  part[(size_t)c * 128 + g] = acc;
+}
+
+// dxg[r] = sum of the gate gradients of every (window, position) that reads frame row r:
+// row 1 + j*E + e is position k of window (t = j - k, e) when 0 <= t < T and k >= nz[t][e].
+__global__ __launch_bounds__(128) void lstm_gather_dxg_kernel(const float *__restrict__ dgates,
+                                                              const int32_t *__restrict__ nz, int T, int E,
+                                                              const float *__restrict__ zpart, int nparts,
+                                                              float *__restrict__ dxg) {
+  const int r = blockIdx.x, g = threadIdx.x;
+  float acc = 0.f;
+  if (r == 0) {
+    for (int c = 0; c < nparts; ++c) acc += zpart[(size_t)c * 128 + g];
+  } else {
+    const int j = (r - 1) / E, e = (r - 1) % E;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int t = j - k;
+      if (t >= 0 && t < T && k >= nz[t * E + e]) acc += dgates[(((size_t)t * E + e) * 5 + k) * 128 + g];
+    }
+  }
+  dxg[(size_t)r * 128 + g] = acc;
+}
+
+template <class Ar>
+static int lstm_frames_fwd_impl(const mt_net *n, const float *P, const uint8_t *fstore, int row0, int nrows,
+                                int E, int T, float *ws, hipStream_t s) {
+  const LstmFrameWs X = lstm_frame_layout<Ar>(n, E, T);
+  MT_CHECK_ARG(row0 >= 0 && nrows >= 1 && row0 + nrows <= X.R_max, "rows [%d, %d) outside the frame store [0, %d)",
+               row0, row0 + nrows, X.R_max);
+  constexpr size_t FB = (size_t)84 * 84 * LayerG<Ar, 0>::CIN;
+  WsLayout Ls = X.L;
+  shift_rows<Ar>(Ls, (size_t)row0);
+  MT_TRY((trunk_forward<Ar>(n, P, fstore + (size_t)row0 * FB, nrows, ws, Ls, s)));
+  return launch_gemm<TileFc>(LdRowMajor{layer_out<Ar, Ar::NCONV - 1>(ws, Ls), Ar::FLAT},
+                             LdColMajor{P + n->off_lstm, Ar::G4, -1},
+                             EpSlab{ws + X.xg + (size_t)row0 * Ar::G4, X.R_max, Ar::G4}, nrows, Ar::G4, Ar::FLAT,
+                             X.S, s);
+}
+
+template <class Ar>
+static int lstm_windows_fwd_impl(const mt_net *n, const float *P, const int32_t *nz_t, int t, int E, int T,
+                                 float *ws, float *v, float *pi, float *rep, hipStream_t s) {
+  MT_CHECK_ARG(t >= 0 && t <= T, "step %d outside [0, %d]", t, T);
+  const LstmFrameWs X = lstm_frame_layout<Ar>(n, E, T);
+  const size_t w0 = (size_t)t * E;
+  const float *Kh = P + n->off_lstm + (size_t)Ar::FLAT * Ar::G4;
+  const float *Wp = P + n->off_proj;
+  const float *W6 = P + n->off_fc;
+  hipLaunchKernelGGL((lstm_fwd_kernel<Ar::NH, Ar::STEPS>), dim3(E), dim3(Ar::G4), 0, s, ws + X.xg, X.S, X.R_max,
+                     XgRows{nz_t, t, E}, Kh, Kh + Ar::NH * Ar::G4, Wp, Wp + Ar::NH * Ar::NH, W6, Ar::F, 1.0f,
+                     ws + X.gates + w0 * Ar::STEPS * Ar::G4, ws + X.cst + w0 * Ar::STEPS * Ar::NH,
+                     ws + X.hprev + w0 * Ar::STEPS * Ar::NH, ws + X.h5 + w0 * Ar::NH, ws + X.out32 + w0 * Ar::NH,
+                     ws + X.slab6 + w0 * Ar::F);
+  MT_LAUNCHED();
+  HeadParams hp = head_params(n, P);
+  hipLaunchKernelGGL(heads_fwd_kernel, dim3(E), dim3(256), 0, s, ws + X.slab6 + w0 * Ar::F, 1, E,
+                     W6 + (size_t)Ar::NH * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp, n->cfg.softmax_temp,
+                     ws + X.L.H + w0 * Ar::F, v, pi, rep, SampleArgs{});
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+template <class Ar>
+static int lstm_frames_bwd_impl(const mt_net *n, const float *P, const uint8_t *fstore, const int32_t *nz, int E,
+                                int T, float *ws, const float *pi, const float *rep, const float *v,
+                                const int32_t *a_idx, const int32_t *r_idx, const float *y, const float *adv,
+                                float beta, float *grad, float *loss_terms, hipStream_t s) {
+  const LstmFrameWs X = lstm_frame_layout<Ar>(n, E, T);
+  const WsLayout &L = X.L;
+  const int W = T * E, rows = W * Ar::STEPS;
+  const int act = n->cfg.activation;
+  const float al = n->cfg.alpha_leaky;
+  MT_TRY(heads_backward<Ar>(n, P, W, ws, L, pi, rep, v, a_idx, r_idx, y, adv, beta, grad, loss_terms, s));
+  const float *Kx = P + n->off_lstm;
+  const float *Kh = Kx + (size_t)Ar::FLAT * Ar::G4;
+  const float *Wp = P + n->off_proj;
+  const float *W6 = P + n->off_fc;
+  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{ws + X.out32, Ar::NH, Ar::NH}, LdColMajor{ws + L.dH, Ar::F, -1},
+                                  EpStore{grad + n->off_fc, Ar::F}, Ar::NH + 1, Ar::F, W, 1, s)));
+  hipLaunchKernelGGL((lstm_bwd_kernel<Ar::NH, Ar::STEPS>), dim3(W), dim3(Ar::G4), 0, s, ws + L.dH, Ar::F, W6, Wp,
+                     Kh, ws + X.gates, ws + X.cst, ws + X.dout32, ws + X.dgates);
+  MT_LAUNCHED();
+  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{ws + X.h5, Ar::NH, Ar::NH}, LdColMajor{ws + X.dout32, Ar::NH, -1},
+                                  EpStore{grad + n->off_proj, Ar::NH}, Ar::NH + 1, Ar::NH, W, 1, s)));
+  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{ws + X.hprev, Ar::NH, Ar::NH}, LdColMajor{ws + X.dgates, Ar::G4, -1},
+                                  EpStore{grad + n->off_lstm + (size_t)Ar::FLAT * Ar::G4, Ar::G4}, Ar::NH + 1,
+                                  Ar::G4, rows, 1, s)));
+  // per-frame gate gradients (the zero frame: chunk partials first)
+  hipLaunchKernelGGL(lstm_zero_partials_kernel, dim3(kZeroParts), dim3(Ar::G4), 0, s, ws + X.dgates, nz, W,
+                     ws + X.zpart);
+  MT_LAUNCHED();
+  hipLaunchKernelGGL(lstm_gather_dxg_kernel, dim3(X.R_bwd), dim3(Ar::G4), 0, s, ws + X.dgates, nz, T, E,
+                     ws + X.zpart, kZeroParts, ws + X.dxg);
+  MT_LAUNCHED();
+  constexpr int K = Ar::NCONV - 1;
+  const float *flat = layer_out<Ar, K>(ws, L);
+  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{flat, Ar::FLAT, -1}, LdColMajor{ws + X.dxg, Ar::G4, -1},
+                                  EpStore{grad + n->off_lstm, Ar::G4}, Ar::FLAT, Ar::G4, X.R_bwd, 1, s)));
+  MT_TRY((launch_gemm<TileDenseX>(LdRowMajor{ws + X.dxg, Ar::G4}, LdRowMajor{Kx, Ar::G4},
+                                  EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, X.R_bwd, Ar::FLAT, Ar::G4, 1,
+                                  s)));
+  return trunk_backward<Ar, K>(n, P, fstore, X.R_bwd, ws, L, grad, s);
 }
 
 }  // namespace mt

@@ -1042,6 +1042,74 @@ extern "C" int mt_loss_backward(const mt_net *net, const float *params, const ui
   return MT_OK;
 }
 
+// ---- LSTM frame-store mode (lstm.h) ----------------------------------------------------------
+#define MT_LSTM_ONLY(net, ...)                                                  \
+  MT_ARCH_SWITCH(net, {                                                         \
+    if constexpr (Ar::LSTM) {                                                   \
+      __VA_ARGS__;                                                              \
+    } else {                                                                    \
+      set_error("frame-store calls need the LSTM arch");                        \
+      return MT_ERR_ARG;                                                        \
+    }                                                                           \
+  })
+
+#define MT_LSTM_WS(E, T)                                                        \
+  const LstmFrameWs X_ = lstm_frame_layout<Ar>(net, E, T);                      \
+  if (ws_bytes < X_.L.total * sizeof(float)) {                                  \
+    set_error("workspace %zu < %zu bytes", ws_bytes, X_.L.total * sizeof(float)); \
+    return MT_ERR_WORKSPACE;                                                    \
+  }
+
+extern "C" int mt_lstm_frames_workspace_bytes(const mt_net *net, int E, int T, size_t *bytes) {
+  MT_CHECK_ARG(net && bytes, "null argument");
+  MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
+  MT_LSTM_ONLY(net, { *bytes = lstm_frame_layout<Ar>(net, E, T).L.total * sizeof(float); });
+  return MT_OK;
+}
+
+extern "C" int mt_lstm_frames_forward(const mt_net *net, const float *params, const uint8_t *fstore, int row0,
+                                      int nrows, int E, int T, void *ws, size_t ws_bytes, mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && fstore && ws, "null argument");
+  MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
+  MT_LSTM_ONLY(net, {
+    MT_LSTM_WS(E, T);
+    return lstm_frames_fwd_impl<Ar>(net, params, fstore, row0, nrows, E, T, (float *)ws, (hipStream_t)stream);
+  });
+  return MT_OK;
+}
+
+extern "C" int mt_lstm_windows_forward(const mt_net *net, const float *params, const int32_t *nz_t, int t, int E,
+                                       int T, void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
+                                       mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && nz_t && ws && v && pi && rep, "null argument");
+  MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
+  MT_LSTM_ONLY(net, {
+    MT_LSTM_WS(E, T);
+    return lstm_windows_fwd_impl<Ar>(net, params, nz_t, t, E, T, (float *)ws, v, pi, rep, (hipStream_t)stream);
+  });
+  return MT_OK;
+}
+
+extern "C" int mt_lstm_frames_backward(const mt_net *net, const float *params, const uint8_t *fstore,
+                                       const int32_t *nz, int E, int T, void *ws, size_t ws_bytes, const float *pi,
+                                       const float *rep, const float *v, const int32_t *a_idx, const int32_t *r_idx,
+                                       const float *y, const float *adv, float entropy_beta, float *grad,
+                                       float *loss_terms, mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && fstore && nz && ws && pi && rep && v && a_idx && r_idx && y && adv && grad,
+               "null argument");
+  MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
+  MT_LSTM_ONLY(net, {
+    MT_LSTM_WS(E, T);
+    if ((size_t)T * E * net->O * sizeof(float) > 160 * 1024) {
+      set_error("batch %d x %d head outputs exceeds the head-gradient LDS stage", T * E, net->O);
+      return MT_ERR_ARG;
+    }
+    return lstm_frames_bwd_impl<Ar>(net, params, fstore, nz, E, T, (float *)ws, pi, rep, v, a_idx, r_idx, y, adv,
+                                    entropy_beta, grad, loss_terms, (hipStream_t)stream);
+  });
+  return MT_OK;
+}
+
 extern "C" int mt_sum_slabs(const float *parts, int nslabs, size_t n, float *out,
                             mt_stream_t stream) {
   MT_CHECK_ARG(parts && out && nslabs >= 1, "bad argument");

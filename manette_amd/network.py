@@ -157,6 +157,43 @@ class DeviceNetwork(object):
         check(_lib.hip().mt_forward_trunk(self._h, _ptr(self.params), _ptr(obs), int(batch), _ptr(ws), ws.numel(),
                                           _stream()), 'mt_forward_trunk')
 
+    # ---- LSTM frame-store mode (include/manette_hip.h, mt_lstm_*) -------------------------------
+    def lstm_workspace(self, E, T):
+        n = C.c_size_t()
+        check(_lib.hip().mt_lstm_frames_workspace_bytes(self._h, int(E), int(T), C.byref(n)))
+        key = ('lstm_frames', E, T)
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < n.value:
+            ws = torch.empty(n.value, dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
+
+    def lstm_frames_forward(self, fstore, row0, nrows, E, T):
+        """Trunk + cell x-product of frame rows [row0, row0 + nrows) of the frame store."""
+        ws = self.lstm_workspace(E, T)
+        check(_lib.hip().mt_lstm_frames_forward(self._h, _ptr(self.params), _ptr(fstore), int(row0), int(nrows),
+                                                int(E), int(T), _ptr(ws), ws.numel(), _stream()),
+              'mt_lstm_frames_forward')
+
+    def lstm_windows_forward(self, nz_t, t, E, T, out):
+        """The E windows of step t (T = bootstrap): out = (v [E], pi [E][A], rep [E][R])."""
+        ws = self.lstm_workspace(E, T)
+        v, pi, rep = out
+        assert nz_t.dtype == torch.int32 and nz_t.is_cuda and nz_t.numel() == E
+        check(_lib.hip().mt_lstm_windows_forward(self._h, _ptr(self.params), _ptr(nz_t), int(t), int(E), int(T),
+                                                 _ptr(ws), ws.numel(), _ptr(v), _ptr(pi), _ptr(rep), _stream()),
+              'mt_lstm_windows_forward')
+        return v, pi, rep
+
+    def lstm_frames_backward(self, fstore, nz, E, T, pi, rep, v, a_idx, r_idx, y, adv, loss_terms=None):
+        """Gradient of the T*E windows of the last rollout into self.grad."""
+        ws = self.lstm_workspace(E, T)
+        check(_lib.hip().mt_lstm_frames_backward(
+            self._h, _ptr(self.params), _ptr(fstore), _ptr(nz), int(E), int(T), _ptr(ws), ws.numel(), _ptr(pi),
+            _ptr(rep), _ptr(v), _ptr(a_idx), _ptr(r_idx), _ptr(y), _ptr(adv), self.beta, _ptr(self.grad),
+            _ptr(loss_terms), _stream()), 'mt_lstm_frames_backward')
+        return self.grad
+
     def loss_backward(self, obs, B, v, pi, rep, a_idx, r_idx, y, adv, loss_terms=None, ws_key=None):
         """Gradient of policy_v_network.py:25-74 into self.grad (needs forward() on obs first)."""
         ws = self.workspace(B, ws_key)

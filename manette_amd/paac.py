@@ -60,11 +60,21 @@ class PAACLearner(ActorLearner):
         self.dev = self.network.device
         E, T, C = self.emulator_counts, self.max_local_steps, self.C
         dev = self.dev
-        self.states = torch.zeros(T + 1, E, 84, 84, C, dtype=torch.uint8, device=dev)
-        if self.lstm_bool:  # paac.py:107-112: the window each forward reads + its per-step record
+        if self.lstm_bool:
+            # LSTM frame store (include/manette_hip.h, mt_lstm_*): row 0 = the zero frame, then
+            # slots 0..T+4 of E states; slots 0..3 = the previous rollout's last 4 states, slot
+            # 4 + t = self.states[t]. The reference's memory / whole_memory (paac.py:107-112,
+            # :79-83, :202-203) become nz[t][e] = the window's leading zero frames.
             self.n_steps = 5
-            self.memory = torch.zeros(E, self.n_steps, 84, 84, C, dtype=torch.uint8, device=dev)
-            self.whole_memory = torch.zeros(T, E, self.n_steps, 84, 84, C, dtype=torch.uint8, device=dev)
+            self.fstore = torch.zeros(1 + (T + 5) * E, 84, 84, C, dtype=torch.uint8, device=dev)
+            self.slots = self.fstore[1:].view(T + 5, E, 84, 84, C)
+            self.states = self.slots[4:]
+            self.nz_h = torch.zeros(T + 1, E, dtype=torch.int32, pin_memory=True)
+            self.nz_d = torch.zeros(T + 1, E, dtype=torch.int32, device=dev)
+            self.pi_all = torch.zeros(T + 1, E, self.num_actions, dtype=torch.float32, device=dev)
+            self.rep_all = torch.zeros(T + 1, E, self.total_repetitions, dtype=torch.float32, device=dev)
+        else:
+            self.states = torch.zeros(T + 1, E, 84, 84, C, dtype=torch.uint8, device=dev)
         self.values = torch.zeros(T, E, dtype=torch.float32, device=dev)
         # [0] = action indices, [1] = repetition indices, each [T][E] (row t*E+e, paac.py:239)
         self.idx = torch.zeros(2, T, E, dtype=torch.int32, device=dev)
@@ -217,8 +227,11 @@ class PAACLearner(ActorLearner):
             self.global_step = self._gs.value
             return
         end = self._mark('rollout_forward')
-        v, pi, rep = net.forward(self.memory if self.lstm_bool else self.states[t], E,
-                                 out=(self.values[t], self.pi_roll, self.rep_roll), ws_key='rollout', infer=True)
+        if self.lstm_bool:
+            v, pi, rep = self._lstm_forward(t, self.values[t])
+        else:
+            v, pi, rep = net.forward(self.states[t], E, out=(self.values[t], self.pi_roll, self.rep_roll),
+                                     ws_key='rollout', infer=True)
         if end is not None:
             end.record()
         if self.sampling == 'device':
@@ -259,9 +272,21 @@ class PAACLearner(ActorLearner):
             reward, over = sh[1], sh[2]
         self.global_step = self.book.step(self.global_step, a, r, reward, over,
                                           self.rewards_h[t].numpy(), self.masks_h[t].numpy())
-        if self.lstm_bool:  # update_memory + episode-end reset (paac.py:173-174, :202-203)
-            self.masks_d[t].copy_(self.masks_h[t], non_blocking=True)
-            devnet.memory_push(self.memory, self.whole_memory[t], self.states[t + 1], self.masks_d[t])
+        if self.lstm_bool:  # update_memory (shift in the new state) + episode-end reset (paac.py:173-174, :202-203)
+            nz = self.nz_h.numpy()
+            nz[t + 1] = np.where(self.masks_h[t].numpy() == 0, 5, np.maximum(nz[t] - 1, 0))
+
+    def _lstm_forward(self, t, v_out):
+        """Step t's new frames (step 0: the zero frame + slots 0..4 again, the parameters having
+        changed) through trunk + cell x-product, then the recurrence of the E windows of step t."""
+        E, T = self.emulator_counts, self.max_local_steps
+        net = self.network
+        if t == 0:
+            net.lstm_frames_forward(self.fstore, 0, 1 + 5 * E, E, T)
+        else:
+            net.lstm_frames_forward(self.fstore, 1 + (4 + t) * E, E, E, T)
+        self.nz_d[t].copy_(self.nz_h[t], non_blocking=True)
+        return net.lstm_windows_forward(self.nz_d[t], t, E, T, out=(v_out, self.pi_all[t], self.rep_all[t]))
 
     def update(self):
         """Bootstrap, n-step returns, fused loss backward, [all-reduce], clip + RMSProp
@@ -270,20 +295,26 @@ class PAACLearner(ActorLearner):
         self.book.drain()
         E, T = self.emulator_counts, self.max_local_steps
         N = E * T
-        net.forward(self.memory if self.lstm_bool else self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll),
-                    ws_key='rollout', infer=True)
+        if self.lstm_bool:
+            self._lstm_forward(T, self.v_boot)
+        else:
+            net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout', infer=True)
         self.rm_d.copy_(self.rm_h, non_blocking=True)
         devnet.returns(self.rewards_d, self.masks_d, self.values, self.v_boot, self.gamma, self.y, self.adv)
         lr = self.get_lr()
         net.set_lr(lr)
-        if self.lstm_bool:  # flat whole_memory (paac.py:233-234)
-            obs = self.whole_memory.reshape(N, self.n_steps, 84, 84, self.C)
+        end = self._mark('train_pass')
+        if self.lstm_bool:
+            # the train step's forward is the rollout's (same parameters, same windows): only the
+            # backward runs, through each distinct frame once (paac.py:233-256)
+            net.lstm_frames_backward(self.fstore, self.nz_d[:T], E, T, self.pi_all[:T], self.rep_all[:T],
+                                     self.values, self.idx[0].view(N), self.idx[1].view(N), self.y.view(N),
+                                     self.adv.view(N), loss_terms=self.loss_terms)
         else:
             obs = self.states[:T].reshape(N, 84, 84, self.C)
-        end = self._mark('train_pass')
-        v, pi, rep = net.forward(obs, N, ws_key='train')
-        net.loss_backward(obs, N, v, pi, rep, self.idx[0].view(N), self.idx[1].view(N), self.y.view(N),
-                          self.adv.view(N), loss_terms=self.loss_terms, ws_key='train')
+            v, pi, rep = net.forward(obs, N, ws_key='train')
+            net.loss_backward(obs, N, v, pi, rep, self.idx[0].view(N), self.idx[1].view(N), self.y.view(N),
+                              self.adv.view(N), loss_terms=self.loss_terms, ws_key='train')
         if end is not None:
             end.record()
         inv = 1.0
@@ -291,7 +322,11 @@ class PAACLearner(ActorLearner):
             torch.distributed.all_reduce(net.grad)
             inv = 1.0 / self.world
         net.apply_gradients(inv)
-        self.states[0].copy_(self.states[T])
+        if self.lstm_bool:  # the next rollout's slots 0..4 = s_{T-4} .. s_T; windows carry over
+            self.slots[0:5].copy_(self.slots[T:T + 5].clone())
+            self.nz_h.numpy()[0] = self.nz_h.numpy()[T]
+        else:
+            self.states[0].copy_(self.states[T])
         return lr
 
     def loss_value(self):
@@ -309,9 +344,8 @@ class PAACLearner(ActorLearner):
             torch.distributed.broadcast(self.network.mom, 0)
         self.global_step_start = self.global_step
         self._start_runners()
-        if self.lstm_bool:  # memory[e, -1] = initial state (paac.py:109-112)
-            self.memory.zero_()
-            self.memory[:, -1].copy_(self.states[0])
+        if self.lstm_bool:  # memory = zeros except memory[:, -1] = initial state (paac.py:109-112)
+            self.nz_h.numpy()[0] = 4
 
     def train(self):
         """Main actor learner loop (paac.py:86-297)."""

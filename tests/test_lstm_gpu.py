@@ -145,11 +145,72 @@ def test_memory_push_bit_exact(E, depth):
         np.testing.assert_array_equal(mem_d.cpu().numpy(), mem)
 
 
+def _windows_from_store(slots, nz, t):
+    """Explicit windows [E][5] of step t from the frame store (the reference's memory array)."""
+    E = slots.shape[1]
+    w = np.zeros((E, 5) + slots.shape[2:], np.uint8)
+    for e in range(E):
+        for k in range(5):
+            if k >= nz[e]:
+                w[e, k] = slots[t + k, e]
+    return w
+
+
+@pytest.mark.parametrize('E,T,depth', [(3, 2, 1), (4, 5, 1), (2, 3, 3)])
+def test_lstm_frame_store_parity(E, T, depth):
+    """mt_lstm_frames_forward / _windows_forward / _frames_backward on a frame store with random
+    window zero-prefixes == the oracle on the explicit windows (paac.py:79-83 layout)."""
+    A, R, act = 9, 11, 'relu'
+    net = _net(depth, A, R, seed=E * 10 + T, act=act)
+    rs = np.random.RandomState(E * 100 + T)
+    C = 4 * depth
+    fstore = rs.randint(0, 256, size=(1 + (T + 5) * E, 84, 84, C)).astype(np.uint8)
+    fstore[0] = 0
+    slots = fstore[1:].reshape(T + 5, E, 84, 84, C)
+    nz = rs.choice([0, 0, 0, 1, 2, 4, 5], size=(T + 1, E)).astype(np.int32)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    fs_d, nz_d = d(fstore), d(nz)
+    net.lstm_frames_forward(fs_d, 0, 1 + 5 * E, E, T)
+    for t in range(1, T + 1):
+        net.lstm_frames_forward(fs_d, 1 + (4 + t) * E, E, E, T)
+    v = torch.zeros(T + 1, E, device='cuda')
+    pi = torch.zeros(T + 1, E, A, device='cuda')
+    rep = torch.zeros(T + 1, E, R, device='cuda')
+    for t in range(T + 1):
+        net.lstm_windows_forward(nz_d[t], t, E, T, out=(v[t], pi[t], rep[t]))
+    torch.cuda.synchronize()
+    spec = nets.arch_spec('LSTM', depth, A, R)
+    P = net.get_variables()
+    win = np.concatenate([_windows_from_store(slots, nz[t], t) for t in range(T + 1)])
+    v0, pi0, rep0, _ = nets.forward(spec, P, win, act=act, alpha=0.1)
+    np.testing.assert_allclose(v.cpu().numpy().reshape(-1), v0, rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(pi.cpu().numpy().reshape(-1, A), pi0, rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(rep.cpu().numpy().reshape(-1, R), rep0, rtol=2e-5, atol=1e-6)
+    # train step over the T*E windows of steps 0..T-1
+    N = T * E
+    a_idx = rs.randint(0, A, size=N).astype(np.int32)
+    r_idx = rs.randint(0, R, size=N).astype(np.int32)
+    y = rs.randn(N).astype(np.float32)
+    adv = rs.randn(N).astype(np.float32)
+    terms = torch.zeros(N, 4, device='cuda')
+    net.lstm_frames_backward(fs_d, nz_d[:T], E, T, pi[:T], rep[:T], v[:T], d(a_idx), d(r_idx), d(y), d(adv),
+                             loss_terms=terms)
+    torch.cuda.synchronize()
+    wt = win[:N]
+    _, G, aux = nets.loss_and_grads(spec, P, wt, a_idx, r_idx, y, adv, 0.02, act=act, alpha=0.1)
+    got = net.get_variables('grad')
+    loose = _near_tie_layers(spec, P, wt, act)
+    errs = {name: _rel(got[name], G[name]) for name, _, _ in spec['vars']}
+    bad = {n: e for n, e in errs.items() if e >= (5e-3 if n in loose else 2e-4)}
+    assert not bad, (bad, sorted(loose))
+    np.testing.assert_allclose(terms.cpu().numpy(), aux['terms'], rtol=1e-4, atol=1e-5)
+
+
 def test_lstm_learner_memory_windows(tmp_path):
-    """The learner's device memory windows (forward input at every step and the flat train
-    batch, paac.py:107-112, :173-174, :202-203, :233-234) equal a numpy replay of the reference
-    bookkeeping over the recorded states and episode-end masks, with resets inside the rollout;
-    the LSTM update runs and changes the parameters."""
+    """The learner's LSTM windows (frame store + nz, read at every step and by the train
+    step) equal a numpy replay of the reference's memory bookkeeping (paac.py:107-112, :173-174,
+    :202-203, :233-234) over the recorded states and episode-end masks, with resets inside the
+    rollout and across updates; the LSTM update runs and changes the parameters."""
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -174,9 +235,8 @@ def test_lstm_learner_memory_windows(tmp_path):
     assert L.native_step is None  # LSTM takes the Python step
     try:
         E, T = 6, L.max_local_steps
-        mem = L.memory.cpu().numpy()
-        s0 = L.states[0].cpu().numpy()
-        assert (mem[:, :-1] == 0).all() and (mem[:, -1] == s0).all()
+        mem = np.zeros((E, 5, 84, 84, 4), np.uint8)
+        mem[:, -1] = L.states[0].cpu().numpy()
         p0 = L.network.params.cpu().numpy().copy()
         resets = 0
         for u in range(3):
@@ -184,14 +244,14 @@ def test_lstm_learner_memory_windows(tmp_path):
             for t in range(T):
                 L.step(t)
             torch.cuda.synchronize()
-            states = L.states.cpu().numpy()
+            slots = L.slots.cpu().numpy()
+            nz = L.nz_h.numpy().copy()
             masks = L.masks_h.numpy().copy()
             resets += int((masks == 0).sum())
-            whole = np.zeros((T,) + mem.shape, np.uint8)
             for t in range(T):
-                whole[t] = _np_memory_push(mem, states[t + 1], masks[t])
-            np.testing.assert_array_equal(L.whole_memory.cpu().numpy(), whole)
-            np.testing.assert_array_equal(L.memory.cpu().numpy(), mem)
+                np.testing.assert_array_equal(_windows_from_store(slots, nz[t], t), mem, err_msg='u%d t%d' % (u, t))
+                _np_memory_push(mem, slots[4 + t + 1], masks[t])
+            np.testing.assert_array_equal(_windows_from_store(slots, nz[T], T), mem)  # bootstrap window
             L.update()
         torch.cuda.synchronize()
         assert resets > 0
