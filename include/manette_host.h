@@ -97,6 +97,11 @@ int mh_book_histogram(const mh_book *b, int64_t *hist, int64_t *nb_actions);
 int mh_book_pop_episodes(mh_book *b, int64_t *global_step, float *reward, int64_t *length, int max,
                          int *n);
 
+/* CRC32C (Castagnoli) of n bytes continuing from crc (0 to start), for the TF tensor-bundle
+ * checkpoints of manette_amd/tf_bundle.py (tensorflow/core/util/tensor_bundle: masked CRC32C of
+ * every tensor and SSTable block). */
+uint32_t mh_crc32c(const void *data, size_t n, uint32_t crc);
+
 #ifdef __cplusplus
 }
 #endif

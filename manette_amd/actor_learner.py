@@ -1,19 +1,25 @@
 """ActorLearner base: actor_learner.py:9-140 interface (folders, LR schedule, reward clip,
 checkpoint save / restore, cleanup) over the HIP network.
 
-Checkpoints: `<df>/checkpoints/-<global_step>.npz` (every variable under its TF name) and
-`<df>/optimizer_checkpoints/-<global_step>.npz` (the RMSProp slots under their TF slot names
-`<var>/OptimizerVariables` = ms and `<var>/OptimizerVariables_1` = mom), each directory with a
-TF-style `checkpoint` index file; resume parses the step after the last '-' of the latest
-checkpoint (networks.py:162-175). numpy archives are written and read without pickles.
+Checkpoints are TensorFlow tensor bundles (manette_amd/tf_bundle.py), as tf.train.Saver writes
+them (actor_learner.py:84-87, :102-106): `<df>/checkpoints/-<global_step>.{index,data-00000-of-00001}`
+holds every variable under its TF name plus its RMSProp slots `<var>/OptimizerVariables` (ms)
+and `<var>/OptimizerVariables_1` (mom) (Saver() of all global variables, max_to_keep 5);
+`<df>/optimizer_checkpoints/-<global_step>.*` holds the slots only (max_to_keep 1). Each folder
+has TF's `checkpoint` text file (model_checkpoint_path + all_model_checkpoint_paths). Restore
+(networks.py:162-175, actor_learner.py:116-130) reads the latest bundle of each folder and the
+step after the last '-' of its name.
 """
 import logging
 import os
 
-import numpy as np
+from . import tf_bundle
+
+SLOT_MS, SLOT_MOM = '/OptimizerVariables', '/OptimizerVariables_1'
 
 
 def _latest(folder):
+    """tf.train.latest_checkpoint: the prefix named by `checkpoint`, if its index exists."""
     idx = os.path.join(folder, 'checkpoint')
     if not os.path.exists(idx):
         return None
@@ -21,23 +27,34 @@ def _latest(folder):
         if line.startswith('model_checkpoint_path:'):
             name = line.split(':', 1)[1].strip().strip('"')
             path = name if os.path.isabs(name) else os.path.join(folder, name)
-            return path if os.path.exists(path + '.npz') else None
+            return path if os.path.exists(path + '.index') else None
     return None
 
 
-def _write(folder, step, arrays, max_to_keep=None):
+def _all_paths(folder):
+    idx = os.path.join(folder, 'checkpoint')
+    if not os.path.exists(idx):
+        return []
+    return [line.split(':', 1)[1].strip().strip('"') for line in open(idx)
+            if line.startswith('all_model_checkpoint_paths:')]
+
+
+def _write(folder, step, arrays, max_to_keep=5):
     os.makedirs(folder, exist_ok=True)
-    base = os.path.join(folder, '-%d' % step)
-    tmp = base + '.tmp.npz'
-    np.savez(tmp, **arrays)
-    os.replace(tmp, base + '.npz')
-    with open(os.path.join(folder, 'checkpoint'), 'w') as f:
-        f.write('model_checkpoint_path: "-%d"\n' % step)
-    if max_to_keep:
-        olds = sorted((int(n[1:-4]) for n in os.listdir(folder)
-                       if n.startswith('-') and n.endswith('.npz') and not n.endswith('.tmp.npz')))
-        for s in olds[:-max_to_keep]:
-            os.remove(os.path.join(folder, '-%d.npz' % s))
+    name = '-%d' % step
+    tf_bundle.write_bundle(os.path.join(folder, name), arrays)
+    keep = [p for p in _all_paths(folder) if p != name] + [name]
+    for old in keep[:-max_to_keep]:
+        for f in os.listdir(folder):
+            if f.startswith(old + '.'):
+                os.remove(os.path.join(folder, f))
+    keep = keep[-max_to_keep:]
+    tmp = os.path.join(folder, 'checkpoint.tmp')
+    with open(tmp, 'w') as f:
+        f.write('model_checkpoint_path: "%s"\n' % name)
+        for k in keep:
+            f.write('all_model_checkpoint_paths: "%s"\n' % k)
+    os.replace(tmp, os.path.join(folder, 'checkpoint'))
 
 
 class ActorLearner(object):
@@ -70,11 +87,11 @@ class ActorLearner(object):
             P = self.network.get_variables('params')
             ms = self.network.get_variables('ms')
             mom = self.network.get_variables('mom')
-            _write(self.network_checkpoint_folder, self.last_saving_step, P)
             slots = {}
             for k in ms:
-                slots[k + '/OptimizerVariables'] = ms[k]
-                slots[k + '/OptimizerVariables_1'] = mom[k]
+                slots[k + SLOT_MS] = ms[k]
+                slots[k + SLOT_MOM] = mom[k]
+            _write(self.network_checkpoint_folder, self.last_saving_step, dict(P, **slots))
             _write(self.optimizer_checkpoint_folder, self.last_saving_step, slots, max_to_keep=1)
 
     def rescale_reward(self, reward):
@@ -84,6 +101,27 @@ class ActorLearner(object):
         elif reward < -1.0:
             reward = -1.0
         return reward
+
+    def _restore(self, tensors):
+        """Variables and RMSProp slots of a bundle into the device buffers (names must match)."""
+        names = {n for n, _, _, _ in self.network.vars}
+        P, ms, mom = {}, {}, {}
+        for k, v in tensors.items():
+            if k.endswith(SLOT_MOM):
+                mom[k[:-len(SLOT_MOM)]] = v
+            elif k.endswith(SLOT_MS):
+                ms[k[:-len(SLOT_MS)]] = v
+            else:
+                P[k] = v
+        unknown = (set(P) | set(ms) | set(mom)) - names
+        if unknown:
+            raise ValueError('checkpoint variables not in this network: %s' % sorted(unknown)[:5])
+        if P:
+            self.network.set_variables(P)
+        if ms:
+            self.network.set_variables(ms, 'ms')
+        if mom:
+            self.network.set_variables(mom, 'mom')
 
     def init_network(self):
         os.makedirs(self.network_checkpoint_folder, exist_ok=True)
@@ -95,17 +133,12 @@ class ActorLearner(object):
             self.network.init_params(getattr(self, 'seed', 0))
         else:
             logging.info('Restoring network variables from previous run')
-            with np.load(path + '.npz', allow_pickle=False) as z:
-                self.network.set_variables({k: z[k] for k in z.files})
+            self._restore(tf_bundle.read_bundle(path))
             last_saving_step = int(path[path.rindex('-') + 1:])
         opath = _latest(self.optimizer_checkpoint_folder)
         if opath is not None:
             logging.info('Restoring optimizer variables from previous run')
-            with np.load(opath + '.npz', allow_pickle=False) as z:
-                ms = {k[:-len('/OptimizerVariables')]: z[k] for k in z.files if k.endswith('/OptimizerVariables')}
-                mom = {k[:-len('/OptimizerVariables_1')]: z[k] for k in z.files if k.endswith('/OptimizerVariables_1')}
-            self.network.set_variables(ms, 'ms')
-            self.network.set_variables(mom, 'mom')
+            self._restore(tf_bundle.read_bundle(opath))
         self.last_saving_step = last_saving_step
         return last_saving_step
 

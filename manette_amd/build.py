@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 HIP_SOURCES = ['net.hip', 'misc.hip', 'rollout.hip']
 HIP_HEADERS = ['common.h', 'gemm.h', 'trunk_fused.h', 'lstm.h']
-HOST_SOURCES = ['runner.cpp']
+HOST_SOURCES = ['runner.cpp', 'crc32c.cpp']
 HIP_LIB = os.path.join(HERE, 'libmanette_hip.so')
 HOST_LIB = os.path.join(HERE, 'libmanette_host.so')
 INCLUDE = os.path.join(os.path.dirname(HERE), 'include')

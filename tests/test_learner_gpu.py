@@ -111,21 +111,47 @@ def test_train_cli_checkpoint_resume(tmp_path):
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     args = json.load(open(df + 'args.json'))
     assert args['arch'] == 'NATURE' and args['nb_choices'] == 11
+    from manette_amd import tf_bundle
     ck = sorted(os.listdir(df + 'checkpoints'))
-    assert 'checkpoint' in ck and '-200.npz' in ck
-    assert os.listdir(df + 'optimizer_checkpoints') == ['-200.npz', 'checkpoint'] or \
-        sorted(os.listdir(df + 'optimizer_checkpoints')) == ['-200.npz', 'checkpoint']
-    with np.load(df + 'checkpoints/-200.npz') as z:
-        assert z['Network/conv3/conv3_weights'].shape == (3, 3, 64, 64)
-        assert z['Training/Repetition/repetition_output/repetition_output_weights'].shape == (512, 11)
-    with np.load(df + 'optimizer_checkpoints/-200.npz') as z:
-        assert 'Network/fc4/fc4_weights/OptimizerVariables' in z.files
+    # TF tensor bundles + TF's `checkpoint` file, as tf.train.Saver writes them (max_to_keep 5)
+    assert 'checkpoint' in ck and '-200.index' in ck and '-200.data-00000-of-00001' in ck
+    assert sorted(os.listdir(df + 'optimizer_checkpoints')) == ['-200.data-00000-of-00001', '-200.index',
+                                                                 'checkpoint']
+    lines = open(df + 'checkpoints/checkpoint').read().splitlines()
+    assert lines[0] == 'model_checkpoint_path: "-200"' and lines[-1] == 'all_model_checkpoint_paths: "-200"'
+    z = tf_bundle.read_bundle(df + 'checkpoints/-200')
+    assert z['Network/conv3/conv3_weights'].shape == (3, 3, 64, 64)
+    assert z['Training/Repetition/repetition_output/repetition_output_weights'].shape == (512, 11)
+    assert 'Network/fc4/fc4_weights/OptimizerVariables_1' in z
+    o = tf_bundle.read_bundle(df + 'optimizer_checkpoints/-200')
+    assert 'Network/fc4/fc4_weights/OptimizerVariables' in o and 'Network/fc4/fc4_weights' not in o
+    np.testing.assert_array_equal(o['Network/fc4/fc4_weights/OptimizerVariables'],
+                                  z['Network/fc4/fc4_weights/OptimizerVariables'])
     # resume: starts from step 200 and continues to 280
     cmd[cmd.index('--max_global_steps') + 1] = '280'
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert 'Restoring network variables' in out.stdout + out.stderr
-    assert '-280.npz' in os.listdir(df + 'checkpoints')
+    assert '-280.index' in os.listdir(df + 'checkpoints')
+
+
+@pytest.mark.parametrize('arch,extra', [('NATURE', ['--max_repetition', '10', '--nb_choices', '11']),
+                                        ('LSTM', ['--max_repetition', '10', '--nb_choices', '11'])])
+def test_eval_cli_restores_training_checkpoint(tmp_path, arch, extra):
+    """train.py writes a TF-bundle checkpoint; test.py (test.py:29-116 flags) restores it and
+    plays its episodes to the end, printing the reference's summary lines."""
+    df = str(tmp_path / 'run') + '/'
+    cmd = [sys.executable, os.path.join(ROOT, 'train.py'), '-g', 'ms_pacman', '--arch', arch, '-ec', '4',
+           '-ew', '2', '--max_global_steps', '40', '--checkpoint_interval', '20', '-df', df] + extra
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    ev = subprocess.run([sys.executable, os.path.join(ROOT, 'test.py'), '-f', df, '-tc', '2', '-np', '3'],
+                        capture_output=True, text=True, timeout=300)
+    assert ev.returncode == 0, ev.stdout[-2000:] + ev.stderr[-2000:]
+    assert 'Restoring network variables' in ev.stdout + ev.stderr
+    lines = ev.stdout.splitlines()
+    assert 'Performed 2 tests for ms_pacman.' in lines
+    assert any(l.startswith('Mean: ') for l in lines) and any(l.startswith('Std: ') for l in lines)
 
 
 def test_dp_two_ranks_gloo_on_one_gpu(tmp_path):
