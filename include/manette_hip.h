@@ -151,8 +151,9 @@ int mt_returns(const float *rewards, const float *masks, const float *values, co
  * Replaces optimizer.compute_gradients(network.loss) (actor_learner.py:49) with the loss of
  * policy_v_network.py:25-74. Requires the activations of mt_forward(obs, batch) in `ws`
  * (pi, rep, v as that call returned them). a_idx/r_idx: selected action / repetition index
- * (argmax of the one-hot feeds, paac.py:239-240). Writes the full flat gradient `grad`
- * (every variable; alignment padding zeroed) and per-row loss terms
+ * (argmax of the one-hot feeds, paac.py:239-240). Overwrites every variable's gradient in the
+ * flat `grad` and never touches its alignment padding, which the caller zeroes once when it
+ * allocates grad (the clip's global norm sums the whole buffer). Also writes per-row loss terms
  * loss_terms [batch][4] = (critic 0.25(y-v)^2, -adv*(logpi_a+logrep_r), entropy_pi, entropy_rep). */
 int mt_loss_backward(const mt_net *net, const float *params, const uint8_t *obs, int batch,
                      void *ws, size_t ws_bytes, const float *pi, const float *rep, const float *v,

@@ -526,37 +526,45 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
 }
 
 // Head weight/bias gradient: G[f][o] = sum_b [H,1][b][f] * dz[b][o], scattered into the three
-// (w, b) variable pairs of the flat gradient. A block owns 64 features x all O outputs; dz is
-// staged in LDS, H is read coalesced (consecutive lanes = consecutive features).
+// (w, b) variable pairs of the flat gradient. Block = (64 features, output o): column o of dz is
+// staged in LDS, the 4 waves take contiguous quarters of the rows (H read coalesced: consecutive
+// lanes = consecutive features, 4 independent accumulators per lane), and the 4 wave partials are
+// added in wave order through LDS (deterministic).
 __global__ __launch_bounds__(256) void head_wgrad_kernel(const float *__restrict__ H,
                                                          const float *__restrict__ dz, int B, int F,
                                                          int A, int R, float *__restrict__ gc,
                                                          float *__restrict__ ga, float *__restrict__ gr) {
-  extern __shared__ __attribute__((aligned(16))) float dzs[];  // [B][O]
-  const int O = 1 + A + R;
-  for (int i = threadIdx.x; i < B * O; i += 256) dzs[i] = dz[i];
+  extern __shared__ __attribute__((aligned(16))) float dzs[];  // [B] column o, then [4][64] partials
+  const int O = 1 + A + R, o = blockIdx.y;
+  for (int i = threadIdx.x; i < B; i += 256) dzs[i] = dz[(size_t)i * O + o];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int f = blockIdx.x * 64 + lane;  // f == F is the bias row
-  if (f > F) return;
-  for (int o = w; o < O; o += 4) {
-    float a0 = 0.f, a1 = 0.f;
-    int b = 0;
-    for (; b + 1 < B; b += 2) {
-      const float h0 = f < F ? H[(size_t)b * F + f] : 1.f;
-      const float h1 = f < F ? H[(size_t)(b + 1) * F + f] : 1.f;
-      a0 += h0 * dzs[b * O + o];
-      a1 += h1 * dzs[(b + 1) * O + o];
+  const int q = (B + 3) / 4, b0 = w * q, b1 = min(B, b0 + q);
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (f <= F) {
+    int b = b0;
+    if (f < F) {
+      for (; b + 3 < b1; b += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] += H[(size_t)(b + u) * F + f] * dzs[b + u];
+      }
+      for (; b < b1; ++b) a[0] += H[(size_t)b * F + f] * dzs[b];
+    } else {
+      for (; b < b1; ++b) a[0] += dzs[b];
     }
-    for (; b < B; ++b) a0 += (f < F ? H[(size_t)b * F + f] : 1.f) * dzs[b * O + o];
-    const float acc = a0 + a1;
-    if (o == 0)
-      gc[f] = acc;  // [F][1] weights then the bias at index F
-    else if (o <= A)
-      ga[(size_t)f * A + (o - 1)] = acc;
-    else
-      gr[(size_t)f * R + (o - 1 - A)] = acc;
   }
+  float *part = dzs + B;
+  part[w * 64 + lane] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (w != 0 || f > F) return;
+  const float acc = ((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane];
+  if (o == 0)
+    gc[f] = acc;  // [F][1] weights then the bias at index F
+  else if (o <= A)
+    ga[(size_t)f * A + (o - 1)] = acc;
+  else
+    gr[(size_t)f * R + (o - 1 - A)] = acc;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -766,8 +774,10 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
   }
 }
 
-// Loss + head gradients (policy_v_network.py:25-74): zeroes grad, writes dz, dH (masked by the
-// trunk output's activation derivative) and the three head (w, b) gradients.
+// Loss + head gradients (policy_v_network.py:25-74): writes dz, dH (masked by the trunk output's
+// activation derivative) and the three head (w, b) gradients. Every variable's gradient is
+// overwritten by the backward (no accumulation), so grad is not cleared: its alignment padding
+// must be zero once (include/manette_hip.h, mt_loss_backward).
 template <class Ar>
 static int heads_backward(const mt_net *n, const float *P, int B, float *ws, const WsLayout &L, const float *pi,
                           const float *rep, const float *v, const int32_t *a_idx, const int32_t *r_idx,
@@ -775,7 +785,6 @@ static int heads_backward(const mt_net *n, const float *P, int B, float *ws, con
                           hipStream_t s) {
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
-  MT_HIP(hipMemsetAsync(grad, 0, n->nparams * sizeof(float), s));
   // loss scaling 5.0 and the batch mean (policy_v_network.py:70-74): scale = 5/B.
   const float scale = 5.0f / (float)B;
   HeadParams hp = head_params(n, P);
@@ -790,13 +799,13 @@ static int heads_backward(const mt_net *n, const float *P, int B, float *ws, con
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       wg_attr = true;
     }
-    if ((size_t)B * n->O * sizeof(float) > 160 * 1024) {
-      set_error("batch %d x %d head outputs exceeds the head-gradient LDS stage", B, n->O);
+    const size_t lds = sizeof(float) * ((size_t)B + 4 * 64);
+    if (lds > 160 * 1024) {
+      set_error("batch %d exceeds the head-gradient LDS stage", B);
       return MT_ERR_ARG;
     }
-    hipLaunchKernelGGL(head_wgrad_kernel, dim3(cdiv(Ar::F + 1, 64)), dim3(256),
-                       sizeof(float) * (size_t)B * n->O, s, ws + L.H, ws + L.dz, B, Ar::F,
-                       n->cfg.num_actions, n->cfg.num_reps, grad + n->off_critic, grad + n->off_actor,
+    hipLaunchKernelGGL(head_wgrad_kernel, dim3(cdiv(Ar::F + 1, 64), n->O), dim3(256), lds, s, ws + L.H, ws + L.dz,
+                       B, Ar::F, n->cfg.num_actions, n->cfg.num_reps, grad + n->off_critic, grad + n->off_actor,
                        grad + n->off_rep);
     MT_LAUNCHED();
   }
@@ -1100,10 +1109,6 @@ extern "C" int mt_lstm_frames_backward(const mt_net *net, const float *params, c
   MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
   MT_LSTM_ONLY(net, {
     MT_LSTM_WS(E, T);
-    if ((size_t)T * E * net->O * sizeof(float) > 160 * 1024) {
-      set_error("batch %d x %d head outputs exceeds the head-gradient LDS stage", T * E, net->O);
-      return MT_ERR_ARG;
-    }
     return lstm_frames_bwd_impl<Ar>(net, params, fstore, nz, E, T, (float *)ws, pi, rep, v, a_idx, r_idx, y, adv,
                                     entropy_beta, grad, loss_terms, (hipStream_t)stream);
   });
