@@ -190,7 +190,7 @@ def main():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--step_impl', default='native', choices=['native', 'python'],
                     help='macro-step orchestration: native (mt_rollout_step) or Python')
-    ap.add_argument('--staging', default='zero_copy', choices=['in_place', 'zero_copy', 'copy', 'pooled'])
+    ap.add_argument('--staging', default='resized', choices=['in_place', 'zero_copy', 'copy', 'pooled', 'resized'])
     ap.add_argument('--no_pipeline', dest='pipeline', action='store_false',
                     help='disable MT_ROLLOUT_PIPELINED (on by default)')
     a = ap.parse_args()

@@ -196,6 +196,12 @@ int mt_preprocess_pooled(const uint8_t *raw, const int32_t *push_offset, const i
                          int E, int depth, int src_rows, const int32_t *row_lut, const int32_t *col_lut,
                          const uint8_t *prev, uint8_t *out, mt_stream_t stream);
 
+/* Resized variant (MT_ROLLOUT_RESIZED): staging slot push_offset[e] + j holds push j's FINAL
+ * 84x84xdepth frame, pooled and resized by the host threads (mh_runner MH_RUNNER_RESIZED):
+ * frames = [slots][84][84][depth]; the kernel only stacks it onto prev. */
+int mt_preprocess_resized(const uint8_t *frames, const int32_t *push_offset, const int32_t *push_count, int E,
+                          int depth, const uint8_t *prev, uint8_t *out, mt_stream_t stream);
+
 /* In-place variant (MT_ROLLOUT_IN_PLACE): the pushes' screens are read where the emulators left
  * them. screens = a bank of whole 210-row screens [..][210][160][depth] (pinned + device-mapped
  * host memory, or device memory); push j's frame f of env e is screen frame_idx[e*8 + 2j + f]
@@ -241,6 +247,9 @@ int mt_memory_push(uint8_t *memory, uint8_t *whole_t, const uint8_t *fresh, cons
  * indices, and after the emulators only stores the step word — no launch on the critical path.
  * sync_host = [2] uint32 pinned + mapped: [0] host step word, [1] device wait timeout status. */
 #define MT_ROLLOUT_PIPELINED 8
+/* flags & MT_ROLLOUT_RESIZED: the runner stages each push's final 84x84 frame (MH_RUNNER_RESIZED,
+ * staging [4E][84*84*depth]) and the preprocess is mt_preprocess_resized (row/col LUTs unused). */
+#define MT_ROLLOUT_RESIZED 16
 typedef struct mt_rollout mt_rollout;
 typedef struct mt_rollout_buffers {
   /* device */

@@ -42,10 +42,17 @@ const char *mh_last_error(void);
  * screens (the emulator's FramePool, atari_emulator.py:79-88), so half the bytes cross PCIe;
  * staging must hold 4*E slots of one staged screen. */
 #define MH_RUNNER_POOLED 2
+/* flags & MH_RUNNER_RESIZED (needs the 84-row row_select and mh_runner_set_col_lut before the
+ * first reset/step): each staging slot holds the FINAL 84x84xdepth frame of a push — the frame
+ * pool max and the nearest resize (atari_emulator.py:79-88, :113-124) done on the host — so
+ * 7,056*depth bytes per push cross PCIe and the device only stacks it (mt_preprocess_resized). */
+#define MH_RUNNER_RESIZED 4
 int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_rep, int n_reps,
                      const uint8_t *screens, int ring, size_t frame_bytes, const float *rewards,
                      int reward_len, int episode_len, const int32_t *row_select, int n_rows,
                      int flags, mh_runner **out);
+/* The resize's column LUT (84 source columns, increasing) for MH_RUNNER_RESIZED. */
+int mh_runner_set_col_lut(mh_runner *r, const int32_t *col_lut, int n_cols);
 void mh_runner_destroy(mh_runner *r);
 
 /* get_initial_state() of every env: 4 pushes each. Outputs as mh_runner_step. */

@@ -33,6 +33,8 @@ MT_ROLLOUT_ZERO_COPY = 1
 MT_ROLLOUT_IN_PLACE = 2
 MT_ROLLOUT_POOLED = 4
 MT_ROLLOUT_PIPELINED = 8
+MT_ROLLOUT_RESIZED = 16
+MH_RUNNER_RESIZED = 4
 MH_RUNNER_FIXED_SLOTS = 1
 MH_RUNNER_POOLED = 2
 
@@ -73,6 +75,7 @@ _HIP_SIGS = {
     'mt_clip_rmsprop': (_I, [_P, _P, _P, _P, _SZ, _P, _P, _F, _F, _F, _F, _I, _F, _P, _P]),
     'mt_preprocess': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
     'mt_preprocess_pooled': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
+    'mt_preprocess_resized': (_I, [_P, _P, _P, _I, _I, _P, _P, _P]),
     'mt_preprocess_frames': (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     'mt_memory_push': (_I, [_P, _P, _P, _P, _I, _SZ, _P]),
     'mt_host_device_pointer': (_I, [_P, C.POINTER(_P)]),
@@ -98,6 +101,7 @@ _HOST_SIGS = {
     'mh_runner_step_frames': (_I, [_P, _P, _P, _P, _P, _P, _P]),
     'mh_runner_env_state': (_I, [_P, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     'mh_crc32c': (C.c_uint32, [_P, _SZ, C.c_uint32]),
+    'mh_runner_set_col_lut': (_I, [_P, _P, _I]),
     'mh_book_create': (_I, [_I, _I, _P, _I, C.POINTER(_P)]),
     'mh_book_destroy': (None, [_P]),
     'mh_book_step': (_I, [_P, C.POINTER(C.c_int64), _P, _P, _P, _P, _P, _P]),

@@ -134,7 +134,10 @@ typedef unsigned char u8x16 __attribute__((ext_vector_type(16)));
 //               taken by the emulator's frame pool on the host (mt_preprocess_pooled);
 //   kSrcBank    frames read where the emulators left them: frame f is screen frame_idx[e*8+2j+f]
 //               of a bank of whole 210-row screens (mt_preprocess_frames).
-enum { kSrcPairs = 0, kSrcPooled = 1, kSrcBank = 2 };
+//   kSrcFinal   staging slot push_offset[e] + j holds the push's FINAL 84x84 frame (pool + resize
+//               done by the host threads, MH_RUNNER_RESIZED; mt_preprocess_resized): the block
+//               streams its 12 output rows (contiguous) and only stacks them.
+enum { kSrcPairs = 0, kSrcPooled = 1, kSrcBank = 2, kSrcFinal = 3 };
 template <int DEPTH, int SRC>
 __global__ __launch_bounds__(256) void preprocess_kernel(
     const uint8_t *__restrict__ raw, const int32_t *__restrict__ push_offset,
@@ -149,18 +152,46 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
   const int e = blockIdx.y, y0 = blockIdx.x * kPreRows;
   const int p = min(max(push_count[e], 1), 4);
   const size_t FR = (size_t)SH * ROWB;  // one screen
-  if (threadIdx.x < kPreRows) rl[threadIdx.x] = row_lut[y0 + threadIdx.x];
-  if (threadIdx.x < 84) cl[threadIdx.x] = col_lut[threadIdx.x];
+  constexpr int FROW = 84 * DEPTH;      // bytes of one final (resized) row
+  if constexpr (SRC != kSrcFinal) {
+    if (threadIdx.x < kPreRows) rl[threadIdx.x] = row_lut[y0 + threadIdx.x];
+    if (threadIdx.x < 84) cl[threadIdx.x] = col_lut[threadIdx.x];
+  }
   if (threadIdx.x < 8) {
     const int j = threadIdx.x >> 1, f = threadIdx.x & 1;
     if constexpr (SRC == kSrcBank)
       foff[threadIdx.x] = j < p ? (size_t)push_offset[e * 8 + threadIdx.x] * FR : 0;
     else if constexpr (SRC == kSrcPooled)
       foff[threadIdx.x] = ((size_t)push_offset[e] + j) * FR;
+    else if constexpr (SRC == kSrcFinal)
+      foff[threadIdx.x] = ((size_t)push_offset[e] + j) * 84 * FROW + (size_t)y0 * FROW;
     else
       foff[threadIdx.x] = ((size_t)push_offset[e] + j) * 2 * FR + f * FR;
   }
   __syncthreads();
+  if constexpr (SRC == kSrcFinal) {
+    // rows y0 .. y0+11 of each push's final frame are contiguous: 12*84*DEPTH/16 loads per push
+    constexpr int N16 = kPreRows * FROW / 16;
+    static_assert(kPreRows * FROW % 16 == 0 && N16 <= kPreRows * Q, "final rows fit the LDS stage");
+    for (int i = threadIdx.x; i < p * N16; i += 256) {
+      const int j = i / N16, q = i - j * N16;
+      (&pooled[j][0][0])[q] = reinterpret_cast<const u8x16 *>(raw + foff[2 * j])[q];
+    }
+    __syncthreads();
+    const uint8_t *pl = reinterpret_cast<const uint8_t *>(&pooled[0][0][0]);
+    for (int i = threadIdx.x; i < kPreRows * 84; i += 256) {
+      const int r = i / 84, x = i - r * 84;
+      const size_t o = (((size_t)e * 84 + y0 + r) * 84 + x) * C;
+#pragma unroll
+      for (int col = 0; col < DEPTH; ++col) {
+        uint32_t v = p < 4 ? *reinterpret_cast<const uint32_t *>(prev + o + col * 4) >> (8 * p) : 0u;
+        for (int j = 0; j < p; ++j)
+          v |= (uint32_t)pl[j * kPreRows * ROWB + r * FROW + x * DEPTH + col] << (8 * (4 - p + j));
+        *reinterpret_cast<uint32_t *>(out + o + col * 4) = v;
+      }
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < p * kPreRows * Q; i += 256) {
     const int j = i / (kPreRows * Q), rem = i - j * (kPreRows * Q);
     const int r = rem / Q, q = rem - r * Q;
@@ -295,6 +326,27 @@ extern "C" int mt_preprocess_pooled(const uint8_t *raw, const int32_t *push_offs
   } else if (depth == 3) {
     hipLaunchKernelGGL((preprocess_kernel<3, kSrcPooled>), grid, dim3(256), 0, (hipStream_t)stream, raw, push_offset,
                        push_count, src_rows, row_lut, col_lut, prev, out);
+  } else {
+    set_error("depth must be 1 or 3");
+    return MT_ERR_ARG;
+  }
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+extern "C" int mt_preprocess_resized(const uint8_t *frames, const int32_t *push_offset, const int32_t *push_count,
+                                     int E, int depth, const uint8_t *prev, uint8_t *out, mt_stream_t stream) {
+  MT_CHECK_ARG(frames && push_offset && push_count && prev && out, "null argument");
+  MT_CHECK_ARG(E >= 1, "E must be >= 1");
+  MT_CHECK_ARG(prev != out, "out may not alias prev");
+  MT_CHECK_ARG(((uintptr_t)frames & 15) == 0, "frames must be 16-byte aligned");
+  const dim3 grid(84 / kPreRows, E);
+  if (depth == 1) {
+    hipLaunchKernelGGL((preprocess_kernel<1, kSrcFinal>), grid, dim3(256), 0, (hipStream_t)stream, frames,
+                       push_offset, push_count, 84, nullptr, nullptr, prev, out);
+  } else if (depth == 3) {
+    hipLaunchKernelGGL((preprocess_kernel<3, kSrcFinal>), grid, dim3(256), 0, (hipStream_t)stream, frames,
+                       push_offset, push_count, 84, nullptr, nullptr, prev, out);
   } else {
     set_error("depth must be 1 or 3");
     return MT_ERR_ARG;

@@ -19,7 +19,7 @@ struct mt_rollout {
   mt_rollout_buffers b;
   uint64_t seed;
   hipEvent_t ev2[2];  // pair of step t ready: ev2[t & 1]
-  bool zero_copy, in_place, pooled, pipelined;
+  bool zero_copy, in_place, pooled, resized, pipelined;
   int armed = -1;     // step whose forward is already enqueued (pipelined), else -1
   uint32_t seq = 0;   // host step sequence word value last stored
   uint8_t *staging_dev;  // device addresses of the host-mapped buffers (zero-copy mode)
@@ -40,10 +40,12 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   const bool zc = ip || (b.flags & MT_ROLLOUT_ZERO_COPY) != 0;
   const bool pl = (b.flags & MT_ROLLOUT_PIPELINED) != 0;
   const bool po = (b.flags & MT_ROLLOUT_POOLED) != 0;
-  MT_CHECK_ARG((b.flags & ~(MT_ROLLOUT_ZERO_COPY | MT_ROLLOUT_IN_PLACE | MT_ROLLOUT_POOLED | MT_ROLLOUT_PIPELINED)) == 0,
+  const bool rz = (b.flags & MT_ROLLOUT_RESIZED) != 0;
+  MT_CHECK_ARG((b.flags & ~(MT_ROLLOUT_ZERO_COPY | MT_ROLLOUT_IN_PLACE | MT_ROLLOUT_POOLED | MT_ROLLOUT_PIPELINED |
+                            MT_ROLLOUT_RESIZED)) == 0,
                "unknown rollout flags %d", b.flags);
   MT_CHECK_ARG(!ip || b.frames_host, "in-place rollout needs frames_host");
-  MT_CHECK_ARG(!ip || !po, "in-place and pooled staging are exclusive");
+  MT_CHECK_ARG((int)ip + (int)po + (int)rz <= 1, "in-place, pooled and resized staging are exclusive");
   MT_CHECK_ARG(!pl || (zc && b.sync_host), "pipelined rollout needs zero-copy or in-place screens and sync_host");
   MT_CHECK_ARG(b.states && b.values && b.idx && b.pi && b.rep && b.ws && b.counters &&
                    (zc || (b.raw && b.meta && b.pair)) && b.row_lut && b.col_lut && b.idx_host &&
@@ -86,6 +88,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->zero_copy = zc;
   ro->in_place = ip;
   ro->pooled = po;
+  ro->resized = rz;
   ro->pipelined = pl;
   ro->frames_dev = (int32_t *)frames_dev;
   ro->seq_dev = (uint32_t *)sync_dev;
@@ -166,12 +169,13 @@ int enqueue_preprocess(mt_rollout *ro, int t, int total, hipStream_t s) {
   const uint8_t *raw = ro->staging_dev;
   const int32_t *meta = ro->meta_dev;
   if (!ro->zero_copy) {
-    const size_t per_push = (ro->pooled ? 1 : 2) * ro->frame_bytes;
+    const size_t per_push = ro->resized ? (size_t)84 * 84 * ro->depth : (ro->pooled ? 1 : 2) * ro->frame_bytes;
     MT_HIP(hipMemcpyAsync(b.raw, b.staging_host, (size_t)total * per_push, hipMemcpyHostToDevice, s));
     MT_HIP(hipMemcpyAsync(b.meta, b.meta_host, sizeof(int32_t) * 2 * E, hipMemcpyHostToDevice, s));
     raw = b.raw;
     meta = b.meta;
   }
+  if (ro->resized) return mt_preprocess_resized(raw, meta, meta + E, E, ro->depth, cur, nxt, st);
   return ro->pooled ? mt_preprocess_pooled(raw, meta, meta + E, E, ro->depth, b.src_rows, b.row_lut, b.col_lut,
                                            cur, nxt, st)
                     : mt_preprocess(raw, meta, meta + E, E, ro->depth, b.src_rows, b.row_lut, b.col_lut, cur,

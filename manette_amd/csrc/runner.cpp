@@ -10,12 +10,17 @@
 //   main: prefix sum of push counts -> compact staging offsets;
 //   B: each worker copies its envs' screens into the staging buffer (pinned, H2D'd whole).
 // Pooled staging (MH_RUNNER_POOLED) stages max(f0, f1) of a push's two screens — the emulator's
-// frame pool — so one screen per push crosses PCIe.
+// frame pool — so one screen per push crosses PCIe. Resized staging (MH_RUNNER_RESIZED) also
+// applies the nearest 84x84 resize on the host (SSE max + pshufb column gather), so only the
+// final 7 KB frame of each push crosses PCIe (3.8x fewer bytes than the 84 staged rows of 2
+// screens) and the GPU only stacks it.
 // Fixed-slot staging (MH_RUNNER_FIXED_SLOTS) does A and B in one phase: env e's screens go to
 // slots [4e, 4e+n), read in place by the GPU.
 // In-place frames (mh_runner_step_frames) copies nothing: each worker writes, per env, the bank
 // indices of the screens its pushes produced, and the GPU reads those screens where the
 // emulators left them (a pinned, device-mapped bank).
+#include <tmmintrin.h>
+
 #include <algorithm>
 #include <climits>
 #include <atomic>
@@ -67,6 +72,53 @@ struct mh_runner {
   std::atomic<bool> quit{false};
   bool fixed = false;
   bool pooled = false;  // stage max(f0, f1) of each push (one screen per slot)
+  bool resized = false;  // stage the final 84x84 frame of each push (pool + nearest resize)
+  int depth = 1;
+  std::vector<int32_t> cols;             // resize column LUT (84)
+  alignas(16) uint8_t shuf[6][2][16];    // gray resize: per 16-column chunk, pshufb masks (lo, hi)
+  int chunk_base[6];                     // first source column of each chunk
+
+  // FramePool max + nearest resize of one push into its 84x84xdepth staging frame
+  // (atari_emulator.py:79-88 + the imresize of :113-124): rows[q] / cols[x] are the LUTs.
+  void resize_push(uint8_t *d, const uint8_t *s0, const uint8_t *s1) const {
+    if (depth == 1) {
+      alignas(16) uint8_t m[192];
+      _mm_store_si128(reinterpret_cast<__m128i *>(m + 160), _mm_setzero_si128());
+      _mm_store_si128(reinterpret_cast<__m128i *>(m + 176), _mm_setzero_si128());
+      for (int q = 0; q < 84; ++q) {
+        const uint8_t *a = s0 + (size_t)rows[q] * row_bytes, *b = s1 + (size_t)rows[q] * row_bytes;
+        for (int x = 0; x < 160; x += 16)
+          _mm_store_si128(reinterpret_cast<__m128i *>(m + x),
+                          _mm_max_epu8(_mm_loadu_si128(reinterpret_cast<const __m128i *>(a + x)),
+                                       _mm_loadu_si128(reinterpret_cast<const __m128i *>(b + x))));
+        uint8_t *o = d + (size_t)q * 84;
+        for (int c = 0; c < 6; ++c) {
+          const __m128i lo = _mm_loadu_si128(reinterpret_cast<const __m128i *>(m + chunk_base[c]));
+          const __m128i hi = _mm_loadu_si128(reinterpret_cast<const __m128i *>(m + chunk_base[c] + 16));
+          const __m128i v =
+              _mm_or_si128(_mm_shuffle_epi8(lo, _mm_load_si128(reinterpret_cast<const __m128i *>(shuf[c][0]))),
+                           _mm_shuffle_epi8(hi, _mm_load_si128(reinterpret_cast<const __m128i *>(shuf[c][1]))));
+          if (c < 5) {
+            _mm_storeu_si128(reinterpret_cast<__m128i *>(o + 16 * c), v);
+          } else {
+            alignas(16) uint8_t t[16];
+            _mm_store_si128(reinterpret_cast<__m128i *>(t), v);
+            std::memcpy(o + 80, t, 4);
+          }
+        }
+      }
+    } else {
+      for (int q = 0; q < 84; ++q) {
+        const uint8_t *a = s0 + (size_t)rows[q] * row_bytes, *b = s1 + (size_t)rows[q] * row_bytes;
+        uint8_t *o = d + (size_t)q * 84 * depth;
+        for (int x = 0; x < 84; ++x)
+          for (int ch = 0; ch < depth; ++ch) {
+            const size_t k = (size_t)cols[x] * depth + ch;
+            o[x * depth + ch] = std::max(a[k], b[k]);
+          }
+      }
+    }
+  }
   int phase = 0;  // 0 = reset, 1 = step A (+ B when fixed), 2 = copy B
   const int32_t *a_idx = nullptr, *r_idx = nullptr;
   uint8_t *staging = nullptr;
@@ -141,6 +193,11 @@ struct mh_runner {
         const int n = std::min(e.npush, 4);
         for (int j = 0; j < n; ++j) {
           const int64_t kk = e.last[(e.npush - n + j) & 3];
+          if (resized) {
+            resize_push(staging + (size_t)(push_offset[i] + j) * sfb,
+                        e.screens + (size_t)((2 * kk) % ring) * fb, e.screens + (size_t)((2 * kk + 1) % ring) * fb);
+            continue;
+          }
           if (pooled) {  // FramePool max (atari_emulator.py:79-88) of the staged rows, on the host
             uint8_t *d = staging + (size_t)(push_offset[i] + j) * sfb;
             const uint8_t *s0 = e.screens + (size_t)((2 * kk) % ring) * fb;
@@ -227,8 +284,12 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
   }
   if (n_envs < 1 || n_workers < 1 || n_reps < 1 || ring < 2 || frame_bytes == 0 ||
       reward_len < 1 || episode_len < 1 || frame_bytes % 210 != 0 || n_rows < 0 ||
-      (flags & ~(MH_RUNNER_FIXED_SLOTS | MH_RUNNER_POOLED)) != 0) {
+      (flags & ~(MH_RUNNER_FIXED_SLOTS | MH_RUNNER_POOLED | MH_RUNNER_RESIZED)) != 0) {
     set_error("bad sizes");
+    return 1;
+  }
+  if ((flags & MH_RUNNER_RESIZED) && (n_rows != 84 || (flags & MH_RUNNER_POOLED))) {
+    set_error("resized staging needs the 84-row row_select (and excludes pooled)");
     return 1;
   }
   for (int q = 0; q < n_rows; ++q)
@@ -246,12 +307,15 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
   r->W = std::min(n_workers, n_envs);
   r->fixed = (flags & MH_RUNNER_FIXED_SLOTS) != 0;
   r->pooled = (flags & MH_RUNNER_POOLED) != 0;
+  r->resized = (flags & MH_RUNNER_RESIZED) != 0;
   r->tab.assign(tab_rep, tab_rep + n_reps);
   r->ring = ring;
   r->fb = frame_bytes;
   r->row_bytes = frame_bytes / 210;
+  r->depth = (int)(r->row_bytes / 160);
   if (n_rows > 0) r->rows.assign(row_select, row_select + n_rows);
   r->sfb = n_rows > 0 ? (size_t)n_rows * r->row_bytes : frame_bytes;
+  if (r->resized) r->sfb = (size_t)84 * 84 * r->depth;
   r->reward_len = reward_len;
   r->episode_len = episode_len;
   r->env.resize(n_envs);
@@ -261,6 +325,38 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
   }
   for (int w = 0; w < r->W; ++w) r->threads.emplace_back([r, w] { r->worker(w); });
   *out = r;
+  return 0;
+}
+
+extern "C" int mh_runner_set_col_lut(mh_runner *r, const int32_t *col_lut, int n_cols) {
+  if (!r || !col_lut) {
+    set_error("null argument");
+    return 1;
+  }
+  if (!r->resized || n_cols != 84 || r->row_bytes % 160 != 0) {
+    set_error("col LUT needs a resized-staging runner and 84 columns");
+    return 1;
+  }
+  for (int x = 0; x < 84; ++x)
+    if (col_lut[x] < 0 || col_lut[x] >= 160 || (x && col_lut[x] < col_lut[x - 1])) {
+      set_error("col_lut[%d] = %d out of [0,160) or not increasing", x, col_lut[x]);
+      return 1;
+    }
+  r->cols.assign(col_lut, col_lut + 84);
+  for (int c = 0; c < 6; ++c) {
+    const int base = col_lut[16 * c];
+    r->chunk_base[c] = base;
+    for (int k = 0; k < 16; ++k) {
+      const int x = 16 * c + k;
+      const int off = x < 84 ? col_lut[x] - base : -1;
+      if (off >= 32) {
+        set_error("resize columns %d..%d span more than 32 source bytes", 16 * c, x);
+        return 1;
+      }
+      r->shuf[c][0][k] = (off >= 0 && off < 16) ? (uint8_t)off : 0x80;
+      r->shuf[c][1][k] = off >= 16 ? (uint8_t)(off - 16) : 0x80;
+    }
+  }
   return 0;
 }
 

@@ -262,10 +262,16 @@ def returns(rewards, masks, values, v_boot, gamma, y, adv):
                                 T, E, _ptr(y), _ptr(adv), _stream()), 'mt_returns')
 
 
-def preprocess(raw, push_offset, push_count, E, depth, row_lut, col_lut, prev, out, src_rows=210, pooled=False):
+def preprocess(raw, push_offset, push_count, E, depth, row_lut, col_lut, prev, out, src_rows=210, pooled=False,
+               resized=False):
     """atari_emulator.py:79-124 frame pool + resize + stack on device (raw screens of src_rows
     rows: 210 = whole screens with the resize LUT, 84 = runner-selected rows, identity LUT).
-    pooled: raw holds one screen per push, the frame-pool max already taken (mt_preprocess_pooled)."""
+    pooled: raw holds one screen per push, the frame-pool max already taken (mt_preprocess_pooled);
+    resized: raw holds each push's final 84x84 frame (mt_preprocess_resized, stacking only)."""
+    if resized:
+        check(_lib.hip().mt_preprocess_resized(_ptr(raw), _ptr(push_offset), _ptr(push_count), E, depth, _ptr(prev),
+                                               _ptr(out), _stream()), 'mt_preprocess_resized')
+        return
     name = 'mt_preprocess_pooled' if pooled else 'mt_preprocess'
     check(getattr(_lib.hip(), name)(_ptr(raw), _ptr(push_offset), _ptr(push_count), E, depth, int(src_rows),
                                     _ptr(row_lut), _ptr(col_lut), _ptr(prev), _ptr(out), _stream()), name)

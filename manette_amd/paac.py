@@ -45,12 +45,13 @@ class PAACLearner(ActorLearner):
         # native runner screens: 'in_place' = the GPU reads them in the emulators' pinned bank (no
         # host copy); 'zero_copy' = staged rows read in place from pinned staging; 'copy' = staged
         # rows hipMemcpyAsync'd to HBM; 'pooled' = zero_copy with the frame-pool max taken by the
-        # emulator threads (one staged screen per push)
-        self.staging = getattr(args, 'staging', 'in_place')
-        if self.staging not in ('in_place', 'zero_copy', 'copy', 'pooled'):
-            raise ValueError('staging must be in_place, zero_copy, copy or pooled')
+        # emulator threads (one staged screen per push); 'resized' = zero_copy of each push's final
+        # 84x84 frame (pool + resize on the emulator threads, the GPU only stacks)
+        self.staging = getattr(args, 'staging', 'resized')
+        if self.staging not in ('in_place', 'zero_copy', 'copy', 'pooled', 'resized'):
+            raise ValueError('staging must be in_place, zero_copy, copy, pooled or resized')
         # native step only: keep the GPU one macro-step ahead (MT_ROLLOUT_PIPELINED)
-        self.pipeline = bool(getattr(args, 'pipeline', False))
+        self.pipeline = bool(getattr(args, 'pipeline', True))
         self.depth = 3 if getattr(args, 'rgb', False) else 1
         self.C = 4 * self.depth
         self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
@@ -130,9 +131,10 @@ class PAACLearner(ActorLearner):
             else:
                 # only the 84 screen rows the nearest resize reads are staged (PCIe); zero_copy:
                 # kernels read env e's pushes in place at staging slots 4e..
-                fixed = self.sampling == 'device' and self.staging in ('zero_copy', 'pooled')
+                fixed = self.sampling == 'device' and self.staging in ('zero_copy', 'pooled', 'resized')
                 self.runners = NativeRunners(bank, self.workers, self.tab_rep, row_select=ROW_LUT,
-                                             fixed_slots=fixed, pooled=self.staging == 'pooled')
+                                             fixed_slots=fixed, pooled=self.staging == 'pooled',
+                                             resized=self.staging == 'resized', col_lut=COL_LUT)
                 self.stage_row_lut = torch.arange(84, dtype=torch.int32, device=self.dev)
                 self.raw_d = torch.zeros(4 * E, self.runners.staging.shape[1], self.runners.frame_bytes,
                                          dtype=torch.uint8, device=self.dev)
@@ -162,9 +164,11 @@ class PAACLearner(ActorLearner):
             flags, staging, frames, src_rows, rows = (_lib.MT_ROLLOUT_IN_PLACE, self.bank.screens_t, r.frames, 210,
                                                       self.row_lut)
         else:
-            flags = _lib.MT_ROLLOUT_ZERO_COPY if self.staging in ('zero_copy', 'pooled') else 0
+            flags = _lib.MT_ROLLOUT_ZERO_COPY if self.staging in ('zero_copy', 'pooled', 'resized') else 0
             if self.staging == 'pooled':
                 flags |= _lib.MT_ROLLOUT_POOLED
+            if self.staging == 'resized':
+                flags |= _lib.MT_ROLLOUT_RESIZED
             staging, frames, src_rows, rows = r.staging, None, r.src_rows, self.stage_row_lut
         self.sync_h = None
         if self.pipeline:
@@ -190,7 +194,8 @@ class PAACLearner(ActorLearner):
         self.raw_d[:total].copy_(r.staging[:total], non_blocking=True)
         self.meta_d.copy_(r.push_meta, non_blocking=True)
         devnet.preprocess(self.raw_d, self.off_d, self.cnt_d, self.emulator_counts, self.depth,
-                          self.stage_row_lut, self.col_lut, prev, out, src_rows=r.src_rows, pooled=r.pooled)
+                          self.stage_row_lut, self.col_lut, prev, out, src_rows=r.src_rows, pooled=r.pooled,
+                          resized=r.resized)
 
     def _upload_frames(self, out, prev):
         """In-place mode: H2D of the frame indices + push counts (a few hundred bytes), then

@@ -27,9 +27,12 @@ class NativeRunners(object):
     """row_select: screen rows to stage (None = whole 210-row screens). The learner passes the
     84 rows the nearest resize reads, so only those cross PCIe. fixed_slots: MH_RUNNER_FIXED_SLOTS
     (env e's pushes at staging slots 4e.., one worker phase per step). pooled: MH_RUNNER_POOLED
-    (one staged screen per push, max of its two frames, atari_emulator.py:79-88)."""
+    (one staged screen per push, max of its two frames, atari_emulator.py:79-88). resized:
+    MH_RUNNER_RESIZED (the final 84x84 frame of each push, pool + resize on the host threads;
+    needs the 84-row row_select and the column LUT col_lut)."""
 
-    def __init__(self, bank, n_workers, tab_rep, row_select=None, fixed_slots=False, pooled=False):
+    def __init__(self, bank, n_workers, tab_rep, row_select=None, fixed_slots=False, pooled=False, resized=False,
+                 col_lut=None):
         """in-place frame mode (reset_frames / step_frames) needs no row_select: the screens stay
         in the bank, only their indices are written (frames [E][8] + push_count)."""
         self.bank = bank
@@ -38,6 +41,8 @@ class NativeRunners(object):
         self.rows = None if row_select is None else np.ascontiguousarray(np.asarray(row_select, np.int32))
         self.src_rows = 210 if self.rows is None else len(self.rows)
         self.frame_bytes = bank.frame_bytes // 210 * self.src_rows  # one staged screen
+        if resized:
+            self.frame_bytes = 84 * 84 * bank.depth
         h = C.c_void_p()
         lib = _lib.host()
         _lib.check_host(lib.mh_runner_create(
@@ -46,14 +51,19 @@ class NativeRunners(object):
             bank.rewards.ctypes.data_as(C.c_void_p), bank.rewards.shape[1], bank.episode_len,
             None if self.rows is None else self.rows.ctypes.data_as(C.c_void_p),
             0 if self.rows is None else len(self.rows),
-            (_lib.MH_RUNNER_FIXED_SLOTS if fixed_slots else 0) | (_lib.MH_RUNNER_POOLED if pooled else 0),
-            C.byref(h)), 'mh_runner_create')
+            (_lib.MH_RUNNER_FIXED_SLOTS if fixed_slots else 0) | (_lib.MH_RUNNER_POOLED if pooled else 0) |
+            (_lib.MH_RUNNER_RESIZED if resized else 0), C.byref(h)), 'mh_runner_create')
         self.fixed_slots = bool(fixed_slots)
         self.pooled = bool(pooled)
+        self.resized = bool(resized)
+        if resized:
+            self._cols = np.ascontiguousarray(np.asarray(col_lut, dtype=np.int32))
+            _lib.check_host(lib.mh_runner_set_col_lut(h, self._cols.ctypes.data_as(C.c_void_p), len(self._cols)),
+                            'mh_runner_set_col_lut')
         self._h = h
         pin = torch.cuda.is_available()
         mk = lambda *shape, dtype: torch.zeros(*shape, dtype=dtype, pin_memory=pin)
-        self.staging = mk(4 * self.E, 1 if pooled else 2, self.frame_bytes, dtype=torch.uint8)
+        self.staging = mk(4 * self.E, 1 if (pooled or resized) else 2, self.frame_bytes, dtype=torch.uint8)
         self.push_meta = mk(2, self.E, dtype=torch.int32)  # [offset; count]: one H2D copy
         self.push_offset = self.push_meta[0]
         self.push_count = self.push_meta[1]

@@ -303,3 +303,37 @@ def test_native_runner_pooled_staging_is_frame_pool_max():
     finally:
         two.stop()
         one.stop()
+
+
+@pytest.mark.parametrize('rgb', [False, True])
+def test_native_runner_resized_staging_is_pool_and_resize(rgb):
+    """MH_RUNNER_RESIZED stages, per push, max(f0, f1) at the nearest-resize LUT rows and columns
+    (atari_emulator.py:79-88, :113-124; SSE max + pshufb gather on the host) == the oracle's
+    pool_and_resize of the two whole screens, byte for byte, with the same counts and rewards."""
+    from manette_amd.environment import COL_LUT, ROW_LUT
+    from manette_amd.runners import NativeRunners
+    from manette_amd.synthetic import SyntheticBank
+    tab = opol.tab_repetitions(10, 11)
+    E = 5
+    bank = SyntheticBank(11, E, rgb=rgb, episode_len=8)
+    full = NativeRunners(bank, 2, tab, fixed_slots=True)
+    rsz = NativeRunners(bank, 3, tab, row_select=ROW_LUT, fixed_slots=True, resized=True, col_lut=COL_LUT)
+    depth = 3 if rgb else 1
+    assert rsz.staging.shape == (4 * E, 1, 84 * 84 * depth)
+    try:
+        full.reset(), rsz.reset()
+        rs = np.random.RandomState(7)
+        for step in range(10):
+            np.testing.assert_array_equal(full.push_count.numpy(), rsz.push_count.numpy())
+            for e in range(E):
+                for j in range(int(full.push_count[e])):
+                    s = full.staging.numpy()[4 * e + j].reshape(2, 210, 160, depth)
+                    want = opre.pool_and_resize(s[0], s[1])
+                    np.testing.assert_array_equal(rsz.staging.numpy()[4 * e + j, 0].reshape(84, 84, depth), want)
+            act = rs.randint(0, 6, E).astype(np.int32)
+            rep = rs.randint(0, 11, E).astype(np.int32)
+            full.step(act, rep), rsz.step(act, rep)
+            np.testing.assert_array_equal(full.reward.numpy(), rsz.reward.numpy())
+    finally:
+        full.stop()
+        rsz.stop()

@@ -212,6 +212,25 @@ def test_preprocess_pooled_bit_exact(depth):
         np.testing.assert_array_equal(got[e], preprocess.stack_update(prev[e], pushes, depth))
 
 
+@pytest.mark.parametrize('depth', [1, 3])
+def test_preprocess_resized_bit_exact(depth):
+    """mt_preprocess_resized: each push's final 84x84 frame staged by the host, only stacked."""
+    from manette_amd.network import preprocess as dev_pre
+    rs = np.random.RandomState(20 + depth)
+    E = 6
+    counts = np.array([4, 1, 3, 2, 4, 1], np.int32)
+    offs = (4 * np.arange(E)).astype(np.int32)
+    final = rs.randint(0, 256, size=(4 * E, 84, 84, depth)).astype(np.uint8)
+    prev = rs.randint(0, 256, size=(E, 84, 84, 4 * depth)).astype(np.uint8)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    out = torch.empty(E, 84, 84, 4 * depth, dtype=torch.uint8, device='cuda')
+    dev_pre(d(final), d(offs), d(counts), E, depth, None, None, d(prev), out, resized=True)
+    got = out.cpu().numpy()
+    for e in range(E):
+        pushes = [final[offs[e] + j] for j in range(counts[e])]
+        np.testing.assert_array_equal(got[e], preprocess.stack_update(prev[e], pushes, depth))
+
+
 def test_sample_distribution():
     from manette_amd.network import sample
     B, A, R = 4096, 6, 3

@@ -52,7 +52,9 @@ def _state(L):
 @pytest.mark.parametrize('max_rep,nb,staging,pipeline', [(0, 1, 'in_place', False), (10, 11, 'in_place', False),
                                                          (10, 11, 'zero_copy', False), (10, 11, 'copy', False),
                                                          (10, 11, 'pooled', False), (0, 1, 'in_place', True),
-                                                         (10, 11, 'in_place', True), (10, 11, 'pooled', True)])
+                                                         (10, 11, 'in_place', True), (10, 11, 'pooled', True),
+                                                         (10, 11, 'resized', False), (0, 1, 'resized', True),
+                                                         (10, 11, 'resized', True)])
 def test_native_step_equals_python_step(tmp_path, max_rep, nb, staging, pipeline):
     """mt_rollout_step (C++ orchestration, sampling fused in the heads kernel; in-place, zero-copy,
     pooled or copied staging; optionally pipelined one step ahead behind a device wait) == the

@@ -2,7 +2,7 @@
 (train.py:1-130), driving the MI355X learner (manette_amd.paac.PAACLearner).
 
 Extra flags (this build only): --runner {native,python}, --sampling {host,device},
---staging {in_place,zero_copy,copy,pooled}, --pipeline, --seed.
+--staging {resized,in_place,zero_copy,copy,pooled}, --no_pipeline, --seed.
 Multi-GPU: launch one process per GPU with torch.distributed.run; each rank trains
 -ec emulators of its own (global env ids offset by rank) and gradients are all-reduced.
 """
@@ -129,13 +129,15 @@ def get_arg_parser():
     parser.add_argument('--alpha_leaky_relu', default=0.1, type=float, help="coef for leaky relu", dest="alpha_leaky_relu")
     # this build
     parser.add_argument('--runner', default='native', choices=['native', 'python'], help='native: C++ emulator threads + GPU preprocess; python: reference-contract emulator processes', dest='runner')
-    parser.add_argument('--staging', default='in_place', choices=['in_place', 'zero_copy', 'copy', 'pooled'],
-                        help='native runner screens: read by the GPU in the emulators\' pinned bank (in_place), '
-                             'staged rows read in place (zero_copy), or staged rows hipMemcpyAsync\'d (copy)',
+    parser.add_argument('--staging', default='resized', choices=['in_place', 'zero_copy', 'copy', 'pooled', 'resized'],
+                        help='native runner screens: each push\'s final 84x84 frame pooled + resized by the emulator '
+                             'threads and read in place from pinned memory (resized), the GPU reading the emulators\' '
+                             'pinned bank (in_place), staged rows read in place (zero_copy, pooled = host frame-pool max) '
+                             'or staged rows hipMemcpyAsync\'d (copy)',
                         dest='staging')
-    parser.add_argument('--pipeline', action='store_true', help='native device-sampling step: enqueue step t+1\'s '
-                        'preprocess + forward behind a device wait on a host step word (MT_ROLLOUT_PIPELINED)',
-                        dest='pipeline')
+    parser.add_argument('--no_pipeline', action='store_false', help='native device-sampling step: do not enqueue '
+                        'step t+1\'s preprocess + forward behind a device wait on a host step word '
+                        '(MT_ROLLOUT_PIPELINED, on by default)', dest='pipeline')
     parser.add_argument('--sampling', default='host', choices=['host', 'device'], help='host: numpy multinomial (reference stream); device: mt_sample', dest='sampling')
     parser.add_argument('--seed', default=0, type=int, help='parameter init / device sampling seed', dest='seed')
     return parser
