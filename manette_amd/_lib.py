@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-HIP_LIB = os.path.join(HERE, 'libmanette_hip.so')
+HIP_LIB = os.environ.get('MANETTE_HIP_LIB') or os.path.join(HERE, 'libmanette_hip.so')  # variant override
 HOST_LIB = os.path.join(HERE, 'libmanette_host.so')
 
 MT_ARCH = {'NIPS': 0, 'NATURE': 1, 'PWYX': 2, 'LSTM': 3}
@@ -26,7 +26,7 @@ class mt_rollout_buffers(C.Structure):
                [(n, C.c_void_p) for n in ('counters', 'raw')] + [('src_rows', C.c_int32)] + \
                [(n, C.c_void_p) for n in ('pair', 'pair_host', 'meta', 'row_lut', 'col_lut', 'idx_host',
                                           'staging_host', 'meta_host', 'reward_host', 'over_host',
-                                          'rm_host', 'frames_host', 'sync_host')] + [('flags', C.c_int32)]
+                                          'rm_host', 'frames_host', 'sync_host', 'ready_host')] + [('flags', C.c_int32)]
 
 
 MT_ROLLOUT_ZERO_COPY = 1

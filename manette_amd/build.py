@@ -32,21 +32,24 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_hip(force=False, verbose=False):
+def build_hip(force=False, verbose=False, out=None, defines=()):
+    """out / defines: an experiment variant (e.g. -DMT_THIN_BM=128) written next to the product
+    library; select it at run time with MANETTE_HIP_LIB (manette_amd/_lib.py)."""
+    target = out or HIP_LIB
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [os.path.join(INCLUDE, 'manette_hip.h'),
                                                                   os.path.join(INCLUDE, 'manette_host.h'), HOST_LIB]
-    if not force and not _stale(HIP_LIB, deps):
-        return HIP_LIB
-    tmp = HIP_LIB + '.tmp'
+    if not force and not _stale(target, deps):
+        return target
+    tmp = target + '.tmp'
     cmd = [_hipcc(), '--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
-           '-Wno-unused-result', '-o', tmp] + srcs + [
+           '-Wno-unused-result'] + ['-D' + d for d in defines] + ['-o', tmp] + srcs + [
                '-L' + HERE, '-lmanette_host', '-Wl,-rpath,$ORIGIN']
     if verbose:
         print(' '.join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(tmp, HIP_LIB)
-    return HIP_LIB
+    os.replace(tmp, target)
+    return target
 
 
 def build_host(force=False, verbose=False):

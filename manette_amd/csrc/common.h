@@ -96,6 +96,10 @@ struct SampleArgs {
   uint64_t seed;
   uint64_t *counters;
   int32_t *a_idx, *r_idx, *pair;
+  // optional: ready[b] = seq is stored (system scope, after the pair) once row b's pair is written,
+  // so a host polling pinned memory sees the pair without an event query (mt_rollout_step)
+  uint32_t *ready = nullptr;
+  uint32_t seq = 0;
 };
 
 }  // namespace mt

@@ -185,13 +185,19 @@ template <int N, int BK>
 struct TileFor {
   using T = Tile<64, 64, 2, 2, BK>;
 };
+// Thin-N conv tiles (COUT or CIN of 16 / 32): the 4 waves split M, each wave TM = MT_THIN_BM/64
+// 16-row fragments, so one B fragment feeds TM MFMAs. BK is capped so the A stage stays <= 64 KB.
+#ifndef MT_THIN_BM
+#define MT_THIN_BM 64
+#endif
+constexpr int thin_bk(int bk) { return MT_THIN_BM * (bk + 4) * 4 > 98304 && bk % 32 == 0 ? thin_bk(bk / 2) : bk; }
 template <int BK>
 struct TileFor<16, BK> {
-  using T = Tile<64, 16, 4, 1, BK>;
+  using T = Tile<MT_THIN_BM, 16, 4, 1, thin_bk(BK)>;
 };
 template <int BK>
 struct TileFor<32, BK> {
-  using T = Tile<64, 32, 4, 1, BK>;
+  using T = Tile<MT_THIN_BM, 32, 4, 1, thin_bk(BK)>;
 };
 
 // K-chunk of a forward conv: the whole K when it fits 256, else the largest of 256/192/128
@@ -396,15 +402,12 @@ __device__ __forceinline__ int wave_draw(float p, int n, double u) {
 //     wave w takes outputs o = w, w+4, ...; lanes split F and reduce with shuffles;
 //  3. wave 0: v = logit_0, pi = softmax(logits_A / temp), rep = softmax(logits_R / temp);
 //  4. rollout path (smp.counters != null): wave 0 draws (a, r) for the row (A3, common.h).
-__global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict__ slabs, int S, int B,
-                                                        const float *__restrict__ fc_b, int act,
-                                                        float alpha, HeadParams hp, float temp,
-                                                        float *__restrict__ H, float *__restrict__ v,
-                                                        float *__restrict__ pi,
-                                                        float *__restrict__ rep, SampleArgs smp) {
+__device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs, int S, int B,
+                                          const float *__restrict__ fc_b, int act, float alpha, const HeadParams &hp,
+                                          float temp, float *__restrict__ H, float *__restrict__ v,
+                                          float *__restrict__ pi, float *__restrict__ rep, const SampleArgs &smp) {
   __shared__ float hs[512];
   __shared__ float zs[64];
-  const int b = blockIdx.x;
   const int F = hp.F, O = 1 + hp.A + hp.R;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int f = threadIdx.x; f < F; f += 256) {
@@ -455,9 +458,23 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict_
         smp.pair[b] = a;
         smp.pair[B + b] = r;
       }
+      if (smp.ready) {  // release: the pair stores are visible to the host before the flag
+        __threadfence_system();
+        __hip_atomic_store(smp.ready + b, smp.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
 }
+
+__global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict__ slabs, int S, int B,
+                                                        const float *__restrict__ fc_b, int act,
+                                                        float alpha, HeadParams hp, float temp,
+                                                        float *__restrict__ H, float *__restrict__ v,
+                                                        float *__restrict__ pi,
+                                                        float *__restrict__ rep, SampleArgs smp) {
+  heads_row(blockIdx.x, slabs, S, B, fc_b, act, alpha, hp, temp, H, v, pi, rep, smp);
+}
+
 
 // dL/dlogit for one softmax head (policy_v_network.py:29-57, :59-74), one wave, lanes [0, n):
 // objective = adv*log(p_sel + 1e-30) + beta*H,  H = -sum p*log(p + 1e-30),  L = -scale*objective.

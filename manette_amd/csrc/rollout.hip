@@ -25,6 +25,8 @@ struct mt_rollout {
   uint8_t *staging_dev;  // device addresses of the host-mapped buffers (zero-copy mode)
   int32_t *meta_dev, *pair_dev, *frames_dev;
   uint32_t *seq_dev, *status_dev;
+  uint32_t *ready_dev = nullptr;  // [E] pair-ready flags (device address of b.ready_host)
+  uint32_t fwd_seq = 0;           // sequence number of the last enqueued forward + draw
   double acc[5];  // host wall us: launch+wait for indices, runner, book, upload+preprocess enqueue; steps
 };
 
@@ -59,6 +61,11 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
     MT_HIP(hipHostGetDevicePointer(&pair_dev, b.pair_host, 0));
     if (ip) MT_HIP(hipHostGetDevicePointer(&frames_dev, b.frames_host, 0));
   }
+  void *ready_dev = nullptr;
+  if (zc && b.ready_host) {
+    MT_HIP(hipHostGetDevicePointer(&ready_dev, b.ready_host, 0));
+    for (int e = 0; e < E; ++e) b.ready_host[e] = 0;
+  }
   void *sync_dev = nullptr;
   if (pl) {
     MT_HIP(hipHostGetDevicePointer(&sync_dev, b.sync_host, 0));
@@ -91,6 +98,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->resized = rz;
   ro->pipelined = pl;
   ro->frames_dev = (int32_t *)frames_dev;
+  ro->ready_dev = (uint32_t *)ready_dev;
   ro->seq_dev = (uint32_t *)sync_dev;
   ro->status_dev = sync_dev ? (uint32_t *)sync_dev + 1 : nullptr;
   ro->staging_dev = (uint8_t *)staging_dev;
@@ -146,7 +154,9 @@ int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s) {
   const int E = ro->E, T = ro->T;
   const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
   int32_t *a_d = b.idx + (size_t)t * E, *r_d = b.idx + (size_t)T * E + (size_t)t * E;
-  const SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
+  SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
+  smp.ready = ro->ready_dev;
+  smp.seq = ++ro->fwd_seq;
   MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)t * slot, E, b.ws, b.ws_bytes,
                          b.values + (size_t)t * E, b.pi, b.rep, &smp, true, s));
   if (!ro->zero_copy)
@@ -214,9 +224,28 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   }
   // 3. wait for the indices of step t (spin: a blocking wait sleeps past the chain and pays the
   //    wake-up latency)
-  hipError_t q;
-  while ((q = hipEventQuery(ro->ev2[t & 1])) == hipErrorNotReady) __builtin_ia32_pause();
-  MT_HIP(q);
+  // (with ready flags: poll the E flags the heads kernel stores after each pair — one cached host
+  //  load each — and query the event only now and then, to surface a device error)
+  const uint32_t want = ro->pipelined && ro->armed == t + 1 ? ro->fwd_seq - 1 : ro->fwd_seq;
+  if (ro->ready_dev) {
+    const volatile uint32_t *rf = b.ready_host;
+    for (int e = 0, spins = 0; e < E;) {
+      if (__atomic_load_n(const_cast<const uint32_t *>(rf + e), __ATOMIC_ACQUIRE) == want) {
+        ++e;
+        continue;
+      }
+      __builtin_ia32_pause();
+      if (++spins == 4096) {
+        spins = 0;
+        const hipError_t q = hipEventQuery(ro->ev2[t & 1]);
+        if (q != hipSuccess && q != hipErrorNotReady) MT_HIP(q);
+      }
+    }
+  } else {
+    hipError_t q;
+    while ((q = hipEventQuery(ro->ev2[t & 1])) == hipErrorNotReady) __builtin_ia32_pause();
+    MT_HIP(q);
+  }
   if (ro->pipelined && __atomic_load_n(&b.sync_host[1], __ATOMIC_ACQUIRE) != 0) {
     set_error("device wait for the host step word timed out (host stalled > 2 s); rollout state is invalid");
     return MT_ERR_HIP;

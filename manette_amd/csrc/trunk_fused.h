@@ -43,14 +43,12 @@ struct FusedNips {
   static constexpr size_t LDS_BYTES = IN_BYTES + sizeof(float) * (RED_FLOATS + M1 * A1S + FEAT);
 };
 
+// One block's work: conv2 row i of env e -> its fc partial slab. Returns e (the env).
 template <int C>
-__global__ __launch_bounds__(256) void nips_fused_trunk_kernel(const uint8_t *__restrict__ obs, int B,
-                                                               const float *__restrict__ W1,
-                                                               const float *__restrict__ W2,
-                                                               const float *__restrict__ Wfc, int act,
-                                                               float alpha, float *__restrict__ slabs) {
+__device__ __forceinline__ int nips_trunk_block(const uint8_t *__restrict__ obs, int B, const float *__restrict__ W1,
+                                                const float *__restrict__ W2, const float *__restrict__ Wfc, int act,
+                                                float alpha, float *__restrict__ slabs, float *smem) {
   using Fz = FusedNips<C>;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   float *red = smem;                              // [4 waves][..] partial accumulators
   float *a1 = red + Fz::RED_FLOATS;               // [80 pixels][A1S] conv1 rows 2i..2i+3
   float *a2 = a1 + Fz::M1 * Fz::A1S;              // [288] conv2 row i (NHWC flatten order)
@@ -181,6 +179,17 @@ __global__ __launch_bounds__(256) void nips_fused_trunk_kernel(const uint8_t *__
     const f32x4 s = ((rp[threadIdx.x] + rp[64 + threadIdx.x]) + rp[128 + threadIdx.x]) + rp[192 + threadIdx.x];
     reinterpret_cast<f32x4 *>(slabs + ((size_t)i * B + e) * Fz::F)[threadIdx.x] = s;
   }
+  return e;
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void nips_fused_trunk_kernel(const uint8_t *__restrict__ obs, int B,
+                                                               const float *__restrict__ W1,
+                                                               const float *__restrict__ W2,
+                                                               const float *__restrict__ Wfc, int act,
+                                                               float alpha, float *__restrict__ slabs) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  (void)nips_trunk_block<C>(obs, B, W1, W2, Wfc, act, alpha, slabs, smem);
 }
 
 }  // namespace mt

@@ -121,7 +121,7 @@ class DeviceNetwork(object):
         check(_lib.hip().mt_net_workspace_bytes(self._h, batch, C.byref(n)))
         ws = self._ws.get(key)
         if ws is None or ws.numel() < n.value:
-            ws = torch.empty(n.value, dtype=torch.uint8, device=self.device)
+            ws = torch.zeros(n.value, dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
         return ws
 

@@ -171,6 +171,9 @@ class PAACLearner(ActorLearner):
                 flags |= _lib.MT_ROLLOUT_RESIZED
             staging, frames, src_rows, rows = r.staging, None, r.src_rows, self.stage_row_lut
         self.sync_h = None
+        # zero-copy modes: the heads kernel flags each env's pair as written (host polls, no event)
+        self.ready_h = torch.zeros(self.emulator_counts, dtype=torch.int32, pin_memory=True) \
+            if flags & (_lib.MT_ROLLOUT_ZERO_COPY | _lib.MT_ROLLOUT_IN_PLACE) else None
         if self.pipeline:
             if flags & (_lib.MT_ROLLOUT_ZERO_COPY | _lib.MT_ROLLOUT_IN_PLACE) == 0:
                 raise ValueError('pipeline needs in_place, zero_copy or pooled staging')
@@ -180,7 +183,7 @@ class PAACLearner(ActorLearner):
             p(self.states), p(self.values), p(self.idx), p(self.pi_roll), p(self.rep_roll), p(ws), ws.numel(),
             p(self.counters), p(self.raw_d), src_rows, p(self.pair_d), p(self.pair_h), p(self.meta_d),
             p(rows), p(self.col_lut), p(self.idx_h), p(staging), p(r.push_meta), p(r.reward),
-            p(r.over), p(self.rm_h), p(frames), p(self.sync_h), flags)
+            p(r.over), p(self.rm_h), p(frames), p(self.sync_h), p(self.ready_h), flags)
         h = C.c_void_p()
         _lib.check(_lib.hip().mt_rollout_create(net._h, self.emulator_counts, self.max_local_steps, r._h,
                                                 self.book.handle, C.byref(self._bufs),
