@@ -98,6 +98,17 @@ int mt_forward(const mt_net *net, const float *params, const uint8_t *obs, int b
 int mt_forward_infer(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                      size_t ws_bytes, float *v, float *pi, float *rep, mt_stream_t stream);
 
+/* Inference forward of `batch` rows that ALSO leaves their activations (and dense outputs H) in
+ * rows [row0, row0 + batch) of a train workspace sized for train_rows rows
+ * (mt_net_workspace_bytes(net, train_rows)). A rollout that forwards state slot t with
+ * row0 = t*E fills the whole batch the update trains on (paac.py:236: row t*E + e), with the
+ * parameters unchanged in between, so mt_loss_backward(train_rows) then needs no mt_forward: pass
+ * it the rollout's v / pi / rep of every row. `ws` (batch rows) holds the split-K partials.
+ * Not for the LSTM arch (its frame store does the same, mt_lstm_*). */
+int mt_forward_rows(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
+                    size_t ws_bytes, void *train_ws, size_t train_ws_bytes, int train_rows, int row0, float *v,
+                    float *pi, float *rep, mt_stream_t stream);
+
 /* Trunk half of mt_forward_infer alone (roofline timing / diagnostics): the convs and the dense
  * layer's partial products, left in `ws` (NIPS: the one fused-trunk launch). */
 int mt_forward_trunk(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
@@ -276,6 +287,10 @@ typedef struct mt_rollout_buffers {
   float *rm_host;              /* [2][T][E]: clipped rewards; masks */
   int32_t *frames_host;        /* [E][8] in-place frame indices (MT_ROLLOUT_IN_PLACE), else NULL */
   uint32_t *sync_host;         /* [2] pipelined step word + wait status (MT_ROLLOUT_PIPELINED), else NULL */
+  void *train_ws;              /* optional: train workspace of T*E rows; the forward of step t then also
+                                  writes rows [t*E, (t+1)*E) (mt_forward_rows) and pi / rep are
+                                  [T][E][.] per-step outputs; NULL: pi / rep are [E][.] */
+  size_t train_ws_bytes;
   uint32_t *ready_host;        /* [E] zero-copy modes: the heads kernel stores a step sequence number per
                                   env after writing its pair; the host polls these instead of an event
                                   (NULL: hipEventQuery) */

@@ -26,7 +26,8 @@ class mt_rollout_buffers(C.Structure):
                [(n, C.c_void_p) for n in ('counters', 'raw')] + [('src_rows', C.c_int32)] + \
                [(n, C.c_void_p) for n in ('pair', 'pair_host', 'meta', 'row_lut', 'col_lut', 'idx_host',
                                           'staging_host', 'meta_host', 'reward_host', 'over_host',
-                                          'rm_host', 'frames_host', 'sync_host', 'ready_host')] + [('flags', C.c_int32)]
+                                          'rm_host', 'frames_host', 'sync_host', 'train_ws')] + \
+               [('train_ws_bytes', C.c_size_t), ('ready_host', C.c_void_p), ('flags', C.c_int32)]
 
 
 MT_ROLLOUT_ZERO_COPY = 1
@@ -66,6 +67,7 @@ _HIP_SIGS = {
     'mt_lstm_frames_forward': (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),
     'mt_lstm_windows_forward': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P, _P, _P, _P]),
     'mt_lstm_frames_backward': (_I, [_P, _P, _P, _P, _I, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
+    'mt_forward_rows': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _SZ, _I, _I, _P, _P, _P, _P]),
     'mt_forward_trunk': (_I, [_P, _P, _P, _I, _P, _SZ, _P]),
     'mt_forward_infer': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P]),
     'mt_sample': (_I, [_P, _P, _I, _I, _I, C.c_uint64, _P, _P, _P, _P, _P]),

@@ -106,8 +106,15 @@ struct SampleArgs {
 
 struct mt_net;
 namespace mt {
-// forward (mt_forward) with the A3 draw fused into the heads kernel; smp may be null.
+// Rows [row0, row0 + batch) of a train workspace sized for `rows` rows: an inference forward
+// given one leaves its activations there, so the update's mt_loss_backward needs no forward.
+struct TrainRows {
+  float *ws;
+  size_t ws_bytes;
+  int rows, row0;
+};
+// forward (mt_forward) with the A3 draw fused into the heads kernel; smp and tr may be null.
 int forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                    size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp, bool infer,
-                   hipStream_t stream);
+                   hipStream_t stream, const TrainRows *tr = nullptr);
 }  // namespace mt

@@ -324,22 +324,6 @@ static size_t max_wgrad_slab(int B) {
   return 0;
 }
 
-template <class Ar, int I = 0>
-static void shift_rows(WsLayout &L, size_t row0) {
-  if constexpr (I < Ar::NCONV) {
-    using G = LayerG<Ar, I>;
-    const size_t a = row0 * G::OH * G::OW * G::COUT;
-    L.act[I] += a;
-    L.dact[I] += a;
-    if constexpr (pooled<Ar, I>()) {
-      const size_t p = row0 * (G::OH / 2) * (G::OW / 2) * G::COUT;
-      L.pool[I] += p;
-      L.dpool[I] += p;
-    }
-    shift_rows<Ar, I + 1>(L, row0);
-  }
-}
-
 template <class Ar>
 static LstmFrameWs lstm_frame_layout(const mt_net *n, int E, int T) {
   LstmFrameWs X{};

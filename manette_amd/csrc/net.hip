@@ -748,12 +748,47 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
   return MT_OK;
 }
 
+// Per-row conv buffers of a layout moved to start at row `row0` (the dense/head buffers stay).
+template <class Ar, int I = 0>
+static void shift_rows(WsLayout &L, size_t row0) {
+  if constexpr (I < Ar::NCONV) {
+    using G = LayerG<Ar, I>;
+    const size_t a = row0 * G::OH * G::OW * G::COUT;
+    L.act[I] += a;
+    L.dact[I] += a;
+    if constexpr (pooled<Ar, I>()) {
+      const size_t p = row0 * (G::OH / 2) * (G::OW / 2) * G::COUT;
+      L.pool[I] += p;
+      L.dpool[I] += p;
+    }
+    shift_rows<Ar, I + 1>(L, row0);
+  }
+}
+
+// Where a forward of B rows leaves its activations: its own workspace, or rows [row0, row0+B)
+// of a train workspace (tr): conv buffers through a shifted layout, H at row0.
+struct ActRows {
+  float *base;
+  WsLayout L;
+  size_t h_off;  // float offset of row 0's H from base
+};
+template <class Ar>
+static ActRows act_rows(const mt_net *n, float *ws, const WsLayout &L, const TrainRows *tr) {
+  if (!tr) return ActRows{ws, L, L.H};
+  ActRows a{tr->ws, ws_layout<Ar>(n, tr->rows), 0};
+  a.h_off = a.L.H + (size_t)tr->row0 * Ar::F;
+  shift_rows<Ar>(a.L, (size_t)tr->row0);
+  return a;
+}
+
 template <class Ar>
 static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
-                        float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s) {
+                        float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s,
+                        const TrainRows *tr = nullptr) {
   const WsLayout L = ws_layout<Ar>(n, B);
-  MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s)));
-  const float *flat = layer_out<Ar, Ar::NCONV - 1>(ws, L);
+  const ActRows A = act_rows<Ar>(n, ws, L, tr);
+  MT_TRY((trunk_forward<Ar>(n, P, obs, B, A.base, A.L, s)));
+  const float *flat = layer_out<Ar, Ar::NCONV - 1>(A.base, A.L);
   // dense layer (networks.py:57-70), split-K partial slabs; heads kernel finishes bias + act.
   const float *Wfc = P + n->off_fc;
   MT_TRY((launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1},
@@ -761,7 +796,7 @@ static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int
   HeadParams hp = head_params(n, P);
   hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, L.fc_splits, B,
                      Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp,
-                     n->cfg.softmax_temp, ws + L.H, v, pi, rep, smp ? *smp : SampleArgs{});
+                     n->cfg.softmax_temp, A.base + A.h_off, v, pi, rep, smp ? *smp : SampleArgs{});
   MT_LAUNCHED();
   return MT_OK;
 }
@@ -770,24 +805,26 @@ static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int
 // (trunk_fused.h), whose 9 conv2-row slabs heads_fwd_kernel finishes; else the layered forward.
 template <class Ar>
 static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
-                              float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s) {
+                              float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s,
+                              const TrainRows *tr = nullptr) {
   if constexpr (Ar::FUSED_SLABS > 0) {
     constexpr int C = LayerG<Ar, 0>::CIN;
     using Fz = FusedNips<C>;
     const WsLayout L = ws_layout<Ar>(n, B);
+    const ActRows A = act_rows<Ar>(n, ws, L, tr);
     const float *Wfc = P + n->off_fc;
     hipLaunchKernelGGL(nips_fused_trunk_kernel<C>, dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, obs, B,
                        P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation, n->cfg.alpha_leaky,
-                       ws + L.fcslab);
+                       ws + L.fcslab, tr ? A.base + A.L.act[0] : nullptr, tr ? A.base + A.L.act[1] : nullptr);
     MT_LAUNCHED();
     HeadParams hp = head_params(n, P);
     hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, Fz::ROWS2, B,
                        Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp,
-                       n->cfg.softmax_temp, ws + L.H, v, pi, rep, smp ? *smp : SampleArgs{});
+                       n->cfg.softmax_temp, A.base + A.h_off, v, pi, rep, smp ? *smp : SampleArgs{});
     MT_LAUNCHED();
     return MT_OK;
   } else {
-    return forward_impl<Ar>(n, P, obs, B, ws, v, pi, rep, smp, s);
+    return forward_impl<Ar>(n, P, obs, B, ws, v, pi, rep, smp, s, tr);
   }
 }
 
@@ -988,7 +1025,7 @@ static int trunk_infer_impl(const mt_net *n, const float *P, const uint8_t *obs,
       using Fz = FusedNips<C>;
       hipLaunchKernelGGL(nips_fused_trunk_kernel<C>, dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, obs, B,
                          P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation, n->cfg.alpha_leaky,
-                         ws + L.fcslab);
+                         ws + L.fcslab, nullptr, nullptr);
       MT_LAUNCHED();
       return MT_OK;
     } else {
@@ -1015,6 +1052,15 @@ extern "C" int mt_forward_trunk(const mt_net *net, const float *params, const ui
   return MT_OK;
 }
 
+extern "C" int mt_forward_rows(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
+                               size_t ws_bytes, void *train_ws, size_t train_ws_bytes, int train_rows, int row0,
+                               float *v, float *pi, float *rep, mt_stream_t stream) {
+  MT_CHECK_ARG(train_ws, "null train workspace");
+  const TrainRows tr{(float *)train_ws, train_ws_bytes, train_rows, row0};
+  return mt::forward_sample(net, params, obs, batch, ws, ws_bytes, v, pi, rep, nullptr, true, (hipStream_t)stream,
+                            &tr);
+}
+
 extern "C" int mt_forward_infer(const mt_net *net, const float *params, const uint8_t *obs, int batch,
                                 void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
                                 mt_stream_t stream) {
@@ -1024,7 +1070,7 @@ extern "C" int mt_forward_infer(const mt_net *net, const float *params, const ui
 
 int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch,
                        void *ws, size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp,
-                       bool infer, hipStream_t stream) {
+                       bool infer, hipStream_t stream, const TrainRows *tr) {
   MT_CHECK_ARG(net && params && obs && ws && v && pi && rep, "null argument");
   MT_CHECK_ARG(!smp || (smp->counters && smp->a_idx && smp->r_idx), "null sample buffer");
   MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
@@ -1034,11 +1080,21 @@ int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *ob
       set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
       return MT_ERR_WORKSPACE;
     }
+    if (tr) {
+      MT_CHECK_ARG(!Ar::LSTM, "train-row forwards are not built for the LSTM arch (frame store: mt_lstm_*)");
+      MT_CHECK_ARG(tr->ws && tr->rows >= 1 && tr->row0 >= 0 && tr->row0 + batch <= tr->rows,
+                   "train rows [%d, %d) outside [0, %d)", tr->row0, tr->row0 + batch, tr->rows);
+      const size_t need = ws_layout<Ar>(net, tr->rows).total * sizeof(float);
+      if (tr->ws_bytes < need) {
+        set_error("train workspace %zu < %zu bytes", tr->ws_bytes, need);
+        return MT_ERR_WORKSPACE;
+      }
+    }
     if constexpr (Ar::LSTM)
       return lstm_forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
     else
-      return infer ? forward_infer_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream)
-                   : forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
+      return infer ? forward_infer_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream, tr)
+                   : forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream, tr);
   });
   return MT_OK;
 }

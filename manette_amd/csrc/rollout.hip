@@ -157,8 +157,12 @@ int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s) {
   SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
   smp.ready = ro->ready_dev;
   smp.seq = ++ro->fwd_seq;
+  // with a train workspace: activations into its rows t*E.., per-step pi / rep (mt_forward_rows)
+  const TrainRows tr{(float *)b.train_ws, b.train_ws_bytes, T * E, t * E};
+  const size_t po = b.train_ws ? (size_t)t * E : 0;
   MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)t * slot, E, b.ws, b.ws_bytes,
-                         b.values + (size_t)t * E, b.pi, b.rep, &smp, true, s));
+                         b.values + (size_t)t * E, b.pi + po * ro->A, b.rep + po * ro->R, &smp, true, s,
+                         b.train_ws ? &tr : nullptr));
   if (!ro->zero_copy)
     MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
   MT_HIP(hipEventRecord(ro->ev2[t & 1], s));

@@ -44,10 +44,14 @@ struct FusedNips {
 };
 
 // One block's work: conv2 row i of env e -> its fc partial slab. Returns e (the env).
+// act1 / act2 (optional): [B][20][20][16] conv1 and [B][9][9][32] conv2 activations of this
+// batch (rows of a train workspace, mt_forward_rows); block (e, i) writes conv1 rows 2i, 2i+1
+// (the last block also 18, 19) and conv2 row i, so every value is written once.
 template <int C>
 __device__ __forceinline__ int nips_trunk_block(const uint8_t *__restrict__ obs, int B, const float *__restrict__ W1,
                                                 const float *__restrict__ W2, const float *__restrict__ Wfc, int act,
-                                                float alpha, float *__restrict__ slabs, float *smem) {
+                                                float alpha, float *__restrict__ slabs, float *smem,
+                                                float *__restrict__ act1, float *__restrict__ act2) {
   using Fz = FusedNips<C>;
   float *red = smem;                              // [4 waves][..] partial accumulators
   float *a1 = red + Fz::RED_FLOATS;               // [80 pixels][A1S] conv1 rows 2i..2i+3
@@ -126,7 +130,10 @@ __device__ __forceinline__ int nips_trunk_block(const uint8_t *__restrict__ obs,
     for (int idx = threadIdx.x; idx < Fz::M1 * Fz::CO1; idx += 256) {
       const int m = idx / Fz::CO1, n = idx - m * Fz::CO1;
       const float s = ((red[idx] + red[P + idx]) + red[2 * P + idx]) + red[3 * P + idx];
-      a1[m * Fz::A1S + n] = act_fwd(s + b1[n], act, alpha);
+      const float y = act_fwd(s + b1[n], act, alpha);
+      a1[m * Fz::A1S + n] = y;
+      if (act1 && (m < 2 * Fz::OW1 || i == Fz::ROWS2 - 1))  // conv1 rows 2i, 2i+1 (+ 18, 19)
+        act1[(((size_t)e * Fz::OW1 + 2 * i) * Fz::OW1 + m) * Fz::CO1 + n] = y;
     }
   }
   __syncthreads();
@@ -157,7 +164,9 @@ __device__ __forceinline__ int nips_trunk_block(const uint8_t *__restrict__ obs,
     for (int idx = threadIdx.x; idx < Fz::FEAT; idx += 256) {
       const int n = idx & (Fz::CO2 - 1);
       const float s = ((red[idx] + red[P + idx]) + red[2 * P + idx]) + red[3 * P + idx];
-      a2[idx] = act_fwd(s + b2[n], act, alpha);
+      const float y = act_fwd(s + b2[n], act, alpha);
+      a2[idx] = y;
+      if (act2) act2[((size_t)e * Fz::ROWS2 + i) * Fz::FEAT + idx] = y;
     }
   }
   __syncthreads();
@@ -187,9 +196,10 @@ __global__ __launch_bounds__(256) void nips_fused_trunk_kernel(const uint8_t *__
                                                                const float *__restrict__ W1,
                                                                const float *__restrict__ W2,
                                                                const float *__restrict__ Wfc, int act,
-                                                               float alpha, float *__restrict__ slabs) {
+                                                               float alpha, float *__restrict__ slabs,
+                                                               float *__restrict__ act1, float *__restrict__ act2) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  (void)nips_trunk_block<C>(obs, B, W1, W2, Wfc, act, alpha, slabs, smem);
+  (void)nips_trunk_block<C>(obs, B, W1, W2, Wfc, act, alpha, slabs, smem, act1, act2);
 }
 
 }  // namespace mt

@@ -151,6 +151,19 @@ class DeviceNetwork(object):
                  _stream()), 'mt_forward_infer' if infer else 'mt_forward')
         return v, pi, rep
 
+    def forward_rows(self, obs, batch, train_ws, train_rows, row0, out, ws_key=None):
+        """mt_forward_rows: inference forward of `batch` rows that also leaves their activations in
+        rows [row0, row0 + batch) of train_ws (a workspace of train_rows rows), so the update's
+        loss_backward on train_rows needs no forward. out = (v, pi, rep)."""
+        B = int(batch)
+        assert obs.dtype == torch.uint8 and obs.is_cuda and obs.is_contiguous()
+        ws = self.workspace(B, ws_key)
+        v, pi, rep = out
+        check(_lib.hip().mt_forward_rows(self._h, _ptr(self.params), _ptr(obs), B, _ptr(ws), ws.numel(),
+                                         _ptr(train_ws), train_ws.numel(), int(train_rows), int(row0), _ptr(v),
+                                         _ptr(pi), _ptr(rep), _stream()), 'mt_forward_rows')
+        return v, pi, rep
+
     def forward_trunk(self, obs, batch, ws_key=None):
         """mt_forward_trunk: the trunk half of the inference forward only (roofline timing)."""
         ws = self.workspace(batch, ws_key)

@@ -72,8 +72,6 @@ class PAACLearner(ActorLearner):
             self.states = self.slots[4:]
             self.nz_h = torch.zeros(T + 1, E, dtype=torch.int32, pin_memory=True)
             self.nz_d = torch.zeros(T + 1, E, dtype=torch.int32, device=dev)
-            self.pi_all = torch.zeros(T + 1, E, self.num_actions, dtype=torch.float32, device=dev)
-            self.rep_all = torch.zeros(T + 1, E, self.total_repetitions, dtype=torch.float32, device=dev)
         else:
             self.states = torch.zeros(T + 1, E, 84, 84, C, dtype=torch.uint8, device=dev)
         self.values = torch.zeros(T, E, dtype=torch.float32, device=dev)
@@ -88,6 +86,11 @@ class PAACLearner(ActorLearner):
         self.adv = torch.zeros(T, E, dtype=torch.float32, device=dev)
         self.pi_roll = torch.zeros(E, self.num_actions, dtype=torch.float32, device=dev)
         self.rep_roll = torch.zeros(E, self.total_repetitions, dtype=torch.float32, device=dev)
+        # per-step policy outputs: the train step reuses the rollout's forward (mt_forward_rows /
+        # the LSTM frame store), the parameters being unchanged between a rollout and its update
+        self.pi_all = torch.zeros(T + 1, E, self.num_actions, dtype=torch.float32, device=dev)
+        self.rep_all = torch.zeros(T + 1, E, self.total_repetitions, dtype=torch.float32, device=dev)
+        self.train_ws = None if self.lstm_bool else self.network.workspace(T * E, 'train')
         self.v_boot = torch.zeros(E, dtype=torch.float32, device=dev)
         self.loss_terms = torch.zeros(T * E, 4, dtype=torch.float32, device=dev)
         self.counters = torch.zeros(E, dtype=torch.int64, device=dev)
@@ -180,10 +183,12 @@ class PAACLearner(ActorLearner):
             flags |= _lib.MT_ROLLOUT_PIPELINED
             self.sync_h = torch.zeros(2, dtype=torch.int32, pin_memory=True)
         self._bufs = _lib.mt_rollout_buffers(
-            p(self.states), p(self.values), p(self.idx), p(self.pi_roll), p(self.rep_roll), p(ws), ws.numel(),
+            p(self.states), p(self.values), p(self.idx), p(self.pi_all), p(self.rep_all), p(ws), ws.numel(),
             p(self.counters), p(self.raw_d), src_rows, p(self.pair_d), p(self.pair_h), p(self.meta_d),
             p(rows), p(self.col_lut), p(self.idx_h), p(staging), p(r.push_meta), p(r.reward),
-            p(r.over), p(self.rm_h), p(frames), p(self.sync_h), p(self.ready_h), flags)
+            p(r.over), p(self.rm_h), p(frames), p(self.sync_h), p(self.train_ws),
+            0 if self.train_ws is None else self.train_ws.numel(),
+            p(self.ready_h), flags)
         h = C.c_void_p()
         _lib.check(_lib.hip().mt_rollout_create(net._h, self.emulator_counts, self.max_local_steps, r._h,
                                                 self.book.handle, C.byref(self._bufs),
@@ -238,8 +243,8 @@ class PAACLearner(ActorLearner):
         if self.lstm_bool:
             v, pi, rep = self._lstm_forward(t, self.values[t])
         else:
-            v, pi, rep = net.forward(self.states[t], E, out=(self.values[t], self.pi_roll, self.rep_roll),
-                                     ws_key='rollout', infer=True)
+            v, pi, rep = net.forward_rows(self.states[t], E, self.train_ws, self.max_local_steps * E, t * E,
+                                          out=(self.values[t], self.pi_all[t], self.rep_all[t]), ws_key='rollout')
         if end is not None:
             end.record()
         if self.sampling == 'device':
@@ -319,10 +324,12 @@ class PAACLearner(ActorLearner):
                                      self.values, self.idx[0].view(N), self.idx[1].view(N), self.y.view(N),
                                      self.adv.view(N), loss_terms=self.loss_terms)
         else:
+            # the rollout's forwards already left every row's activations in the train workspace
+            # (mt_forward_rows, row t*E + e as paac.py:236): the train step is the backward only
             obs = self.states[:T].reshape(N, 84, 84, self.C)
-            v, pi, rep = net.forward(obs, N, ws_key='train')
-            net.loss_backward(obs, N, v, pi, rep, self.idx[0].view(N), self.idx[1].view(N), self.y.view(N),
-                              self.adv.view(N), loss_terms=self.loss_terms, ws_key='train')
+            net.loss_backward(obs, N, self.values.view(N), self.pi_all[:T].reshape(N, -1),
+                              self.rep_all[:T].reshape(N, -1), self.idx[0].view(N), self.idx[1].view(N),
+                              self.y.view(N), self.adv.view(N), loss_terms=self.loss_terms, ws_key='train')
         if end is not None:
             end.record()
         inv = 1.0

@@ -99,6 +99,45 @@ def test_loss_backward_parity(arch, depth, A, R, B):
     assert not flat[mask].any()
 
 
+@pytest.mark.parametrize('arch,depth,A,R', [('NIPS', 1, 6, 1), ('NIPS', 3, 4, 11), ('NATURE', 1, 4, 11),
+                                            ('PWYX', 1, 4, 11)])
+@pytest.mark.parametrize('E,T', [(7, 3), (32, 2)])
+def test_forward_rows_then_backward_only(arch, depth, A, R, E, T):
+    """mt_forward_rows of T batches of E rows into one train workspace (the rollout), then
+    mt_loss_backward on the T*E rows with NO forward (the update) == the oracle's gradients of
+    the flattened batch; the per-step outputs == the oracle forward (NIPS: the fused trunk also
+    writes its conv activations)."""
+    net = _net(arch, depth, A, R, seed=40 + E)
+    rs = np.random.RandomState(E * 10 + T)
+    N = T * E
+    obs = rs.randint(0, 256, size=(T, E, 84, 84, 4 * depth)).astype(np.uint8)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    obs_d = d(obs)
+    tws = net.workspace(N, 'train_rows')
+    v = torch.zeros(T, E, device='cuda')
+    pi = torch.zeros(T, E, A, device='cuda')
+    rep = torch.zeros(T, E, R, device='cuda')
+    for t in range(T):
+        net.forward_rows(obs_d[t], E, tws, N, t * E, out=(v[t], pi[t], rep[t]), ws_key='rows')
+    a_idx = rs.randint(0, A, size=N).astype(np.int32)
+    r_idx = rs.randint(0, R, size=N).astype(np.int32)
+    y = rs.randn(N).astype(np.float32)
+    adv = rs.randn(N).astype(np.float32)
+    flat = obs_d.view(N, 84, 84, 4 * depth)
+    net.loss_backward(flat, N, v.view(N), pi.view(N, A), rep.view(N, R), d(a_idx), d(r_idx), d(y), d(adv),
+                      ws_key='train_rows')
+    torch.cuda.synchronize()
+    spec = nets.arch_spec(arch, depth, A, R)
+    P = net.get_variables()
+    obs_n = obs.reshape(N, 84, 84, 4 * depth)
+    v0, pi0, rep0, _ = nets.forward(spec, P, obs_n)
+    np.testing.assert_allclose(v.cpu().numpy().reshape(-1), v0, rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(pi.cpu().numpy().reshape(N, A), pi0, rtol=2e-5, atol=1e-6)
+    _, G, _ = nets.loss_and_grads(spec, P, obs_n, a_idx, r_idx, y, adv, 0.02)
+    import parity_util
+    parity_util.check_grads(spec, net.get_variables('grad'), G, parity_util.near_tie_layers(spec, P, obs_n))
+
+
 def test_leaky_relu_backward():
     net = _net('NIPS', 1, 6, 3, seed=3, act='leaky_relu')
     rs = np.random.RandomState(3)

@@ -41,23 +41,8 @@ def _rel(a, b):
 
 
 def _near_tie_layers(spec, P, obs, act):
-    """Names of pooled convs at or below a max-pool window with a near-tie (< 1e-5 relative)."""
-    _, _, _, cache = nets.forward(spec, P, obs, act=act, alpha=0.1)
-    hit = []
-    for L in cache['layers']:
-        if not L['pool']:
-            continue
-        y = L['y']
-        B, H, W, C = y.shape
-        w = y[:, :H // 2 * 2, :W // 2 * 2].reshape(B, H // 2, 2, W // 2, 2, C).transpose(0, 1, 3, 5, 2, 4)
-        s = np.sort(w.reshape(-1, 4), axis=1)
-        gap = (s[:, 3] - s[:, 2]) / np.maximum(np.abs(s[:, 3]), 1e-30)
-        if ((gap > 0) & (gap < 1e-5)).any():
-            hit.append(L['name'])
-    if not hit:
-        return set()
-    last = max(int(n[4:]) for n in hit)
-    return {'Network/conv%d/conv%d_%s' % (i, i, k) for i in range(1, last + 1) for k in ('weights', 'biases')}
+    import parity_util
+    return parity_util.near_tie_layers(spec, P, obs, act)
 
 
 def _windows(rs, B, depth, zero_frac=0.3):
