@@ -20,6 +20,7 @@
 // indices of the screens its pushes produced, and the GPU reads those screens where the
 // emulators left them (a pinned, device-mapped bank).
 #include <tmmintrin.h>
+#include <xmmintrin.h>
 
 #include <algorithm>
 #include <climits>
@@ -75,50 +76,54 @@ struct mh_runner {
   bool resized = false;  // stage the final 84x84 frame of each push (pool + nearest resize)
   int depth = 1;
   std::vector<int32_t> cols;             // resize column LUT (84)
-  alignas(16) uint8_t shuf[6][2][16];    // gray resize: per 16-column chunk, pshufb masks (lo, hi)
-  int chunk_base[6];                     // first source column of each chunk
+  // resize column gather, per 16-byte output chunk c of a row (84*depth bytes): the source bytes
+  // lie in [chunk_base[c], chunk_base[c] + 48); shuf[c][v] picks them out of source vector v
+  static constexpr int kMaxChunks = 16, kSrcVecs = 3;
+  alignas(16) uint8_t shuf[kMaxChunks][kSrcVecs][16];
+  int chunk_base[kMaxChunks];
+  int nchunks = 0;
 
   // FramePool max + nearest resize of one push into its 84x84xdepth staging frame
-  // (atari_emulator.py:79-88 + the imresize of :113-124): rows[q] / cols[x] are the LUTs.
+  // (atari_emulator.py:79-88 + the imresize of :113-124): rows[q] / cols[x] are the LUTs. Per
+  // output row: SSE max of the two source rows into a buffer, then each 16-byte output chunk is
+  // OR-ed from pshufb of up to 3 source vectors (gray and RGB alike); the next row's source lines
+  // are prefetched while this one is gathered.
   void resize_push(uint8_t *d, const uint8_t *s0, const uint8_t *s1) const {
-    if (depth == 1) {
-      alignas(16) uint8_t m[192];
-      _mm_store_si128(reinterpret_cast<__m128i *>(m + 160), _mm_setzero_si128());
-      _mm_store_si128(reinterpret_cast<__m128i *>(m + 176), _mm_setzero_si128());
-      for (int q = 0; q < 84; ++q) {
-        const uint8_t *a = s0 + (size_t)rows[q] * row_bytes, *b = s1 + (size_t)rows[q] * row_bytes;
-        for (int x = 0; x < 160; x += 16)
-          _mm_store_si128(reinterpret_cast<__m128i *>(m + x),
-                          _mm_max_epu8(_mm_loadu_si128(reinterpret_cast<const __m128i *>(a + x)),
-                                       _mm_loadu_si128(reinterpret_cast<const __m128i *>(b + x))));
-        uint8_t *o = d + (size_t)q * 84;
-        for (int c = 0; c < 6; ++c) {
-          const __m128i lo = _mm_loadu_si128(reinterpret_cast<const __m128i *>(m + chunk_base[c]));
-          const __m128i hi = _mm_loadu_si128(reinterpret_cast<const __m128i *>(m + chunk_base[c] + 16));
-          const __m128i v =
-              _mm_or_si128(_mm_shuffle_epi8(lo, _mm_load_si128(reinterpret_cast<const __m128i *>(shuf[c][0]))),
-                           _mm_shuffle_epi8(hi, _mm_load_si128(reinterpret_cast<const __m128i *>(shuf[c][1]))));
-          if (c < 5) {
-            _mm_storeu_si128(reinterpret_cast<__m128i *>(o + 16 * c), v);
-          } else {
-            alignas(16) uint8_t t[16];
-            _mm_store_si128(reinterpret_cast<__m128i *>(t), v);
-            std::memcpy(o + 80, t, 4);
-          }
+    const int rb = (int)row_bytes, ob = 84 * depth;
+    alignas(16) uint8_t m[480 + 64];
+    for (int x = rb; x < rb + 64; x += 16) _mm_store_si128(reinterpret_cast<__m128i *>(m + x), _mm_setzero_si128());
+    for (int q = 0; q < 84; ++q) {
+      const uint8_t *a = s0 + (size_t)rows[q] * row_bytes, *b = s1 + (size_t)rows[q] * row_bytes;
+      if (q + 1 < 84) {
+        const uint8_t *na = s0 + (size_t)rows[q + 1] * row_bytes, *nb = s1 + (size_t)rows[q + 1] * row_bytes;
+        for (int x = 0; x < rb; x += 64) {
+          _mm_prefetch(reinterpret_cast<const char *>(na + x), _MM_HINT_T0);
+          _mm_prefetch(reinterpret_cast<const char *>(nb + x), _MM_HINT_T0);
         }
       }
-    } else {
-      for (int q = 0; q < 84; ++q) {
-        const uint8_t *a = s0 + (size_t)rows[q] * row_bytes, *b = s1 + (size_t)rows[q] * row_bytes;
-        uint8_t *o = d + (size_t)q * 84 * depth;
-        for (int x = 0; x < 84; ++x)
-          for (int ch = 0; ch < depth; ++ch) {
-            const size_t k = (size_t)cols[x] * depth + ch;
-            o[x * depth + ch] = std::max(a[k], b[k]);
-          }
+      for (int x = 0; x < rb; x += 16)
+        _mm_store_si128(reinterpret_cast<__m128i *>(m + x),
+                        _mm_max_epu8(_mm_loadu_si128(reinterpret_cast<const __m128i *>(a + x)),
+                                     _mm_loadu_si128(reinterpret_cast<const __m128i *>(b + x))));
+      uint8_t *o = d + (size_t)q * ob;
+      for (int c = 0; c < nchunks; ++c) {
+        const uint8_t *src = m + chunk_base[c];
+        __m128i v = _mm_setzero_si128();
+#pragma GCC unroll 3
+        for (int k = 0; k < kSrcVecs; ++k)
+          v = _mm_or_si128(v, _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 16 * k)),
+                                               _mm_load_si128(reinterpret_cast<const __m128i *>(shuf[c][k]))));
+        if (16 * c + 16 <= ob) {
+          _mm_storeu_si128(reinterpret_cast<__m128i *>(o + 16 * c), v);
+        } else {
+          alignas(16) uint8_t t[16];
+          _mm_store_si128(reinterpret_cast<__m128i *>(t), v);
+          std::memcpy(o + 16 * c, t, ob - 16 * c);
+        }
       }
     }
   }
+
   int phase = 0;  // 0 = reset, 1 = step A (+ B when fixed), 2 = copy B
   const int32_t *a_idx = nullptr, *r_idx = nullptr;
   uint8_t *staging = nullptr;
@@ -333,7 +338,7 @@ extern "C" int mh_runner_set_col_lut(mh_runner *r, const int32_t *col_lut, int n
     set_error("null argument");
     return 1;
   }
-  if (!r->resized || n_cols != 84 || r->row_bytes % 160 != 0) {
+  if (!r->resized || n_cols != 84 || r->row_bytes % 160 != 0 || (r->depth != 1 && r->depth != 3)) {
     set_error("col LUT needs a resized-staging runner and 84 columns");
     return 1;
   }
@@ -343,18 +348,25 @@ extern "C" int mh_runner_set_col_lut(mh_runner *r, const int32_t *col_lut, int n
       return 1;
     }
   r->cols.assign(col_lut, col_lut + 84);
-  for (int c = 0; c < 6; ++c) {
-    const int base = col_lut[16 * c];
+  const int depth = r->depth, ob = 84 * depth;
+  r->nchunks = (ob + 15) / 16;
+  if (r->nchunks > mh_runner::kMaxChunks || (int)r->row_bytes + 64 > 480 + 64) {
+    set_error("resize supports depth 1 or 3");
+    return 1;
+  }
+  for (int c = 0; c < r->nchunks; ++c) {
+    const int b0 = 16 * c;
+    const int base = col_lut[b0 / depth] * depth + b0 % depth;  // source byte of the chunk's first byte
     r->chunk_base[c] = base;
     for (int k = 0; k < 16; ++k) {
-      const int x = 16 * c + k;
-      const int off = x < 84 ? col_lut[x] - base : -1;
-      if (off >= 32) {
-        set_error("resize columns %d..%d span more than 32 source bytes", 16 * c, x);
+      const int ob_k = b0 + k;
+      const int off = ob_k < ob ? col_lut[ob_k / depth] * depth + ob_k % depth - base : -1;
+      if (off >= 16 * mh_runner::kSrcVecs) {
+        set_error("resize chunk %d spans more than %d source bytes", c, 16 * mh_runner::kSrcVecs);
         return 1;
       }
-      r->shuf[c][0][k] = (off >= 0 && off < 16) ? (uint8_t)off : 0x80;
-      r->shuf[c][1][k] = off >= 16 ? (uint8_t)(off - 16) : 0x80;
+      for (int v = 0; v < mh_runner::kSrcVecs; ++v)
+        r->shuf[c][v][k] = (off >= 16 * v && off < 16 * v + 16) ? (uint8_t)(off - 16 * v) : 0x80;
     }
   }
   return 0;
