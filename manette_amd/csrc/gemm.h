@@ -507,6 +507,78 @@ struct LdConvBwdB {
   }
 };
 
+// Stride-phase decomposition of the backward-data product of a VALID stride-S conv with K % S == 0
+// and H, W % S == 0: input pixel (iy, ix) only receives taps ky = py + S*a, kx = px + S*b of its
+// phase (py, px) = (iy % S, ix % S), so the dense gather above multiplies (S*S - 1)/(S*S) zeros.
+// Rows are regrouped by phase — row m' = phase * MP + l, l = (b, qy, qx) with iy = S*qy + py —
+// and K shrinks to (KH/S)(KW/S)*COUT. MP (rows per phase, padded to the tile height) keeps every
+// workgroup inside one phase, which the B loader reads from blockIdx.x.
+template <class G>
+struct PhaseGeom {
+  static constexpr bool OK = G::S > 1 && !G::SAME && G::KH % G::S == 0 && G::KW % G::S == 0 &&
+                             G::H % G::S == 0 && G::W % G::S == 0;
+  static constexpr int HQ = G::H / G::S, WQ = G::W / G::S, KA = G::KH / G::S, KB = G::KW / G::S;
+  static constexpr int KP = KA * KB * G::COUT;  // GEMM-K per phase
+};
+
+template <class G>
+struct LdConvBwdAPhase {
+  static constexpr bool KMAJOR = true;
+  using P = PhaseGeom<G>;
+  const float *dY;  // [B][OH][OW][COUT]
+  int mp, B;        // rows per phase (padded), batch
+  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
+    return row0 + rows <= nrows && k0 + bk <= ke;
+  }
+  __device__ __forceinline__ f32x4 at(int m, int k) const {
+    const int ph = m / mp, l = m - ph * mp;
+    const int py = ph / G::S, px = ph - py * G::S;
+    const int b = l / (P::HQ * P::WQ);
+    const int rem = l - b * (P::HQ * P::WQ);
+    const int qy = rem / P::WQ, qx = rem - qy * P::WQ;
+    const int a = k / (P::KB * G::COUT);
+    const int r2 = k - a * (P::KB * G::COUT);
+    const int bb = r2 / G::COUT, co = r2 - bb * G::COUT;
+    const int oy = qy - a, ox = qx - bb;  // (iy - ky) / S with ky = py + S*a
+    const bool ok = b < B && oy >= 0 && ox >= 0 && oy < G::OH && ox < G::OW;
+    (void)py;
+    (void)px;
+    const int oyc = min(max(oy, 0), G::OH - 1), oxc = min(max(ox, 0), G::OW - 1), bc = min(b, B - 1);
+    const f32x4 v = *reinterpret_cast<const f32x4 *>(dY + (((size_t)bc * G::OH + oyc) * G::OW + oxc) * G::COUT + co);
+    return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __device__ __forceinline__ f32x4 fetch_fast(int m, int k) const { return at(m, k); }
+  __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
+    const int m = row0 + rr, k = k0 + kk;
+    return (m < nrows && k < ke) ? at(m, k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+};
+
+template <class G>
+struct LdConvBwdBPhase {
+  static constexpr bool KMAJOR = true;
+  using P = PhaseGeom<G>;
+  const float *Wt;  // HWIO
+  int blocks_per_phase;
+  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
+    return row0 + rows <= nrows && k0 + bk <= ke;
+  }
+  __device__ __forceinline__ f32x4 at(int ci, int k) const {
+    const int ph = (int)blockIdx.x / blocks_per_phase;
+    const int py = ph / G::S, px = ph - py * G::S;
+    const int a = k / (P::KB * G::COUT);
+    const int r2 = k - a * (P::KB * G::COUT);
+    const int bb = r2 / G::COUT, co = r2 - bb * G::COUT;
+    const int ky = py + G::S * a, kx = px + G::S * bb;
+    return *reinterpret_cast<const f32x4 *>(Wt + (((size_t)(ky * G::KW + kx) * G::CIN + ci) * G::COUT + co));
+  }
+  __device__ __forceinline__ f32x4 fetch_fast(int ci, int k) const { return at(ci, k); }
+  __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
+    const int ci = row0 + rr, k = k0 + kk;
+    return (ci < nrows && k < ke) ? at(ci, k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+};
+
 // ------------------------------------------------------------------------------------------
 // Epilogues: ep(m, n, z, value)
 // ------------------------------------------------------------------------------------------
@@ -545,6 +617,26 @@ struct EpStore {
   int ld;
   __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
     P[(size_t)m * ld + n] = v;
+  }
+};
+
+// Phase-grouped rows of LdConvBwdAPhase back to pixels, then dX = v * act'(Yact).
+template <class G>
+struct EpMaskedPhase {
+  using P = PhaseGeom<G>;
+  float *dX;
+  const float *Yact;
+  int mp, B, act;
+  float alpha;
+  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
+    const int ph = m / mp, l = m - ph * mp;
+    const int py = ph / G::S, px = ph - py * G::S;
+    const int b = l / (P::HQ * P::WQ);
+    if (b >= B) return;  // phase padding rows
+    const int rem = l - b * (P::HQ * P::WQ);
+    const int qy = rem / P::WQ, qx = rem - qy * P::WQ;
+    const size_t i = (((size_t)b * G::H + G::S * qy + py) * G::W + G::S * qx + px) * G::CIN + n;
+    dX[i] = v * act_bwd(Yact[i], act, alpha);
   }
 };
 

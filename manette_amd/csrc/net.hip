@@ -617,6 +617,14 @@ template <class G>
 static int conv_dgrad(const float *dY, const float *Wt, const float *Xact, float *dX, int B,
                       int act, float alpha, hipStream_t s) {
   using T = TileConvDgrad<G>;
+  if constexpr (PhaseGeom<G>::OK) {  // stride phases: K / (S*S), no multiplications by holes
+    constexpr int S2 = G::S * G::S;
+    const int mp = cdiv(B * PhaseGeom<G>::HQ * PhaseGeom<G>::WQ, T::BM) * T::BM;
+    LdConvBwdAPhase<G> la{dY, mp, B};
+    LdConvBwdBPhase<G> lb{Wt, mp / T::BM};
+    EpMaskedPhase<G> ep{dX, Xact, mp, B, act, alpha};
+    return launch_gemm<T>(la, lb, ep, S2 * mp, G::CIN, PhaseGeom<G>::KP, 1, s);
+  }
   LdConvBwdA<G> la{dY};
   LdConvBwdB<G> lb{Wt};
   EpMasked ep{dX, Xact, G::CIN, act, alpha};
