@@ -157,6 +157,8 @@ int mt_sample(const float *pi, const float *rep, int batch, int num_actions, int
  * v_boot: [E] (V(s_T)). Writes y, adv: [T][E] fp32 (row t*E+e). Arithmetic follows the
  * reference's numpy dtypes exactly (gamma is the python float: the first product gamma*V_T in
  * fp32, the rest fp64, fp32 output). */
+/* rewards / masks may be device addresses of pinned host memory (the learner's [2][T][E]
+ * bookkeeping output, read in place). */
 int mt_returns(const float *rewards, const float *masks, const float *values, const float *v_boot,
                double gamma, int T, int E, float *y, float *adv, mt_stream_t stream);
 
@@ -179,8 +181,10 @@ int mt_loss_backward(const mt_net *net, const float *params, const uint8_t *obs,
  * mt_clip_rmsprop: g' = inv_scale*g; norm = sqrt(sum partials);
  *   clip_type GLOBAL: g' *= clip * min(1/norm, 1/clip);
  *   ms += (g'^2 - ms)*(1 - decay); mom = momentum*mom + g'*lr/sqrt(ms + eps); w -= mom.
- * lr is read from device memory (*lr_dev) so a captured graph picks up the schedule
- * (actor_learner.py:132-136). norm_out (device, may be NULL) receives the pre-clip norm.
+ * lr is read by the kernel from *lr_dev (device memory, or — as the learner does — the device
+ * address of pinned host memory the host writes the schedule into, actor_learner.py:132-136), so
+ * no copy is needed and a captured graph picks up the schedule. norm_out (device, may be NULL)
+ * receives the pre-clip norm.
  * inv_scale folds the 1/world of a data-parallel all-reduce (sum) into the update. */
 int mt_grad_sumsq(const float *g, size_t n, float inv_scale, float *partials, mt_stream_t stream);
 int mt_clip_rmsprop(float *w, float *ms, float *mom, const float *g, size_t n,
@@ -291,6 +295,9 @@ typedef struct mt_rollout_buffers {
                                   writes rows [t*E, (t+1)*E) (mt_forward_rows) and pi / rep are
                                   [T][E][.] per-step outputs; NULL: pi / rep are [E][.] */
   size_t train_ws_bytes;
+  float *v_boot;               /* optional [E] (MT_ROLLOUT_PIPELINED): the last step's chain also runs the
+                                  bootstrap forward of slot T (paac.py:219-224) into it, in the shadow
+                                  of the host's last emulator step */
   uint32_t *ready_host;        /* [E] zero-copy modes: the heads kernel stores a step sequence number per
                                   env after writing its pair; the host polls these instead of an event
                                   (NULL: hipEventQuery) */

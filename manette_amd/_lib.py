@@ -27,7 +27,7 @@ class mt_rollout_buffers(C.Structure):
                [(n, C.c_void_p) for n in ('pair', 'pair_host', 'meta', 'row_lut', 'col_lut', 'idx_host',
                                           'staging_host', 'meta_host', 'reward_host', 'over_host',
                                           'rm_host', 'frames_host', 'sync_host', 'train_ws')] + \
-               [('train_ws_bytes', C.c_size_t), ('ready_host', C.c_void_p), ('flags', C.c_int32)]
+               [('train_ws_bytes', C.c_size_t), ('v_boot', C.c_void_p), ('ready_host', C.c_void_p), ('flags', C.c_int32)]
 
 
 MT_ROLLOUT_ZERO_COPY = 1

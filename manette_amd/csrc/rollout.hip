@@ -224,6 +224,11 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
     if (t + 1 < T) {
       MT_TRY_(enqueue_forward(ro, params, t + 1, s));
       ro->armed = t + 1;
+    } else if (b.v_boot) {  // bootstrap V(s_T) (paac.py:219-224), no draw, no train rows
+      const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
+      const size_t po = b.train_ws ? (size_t)T * E : 0;
+      MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)T * slot, E, b.ws, b.ws_bytes, b.v_boot,
+                             b.pi + po * ro->A, b.rep + po * ro->R, nullptr, true, s));
     }
   }
   // 3. wait for the indices of step t (spin: a blocking wait sleeps past the chain and pays the

@@ -74,9 +74,10 @@ class DeviceNetwork(object):
         self.ms = torch.ones_like(self.params)
         self.mom = torch.zeros_like(self.params)
         self.partials = torch.zeros(_lib.MT_NORM_PARTIALS, dtype=torch.float32, device=dev)
-        self.lr_dev = torch.zeros(1, dtype=torch.float32, device=dev)
         self.norm_dev = torch.zeros(1, dtype=torch.float32, device=dev)
+        # the LR lives in pinned, device-mapped host memory: mt_clip_rmsprop reads it in place
         self._lr_host = torch.zeros(1, dtype=torch.float32).pin_memory()
+        self._lr_dev_addr = host_device_pointer(self._lr_host)
         self._ws = {}
         self._out = {}
 
@@ -219,9 +220,9 @@ class DeviceNetwork(object):
         return self.grad
 
     def set_lr(self, lr):
-        """LR lives in device memory so captured graphs pick up the schedule."""
+        """The LR of the next apply_gradients: written into pinned host memory that the RMSProp
+        kernel reads in place (no copy; a captured graph also picks up the schedule)."""
         self._lr_host[0] = float(lr)
-        self.lr_dev.copy_(self._lr_host, non_blocking=True)
 
     def apply_gradients(self, inv_scale=1.0):
         """clip_by_global_norm + ApplyRMSProp on self.grad (actor_learner.py:47-74).
@@ -231,7 +232,7 @@ class DeviceNetwork(object):
         check(lib.mt_grad_sumsq(_ptr(self.grad), self.nparams, float(inv_scale), _ptr(self.partials), s),
               'mt_grad_sumsq')
         check(lib.mt_clip_rmsprop(_ptr(self.params), _ptr(self.ms), _ptr(self.mom), _ptr(self.grad),
-                                  self.nparams, _ptr(self.partials), _ptr(self.lr_dev), self.decay, 0.0,
+                                  self.nparams, _ptr(self.partials), C.c_void_p(self._lr_dev_addr), self.decay, 0.0,
                                   self.eps, self.clip_norm, self.clip_type, float(inv_scale),
                                   _ptr(self.norm_dev), s), 'mt_clip_rmsprop')
 
@@ -269,9 +270,11 @@ def memory_push(memory, whole_t, fresh, masks):
 
 
 def returns(rewards, masks, values, v_boot, gamma, y, adv):
-    """paac.py:219-231 on device."""
-    T, E = rewards.shape
-    check(_lib.hip().mt_returns(_ptr(rewards), _ptr(masks), _ptr(values), _ptr(v_boot), float(gamma),
+    """paac.py:219-231 on device. rewards / masks: [T][E] device tensors, or device addresses
+    (e.g. of pinned, device-mapped host memory the kernel reads in place)."""
+    T, E = values.shape
+    addr = lambda x: C.c_void_p(x) if isinstance(x, int) else _ptr(x)
+    check(_lib.hip().mt_returns(addr(rewards), addr(masks), _ptr(values), _ptr(v_boot), float(gamma),
                                 T, E, _ptr(y), _ptr(adv), _stream()), 'mt_returns')
 
 

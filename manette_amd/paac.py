@@ -79,9 +79,6 @@ class PAACLearner(ActorLearner):
         self.idx = torch.zeros(2, T, E, dtype=torch.int32, device=dev)
         self.a_idx = self.idx[0]
         self.r_idx = self.idx[1]
-        self.rm_d = torch.zeros(2, T, E, dtype=torch.float32, device=dev)  # rewards; masks
-        self.rewards_d = self.rm_d[0]
-        self.masks_d = self.rm_d[1]
         self.y = torch.zeros(T, E, dtype=torch.float32, device=dev)
         self.adv = torch.zeros(T, E, dtype=torch.float32, device=dev)
         self.pi_roll = torch.zeros(E, self.num_actions, dtype=torch.float32, device=dev)
@@ -96,6 +93,8 @@ class PAACLearner(ActorLearner):
         self.counters = torch.zeros(E, dtype=torch.int64, device=dev)
         pin = dict(pin_memory=True)
         self.rm_h = torch.zeros(2, T, E, dtype=torch.float32, **pin)
+        # the returns kernel reads the rollout's clipped rewards / masks in place (no H2D copy)
+        self.rm_h_dev = devnet.host_device_pointer(self.rm_h)
         self.rewards_h = self.rm_h[0]
         self.masks_h = self.rm_h[1]
         self.idx_h = torch.zeros(2, T, E, dtype=torch.int32, **pin)
@@ -108,6 +107,7 @@ class PAACLearner(ActorLearner):
         self.event = torch.cuda.Event()
         self.book = NativeBook(E, self.num_actions, self.tab_rep)
         self.native_step = None  # mt_rollout handle (native runner + device sampling)
+        self.boot_in_rollout = False
         self.runners = None
         self.profile = None      # name -> [(start_event, end_event)] when profiling (bench.py)
         self.sample_seed = (self.seed * 1000003 + self.rank * 7919 + 1) & 0xffffffffffff
@@ -188,12 +188,13 @@ class PAACLearner(ActorLearner):
             p(rows), p(self.col_lut), p(self.idx_h), p(staging), p(r.push_meta), p(r.reward),
             p(r.over), p(self.rm_h), p(frames), p(self.sync_h), p(self.train_ws),
             0 if self.train_ws is None else self.train_ws.numel(),
-            p(self.ready_h), flags)
+            p(self.v_boot if self.pipeline else None), p(self.ready_h), flags)
         h = C.c_void_p()
         _lib.check(_lib.hip().mt_rollout_create(net._h, self.emulator_counts, self.max_local_steps, r._h,
                                                 self.book.handle, C.byref(self._bufs),
                                                 C.c_uint64(self.sample_seed), C.byref(h)), 'mt_rollout_create')
         self.native_step = h
+        self.boot_in_rollout = self.pipeline  # the last step's chain runs the bootstrap forward
         self._gs = C.c_int64(0)
 
     def _upload_pushes(self, total, out, prev):
@@ -310,10 +311,10 @@ class PAACLearner(ActorLearner):
         N = E * T
         if self.lstm_bool:
             self._lstm_forward(T, self.v_boot)
-        else:
+        elif not (self.boot_in_rollout and self.native_step is not None):  # (else queued behind the last step)
             net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout', infer=True)
-        self.rm_d.copy_(self.rm_h, non_blocking=True)
-        devnet.returns(self.rewards_d, self.masks_d, self.values, self.v_boot, self.gamma, self.y, self.adv)
+        devnet.returns(self.rm_h_dev, self.rm_h_dev + 4 * T * E, self.values, self.v_boot, self.gamma, self.y,
+                       self.adv)
         lr = self.get_lr()
         net.set_lr(lr)
         end = self._mark('train_pass')
