@@ -235,7 +235,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    learner.profile = {}
     stats = None
     if learner.native_step is not None:
         import ctypes as C
@@ -260,8 +259,17 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    prof = {k: [s.elapsed_time(e) for (s, e) in v] for k, v in learner.profile.items()}
-    learner.profile = None
+    # the update's train pass (backward of the last rollout) alone: 20 launches back to back
+    # between one event pair, after the timed region (which runs the update as a hipGraph)
+    prof = {}
+    learner.train_backward()
+    s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_ev.record()
+    for _ in range(20):
+        learner.train_backward()
+    e_ev.record()
+    torch.cuda.synchronize()
+    prof['train_pass'] = [s_ev.elapsed_time(e_ev) / 20.0]
     # rollout-batch forward (E rows) and its trunk half alone (the roofline kernel: mt_forward_trunk,
     # one launch of the fused NIPS trunk), each timed with HIP events on the stream they are
     # launched on (torch's current stream, passed to every C-ABI call), back to back

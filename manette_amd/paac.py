@@ -111,6 +111,10 @@ class PAACLearner(ActorLearner):
         self.runners = None
         self.profile = None      # name -> [(start_event, end_event)] when profiling (bench.py)
         self.sample_seed = (self.seed * 1000003 + self.rank * 7919 + 1) & 0xffffffffffff
+        # replay the update as hipGraph(s) from the second update on (native pipelined step)
+        self.use_update_graph = bool(getattr(args, 'update_graph', True))
+        self._graphs = None
+        self._eager_updates = 0
 
     # ------------------------------------------------------------------------------------------
     def _start_runners(self):
@@ -304,46 +308,117 @@ class PAACLearner(ActorLearner):
 
     def update(self):
         """Bootstrap, n-step returns, fused loss backward, [all-reduce], clip + RMSProp
-        (paac.py:219-256)."""
-        net = self.network
+        (paac.py:219-256).
+
+        Native pipelined step (non-LSTM): the device work of an update is a fixed sequence over
+        fixed buffers (the LR is read from pinned host memory, the returns kernel reads the
+        rollout's rewards / masks in place), so from the second update on it is replayed as one
+        or two hipGraphs (mt_graph_*; split around the all_reduce when world > 1): one launch
+        instead of a dozen, and no host launch gaps between the backward's kernels."""
         self.book.drain()
+        lr = self.get_lr()
+        self.network.set_lr(lr)
+        if self._graph_ok():
+            if self._graphs is None and self._eager_updates >= 1:
+                self._capture_update()
+            if self._graphs is not None:
+                s = devnet._stream()
+                self._launch_graph(self._graphs[0], s)
+                if self.world > 1:
+                    torch.distributed.all_reduce(self.network.grad)
+                    self._launch_graph(self._graphs[1], s)
+                return lr
+        self._eager_updates += 1
+        self._update_backward()
+        if self.world > 1:
+            torch.distributed.all_reduce(self.network.grad)
+        self._update_apply()
+        return lr
+
+    def _graph_ok(self):
+        return (self.use_update_graph and self.profile is None and not self.lstm_bool
+                and self.native_step is not None and self.boot_in_rollout)
+
+    def _update_backward(self):
+        net = self.network
         E, T = self.emulator_counts, self.max_local_steps
-        N = E * T
         if self.lstm_bool:
             self._lstm_forward(T, self.v_boot)
         elif not (self.boot_in_rollout and self.native_step is not None):  # (else queued behind the last step)
             net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout', infer=True)
         devnet.returns(self.rm_h_dev, self.rm_h_dev + 4 * T * E, self.values, self.v_boot, self.gamma, self.y,
                        self.adv)
-        lr = self.get_lr()
-        net.set_lr(lr)
         end = self._mark('train_pass')
+        self.train_backward()
+        if end is not None:
+            end.record()
+
+    def train_backward(self):
+        """The train step of the last rollout (paac.py:233-256), backward only: its forward is the
+        rollout's (same parameters, same rows / windows). Idempotent (bench.py times it alone)."""
+        net = self.network
+        E, T = self.emulator_counts, self.max_local_steps
+        N = E * T
         if self.lstm_bool:
-            # the train step's forward is the rollout's (same parameters, same windows): only the
-            # backward runs, through each distinct frame once (paac.py:233-256)
+            # through each distinct frame once
             net.lstm_frames_backward(self.fstore, self.nz_d[:T], E, T, self.pi_all[:T], self.rep_all[:T],
                                      self.values, self.idx[0].view(N), self.idx[1].view(N), self.y.view(N),
                                      self.adv.view(N), loss_terms=self.loss_terms)
-        else:
-            # the rollout's forwards already left every row's activations in the train workspace
-            # (mt_forward_rows, row t*E + e as paac.py:236): the train step is the backward only
-            obs = self.states[:T].reshape(N, 84, 84, self.C)
-            net.loss_backward(obs, N, self.values.view(N), self.pi_all[:T].reshape(N, -1),
-                              self.rep_all[:T].reshape(N, -1), self.idx[0].view(N), self.idx[1].view(N),
-                              self.y.view(N), self.adv.view(N), loss_terms=self.loss_terms, ws_key='train')
-        if end is not None:
-            end.record()
-        inv = 1.0
-        if self.world > 1:
-            torch.distributed.all_reduce(net.grad)
-            inv = 1.0 / self.world
-        net.apply_gradients(inv)
+            return
+        # the rollout's forwards already left every row's activations in the train workspace
+        # (mt_forward_rows, row t*E + e as paac.py:236)
+        obs = self.states[:T].reshape(N, 84, 84, self.C)
+        self.network.loss_backward(obs, N, self.values.view(N), self.pi_all[:T].reshape(N, -1),
+                                   self.rep_all[:T].reshape(N, -1), self.idx[0].view(N), self.idx[1].view(N),
+                                   self.y.view(N), self.adv.view(N), loss_terms=self.loss_terms, ws_key='train')
+
+    def _update_apply(self):
+        T = self.max_local_steps
+        self.network.apply_gradients(1.0 / self.world if self.world > 1 else 1.0)
         if self.lstm_bool:  # the next rollout's slots 0..4 = s_{T-4} .. s_T; windows carry over
             self.slots[0:5].copy_(self.slots[T:T + 5].clone())
             self.nz_h.numpy()[0] = self.nz_h.numpy()[T]
         else:
             self.states[0].copy_(self.states[T])
-        return lr
+
+    def _capture_update(self):
+        """Record the update's device work on a side stream (nothing executes while capturing)."""
+        import ctypes as C
+        from . import _lib
+        lib = _lib.hip()
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        torch.cuda.synchronize()
+        parts = [self._update_backward, self._update_apply]
+        if self.world == 1:
+            parts = [lambda: (self._update_backward(), self._update_apply())]
+        graphs = []
+        with torch.cuda.stream(side):
+            sp = devnet._stream()
+            for fn in parts:
+                _lib.check(lib.mt_graph_begin(sp), 'mt_graph_begin')
+                try:
+                    fn()
+                finally:
+                    g = C.c_void_p()
+                    rc = lib.mt_graph_end(sp, C.byref(g))
+                _lib.check(rc, 'mt_graph_end')
+                graphs.append(g)
+        self._graphs = graphs
+        self._graph_stream = side  # keep the capture stream alive with the graphs
+
+    @staticmethod
+    def _launch_graph(g, s):
+        from . import _lib
+        _lib.check(_lib.hip().mt_graph_launch(g, s), 'mt_graph_launch')
+
+    def _destroy_graphs(self):
+        if getattr(self, '_graphs', None):
+            from . import _lib
+            for g in self._graphs:
+                _lib.hip().mt_graph_destroy(g)
+        self._graphs = None
 
     def loss_value(self):
         """5*(mean(-(adv*logp + beta*H)) + mean(0.25(y-v)^2)) of the last update (host sync)."""
@@ -393,6 +468,7 @@ class PAACLearner(ActorLearner):
     def cleanup(self):
         try:
             torch.cuda.synchronize()
+            self._destroy_graphs()
             super(PAACLearner, self).cleanup()
         finally:
             if self.native_step is not None:
