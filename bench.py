@@ -39,23 +39,28 @@ CONFIGS = {
 }
 MI355X_FP32_TFLOPS = 157.3   # dense fp32 (vector = MFMA), MI355X_MICROARCH.md
 MI355X_HBM_GBS = 8000.0      # HBM3E peak, MI355X_MICROARCH.md
-# the one kernel mt_forward_trunk launches (its rocprof name), per arch where it is a single kernel
-TRUNK_KERNEL = {'NIPS': 'nips_fused_trunk_kernel'}
+# the kernels one mt_forward_trunk call launches (rocprof names, template arguments for gray
+# frames), per arch where the trunk has dedicated kernels: NIPS conv (no stacking) + fc
+TRUNK_KERNELS = {'NIPS': ['nips_conv_kernel<4, false>', 'nips_fc_kernel<4>']}
 
 
-def load_pmc(config, kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
-    (profiles/pmc_<config>.json, written by tools/pmc.sh + tools/pmc_summary.py), or None."""
-    if not kernel:
+def load_pmc(config, kernels):
+    """HBM bytes per mt_forward_trunk call (the sum over its kernels of bytes per launch) from the
+    committed PMC summary of this workload (profiles/pmc_<config>.json, written by tools/pmc.sh +
+    tools/pmc_summary.py), or None when a kernel is missing from it."""
+    if not kernels:
         return None
     path = os.path.join(ROOT, 'profiles', 'pmc_%s.json' % config)
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
-    for k, v in d.items():
-        if k.split('<')[0].endswith(kernel):
-            return dict(hbm_bytes=v['hbm_bytes'], source='profiles/pmc_%s.json' % config)
-    return None
+    total = 0
+    for kern in kernels:
+        hit = [v for k, v in d.items() if k.replace('void ', '').endswith(kern)]
+        if not hit:
+            return None
+        total += hit[0]['hbm_bytes']
+    return dict(hbm_bytes=total, source='profiles/pmc_%s.json' % config)
 
 
 def conv_out(h, k, s):
@@ -324,7 +329,7 @@ def main():
         tk_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in trunk) + 4 * ec * out_floats
         tk_flops = ec * sum(l[1] for l in trunk)
         tk_gbs = tk_bytes / (tk_ms * 1e-3) / 1e9
-        pmc = load_pmc(a.config, TRUNK_KERNEL.get(cfg['arch']))
+        pmc = load_pmc(a.config, TRUNK_KERNELS.get(cfg['arch']) if not cfg['rgb'] else None)
         achieved = tp_flops / (tp_ms * 1e-3) / 1e12
         line = {
             'metric': 'env-steps/sec (ec x t_max frames per update)',
@@ -342,7 +347,7 @@ def main():
             'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step, %s staging%s' % (
                 a.config, ec, cfg['ew'], T, a.sampling, a.step_impl, a.staging, ', pipelined' if a.pipeline else ''), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
                 'global_emulators': ec * world, 'parallelism': 'dp%d' % world},
-            'roofline': {'bound': 'hbm', 'kernel': TRUNK_KERNEL.get(cfg['arch'], 'mt_forward_trunk (layered)'),
+            'roofline': {'bound': 'hbm', 'kernel': ' + '.join(TRUNK_KERNELS.get(cfg['arch'], ['mt_forward_trunk (layered)'])),
                          'achieved': round(tk_gbs, 1), 'peak': MI355X_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(tk_gbs / MI355X_HBM_GBS, 4),
                          'traffic': pmc['hbm_bytes'] if pmc else None,

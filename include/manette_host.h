@@ -72,6 +72,21 @@ int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx, uin
                    int32_t *push_offset, int32_t *push_count, float *reward, float *over,
                    int *total_pushes);
 
+/* mh_runner_step split in two: _begin hands the step to the worker threads and returns at once
+ * (the caller may enqueue GPU work meanwhile); _end waits for them and returns total_pushes.
+ * No other runner call may come in between. */
+int mh_runner_step_begin(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx, uint8_t *staging,
+                         int32_t *push_offset, int32_t *push_count, float *reward, float *over);
+int mh_runner_step_end(mh_runner *r, int *total_pushes);
+
+/* Per-env ready words (fixed + resized staging only; ready = NULL turns them off): during the
+ * following mh_runner_step calls, the worker that steps env e stages e's pushes and its push count
+ * and then stores ready[e] = (value << 3) | push_count[e] (release), so a consumer polling ready[e]
+ * (a GPU kernel reading pinned, device-mapped memory: mt_rollout_step's pull kernel) can take env
+ * e while the other envs are still being emulated. Call before every step with that step's value
+ * (compared modulo 2^29). */
+int mh_runner_set_ready(mh_runner *r, uint32_t *ready, uint32_t value);
+
 /* In-place frames: the same macro-step (and reset), but no screen is copied. Per env e,
  * push_count[e] in 1..4 and frame_idx[e*8 + 2j + f] (j < push_count[e], f = 0, 1) = index of the
  * f-th pooled screen of push j (oldest first) in the `screens` bank given to mh_runner_create,

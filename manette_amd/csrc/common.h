@@ -100,6 +100,10 @@ struct SampleArgs {
   // so a host polling pinned memory sees the pair without an event query (mt_rollout_step)
   uint32_t *ready = nullptr;
   uint32_t seq = 0;
+  // optional, replaces pair + ready: one 8-byte store per row into host-mapped memory,
+  // lo = (seq16 << 16) | a, hi = (seq16 << 16) | r (seq16 = seq & 0xffff): both halves carry the
+  // tag, so a host that sees the tag in both has the pair, with no fence on the device side
+  uint64_t *packed = nullptr;
 };
 
 }  // namespace mt
@@ -113,8 +117,20 @@ struct TrainRows {
   size_t ws_bytes;
   int rows, row0;
 };
-// forward (mt_forward) with the A3 draw fused into the heads kernel; smp and tr may be null.
+// A2 stacking source of the NIPS conv kernel (trunk_fused.h): new state = prev shifted by p
+// channels + the p newest final frames; push j of env e is the 84x84xD frame at
+// frames + (4e + j) * 7056 D (the runner's fixed staging slots, or their HBM copy made by
+// mt_rollout_step's pull kernel).
+struct StackSrc {
+  const uint8_t *prev;    // state slot t [B][84][84][C] (HBM)
+  const uint8_t *frames;  // device address of the pinned staging
+  const int32_t *count;   // device address of push_count [B] (pinned)
+  uint8_t *out;           // state slot t + 1 (the forward's input)
+};
+// forward (mt_forward) with the A3 draw fused into the heads kernel; smp, tr and st may be null.
+// st (NIPS inference only): the conv kernel first stacks the new state st->out (== obs) from
+// st->prev and the pushed frames (mt_preprocess_resized's op, fused into the forward).
 int forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                    size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp, bool infer,
-                   hipStream_t stream, const TrainRows *tr = nullptr);
+                   hipStream_t stream, const TrainRows *tr = nullptr, const StackSrc *st = nullptr);
 }  // namespace mt

@@ -410,6 +410,18 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   __shared__ float zs[64];
   const int F = hp.F, O = 1 + hp.A + hp.R;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the head weights of this wave's first two outputs (o = w, w + 4) and the row's draw counter
+  // do not depend on the slabs: requested before the slab loads so their latency overlaps
+  constexpr int PRE = 2, FMAX = 8;  // F <= 512
+  float wpre[PRE][FMAX];
+#pragma unroll
+  for (int k = 0; k < PRE; ++k)
+#pragma unroll
+    for (int j = 0; j < FMAX; ++j) {
+      const int o = w + 4 * k, f = lane + 64 * j;
+      wpre[k][j] = (o < O && f < F) ? head_w(hp, f, o) : 0.f;
+    }
+  const uint64_t cnt = smp.counters ? smp.counters[b] : 0;
   for (int f = threadIdx.x; f < F; f += 256) {
     const float *p = slabs + (size_t)b * F + f;
     const size_t zs_stride = (size_t)B * F;
@@ -428,13 +440,27 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
     H[(size_t)b * F + f] = h;
   }
   __syncthreads();
-  for (int o = w; o < O; o += 4) {
+  MT_PROBE_AT(2, b, 1);
+#pragma unroll
+  for (int k = 0; k < PRE; ++k) {
+    const int o = w + 4 * k;
+    if (o < O) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < FMAX; ++j)
+        if (lane + 64 * j < F) acc += hs[lane + 64 * j] * wpre[k][j];
+      acc = wave_sum(acc);
+      if (lane == 0) zs[o] = acc + head_w(hp, F, o);
+    }
+  }
+  for (int o = w + 4 * PRE; o < O; o += 4) {
     float acc = 0.f;
     for (int f = lane; f < F; f += 64) acc += hs[f] * head_w(hp, f, o);
     acc = wave_sum(acc);
     if (lane == 0) zs[o] = acc + head_w(hp, F, o);
   }
   __syncthreads();
+  MT_PROBE_AT(2, b, 2);
   if (w != 0) return;
   const float z = lane < O ? zs[lane] : 0.f;
   if (lane == 0) v[b] = z;
@@ -446,7 +472,7 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   const float pr = wave_softmax(zr, lane, hp.R);
   if (lane < hp.R) rep[(size_t)b * hp.R + lane] = pr;
   if (smp.counters) {
-    const uint64_t c = smp.counters[b];
+    const uint64_t c = cnt;
     double ua, ur;
     row_uniforms(smp.seed, b, c, &ua, &ur);
     const int a = wave_draw(pa, hp.A, ua), r = wave_draw(pr, hp.R, ur);
@@ -454,11 +480,15 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
       smp.counters[b] = c + 1;
       smp.a_idx[b] = a;
       smp.r_idx[b] = r;
-      if (smp.pair) {
+      if (smp.packed) {  // tagged pair, one 8-byte store, no fence (SampleArgs::packed)
+        const uint64_t tag = (uint64_t)(smp.seq & 0xffffu) << 16;
+        const uint64_t word = ((tag | (uint32_t)r) << 32) | tag | (uint32_t)a;
+        __hip_atomic_store(smp.packed + b, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else if (smp.pair) {
         smp.pair[b] = a;
         smp.pair[B + b] = r;
       }
-      if (smp.ready) {  // release: the pair stores are visible to the host before the flag
+      if (smp.ready && !smp.packed) {  // release: the pair stores are visible to the host before the flag
         __threadfence_system();
         __hip_atomic_store(smp.ready + b, smp.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
@@ -472,8 +502,17 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict_
                                                         float *__restrict__ H, float *__restrict__ v,
                                                         float *__restrict__ pi,
                                                         float *__restrict__ rep, SampleArgs smp) {
+  MT_PROBE_AT(2, blockIdx.x, 0);
   heads_row(blockIdx.x, slabs, S, B, fc_b, act, alpha, hp, temp, H, v, pi, rep, smp);
+  MT_PROBE_AT(2, blockIdx.x, 3);
 }
+
+#ifdef MT_PROBE
+extern "C" int mt_probe_read(unsigned long long *out, size_t n) {
+  MT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(mt_probe_buf), std::min(n, sizeof(mt_probe_buf) / 8) * 8));
+  return MT_OK;
+}
+#endif
 
 
 // dL/dlogit for one softmax head (policy_v_network.py:29-57, :59-74), one wave, lanes [0, n):
@@ -809,21 +848,22 @@ static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int
   return MT_OK;
 }
 
-// Inference forward (rollout steps, bootstrap): the fused trunk where the arch has one
-// (trunk_fused.h), whose 9 conv2-row slabs heads_fwd_kernel finishes; else the layered forward.
+// Inference forward (rollout steps, bootstrap): the NIPS trunk kernels where the arch has them
+// (trunk_fused.h: conv -> act2, fc -> 9 slabs), whose slabs heads_fwd_kernel finishes; else the
+// layered forward. st (NIPS only): stack the new state in the conv kernel (mt_rollout_step).
 template <class Ar>
 static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
                               float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s,
-                              const TrainRows *tr = nullptr) {
+                              const TrainRows *tr = nullptr, const StackSrc *st = nullptr) {
   if constexpr (Ar::FUSED_SLABS > 0) {
     constexpr int C = LayerG<Ar, 0>::CIN;
     using Fz = FusedNips<C>;
     const WsLayout L = ws_layout<Ar>(n, B);
     const ActRows A = act_rows<Ar>(n, ws, L, tr);
     const float *Wfc = P + n->off_fc;
-    hipLaunchKernelGGL(nips_fused_trunk_kernel<C>, dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, obs, B,
-                       P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation, n->cfg.alpha_leaky,
-                       ws + L.fcslab, tr ? A.base + A.L.act[0] : nullptr, tr ? A.base + A.L.act[1] : nullptr);
+    MT_TRY((launch_nips_trunk<C>(obs, st, B, P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation,
+                                 n->cfg.alpha_leaky, A.base + A.L.act[1], tr ? A.base + A.L.act[0] : nullptr,
+                                 ws + L.fcslab, s)));
     MT_LAUNCHED();
     HeadParams hp = head_params(n, P);
     hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, Fz::ROWS2, B,
@@ -832,6 +872,10 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
     MT_LAUNCHED();
     return MT_OK;
   } else {
+    if (st) {
+      set_error("stacking forward is built for the NIPS arch only");
+      return MT_ERR_ARG;
+    }
     return forward_impl<Ar>(n, P, obs, B, ws, v, pi, rep, smp, s, tr);
   }
 }
@@ -1030,10 +1074,8 @@ static int trunk_infer_impl(const mt_net *n, const float *P, const uint8_t *obs,
     const float *Wfc = P + n->off_fc;
     if constexpr (Ar::FUSED_SLABS > 0) {
       constexpr int C = LayerG<Ar, 0>::CIN;
-      using Fz = FusedNips<C>;
-      hipLaunchKernelGGL(nips_fused_trunk_kernel<C>, dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, obs, B,
-                         P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation, n->cfg.alpha_leaky,
-                         ws + L.fcslab, nullptr, nullptr);
+      MT_TRY((launch_nips_trunk<C>(obs, nullptr, B, P + n->off_conv[0], P + n->off_conv[1], Wfc,
+                                   n->cfg.activation, n->cfg.alpha_leaky, ws + L.act[1], nullptr, ws + L.fcslab, s)));
       MT_LAUNCHED();
       return MT_OK;
     } else {
@@ -1078,7 +1120,7 @@ extern "C" int mt_forward_infer(const mt_net *net, const float *params, const ui
 
 int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch,
                        void *ws, size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp,
-                       bool infer, hipStream_t stream, const TrainRows *tr) {
+                       bool infer, hipStream_t stream, const TrainRows *tr, const StackSrc *st) {
   MT_CHECK_ARG(net && params && obs && ws && v && pi && rep, "null argument");
   MT_CHECK_ARG(!smp || (smp->counters && smp->a_idx && smp->r_idx), "null sample buffer");
   MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
@@ -1101,7 +1143,8 @@ int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *ob
     if constexpr (Ar::LSTM)
       return lstm_forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
     else
-      return infer ? forward_infer_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream, tr)
+      MT_CHECK_ARG(!st || infer, "stacking forward is an inference forward");
+      return infer ? forward_infer_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream, tr, st)
                    : forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream, tr);
   });
   return MT_OK;

@@ -1,7 +1,9 @@
 // Native rollout macro-step: the per-step orchestration of paac.py:140-205 without Python.
 // See include/manette_hip.h (mt_rollout_*). Host code + HIP runtime calls; the emulator threads
 // and the bookkeeping live in libmanette_host.so (include/manette_host.h).
+#include <algorithm>
 #include <chrono>
+#include <vector>
 
 #include "common.h"
 #include "../../include/manette_host.h"
@@ -18,15 +20,24 @@ struct mt_rollout {
   mh_book *book;
   mt_rollout_buffers b;
   uint64_t seed;
-  hipEvent_t ev2[2];  // pair of step t ready: ev2[t & 1]
+  hipEvent_t ev2[4];  // pair of step t ready: ev2[t & 3]
   bool zero_copy, in_place, pooled, resized, pipelined;
-  int armed = -1;     // step whose forward is already enqueued (pipelined), else -1
+  bool stack_fwd;     // pipelined + resized + NIPS: the forward's conv kernel stacks (no preprocess)
+  int armed_upto = -1;  // pipelined: last step whose chain (forward) is already enqueued
+  int ahead = 1;        // pipelined: steps armed ahead (2 with stack_fwd)
+  std::vector<uint32_t> fwd_of;  // [T] draw sequence number of step t's forward
   uint32_t seq = 0;   // host step sequence word value last stored
   uint8_t *staging_dev;  // device addresses of the host-mapped buffers (zero-copy mode)
   int32_t *meta_dev, *pair_dev, *frames_dev;
   uint32_t *seq_dev, *status_dev;
   uint32_t *ready_dev = nullptr;  // [E] pair-ready flags (device address of b.ready_host)
   uint32_t fwd_seq = 0;           // sequence number of the last enqueued forward + draw
+  // stack_fwd: per-env ready words the emulator threads store (mh_runner_set_ready) and the
+  // tagged (a, r) words the heads kernel stores (SampleArgs::packed); pinned, device-mapped
+  uint32_t *env_ready_host = nullptr, *env_ready_dev = nullptr;
+  uint64_t *packed_host = nullptr, *packed_dev = nullptr;
+  uint8_t *frames_hbm = nullptr;   // [4E][84*84*depth] HBM copy of the pushes (pull kernel)
+  int32_t *count_hbm = nullptr;    // [E] push counts
   double acc[5];  // host wall us: launch+wait for indices, runner, book, upload+preprocess enqueue; steps
 };
 
@@ -97,6 +108,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->pooled = po;
   ro->resized = rz;
   ro->pipelined = pl;
+  ro->stack_fwd = pl && rz && cfg.arch == MT_ARCH_NIPS;
   ro->frames_dev = (int32_t *)frames_dev;
   ro->ready_dev = (uint32_t *)ready_dev;
   ro->seq_dev = (uint32_t *)sync_dev;
@@ -104,10 +116,31 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->staging_dev = (uint8_t *)staging_dev;
   ro->meta_dev = (int32_t *)meta_dev;
   ro->pair_dev = (int32_t *)pair_dev;
-  for (int i = 0; i < 2; ++i) {
+  if (ro->stack_fwd) {
+    hipError_t e = hipHostMalloc((void **)&ro->env_ready_host, sizeof(uint32_t) * E, hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&ro->packed_host, sizeof(uint64_t) * E, hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&ro->env_ready_dev, ro->env_ready_host, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&ro->packed_dev, ro->packed_host, 0);
+    if (e == hipSuccess) e = hipMalloc((void **)&ro->frames_hbm, (size_t)4 * E * 84 * 84 * cfg.depth);
+    if (e == hipSuccess) e = hipMalloc((void **)&ro->count_hbm, sizeof(int32_t) * E);
+    if (e != hipSuccess) {
+      if (ro->env_ready_host) (void)hipHostFree(ro->env_ready_host);
+      if (ro->packed_host) (void)hipHostFree(ro->packed_host);
+      if (ro->frames_hbm) (void)hipFree(ro->frames_hbm);
+      if (ro->count_hbm) (void)hipFree(ro->count_hbm);
+      delete ro;
+      set_error("pinned step words: %s", hipGetErrorString(e));
+      return MT_ERR_HIP;
+    }
+    std::memset(ro->env_ready_host, 0, sizeof(uint32_t) * E);
+    std::memset(ro->packed_host, 0, sizeof(uint64_t) * E);
+  }
+  ro->ahead = ro->stack_fwd ? 2 : 1;
+  ro->fwd_of.assign(T, 0);
+  for (int i = 0; i < 4; ++i) {
     hipError_t e = hipEventCreateWithFlags(&ro->ev2[i], hipEventDisableTiming);
     if (e != hipSuccess) {
-      if (i) (void)hipEventDestroy(ro->ev2[0]);
+      for (int j = 0; j < i; ++j) (void)hipEventDestroy(ro->ev2[j]);
       delete ro;
       set_error("hipEventCreate: %s", hipGetErrorString(e));
       return MT_ERR_HIP;
@@ -119,8 +152,14 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
 
 extern "C" void mt_rollout_destroy(mt_rollout *ro) {
   if (!ro) return;
-  (void)hipEventDestroy(ro->ev2[0]);
-  (void)hipEventDestroy(ro->ev2[1]);
+  for (int i = 0; i < 4; ++i) (void)hipEventDestroy(ro->ev2[i]);
+  if (ro->stack_fwd) {
+    (void)mh_runner_set_ready(ro->runner, nullptr, 0);
+    (void)hipHostFree(ro->env_ready_host);
+    (void)hipHostFree(ro->packed_host);
+    (void)hipFree(ro->frames_hbm);
+    (void)hipFree(ro->count_hbm);
+  }
   delete ro;
 }
 
@@ -146,26 +185,85 @@ __global__ void wait_seq_kernel(const uint32_t *seq_word, uint32_t seq, uint32_t
   }
 }
 
+// Pull kernel (stack_fwd): copies each env's pushes from the pinned staging into HBM as soon as
+// its emulator thread has published it (ready[e] = (step << 3) | push count,
+// mh_runner_set_ready), so the PCIe transfer of a step's frames overlaps the emulation of the
+// other envs and the stacking conv kernel reads HBM only. Block = kPullEnvs consecutive envs
+// (one runner worker's share at E = 32, ew = 8; a worker steps its envs in index order, so lane 0
+// polls only the next one: one PCIe read in flight per block, s_sleep between polls). Bounded
+// like wait_seq_kernel: after ~2 s it records the failure in status and returns.
+constexpr int kPullEnvs = 4;
+#ifdef MT_PROBE  // experiment builds: per env, when its word was seen and its copy done (tools/probe.py)
+static __device__ unsigned long long mt_probe_ro[512 * 4];
+extern "C" int mt_probe_read_rollout(unsigned long long *out, size_t n) {
+  MT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(mt_probe_ro), std::min(n, sizeof(mt_probe_ro) / 8) * 8));
+  return MT_OK;
+}
+#define MT_PROBE_RO(e, p) \
+  if ((e) < 512) mt_probe_ro[(e) * 4 + (p)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define MT_PROBE_RO(e, p)
+#endif
+__global__ __launch_bounds__(256) void pull_frames_kernel(const uint4 *__restrict__ staging, const uint32_t *ready,
+                                                          uint32_t want, uint32_t *status, int E, int frame16,
+                                                          uint4 *__restrict__ frames, int32_t *__restrict__ count) {
+  __shared__ int s_p;
+  const int e0 = blockIdx.x * kPullEnvs, n = min(kPullEnvs, E - e0);
+  const uint32_t tag = want & 0x1fffffffu;
+  if (threadIdx.x == 0) MT_PROBE_RO(e0, 2);
+  for (int k = 0; k < n; ++k) {
+    const int e = e0 + k;
+    if (threadIdx.x == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t v;
+      while (((v = __hip_atomic_load(ready + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> 3) != tag) {
+        __builtin_amdgcn_s_sleep(8);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+          __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          v = 0xffffffffu;  // timed out
+          break;
+        }
+      }
+      MT_PROBE_RO(e, 0);
+      s_p = v == 0xffffffffu ? -1 : (int)(v & 7u);
+    }
+    __syncthreads();
+    const int p0 = s_p;
+    if (p0 < 0) return;  // timed out (uniform over the block)
+    const int p = min(max(p0, 1), 4);
+    const size_t base = (size_t)4 * e * frame16;  // slots 4e .. 4e + p - 1 are contiguous
+    for (int q = threadIdx.x; q < p * frame16; q += 256) frames[base + q] = staging[base + q];
+    if (threadIdx.x == 0) count[e] = p;
+    __syncthreads();  // s_p is rewritten by the next round
+    if (threadIdx.x == 0) MT_PROBE_RO(e, 1);
+  }
+}
+
 namespace {
 // forward of state slot t with the A3 draw fused into its heads kernel (paac.py:144-147); the
 // indices land in idx[.][t] and the [2][E] pair; ev[t & 1] marks the pair ready.
-int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s) {
+// stacked: state slot t is built from slot t-1 + step t-1's pushes inside the forward's conv
+// kernel (fused mt_preprocess_resized; ro->stack_fwd).
+int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, bool stacked = false) {
   const mt_rollout_buffers &b = ro->b;
   const int E = ro->E, T = ro->T;
   const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
+  const StackSrc st{b.states + (size_t)(t - 1) * slot, ro->frames_hbm, ro->count_hbm, b.states + (size_t)t * slot};
   int32_t *a_d = b.idx + (size_t)t * E, *r_d = b.idx + (size_t)T * E + (size_t)t * E;
   SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
   smp.ready = ro->ready_dev;
   smp.seq = ++ro->fwd_seq;
+  ro->fwd_of[t] = smp.seq;
+  smp.packed = ro->packed_dev;
   // with a train workspace: activations into its rows t*E.., per-step pi / rep (mt_forward_rows)
   const TrainRows tr{(float *)b.train_ws, b.train_ws_bytes, T * E, t * E};
   const size_t po = b.train_ws ? (size_t)t * E : 0;
   MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)t * slot, E, b.ws, b.ws_bytes,
                          b.values + (size_t)t * E, b.pi + po * ro->A, b.rep + po * ro->R, &smp, true, s,
-                         b.train_ws ? &tr : nullptr));
+                         b.train_ws ? &tr : nullptr, stacked ? &st : nullptr));
   if (!ro->zero_copy)
     MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
-  MT_HIP(hipEventRecord(ro->ev2[t & 1], s));
+  MT_HIP(hipEventRecord(ro->ev2[t & 3], s));
   return MT_OK;
 }
 
@@ -195,6 +293,39 @@ int enqueue_preprocess(mt_rollout *ro, int t, int total, hipStream_t s) {
                     : mt_preprocess(raw, meta, meta + E, E, ro->depth, b.src_rows, b.row_lut, b.col_lut, cur,
                                     nxt, st);
 }
+// pipelined: arm step k's chain — it waits on the device for the host's step k-1, so it can be
+// enqueued `ahead` = k - t >= 1 host steps early (t = the host's current step): the chain's
+// wait (pull kernel per env, else wait_seq_kernel) is for the host step word value seq + ahead.
+// Step T's chain is the bootstrap forward V(s_T) (paac.py:219-224).
+int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t s) {
+  const mt_rollout_buffers &b = ro->b;
+  const int E = ro->E, T = ro->T;
+  const uint32_t want = ro->seq + (uint32_t)ahead;
+  // stack_fwd: the pull kernel waits per env and copies the pushes into HBM; the preprocess
+  // of step k-1 runs inside step k's forward conv kernel
+  const bool stk = ro->stack_fwd && (k < T || b.v_boot);
+  if (stk) {
+    hipLaunchKernelGGL(pull_frames_kernel, dim3((E + kPullEnvs - 1) / kPullEnvs), dim3(256), 0, s,
+                       reinterpret_cast<const uint4 *>(ro->staging_dev), ro->env_ready_dev, want, ro->status_dev, E,
+                       (int)(84 * 84 * ro->depth / 16), reinterpret_cast<uint4 *>(ro->frames_hbm), ro->count_hbm);
+    MT_LAUNCHED();
+  } else {
+    hipLaunchKernelGGL(wait_seq_kernel, dim3(1), dim3(64), 0, s, ro->seq_dev, want, ro->status_dev);
+    MT_LAUNCHED();
+    MT_TRY_(enqueue_preprocess(ro, k - 1, 4 * E, s));
+  }
+  if (k < T) {
+    MT_TRY_(enqueue_forward(ro, params, k, s, stk));
+  } else if (b.v_boot) {  // bootstrap V(s_T), no draw, no train rows
+    const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
+    const size_t po = b.train_ws ? (size_t)T * E : 0;
+    const StackSrc st{b.states + (size_t)(T - 1) * slot, ro->frames_hbm, ro->count_hbm, b.states + (size_t)T * slot};
+    MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)T * slot, E, b.ws, b.ws_bytes, b.v_boot,
+                           b.pi + po * ro->A, b.rep + po * ro->R, nullptr, true, s, nullptr, stk ? &st : nullptr));
+  }
+  ro->armed_upto = k;
+  return MT_OK;
+}
 }  // namespace
 
 // One macro-step t (paac.py:140-205). Pipelined mode keeps the GPU one step ahead of the host's
@@ -213,30 +344,41 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   const int E = ro->E, T = ro->T;
   const double t0 = now_us();
   int32_t *a_h = b.idx_host + (size_t)t * E, *r_h = b.idx_host + (size_t)T * E + (size_t)t * E;
-  // 1. forward + draw of step t, unless the previous call already enqueued it
-  if (ro->armed != t) MT_TRY_(enqueue_forward(ro, params, t, s));
-  ro->armed = -1;
-  // 2. pipelined: arm step t+1 while the GPU works on step t
-  if (ro->pipelined) {
-    hipLaunchKernelGGL(wait_seq_kernel, dim3(1), dim3(64), 0, s, ro->seq_dev, ro->seq + 1, ro->status_dev);
-    MT_LAUNCHED();
-    MT_TRY_(enqueue_preprocess(ro, t, 4 * E, s));
-    if (t + 1 < T) {
-      MT_TRY_(enqueue_forward(ro, params, t + 1, s));
-      ro->armed = t + 1;
-    } else if (b.v_boot) {  // bootstrap V(s_T) (paac.py:219-224), no draw, no train rows
-      const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
-      const size_t po = b.train_ws ? (size_t)T * E : 0;
-      MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)T * slot, E, b.ws, b.ws_bytes, b.v_boot,
-                             b.pi + po * ro->A, b.rep + po * ro->R, nullptr, true, s));
-    }
+  // 1. forward + draw of step t, unless a previous call already enqueued it
+  if (t == 0 || !ro->pipelined) ro->armed_upto = -1;  // a new rollout (parameters changed)
+  if (ro->armed_upto < t) {
+    MT_TRY_(enqueue_forward(ro, params, t, s));
+    ro->armed_upto = t;
   }
+  // 2. pipelined: arm steps up to t + depth (at most T) while the GPU works on step t, so the
+  //    launches are off the critical path (stack_fwd: two steps ahead — the GPU chain after the
+  //    emulators is shorter than the launches of a chain)
+  if (ro->pipelined)
+    for (int k = ro->armed_upto + 1; k <= std::min(t + ro->ahead, T); ++k) MT_TRY_(arm_step(ro, params, k, k - t, s));
   // 3. wait for the indices of step t (spin: a blocking wait sleeps past the chain and pays the
   //    wake-up latency)
   // (with ready flags: poll the E flags the heads kernel stores after each pair — one cached host
   //  load each — and query the event only now and then, to surface a device error)
-  const uint32_t want = ro->pipelined && ro->armed == t + 1 ? ro->fwd_seq - 1 : ro->fwd_seq;
-  if (ro->ready_dev) {
+  const uint32_t want = ro->fwd_of[t];
+  if (ro->packed_host) {  // tagged (a, r) words: both halves carry the step's tag
+    const uint32_t tag = want & 0xffffu;
+    const volatile uint64_t *pw = ro->packed_host;
+    for (int e = 0, spins = 0; e < E;) {
+      const uint64_t v = __atomic_load_n(const_cast<const uint64_t *>(pw + e), __ATOMIC_ACQUIRE);
+      if (((v >> 16) & 0xffffu) == tag && (v >> 48) == tag) {
+        a_h[e] = (int32_t)(v & 0xffffu);
+        r_h[e] = (int32_t)((v >> 32) & 0xffffu);
+        ++e;
+        continue;
+      }
+      __builtin_ia32_pause();
+      if (++spins == 4096) {
+        spins = 0;
+        const hipError_t q = hipEventQuery(ro->ev2[t & 3]);
+        if (q != hipSuccess && q != hipErrorNotReady) MT_HIP(q);
+      }
+    }
+  } else if (ro->ready_dev) {
     const volatile uint32_t *rf = b.ready_host;
     for (int e = 0, spins = 0; e < E;) {
       if (__atomic_load_n(const_cast<const uint32_t *>(rf + e), __ATOMIC_ACQUIRE) == want) {
@@ -246,29 +388,34 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
       __builtin_ia32_pause();
       if (++spins == 4096) {
         spins = 0;
-        const hipError_t q = hipEventQuery(ro->ev2[t & 1]);
+        const hipError_t q = hipEventQuery(ro->ev2[t & 3]);
         if (q != hipSuccess && q != hipErrorNotReady) MT_HIP(q);
       }
     }
   } else {
     hipError_t q;
-    while ((q = hipEventQuery(ro->ev2[t & 1])) == hipErrorNotReady) __builtin_ia32_pause();
+    while ((q = hipEventQuery(ro->ev2[t & 3])) == hipErrorNotReady) __builtin_ia32_pause();
     MT_HIP(q);
   }
   if (ro->pipelined && __atomic_load_n(&b.sync_host[1], __ATOMIC_ACQUIRE) != 0) {
     set_error("device wait for the host step word timed out (host stalled > 2 s); rollout state is invalid");
     return MT_ERR_HIP;
   }
-  std::memcpy(a_h, b.pair_host, sizeof(int32_t) * E);
-  std::memcpy(r_h, b.pair_host + E, sizeof(int32_t) * E);
+  if (!ro->packed_host) {
+    std::memcpy(a_h, b.pair_host, sizeof(int32_t) * E);
+    std::memcpy(r_h, b.pair_host + E, sizeof(int32_t) * E);
+  }
   const double t1 = now_us();
   // 4. emulators (runners.py:44-50 / emulator_runner.py:24-41) + bookkeeping (paac.py:176-205)
   int total = 0;
-  const int rs = ro->in_place
-                     ? mh_runner_step_frames(ro->runner, a_h, r_h, b.frames_host, b.meta_host + E, b.reward_host,
-                                             b.over_host)
-                     : mh_runner_step(ro->runner, a_h, r_h, b.staging_host, b.meta_host, b.meta_host + E,
-                                      b.reward_host, b.over_host, &total);
+  if (ro->stack_fwd && mh_runner_set_ready(ro->runner, ro->env_ready_host, ro->seq + 1) != 0) {
+    set_error("mh_runner_set_ready: %s", mh_last_error());
+    return MT_ERR_ARG;
+  }
+  const int rs = ro->in_place ? mh_runner_step_frames(ro->runner, a_h, r_h, b.frames_host, b.meta_host + E,
+                                                    b.reward_host, b.over_host)
+                              : mh_runner_step(ro->runner, a_h, r_h, b.staging_host, b.meta_host, b.meta_host + E,
+                                               b.reward_host, b.over_host, &total);
   if (rs != 0) {
     set_error("mh_runner_step: %s", mh_last_error());
     return MT_ERR_ARG;

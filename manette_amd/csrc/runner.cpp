@@ -88,6 +88,13 @@ struct mh_runner {
   // output row: SSE max of the two source rows into a buffer, then each 16-byte output chunk is
   // OR-ed from pshufb of up to 3 source vectors (gray and RGB alike); the next row's source lines
   // are prefetched while this one is gathered.
+  // d (16-byte aligned, n a multiple of 16 — a final frame: 7056 * depth) <- s with streaming
+  // stores; the caller fences (sfence) before publishing d
+  static void stream_copy(uint8_t *d, const uint8_t *s, size_t n) {
+    for (size_t x = 0; x < n; x += 16)
+      _mm_stream_si128(reinterpret_cast<__m128i *>(d + x), _mm_load_si128(reinterpret_cast<const __m128i *>(s + x)));
+  }
+
   void resize_push(uint8_t *d, const uint8_t *s0, const uint8_t *s1) const {
     const int rb = (int)row_bytes, ob = 84 * depth;
     alignas(16) uint8_t m[480 + 64];
@@ -130,6 +137,12 @@ struct mh_runner {
   int32_t *push_offset = nullptr, *push_count = nullptr;
   int32_t *frame_idx = nullptr;  // in-place mode: [E][8] bank frame indices (else null)
   float *reward = nullptr, *over = nullptr;
+  // per-env ready words (fixed slots): env i's staging + push count are complete once
+  // ready[i] == (ready_value << 3) | push count (mh_runner_set_ready); the GPU pulls env i while
+  // the others are still being emulated
+  uint32_t *ready = nullptr;
+  uint32_t ready_value = 0;
+  bool busy = false;  // mh_runner_step_begin dispatched, mh_runner_step_end not yet called
 
   int block_begin(int w) const { return (int)((int64_t)E * w / W); }
   int block_end(int w) const { return (int)((int64_t)E * (w + 1) / W); }
@@ -160,6 +173,7 @@ struct mh_runner {
         initial(env[i]);
       }
     } else if (phase == 1) {
+      const bool per_env = ready && fixed && !frame_idx;
       for (int i = b0; i < b1; ++i) {
         Env &e = env[i];
         e.npush = 0;
@@ -178,7 +192,13 @@ struct mh_runner {
           push_offset[i] = 4 * i;
           push_count[i] = std::min(e.npush, 4);
         }
+        if (per_env) {  // stage env i now and publish it (sfence: the streaming stores first)
+          stage_env(i);
+          _mm_sfence();
+          __atomic_store_n(ready + i, (ready_value << 3) | (uint32_t)std::min(e.npush, 4), __ATOMIC_RELEASE);
+        }
       }
+      if (per_env) return;
     }
     if (frame_idx) {  // in place: record where the pushed screens are, oldest first
       for (int i = b0; i < b1; ++i) {
@@ -193,39 +213,47 @@ struct mh_runner {
       return;
     }
     if (phase == 0 || phase == 2 || fixed) {
-      for (int i = b0; i < b1; ++i) {
-        const Env &e = env[i];
-        const int n = std::min(e.npush, 4);
-        for (int j = 0; j < n; ++j) {
-          const int64_t kk = e.last[(e.npush - n + j) & 3];
-          if (resized) {
-            resize_push(staging + (size_t)(push_offset[i] + j) * sfb,
-                        e.screens + (size_t)((2 * kk) % ring) * fb, e.screens + (size_t)((2 * kk + 1) % ring) * fb);
-            continue;
-          }
-          if (pooled) {  // FramePool max (atari_emulator.py:79-88) of the staged rows, on the host
-            uint8_t *d = staging + (size_t)(push_offset[i] + j) * sfb;
-            const uint8_t *s0 = e.screens + (size_t)((2 * kk) % ring) * fb;
-            const uint8_t *s1 = e.screens + (size_t)((2 * kk + 1) % ring) * fb;
-            const size_t nr = rows.empty() ? 210 : rows.size();
-            for (size_t q = 0; q < nr; ++q) {
-              const size_t so = (rows.empty() ? q : (size_t)rows[q]) * row_bytes;
-              uint8_t *dq = d + q * row_bytes;
-              for (size_t x = 0; x < row_bytes; ++x) dq[x] = std::max(s0[so + x], s1[so + x]);
-            }
-            continue;
-          }
-          uint8_t *dst = staging + (size_t)(push_offset[i] + j) * 2 * sfb;
-          for (int f = 0; f < 2; ++f) {
-            const uint8_t *src = e.screens + (size_t)((2 * kk + f) % ring) * fb;
-            uint8_t *d = dst + f * sfb;
-            if (rows.empty()) {
-              std::memcpy(d, src, fb);
-            } else {
-              for (size_t q = 0; q < rows.size(); ++q)
-                std::memcpy(d + q * row_bytes, src + (size_t)rows[q] * row_bytes, row_bytes);
-            }
-          }
+      for (int i = b0; i < b1; ++i) stage_env(i);
+      _mm_sfence();  // streaming stores visible before the phase is reported done
+    }
+  }
+
+  // the pushes of env i into the staging (resized / pooled / raw rows)
+  void stage_env(int i) {
+    const Env &e = env[i];
+    const int n = std::min(e.npush, 4);
+    for (int j = 0; j < n; ++j) {
+      const int64_t kk = e.last[(e.npush - n + j) & 3];
+      if (resized) {
+        // resized into an L1-resident buffer, then streamed to the staging with non-temporal
+        // stores: the lines never sit modified in this core's cache, so the GPU reading them
+        // over PCIe (while this thread works on the next env) does not snoop them out of it
+        alignas(64) uint8_t buf[84 * 84 * 3 + 64];
+        resize_push(buf, e.screens + (size_t)((2 * kk) % ring) * fb, e.screens + (size_t)((2 * kk + 1) % ring) * fb);
+        stream_copy(staging + (size_t)(push_offset[i] + j) * sfb, buf, sfb);
+        continue;
+      }
+      if (pooled) {  // FramePool max (atari_emulator.py:79-88) of the staged rows, on the host
+        uint8_t *d = staging + (size_t)(push_offset[i] + j) * sfb;
+        const uint8_t *s0 = e.screens + (size_t)((2 * kk) % ring) * fb;
+        const uint8_t *s1 = e.screens + (size_t)((2 * kk + 1) % ring) * fb;
+        const size_t nr = rows.empty() ? 210 : rows.size();
+        for (size_t q = 0; q < nr; ++q) {
+          const size_t so = (rows.empty() ? q : (size_t)rows[q]) * row_bytes;
+          uint8_t *dq = d + q * row_bytes;
+          for (size_t x = 0; x < row_bytes; ++x) dq[x] = std::max(s0[so + x], s1[so + x]);
+        }
+        continue;
+      }
+      uint8_t *dst = staging + (size_t)(push_offset[i] + j) * 2 * sfb;
+      for (int f = 0; f < 2; ++f) {
+        const uint8_t *src = e.screens + (size_t)((2 * kk + f) % ring) * fb;
+        uint8_t *d = dst + f * sfb;
+        if (rows.empty()) {
+          std::memcpy(d, src, fb);
+        } else {
+          for (size_t q = 0; q < rows.size(); ++q)
+            std::memcpy(d + q * row_bytes, src + (size_t)rows[q] * row_bytes, row_bytes);
         }
       }
     }
@@ -252,10 +280,16 @@ struct mh_runner {
   }
 
   void dispatch(int ph) {
+    dispatch_begin(ph);
+    dispatch_wait();
+  }
+  void dispatch_begin(int ph) {
     phase = ph;
     arrived.store(0, std::memory_order_relaxed);
     gen.fetch_add(1, std::memory_order_acq_rel);
     gen.notify_all();
+  }
+  void dispatch_wait() {
     int spins = 0;
     int a;
     while ((a = arrived.load(std::memory_order_acquire)) != W) {
@@ -399,12 +433,29 @@ extern "C" int mh_runner_reset(mh_runner *r, uint8_t *staging, int32_t *push_off
   return 0;
 }
 
-extern "C" int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx,
-                              uint8_t *staging, int32_t *push_offset, int32_t *push_count,
-                              float *reward, float *over, int *total_pushes) {
-  if (!r || !a_idx || !r_idx || !staging || !push_offset || !push_count || !reward || !over ||
-      !total_pushes) {
+extern "C" int mh_runner_set_ready(mh_runner *r, uint32_t *ready, uint32_t value) {
+  if (!r) {
     set_error("null argument");
+    return 1;
+  }
+  if (ready && !(r->fixed && r->resized)) {
+    set_error("per-env ready words need fixed, resized staging");
+    return 1;
+  }
+  r->ready = ready;
+  r->ready_value = value;
+  return 0;
+}
+
+extern "C" int mh_runner_step_begin(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx,
+                                    uint8_t *staging, int32_t *push_offset, int32_t *push_count,
+                                    float *reward, float *over) {
+  if (!r || !a_idx || !r_idx || !staging || !push_offset || !push_count || !reward || !over) {
+    set_error("null argument");
+    return 1;
+  }
+  if (r->busy) {
+    set_error("a step is already in flight");
     return 1;
   }
   const int nr = (int)r->tab.size();
@@ -413,6 +464,64 @@ extern "C" int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t 
       set_error("r_idx[%d] = %d out of range [0,%d)", i, r_idx[i], nr);
       return 1;
     }
+  if (r->resized && ((uintptr_t)staging & 15)) {
+    set_error("resized staging must be 16-byte aligned");
+    return 1;
+  }
+  r->a_idx = a_idx;
+  r->r_idx = r_idx;
+  r->staging = staging;
+  r->push_offset = push_offset;
+  r->push_count = push_count;
+  r->reward = reward;
+  r->over = over;
+  r->busy = true;
+  r->dispatch_begin(1);
+  return 0;
+}
+
+extern "C" int mh_runner_step_end(mh_runner *r, int *total_pushes) {
+  if (!r || !total_pushes) {
+    set_error("null argument");
+    return 1;
+  }
+  if (!r->busy) {
+    set_error("no step in flight");
+    return 1;
+  }
+  r->dispatch_wait();
+  r->busy = false;
+  if (r->fixed) {
+    *total_pushes = 4 * r->E;
+    return 0;
+  }
+  r->compact(total_pushes);
+  r->dispatch(2);
+  return 0;
+}
+
+extern "C" int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t *r_idx,
+                              uint8_t *staging, int32_t *push_offset, int32_t *push_count,
+                              float *reward, float *over, int *total_pushes) {
+  if (!r || !a_idx || !r_idx || !staging || !push_offset || !push_count || !reward || !over ||
+      !total_pushes) {
+    set_error("null argument");
+    return 1;
+  }
+  if (r->busy) {
+    set_error("a step is already in flight");
+    return 1;
+  }
+  const int nr = (int)r->tab.size();
+  for (int i = 0; i < r->E; ++i)
+    if (r_idx[i] < 0 || r_idx[i] >= nr) {
+      set_error("r_idx[%d] = %d out of range [0,%d)", i, r_idx[i], nr);
+      return 1;
+    }
+  if (r->resized && ((uintptr_t)staging & 15)) {
+    set_error("resized staging must be 16-byte aligned");
+    return 1;
+  }
   r->a_idx = a_idx;
   r->r_idx = r_idx;
   r->staging = staging;

@@ -1,30 +1,54 @@
-// Fused NIPS trunk for the rollout-batch forward (E small, latency-bound): one launch computes
-// conv1 -> conv2 -> the dense layer's partial products (networks.py:178-192, :57-70), replacing
-// three GEMM launches (conv1, conv2, split-K fc). Only the inference forward uses it (rollout
-// steps and the bootstrap V(s_T)): no activations are kept for a backward pass.
+// NIPS trunk of the inference forward (rollout steps, bootstrap V(s_T)), E small and
+// latency-bound: networks.py:178-192 (conv1 -> conv2) and :57-70 (the dense layer's products) as
+// two launches, whose 9 split-K slabs heads_fwd_kernel finishes (sum in fixed order + bias + act,
+// heads, softmax, A3 draw).
 //
-// Workgroup = (env e, conv2 output row i), 9 per env. Its conv2 row reads conv1 rows 2i..2i+3,
-// which read input rows 8i..8i+19: the block stages those 20 uint8 rows (contiguous in NHWC) in
-// LDS, recomputes its 4 conv1 rows (1.8x the conv1 FLOPs over the 9 blocks of an env, in exchange
-// for no inter-block hand-off), computes its conv2 row, and multiplies that row's 288 features by
-// the matching 288 rows of the fc weight: the slab z = i of the split-K layout heads_fwd_kernel
-// finishes (sum of the 9 slabs in fixed order + bias + act, heads, softmax, A3 draw).
+// 1. nips_conv_kernel — workgroup = (env e, conv2 output row i), 9 per env. Its conv2 row reads
+//    conv1 rows 2i..2i+3, which read input rows 8i..8i+19: the block stages those 20 uint8 rows
+//    (contiguous in NHWC) in LDS, recomputes its 4 conv1 rows (1.8x the conv1 FLOPs over the 9
+//    blocks of an env, in exchange for no inter-block hand-off), computes its conv2 row and
+//    writes those 288 activations to act2 [B][2592] (NHWC flatten order).
+//    STACK variant (the pipelined rollout, resized staging): the block also does the A2 stacking
+//    of mt_preprocess_resized (atari_emulator.py:79-124, environment.py:42-80) for its rows — the
+//    previous state's rows from HBM and the env's p new final frames read in place from pinned
+//    host staging (fixed slots 4e + j), stacked in LDS, the block's own rows (8i..8i+7; the last
+//    block 64..83) written to the new state slot — so no separate preprocess launch sits on the
+//    step's critical path.
+// 2. nips_fc_kernel — the dense layer as a real GEMM: block = (16 output columns, conv2 row i,
+//    32 envs); slab[i][e][n] = sum_{f < 288} act2[e][288 i + f] Wfc[288 i + f][n] on MFMA. Each
+//    fc weight is read once per 32 envs (the former one-launch trunk streamed the row's 295 KB
+//    weight chunk through every (env, row) block: 85 MB of L2 -> CU traffic at E = 32).
 //
-// Convs run on v_mfma_f32_16x16x4_f32 (exact fp32) with the 4 waves splitting K; the 4 partial
-// accumulators are added in wave order through LDS (deterministic). Input scaling x = u8 * (1/255)
-// in fp32 as networks.py:155 (same expression as LdIm2col's loader).
+// Convs and fc run on v_mfma_f32_16x16x4_f32 (exact fp32) with the 4 waves splitting K; the 4
+// partial accumulators are added in wave order through LDS (deterministic). Input scaling
+// x = u8 * (1/255) in fp32 as networks.py:155 (same expression as LdIm2col's loader).
 //
-// blockIdx -> (i, e) is XCD-aware: blocks are dealt round-robin over the 8 XCDs, so the linear
-// index L = (bid % 8) * (grid / 8) + bid / 8 gives each XCD a contiguous run of L, i.e. 1-2 conv2
-// rows, and the 295 KB fc weight chunk of a row is read from HBM by one or two XCDs' L2s instead
-// of all eight (speed only; any placement computes the same values).
+// blockIdx -> (i, e) of the conv kernel is XCD-aware: blocks are dealt round-robin over the 8
+// XCDs, so the linear index L = (bid % 8) * (grid / 8) + bid / 8 gives each XCD a contiguous run
+// of L, i.e. 1-2 conv2 rows (speed only; any placement computes the same values).
 #pragma once
 #include "gemm.h"
+
+// Phase timestamps (experiment builds only, -DMT_PROBE: build_hip(out=..., defines=['MT_PROBE'])):
+// s_memrealtime (100 MHz, one clock for the whole device) of lane 0 at phase boundaries of every
+// block of the rollout-forward kernels, read back with mt_probe_read (tools/probe.py).
+#ifdef MT_PROBE
+static __device__ unsigned long long mt_probe_buf[4 * 512 * 8];
+#define MT_PROBE_AT(k, b, p)                                                                     \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && (b) < 512) mt_probe_buf[((k) * 512 + (b)) * 8 + (p)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define MT_PROBE_AT(k, b, p) \
+  do {                       \
+  } while (0)
+#endif
 
 namespace mt {
 
 template <int C>
 struct FusedNips {
+  static constexpr int D = C / 4;         // 1 gray, 3 RGB
   static constexpr int ROWS2 = 9;         // conv2 output rows = blocks per env
   static constexpr int ROWS1 = 4;         // conv1 rows a block computes
   static constexpr int RIN = 20;          // input rows a block stages
@@ -32,45 +56,96 @@ struct FusedNips {
   static constexpr int OW2 = 9, CO2 = 32, KK2 = 256;
   static constexpr int A1S = 20;          // padded float stride of one conv1 pixel in LDS
   static constexpr int FEAT = OW2 * CO2;  // 288 features per conv2 row
+  static constexpr int FLAT = ROWS2 * FEAT;
   static constexpr int F = 256;
   static constexpr int M1 = ROWS1 * OW1;  // 80 conv1 pixels
   static constexpr int MT1 = (M1 + 15) / 16;  // 5 m-tiles
   static constexpr int KC1 = KK1 / 16, KC2 = KK2 / 16;
   static_assert(KC1 % 4 == 0 && KC2 % 4 == 0, "K chunks split over 4 waves");
   static constexpr int IN_BYTES = RIN * 84 * C;
+  static constexpr int FR_BYTES = RIN * 84 * D;  // the block's rows of one new frame
   // LDS (floats unless noted)
-  static constexpr int RED_FLOATS = 4 * MT1 * 16 * CO1;  // >= 4*16*32 (conv2) and 4*256 (fc)
-  static constexpr size_t LDS_BYTES = IN_BYTES + sizeof(float) * (RED_FLOATS + M1 * A1S + FEAT);
+  static constexpr int RED_FLOATS = 4 * MT1 * 16 * CO1;  // >= 4*16*32 (conv2)
+  static_assert(4 * FR_BYTES <= RED_FLOATS * 4, "staged frames alias the reduction buffer");
+  static constexpr size_t LDS_BYTES = IN_BYTES + sizeof(float) * (RED_FLOATS + M1 * A1S);
+  // fc kernel
+  static constexpr int FC_BN = 16, FC_BM = 32, FC_KC = FEAT / 16;  // 18 K chunks of 16
 };
 
-// One block's work: conv2 row i of env e -> its fc partial slab. Returns e (the env).
-// act1 / act2 (optional): [B][20][20][16] conv1 and [B][9][9][32] conv2 activations of this
-// batch (rows of a train workspace, mt_forward_rows); block (e, i) writes conv1 rows 2i, 2i+1
-// (the last block also 18, 19) and conv2 row i, so every value is written once.
-template <int C>
-__device__ __forceinline__ int nips_trunk_block(const uint8_t *__restrict__ obs, int B, const float *__restrict__ W1,
-                                                const float *__restrict__ W2, const float *__restrict__ Wfc, int act,
-                                                float alpha, float *__restrict__ slabs, float *smem,
-                                                float *__restrict__ act1, float *__restrict__ act2) {
+// Stage input rows 8i..8i+19 of env e into xin. STACK: build them from the previous state and
+// the new frames, writing the block's own rows of the new state.
+template <int C, bool STACK>
+__device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs, const StackSrc &st, int e, int i,
+                                                uint8_t *xin, uint8_t *fr) {
   using Fz = FusedNips<C>;
+  const size_t row0 = ((size_t)e * 84 + 8 * i) * 84 * C;  // byte offset of row 8i of env e
+  if constexpr (!STACK) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(obs + row0);
+    uint4 *dst = reinterpret_cast<uint4 *>(xin);
+    for (int q = threadIdx.x; q < Fz::IN_BYTES / 16; q += 256) dst[q] = src[q];
+    return;
+  } else {
+    __shared__ int s_p;
+    {  // the previous state's rows
+      const uint4 *src = reinterpret_cast<const uint4 *>(st.prev + row0);
+      uint4 *dst = reinterpret_cast<uint4 *>(xin);
+      for (int q = threadIdx.x; q < Fz::IN_BYTES / 16; q += 256) dst[q] = src[q];
+    }
+    // one round trip for the common case: the push count and push 0's rows with the prev rows
+    if (threadIdx.x == 0) s_p = st.count[e];
+    {
+      const size_t f0 = ((size_t)4 * e * 84 + 8 * i) * 84 * Fz::D;  // push 0 = slot 4e
+      const uint4 *fs = reinterpret_cast<const uint4 *>(st.frames + f0);
+      for (int q = threadIdx.x; q < Fz::FR_BYTES / 16; q += 256) reinterpret_cast<uint4 *>(fr)[q] = fs[q];
+    }
+    __syncthreads();
+    const int p = min(max(s_p, 1), 4);
+    if (p > 1) {  // FiGAR repeats: pushes 1..p-1 (slots 4e+1..)
+      for (int q = threadIdx.x; q < (p - 1) * (Fz::FR_BYTES / 16); q += 256) {
+        const int j = 1 + q / (Fz::FR_BYTES / 16), qq = q - (j - 1) * (Fz::FR_BYTES / 16);
+        const size_t fj = (((size_t)4 * e + j) * 84 + 8 * i) * 84 * Fz::D;
+        reinterpret_cast<uint4 *>(fr + j * Fz::FR_BYTES)[qq] = reinterpret_cast<const uint4 *>(st.frames + fj)[qq];
+      }
+      __syncthreads();
+    }
+    // word w of the rows = channels 4c..4c+3 of pixel (r, x), c < D: byte offset 4w in the state
+    // rows and byte w in each frame's rows (C = 4D). Same op as preprocess_kernel<D, kSrcFinal>.
+    uint32_t *xw = reinterpret_cast<uint32_t *>(xin);
+    uint32_t *ow = reinterpret_cast<uint32_t *>(st.out + row0);
+    const int own = (i == Fz::ROWS2 - 1 ? Fz::RIN : 8) * 84 * Fz::D;  // words this block writes
+    for (int w = threadIdx.x; w < Fz::RIN * 84 * Fz::D; w += 256) {
+      uint32_t v = p < 4 ? xw[w] >> (8 * p) : 0u;
+      for (int j = 0; j < p; ++j) v |= (uint32_t)fr[j * Fz::FR_BYTES + w] << (8 * (4 - p + j));
+      xw[w] = v;
+      if (w < own) ow[w] = v;
+    }
+  }
+}
+
+// conv1 -> conv2 of conv2 row i of env e; writes act2 [B][2592] row e's 288 features of row i.
+// act1 (optional): [B][20][20][16] conv1 activations (rows of a train workspace, mt_forward_rows);
+// block (e, i) writes conv1 rows 2i, 2i+1 (the last block also 18, 19), so each value is written
+// once.
+template <int C, bool STACK>
+__global__ __launch_bounds__(256) void nips_conv_kernel(const uint8_t *__restrict__ obs, StackSrc st, int B,
+                                                        const float *__restrict__ W1, const float *__restrict__ W2,
+                                                        int act, float alpha, float *__restrict__ act2,
+                                                        float *__restrict__ act1) {
+  using Fz = FusedNips<C>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   float *red = smem;                              // [4 waves][..] partial accumulators
   float *a1 = red + Fz::RED_FLOATS;               // [80 pixels][A1S] conv1 rows 2i..2i+3
-  float *a2 = a1 + Fz::M1 * Fz::A1S;              // [288] conv2 row i (NHWC flatten order)
-  uint8_t *xin = reinterpret_cast<uint8_t *>(a2 + Fz::FEAT);  // [20][84][C] input rows 8i..
+  uint8_t *xin = reinterpret_cast<uint8_t *>(a1 + Fz::M1 * Fz::A1S);  // [20][84][C] input rows 8i..
+  uint8_t *fr = reinterpret_cast<uint8_t *>(red);  // STACK: [4][20][84][D] new frames (before conv1)
 
   const int nb = gridDim.x;
   const int bid = blockIdx.x;
+  MT_PROBE_AT(0, bid, 0);
   const int L = (nb % 8 == 0) ? (bid % 8) * (nb / 8) + bid / 8 : bid;
   const int i = L / B, e = L - i * B;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
 
-  // ---- stage input rows 8i..8i+19 (one contiguous run of 20*84*C bytes) ----
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(obs + ((size_t)e * 84 + 8 * i) * 84 * C);
-    uint4 *dst = reinterpret_cast<uint4 *>(xin);
-    for (int q = threadIdx.x; q < Fz::IN_BYTES / 16; q += 256) dst[q] = src[q];
-  }
   // conv1 weight fragments of this wave's K chunks (c = w + 4j): B[k][n] = W1[k*16 + n]
   constexpr int J1 = Fz::KC1 / 4;
   float b1f[J1][4];
@@ -80,7 +155,9 @@ __device__ __forceinline__ int nips_trunk_block(const uint8_t *__restrict__ obs,
 #pragma unroll
     for (int s = 0; s < 4; ++s) b1f[j][s] = W1[(size_t)(k0 + s) * Fz::CO1 + r];
   }
+  nips_stage_rows<C, STACK>(obs, st, e, i, xin, fr);
   __syncthreads();
+  MT_PROBE_AT(0, bid, 1);
 
   // ---- conv1 (VALID 8x8 stride 4): M = 80 pixels (4 rows x 20), N = 16, K = 64*C ----
   {
@@ -137,6 +214,7 @@ __device__ __forceinline__ int nips_trunk_block(const uint8_t *__restrict__ obs,
     }
   }
   __syncthreads();
+  MT_PROBE_AT(0, bid, 2);
 
   // ---- conv2 row i (VALID 4x4 stride 2): M = 9 pixels (padded to 16), N = 32, K = 256 ----
   {
@@ -158,48 +236,86 @@ __device__ __forceinline__ int nips_trunk_block(const uint8_t *__restrict__ obs,
       for (int q = 0; q < 4; ++q) red[(w * 16 + g * 4 + q) * Fz::CO2 + nt * 16 + r] = acc[nt][q];
   }
   __syncthreads();
+  MT_PROBE_AT(0, bid, 3);
   {
     const float *b2 = W2 + (size_t)Fz::KK2 * Fz::CO2;
     constexpr int P = 16 * Fz::CO2;
     for (int idx = threadIdx.x; idx < Fz::FEAT; idx += 256) {
       const int n = idx & (Fz::CO2 - 1);
       const float s = ((red[idx] + red[P + idx]) + red[2 * P + idx]) + red[3 * P + idx];
-      const float y = act_fwd(s + b2[n], act, alpha);
-      a2[idx] = y;
-      if (act2) act2[((size_t)e * Fz::ROWS2 + i) * Fz::FEAT + idx] = y;
+      act2[((size_t)e * Fz::ROWS2 + i) * Fz::FEAT + idx] = act_fwd(s + b2[n], act, alpha);
     }
   }
-  __syncthreads();
-
-  // ---- fc partial: slab[i][e][n] = sum_{f < 288} a2[f] * Wfc[i*288 + f][n] ----
-  {
-    const int c4 = threadIdx.x & 63, fg = threadIdx.x >> 6;  // 4 output columns x 72 features
-    constexpr int FPG = Fz::FEAT / 4;
-    const f32x4 *wp = reinterpret_cast<const f32x4 *>(Wfc + ((size_t)i * Fz::FEAT + fg * FPG) * Fz::F) + c4;
-    const float *xp = a2 + fg * FPG;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-    for (int f = 0; f < FPG; ++f) acc += xp[f] * wp[(size_t)f * (Fz::F / 4)];
-    reinterpret_cast<f32x4 *>(red)[fg * 64 + c4] = acc;
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const f32x4 *rp = reinterpret_cast<const f32x4 *>(red);
-    const f32x4 s = ((rp[threadIdx.x] + rp[64 + threadIdx.x]) + rp[128 + threadIdx.x]) + rp[192 + threadIdx.x];
-    reinterpret_cast<f32x4 *>(slabs + ((size_t)i * B + e) * Fz::F)[threadIdx.x] = s;
-  }
-  return e;
+  MT_PROBE_AT(0, bid, 4);
 }
 
+// Dense layer partial products: slabs[i][e][n] = sum_{f < 288} act2[e][288 i + f] Wfc[288 i + f][n].
+// Grid (F / 16, 9, ceil(B / 32)); 4 waves split the 18 K chunks of 16 (c = w + 4j), every operand
+// load of a wave issued before its first MFMA; partials added in wave order through LDS.
 template <int C>
-__global__ __launch_bounds__(256) void nips_fused_trunk_kernel(const uint8_t *__restrict__ obs, int B,
-                                                               const float *__restrict__ W1,
-                                                               const float *__restrict__ W2,
-                                                               const float *__restrict__ Wfc, int act,
-                                                               float alpha, float *__restrict__ slabs,
-                                                               float *__restrict__ act1, float *__restrict__ act2) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  (void)nips_trunk_block<C>(obs, B, W1, W2, Wfc, act, alpha, slabs, smem, act1, act2);
+__global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ act2, int B,
+                                                      const float *__restrict__ Wfc, float *__restrict__ slabs) {
+  using Fz = FusedNips<C>;
+  __shared__ __attribute__((aligned(16))) float red[4][Fz::FC_BM][Fz::FC_BN];
+  const int n0 = blockIdx.x * Fz::FC_BN, i = blockIdx.y, e0 = blockIdx.z * Fz::FC_BM;
+  const int pb = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  MT_PROBE_AT(1, pb, 0);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  constexpr int JN = (Fz::FC_KC + 3) / 4;  // 5
+  f32x4 a[JN][2];
+  float b[JN][4];
+  const int row0 = min(e0 + r, B - 1), row1 = min(e0 + 16 + r, B - 1);
+#pragma unroll
+  for (int j = 0; j < JN; ++j) {
+    const int c = min(w + 4 * j, Fz::FC_KC - 1);  // (chunks past 17 are loaded but not used)
+    const int k0 = i * Fz::FEAT + 16 * c + 4 * g;
+    a[j][0] = *reinterpret_cast<const f32x4 *>(act2 + (size_t)row0 * Fz::FLAT + k0);
+    a[j][1] = *reinterpret_cast<const f32x4 *>(act2 + (size_t)row1 * Fz::FLAT + k0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) b[j][s] = Wfc[(size_t)(k0 + s) * Fz::F + n0 + r];
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int j = 0; j < JN; ++j) {
+    if (w + 4 * j < Fz::FC_KC) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][t][s], b[j][s], acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[w][t * 16 + g * 4 + q][r] = acc[t][q];
+  __syncthreads();
+  MT_PROBE_AT(1, pb, 1);
+  for (int idx = threadIdx.x; idx < Fz::FC_BM * Fz::FC_BN; idx += 256) {
+    const int m = idx / Fz::FC_BN, n = idx - m * Fz::FC_BN;
+    const float s = ((red[0][m][n] + red[1][m][n]) + red[2][m][n]) + red[3][m][n];
+    if (e0 + m < B) slabs[((size_t)i * B + e0 + m) * Fz::F + n0 + n] = s;
+  }
+  MT_PROBE_AT(1, pb, 2);
+}
+
+// Launch the two trunk kernels: conv (optionally stacking) -> act2, fc -> slabs.
+template <int C>
+static inline int launch_nips_trunk(const uint8_t *obs, const StackSrc *st, int B, const float *W1, const float *W2,
+                                    const float *Wfc, int act, float alpha, float *act2, float *act1, float *slabs,
+                                    hipStream_t s) {
+  using Fz = FusedNips<C>;
+  static_assert(Fz::LDS_BYTES <= 64 * 1024, "conv kernel LDS fits the default limit");
+  if (st) {
+    hipLaunchKernelGGL((nips_conv_kernel<C, true>), dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, st->out, *st,
+                       B, W1, W2, act, alpha, act2, act1);
+  } else {
+    hipLaunchKernelGGL((nips_conv_kernel<C, false>), dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, obs,
+                       StackSrc{}, B, W1, W2, act, alpha, act2, act1);
+  }
+  hipLaunchKernelGGL(nips_fc_kernel<C>, dim3(Fz::F / Fz::FC_BN, Fz::ROWS2, (B + Fz::FC_BM - 1) / Fz::FC_BM),
+                     dim3(256), 0, s, act2, B, Wfc, slabs);
+  return MT_OK;
 }
 
 }  // namespace mt

@@ -20,6 +20,7 @@ for step in ${STEPS:-smoke tests bench}; do
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof) run prof 600 bash tools/prof.sh ${PROF_NAME:-prof} ${PROF_ARGS:-} ;;
     pmc) run pmc 600 bash tools/pmc.sh ${PMC_NAME:-pmc} ${PMC_ARGS:-} ;;
+    probe) MANETTE_HIP_LIB=$PWD/manette_amd/libmanette_hip_probe.so run probe 300 python tools/probe.py ${PROBE_ARGS:-} ;;
     variants)  # BENCH_VARIANTS="name1:args1;name2:args2" -> bench_<name>.log each
       IFS=';' read -ra VS <<< "${BENCH_VARIANTS:-}"
       for v in "${VS[@]}"; do run "bench_${v%%:*}" 300 python bench.py --no_cpu_baseline ${v#*:}; done ;;

@@ -1,0 +1,100 @@
+"""Phase timeline of one pipelined rollout step's GPU chain from in-kernel timestamps.
+
+Needs the probe build of the HIP library (s_memrealtime at phase boundaries of every block of
+nips_conv_kernel, nips_fc_kernel and heads_fwd_kernel):
+
+    python -c "from manette_amd import build as b; b.build_hip(out='/root/repo/manette_amd/libmanette_hip_probe.so', defines=['MT_PROBE'])"
+    MANETTE_HIP_LIB=manette_amd/libmanette_hip_probe.so python tools/probe.py [--config pong-nips]
+
+Runs a few warm updates of the bench workload, then one rollout step (whose pipelined chain
+stacks + forwards the next step), and prints, per kernel, when its blocks started (relative to
+the first conv block), the median / max duration of each phase and the gaps between kernels.
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PHASES = {0: ('conv', ['stage', 'conv1', 'conv2', 'act2']),
+          1: ('fc', ['load+mfma', 'reduce+store']),
+          2: ('heads', ['slab sum', 'heads gemv', 'softmax+draw+flag'])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='pong-nips')
+    ap.add_argument('--updates', type=int, default=20)
+    a = ap.parse_args()
+    import torch
+    import bench
+    import train as train_cli
+    from manette_amd import _lib
+    from manette_amd.exploration_policy import ExplorationPolicy
+    from manette_amd.paac import PAACLearner
+    cfg = bench.CONFIGS[a.config]
+    args = bench.build_args(cfg, 5, 'device', 0)
+    explo = ExplorationPolicy(args)
+    nc, ec_ = train_cli.get_network_and_environment_creator(args, explo)
+    L = PAACLearner(nc, ec_, explo, args)
+    L.is_chief = False
+    L.start()
+    lib = _lib.hip()
+    lib.mt_probe_read.restype = C.c_int
+    lib.mt_probe_read.argtypes = [C.c_void_p, C.c_size_t]
+    buf = np.zeros(4 * 512 * 8, dtype=np.uint64)
+    for _ in range(a.updates):
+        L.book.new_update()
+        for t in range(L.max_local_steps):
+            L.step(t)
+        L.update()
+    torch.cuda.synchronize()
+    L.book.new_update()
+    for t in range(L.max_local_steps):  # the last chain armed is the bootstrap forward's
+        L.step(t)
+    torch.cuda.synchronize()
+    buf[:] = 0
+    _lib.check(lib.mt_probe_read(C.c_void_p(buf.ctypes.data), buf.size), 'mt_probe_read')
+    P = buf.reshape(4, 512, 8).astype(np.int64)
+    E = cfg['ec']
+    ro = np.zeros(512 * 4, dtype=np.uint64)
+    lib.mt_probe_read_rollout.restype = C.c_int
+    lib.mt_probe_read_rollout.argtypes = [C.c_void_p, C.c_size_t]
+    _lib.check(lib.mt_probe_read_rollout(C.c_void_p(ro.ctypes.data), ro.size), 'mt_probe_read_rollout')
+    R = ro.reshape(512, 4)[:E].astype(np.int64)
+    nblocks = {0: 9 * E, 1: 16 * 9 * ((E + 31) // 32), 2: E}
+    t0 = P[0, :nblocks[0], 0].min()
+    us = lambda x: x * 0.01  # 100 MHz ticks
+    seen, done = R[:, 0] - t0, R[:, 1] - t0
+    pstart = R[::4, 2] - t0
+    print('pull   per env: seen / done (us):', ' '.join('%d:%.1f/%.1f' % (e, us(seen[e]), us(done[e])) for e in range(E)))
+    print('pull   start %+7.2f us (after the previous heads kernel), env words seen %+7.2f..%+7.2f us '
+          '(median %+7.2f), copies done ..%+7.2f us, copy med %.2f us' % (
+              us(pstart.min()), us(seen.min()), us(seen.max()), us(np.median(seen)), us(done.max()),
+              us(np.median(done - seen))))
+    prev_end = None
+    for k in (0, 1, 2):
+        name, ph = PHASES[k]
+        n = nblocks[k]
+        p = P[k, :n, :len(ph) + 1]
+        start, end = p[:, 0], p[:, -1]
+        line = '%-6s blocks %4d  start %+7.2f..%+7.2f us  end %+7.2f..%+7.2f us  block dur med %.2f max %.2f' % (
+            name, n, us(start.min() - t0), us(start.max() - t0), us(end.min() - t0), us(end.max() - t0),
+            us(np.median(end - start)), us((end - start).max()))
+        if prev_end is not None:
+            line += '  gap after previous kernel %.2f us' % us(start.min() - prev_end)
+        print(line)
+        for j, nm in enumerate(ph):
+            d = p[:, j + 1] - p[:, j]
+            print('    %-20s med %6.2f  p90 %6.2f  max %6.2f us' % (nm, us(np.median(d)), us(np.percentile(d, 90)),
+                                                                     us(d.max())))
+        prev_end = end.max()
+    L.cleanup()
+
+
+if __name__ == '__main__':
+    main()
