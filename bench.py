@@ -198,6 +198,8 @@ def main():
     ap.add_argument('--staging', default='resized', choices=['in_place', 'zero_copy', 'copy', 'pooled', 'resized'])
     ap.add_argument('--no_pipeline', dest='pipeline', action='store_false',
                     help='disable MT_ROLLOUT_PIPELINED (on by default)')
+    ap.add_argument('--no_update_graph', dest='update_graph', action='store_false',
+                    help='launch the update eagerly instead of replaying it as a hipGraph')
     a = ap.parse_args()
 
     import torch
@@ -214,6 +216,7 @@ def main():
     args.env_id_offset = rank * cfg['ec']
     args.staging = a.staging
     args.pipeline = a.pipeline
+    args.update_graph = a.update_graph
 
     from manette_amd.exploration_policy import ExplorationPolicy
     from manette_amd.paac import PAACLearner
@@ -231,8 +234,7 @@ def main():
 
     def one_update():
         learner.book.new_update()
-        for t in range(T):
-            learner.step(t)
+        learner.rollout()
         learner.update()
 
     for _ in range(a.warmup):

@@ -175,6 +175,20 @@ int mt_loss_backward(const mt_net *net, const float *params, const uint8_t *obs,
                      const int32_t *a_idx, const int32_t *r_idx, const float *y, const float *adv,
                      float entropy_beta, float *grad, float *loss_terms, mt_stream_t stream);
 
+/* mt_returns + mt_loss_backward in one call (the update of a rollout, batch = T*E rows t*E+e):
+ * the loss kernel block of row (t, e) runs the n-step scan of env e from T-1 down to t itself
+ * (the same arithmetic as mt_returns, bit for bit) — one launch fewer on the update's critical
+ * path. y and adv ([T][E]) are still written. values: [T][E] = the v the rollout returned.
+ * norm_partials (may be NULL): also write the MT_NORM_PARTIALS global-norm partials of the
+ * gradient, as mt_grad_sumsq(grad, n, 1.0f) would for mt_clip_rmsprop (no data-parallel
+ * all-reduce in between); the sum of squares is taken in the backward's last launch. */
+int mt_returns_loss_backward(const mt_net *net, const float *params, const uint8_t *obs, int T, int E, void *ws,
+                             size_t ws_bytes, const float *pi, const float *rep, const float *values,
+                             const int32_t *a_idx, const int32_t *r_idx, const float *rewards,
+                             const float *masks, const float *v_boot, double gamma, float *y, float *adv,
+                             float entropy_beta, float *grad, float *loss_terms, float *norm_partials,
+                             mt_stream_t stream);
+
 /* ---- global-norm clip + TF1 ApplyRMSProp (A11) ----------------------------------------------
  * Replaces clip_by_global_norm (actor_learner.py:59-63) + ApplyRMSProp (actor_learner.py:47-48,74).
  * mt_grad_sumsq writes MT_NORM_PARTIALS fp32 partial sums of (inv_scale*g)^2.
@@ -308,6 +322,9 @@ int mt_rollout_create(const mt_net *net, int E, int T, void *runner, void *book,
 void mt_rollout_destroy(mt_rollout *ro);
 int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64_t *global_step,
                     mt_stream_t stream);
+/* The whole rollout: mt_rollout_step for t = 0 .. T-1 in one call (paac.py:140-205 without a
+ * return to the caller between macro-steps). */
+int mt_rollout_run(mt_rollout *ro, const float *params, int64_t *global_step, mt_stream_t stream);
 /* Host wall-clock microseconds accumulated by mt_rollout_step, per phase: [0] launch + wait
  * for the sampled indices, [1] emulator step, [2] bookkeeping, [3] upload + preprocess
  * enqueue, [4] number of steps. reset != 0 zeroes the counters. */

@@ -73,6 +73,8 @@ _HIP_SIGS = {
     'mt_sample': (_I, [_P, _P, _I, _I, _I, C.c_uint64, _P, _P, _P, _P, _P]),
     'mt_returns': (_I, [_P, _P, _P, _P, C.c_double, _I, _I, _P, _P, _P]),
     'mt_loss_backward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
+    'mt_returns_loss_backward': (_I, [_P, _P, _P, _I, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _P, C.c_double, _P, _P,
+                                      _F, _P, _P, _P, _P]),
     'mt_grad_sumsq': (_I, [_P, _SZ, _F, _P, _P]),
     'mt_clip_rmsprop': (_I, [_P, _P, _P, _P, _SZ, _P, _P, _F, _F, _F, _F, _I, _F, _P, _P]),
     'mt_preprocess': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
@@ -86,6 +88,7 @@ _HIP_SIGS = {
     'mt_rollout_create': (_I, [_P, _I, _I, _P, _P, C.POINTER(mt_rollout_buffers), C.c_uint64, C.POINTER(_P)]),
     'mt_rollout_destroy': (None, [_P]),
     'mt_rollout_step': (_I, [_P, _P, _I, C.POINTER(C.c_int64), _P]),
+    'mt_rollout_run': (_I, [_P, _P, C.POINTER(C.c_int64), _P]),
     'mt_rollout_stats': (_I, [_P, C.POINTER(C.c_double), _I]),
     'mt_graph_begin': (_I, [_P]),
     'mt_graph_end': (_I, [_P, C.POINTER(_P)]),

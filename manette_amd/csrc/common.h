@@ -124,7 +124,7 @@ struct TrainRows {
 struct StackSrc {
   const uint8_t *prev;    // state slot t [B][84][84][C] (HBM)
   const uint8_t *frames;  // device address of the pinned staging
-  const int32_t *count;   // device address of push_count [B] (pinned)
+  const int32_t *count;   // push_count [B]; NULL: no pushes (out = a copy of prev)
   uint8_t *out;           // state slot t + 1 (the forward's input)
 };
 // forward (mt_forward) with the A3 draw fused into the heads kernel; smp, tr and st may be null.

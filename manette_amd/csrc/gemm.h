@@ -21,6 +21,8 @@
 // operands, so MFMA s multiplies A[r][k] by B[k][r'] with the same k (the k order inside a
 // 16-chunk is permuted, which a sum does not see).
 #pragma once
+#include <algorithm>
+
 #include "common.h"
 
 namespace mt {
@@ -121,18 +123,19 @@ struct Stage {
   }
 };
 
+// One output tile (bx, by) of K-split bz; smem = the dynamic LDS (gemm_lds_bytes). A device
+// function so grouped launches (GemmJob, group_kernel) can run several products in one grid.
 template <class T, class LA, class LB, class EP>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EP ep, int M, int N, int K,
-                                                       int kchunk) {
+__device__ __forceinline__ void gemm_body(const LA &la, const LB &lb, const EP &ep, int M, int N, int K, int kchunk,
+                                          int bx, int by, int bz, float *smem) {
   using SA = LdsShape<LA::KMAJOR, T::BM, T::BK>;
   using SB = LdsShape<LB::KMAJOR, T::BN, T::BK>;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   float *As = smem;
   float *Bs = smem + SA::SIZE;
 
-  const int m0 = blockIdx.x * T::BM;
-  const int n0 = blockIdx.y * T::BN;
-  const int kb = blockIdx.z * kchunk;
+  const int m0 = bx * T::BM;
+  const int n0 = by * T::BN;
+  const int kb = bz * kchunk;
   const int ke = min(K, kb + kchunk);
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -189,9 +192,16 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EP ep, int 
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int m = m0 + (wm * T::TM + i) * 16 + g * 4 + q;
-        if (m < M && n < N) ep(m, n, (int)blockIdx.z, acc[i][j][q]);
+        if (m < M && n < N) ep(m, n, bz, acc[i][j][q]);
       }
     }
+}
+
+template <class T, class LA, class LB, class EP>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EP ep, int M, int N, int K,
+                                                       int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  gemm_body<T>(la, lb, ep, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 template <class T, class LA, class LB>
@@ -229,6 +239,81 @@ inline int launch_gemm(const LA &la, const LB &lb, const EP &ep, int M, int N, i
   dim3 grid(cdiv(M, T::BM), cdiv(N, T::BN), splits);
   hipLaunchKernelGGL((gemm_f32_kernel<T, LA, LB, EP>), grid, dim3(256), lds, s, la, lb, ep, M, N,
                      K, kchunk);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Grouped launches: independent products (and other block-parallel jobs: slab sums, the head
+// weight gradient) that become ready together run as ONE grid — each dependent kernel boundary
+// costs microseconds at these sizes, more than most of the jobs themselves. A job is a value type
+// with blocks() (host and device), lds() (dynamic bytes, host) and run(block, smem) (device).
+// ------------------------------------------------------------------------------------------
+template <class T, class LA, class LB, class EP>
+struct GemmJob {
+  LA la;
+  LB lb;
+  EP ep;
+  int M, N, K, kchunk, gx, gy, gz;
+  __host__ __device__ int blocks() const { return gx * gy * gz; }
+  size_t lds() const { return gemm_lds_bytes<T, LA, LB>(); }
+  __device__ __forceinline__ void run(int id, float *smem) const {
+    const int bx = id % gx, t = id / gx;
+    gemm_body<T>(la, lb, ep, M, N, K, kchunk, bx, t % gy, t / gy, smem);
+  }
+};
+
+// The job launch_gemm<T>(la, lb, ep, M, N, K, splits) would run (same grid, same K chunks).
+template <class T, class LA, class LB, class EP>
+inline GemmJob<T, LA, LB, EP> gemm_job(const LA &la, const LB &lb, const EP &ep, int M, int N, int K, int splits) {
+  const int nchunks = cdiv(K, T::BK);
+  if (splits < 1) splits = 1;
+  if (splits > nchunks) splits = nchunks;
+  const int kchunk = cdiv(nchunks, splits) * T::BK;
+  splits = cdiv(K, kchunk);
+  const bool empty = M <= 0 || N <= 0;
+  return GemmJob<T, LA, LB, EP>{la, lb, ep, M, N, K, kchunk, empty ? 0 : cdiv(M, T::BM), cdiv(N, T::BN), splits};
+}
+
+struct NoJob {
+  __host__ __device__ int blocks() const { return 0; }
+  size_t lds() const { return 0; }
+  __device__ __forceinline__ void run(int, float *) const {}
+};
+
+template <class J1, class J2, class J3>
+__global__ __launch_bounds__(256) void group_kernel(J1 j1, J2 j2, J3 j3) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int id = blockIdx.x;
+  if (id < j1.blocks()) {
+    j1.run(id, smem);
+    return;
+  }
+  id -= j1.blocks();
+  if (id < j2.blocks()) {
+    j2.run(id, smem);
+    return;
+  }
+  j3.run(id - j2.blocks(), smem);
+}
+
+// One grid for up to three jobs (blocks in argument order: put the critical path first).
+template <class J1, class J2 = NoJob, class J3 = NoJob>
+inline int launch_group(hipStream_t s, const J1 &j1, const J2 &j2 = NoJob{}, const J3 &j3 = NoJob{}) {
+  const int nb = j1.blocks() + j2.blocks() + j3.blocks();
+  if (nb == 0) return MT_OK;
+  const size_t lds = std::max(j1.blocks() ? j1.lds() : 0, std::max(j2.blocks() ? j2.lds() : 0, j3.blocks() ? j3.lds() : 0));
+  if (lds > 160 * 1024) {
+    set_error("grouped launch needs %zu bytes of LDS", lds);
+    return MT_ERR_ARG;
+  }
+  static bool attr_set = false;  // per instantiation: allow up to 160 KB of dynamic LDS once
+  if (!attr_set && lds > 64 * 1024) {
+    MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&group_kernel<J1, J2, J3>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((group_kernel<J1, J2, J3>), dim3(nb), dim3(256), lds, s, j1, j2, j3);
   MT_LAUNCHED();
   return MT_OK;
 }

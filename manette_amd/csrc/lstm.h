@@ -72,6 +72,7 @@ static WsLayout lstm_ws_layout(const mt_net *n, int B, LstmWs *X) {
   L.dz = take((size_t)B * n->O);
   L.dH = take((size_t)B * Ar::F);
   L.wslab = take(wslab);
+  L.wslab2 = take(wslab);
   L.total = off;
   if (X) *X = W;
   return L;
@@ -359,6 +360,7 @@ static LstmFrameWs lstm_frame_layout(const mt_net *n, int E, int T) {
   X.L.dz = take(WT * n->O);
   X.L.dH = take(WT * Ar::F);
   X.L.wslab = take(wslab);
+  X.L.wslab2 = take(wslab);
   X.L.total = off;
   return X;
 }

@@ -177,7 +177,7 @@ static void build_layout(mt_net *n) {
 struct WsLayout {
   // per conv layer: act = post-activation conv output, pool = pooled output (if pooled),
   // dact = its gradient (pre-activation after masking), dpool = gradient w.r.t. the pooled output
-  size_t act[4], pool[4], dact[4], dpool[4], fcslab, H, dz, dH, wslab, total;
+  size_t act[4], pool[4], dact[4], dpool[4], fcslab, H, dz, dH, wslab, wslab2, total;
   int fc_splits;
 };
 
@@ -215,8 +215,8 @@ template <class G>
 using TileConvDgrad = typename TileFor<G::CIN, 128>::T;
 
 using TileFc = Tile<32, 64, 2, 2, 64>;       // dense forward, M = batch (small), split-K
-using TileDenseW = Tile<64, 64, 2, 2, 32>;   // dense dW (GEMM-K = batch)
-using TileDenseX = Tile<64, 64, 2, 2, 128>;  // dense dX (GEMM-K = F)
+using TileDenseW = Tile<64, 64, 2, 2, 80>;   // dense dW (GEMM-K = batch: 160 = 2 chunks at ec=32)
+using TileDenseX = Tile<32, 64, 2, 2, 128>;  // dense dX (GEMM-K = F; M = batch: 32-row tiles, 2x the blocks)
 
 static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
   int s = target / (grid_mn > 0 ? grid_mn : 1);
@@ -226,12 +226,19 @@ static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
   return s;
 }
 
+// K splits of a conv weight gradient (GEMM-K = B*OH*OW, tiny M x N): enough that a block walks
+// at most kWgradChunks BK-chunks (each chunk is one load latency: with only M x N / 1024 MFMA
+// tiles per wave the chunk chain, not the MFMA, sets a block's time), capped so the partial slabs
+// stay <= kSlabFloats.
+constexpr int kWgradChunks = 4;
+constexpr size_t kSlabFloats = (size_t)4 << 20;
 template <class G>
 static int conv_wgrad_splits(int B) {
   using T = TileConvWgrad<G>;
   const int M = G::KK + 1;
   const int K = B * G::OH * G::OW;
-  const int s = pick_splits(cdiv(M, T::BM) * cdiv(G::COUT, T::BN), K, T::BK);
+  int s = std::max(pick_splits(cdiv(M, T::BM) * cdiv(G::COUT, T::BN), K, T::BK), cdiv(cdiv(K, T::BK), kWgradChunks));
+  s = std::min<int>(s, (int)std::max<size_t>(kSlabFloats / ((size_t)M * G::COUT), 1));
   return gemm_splits<T>(K, s);
 }
 
@@ -289,6 +296,7 @@ static WsLayout ws_layout(const mt_net *n, int B) {
   L.dz = take((size_t)B * n->O);
   L.dH = take((size_t)B * Ar::F);
   L.wslab = take(wslab);
+  L.wslab2 = take(wslab);  // ping-pong slab regions of consecutive conv layers (trunk_backward)
   L.total = off;
   return L;
 }
@@ -296,50 +304,106 @@ static WsLayout ws_layout(const mt_net *n, int B) {
 // ---------------------------------------------------------------------------------------------
 // Kernels: slab sum, heads forward, loss + heads backward, heads weight gradient.
 // ---------------------------------------------------------------------------------------------
-// out[i] = sum_z P[z*n + i], fixed order. A block owns 64 float4 columns; its 4 waves sum
-// interleaved slab subsets (z = w, w+4, ...) and the 4 partials are added in wave order.
-__global__ __launch_bounds__(256) void sum_slabs_kernel(const float *__restrict__ P, int S, size_t n,
-                                                        float *__restrict__ out) {
-  __shared__ f32x4 part[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// out[i] = sum_z P[z*n + i], fixed order. A block owns kSlabCols float4 columns; its 256 threads
+// are 16 slab subsets x kSlabCols columns, each thread adding slabs z = sub, sub+16, ... with 16
+// loads in flight (a few hundred slabs: one round trip), then the 16 subset sums of a column are
+// added in subset order. smem: 4 KB.
+constexpr int kSlabCols = 16;
+__device__ __forceinline__ void sum_slabs_body(const float *__restrict__ P, int S, size_t n, float *__restrict__ out,
+                                               int bid, float *smem, float *__restrict__ sq_out = nullptr) {
+  f32x4 *part = reinterpret_cast<f32x4 *>(smem);  // [16][kSlabCols]
+  const int col = threadIdx.x % kSlabCols, sub = threadIdx.x / kSlabCols;
   const size_t n4 = n / 4;
-  const size_t c = (size_t)blockIdx.x * 64 + lane;  // float4 column
+  const size_t c = (size_t)bid * kSlabCols + col;  // float4 column
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (c < n4) {
     const f32x4 *p = reinterpret_cast<const f32x4 *>(P) + c;
-    int z = w;
-    for (; z + 12 < S; z += 16) {
-      const f32x4 a0 = p[(size_t)z * n4], a1 = p[(size_t)(z + 4) * n4];
-      const f32x4 a2 = p[(size_t)(z + 8) * n4], a3 = p[(size_t)(z + 12) * n4];
-      acc += a0;
-      acc += a1;
-      acc += a2;
-      acc += a3;
+    int z = sub;
+    for (; z + 16 * 15 < S; z += 256) {
+      f32x4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = p[(size_t)(z + 16 * u) * n4];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u];
     }
-    for (; z < S; z += 4) acc += p[(size_t)z * n4];
+    for (; z < S; z += 16) acc += p[(size_t)z * n4];
   }
-  part[w][lane] = acc;
+  part[sub * kSlabCols + col] = acc;
   __syncthreads();
-  if (w == 0 && c < n4) {
-    const f32x4 t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  double sq = 0.0;  // sq_out: sum of the squares of this block's outputs (global-norm partial)
+  if (sub == 0 && c < n4) {
+    f32x4 t = part[col];
+#pragma unroll
+    for (int u = 1; u < 16; ++u) t += part[u * kSlabCols + col];
     reinterpret_cast<f32x4 *>(out)[c] = t;
+    sq = (double)(t[0] * t[0]) + (double)(t[1] * t[1]) + (double)(t[2] * t[2]) + (double)(t[3] * t[3]);
   }
   // scalar tail (n not a multiple of 4)
-  if (blockIdx.x == 0) {
+  if (bid == 0) {
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += 256) {
       float t = 0.f;
       for (int z = 0; z < S; ++z) t += P[(size_t)z * n + i];
       out[i] = t;
+      sq += (double)(t * t);
     }
+  }
+  if (sq_out) {
+    double *red = reinterpret_cast<double *>(smem);
+    sq = wave_sum_d(sq);
+    __syncthreads();  // part[] is no longer read
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) *sq_out = (float)(red[0] + red[1] + red[2] + red[3]);
   }
 }
 
+// Global-norm partials of g outside [skip_b, skip_e) (float offsets, multiples of 4), as a job of a
+// grouped launch: block b writes partials[b] = sum of the squares of its grid-stride share
+// (sumsq_kernel's arithmetic; the grid of this job is fixed, so the partials are deterministic).
+struct SumsqJob {
+  const float *g = nullptr;
+  size_t n = 0, skip_b = 0, skip_e = 0;
+  float *partials = nullptr;
+  int nb = 0;
+  __host__ __device__ int blocks() const { return nb; }
+  size_t lds() const { return 64; }
+  __device__ __forceinline__ void run(int bid, float *smem) const {
+    double acc = 0.0;
+    const size_t n4 = n / 4, sb = skip_b / 4, se = skip_e / 4;
+    const size_t stride = (size_t)nb * 256;
+    for (size_t i = (size_t)bid * 256 + threadIdx.x; i < n4; i += stride) {
+      if (i >= sb && i < se) continue;
+      const f32x4 v = reinterpret_cast<const f32x4 *>(g)[i];
+      acc += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
+    }
+    for (size_t i = n4 * 4 + (size_t)bid * 256 + threadIdx.x; i < n; i += stride) acc += (double)(g[i] * g[i]);
+    double *red = reinterpret_cast<double *>(smem);
+    acc = wave_sum_d(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[bid] = (float)(red[0] + red[1] + red[2] + red[3]);
+  }
+};
+
+// Slab sum as a job of a grouped launch (gemm.h); n = 0: no job.
+struct SlabJob {
+  const float *P = nullptr;
+  int S = 0;
+  size_t n = 0;
+  float *out = nullptr;
+  float *sq = nullptr;  // optional: per-block global-norm partials sq[block]
+  __host__ __device__ int blocks() const {
+    const size_t b = (n / 4 + kSlabCols - 1) / kSlabCols;
+    return n ? (int)(b ? b : 1) : 0;
+  }
+  size_t lds() const { return 4096; }
+  __device__ __forceinline__ void run(int id, float *smem) const {
+    sum_slabs_body(P, S, n, out, id, smem, sq ? sq + id : nullptr);
+  }
+};
+
 static int sum_slabs(const float *P, int S, size_t n, float *out, hipStream_t s) {
-  if (n == 0) return MT_OK;
-  const int blocks = (int)std::max<size_t>((n / 4 + 63) / 64, 1);
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3(blocks), dim3(256), 0, s, P, S, n, out);
-  MT_LAUNCHED();
-  return MT_OK;
+  return launch_group(s, SlabJob{P, S, n, out});
 }
 
 struct HeadParams {
@@ -380,6 +444,7 @@ __device__ __forceinline__ float wave_softmax(float x, int lane, int n) {
 }
 
 constexpr int kMaxHeads = 64;  // 1 + A + R <= 64
+constexpr int kMaxScan = 1024;  // max t_max of the fused n-step scan (mt_returns_loss_backward)
 
 // draw_index (common.h) over probabilities held in lanes [0, n): same order and rounding.
 __device__ __forceinline__ int wave_draw(float p, int n, double u) {
@@ -538,26 +603,64 @@ __device__ __forceinline__ float head_softmax_grad(float p, int lane, int n, int
 }
 
 // One workgroup per row b: head gradients dz[b][0..O) and dH[b][f] = act'(H) * sum_o dz_o W[f][o].
+// Optional n-step scan inside the loss kernel (mt_returns_loss_backward): row b = t*E + e.
+struct ReturnsSrc {
+  const float *r = nullptr, *mask = nullptr, *VT = nullptr;  // r / mask [T][E] (host-mapped ok)
+  double gamma = 0.0;
+  int T = 0, E = 0;
+  float *y_out = nullptr, *adv_out = nullptr;
+};
+
+// returns_kernel's arithmetic for row b = (t, e): R from T-1 down to t, bit-identical to
+// mt_returns. All threads load the rewards / masks of steps t.. (one round trip), thread 0 scans.
+// Called by the whole block.
+__device__ __forceinline__ void row_return(const ReturnsSrc &rs, const float *__restrict__ V, int b, float *ya,
+                                           float *buf) {
+#pragma clang fp contract(off)
+  const int T = rs.T, E = rs.E;
+  const int t = b / E, e = b - t * E, n = T - t;  // steps t .. T-1
+  for (int k = threadIdx.x; k < n; k += 256) {
+    buf[2 * k] = rs.r[(size_t)(t + k) * E + e];
+    buf[2 * k + 1] = rs.mask[(size_t)(t + k) * E + e];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float g32 = __fmul_rn((float)rs.gamma, rs.VT[e]);
+    double R = (double)buf[2 * (n - 1)] + (double)g32 * (double)buf[2 * (n - 1) + 1];
+    const double gd = rs.gamma;
+    for (int k = n - 2; k >= 0; --k) R = (double)buf[2 * k] + (gd * R) * (double)buf[2 * k + 1];
+    ya[0] = (float)R;
+    ya[1] = (float)(R - (double)V[b]);
+    rs.y_out[b] = ya[0];
+    rs.adv_out[b] = ya[1];
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void loss_bwd_kernel(
     HeadParams hp, const float *__restrict__ H, const float *__restrict__ pi,
     const float *__restrict__ rep, const float *__restrict__ v, const int32_t *__restrict__ a_idx,
     const int32_t *__restrict__ r_idx, const float *__restrict__ y, const float *__restrict__ adv,
     float beta, float scale, float temp, int act, float alpha, float *__restrict__ dz,
-    float *__restrict__ dH, float *__restrict__ loss_terms) {
+    float *__restrict__ dH, float *__restrict__ loss_terms, ReturnsSrc rs) {
   __shared__ float dzs[kMaxHeads];
+  __shared__ float ya[2];
+  __shared__ float buf[2 * kMaxScan];
   const int b = blockIdx.x;
   const int A = hp.A, R = hp.R, O = 1 + A + R, F = hp.F;
+  if (rs.r) row_return(rs, v, b, ya, buf);
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    const float ad = adv[b];
+    const float ad = rs.r ? ya[1] : adv[b];
+    const float yb = rs.r ? ya[0] : y[b];
     const float pa = lane < A ? pi[(size_t)b * A + lane] : 0.f;
     const float pr = lane < R ? rep[(size_t)b * R + lane] : 0.f;
     float ent_a, ls_a, ent_r, ls_r;
     const float ga = head_softmax_grad(pa, lane, A, a_idx[b], ad, beta, scale, temp, &ent_a, &ls_a);
     const float gr = head_softmax_grad(pr, lane, R, r_idx[b], ad, beta, scale, temp, &ent_r, &ls_r);
-    const float diff = y[b] - v[b];
+    const float diff = yb - v[b];
     // d/dv of scale * 0.25 * (y - v)^2  (policy_v_network.py:25-26)
-    const float gv = scale * 0.25f * 2.0f * (v[b] - y[b]);
+    const float gv = scale * 0.25f * 2.0f * (v[b] - yb);
     if (lane == 0) dzs[0] = gv;
     if (lane < A) dzs[1 + lane] = ga;
     if (lane < R) dzs[1 + A + lane] = gr;
@@ -586,16 +689,15 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
 // staged in LDS, the 4 waves take contiguous quarters of the rows (H read coalesced: consecutive
 // lanes = consecutive features, 4 independent accumulators per lane), and the 4 wave partials are
 // added in wave order through LDS (deterministic).
-__global__ __launch_bounds__(256) void head_wgrad_kernel(const float *__restrict__ H,
-                                                         const float *__restrict__ dz, int B, int F,
-                                                         int A, int R, float *__restrict__ gc,
-                                                         float *__restrict__ ga, float *__restrict__ gr) {
-  extern __shared__ __attribute__((aligned(16))) float dzs[];  // [B] column o, then [4][64] partials
-  const int O = 1 + A + R, o = blockIdx.y;
+__device__ __forceinline__ void head_wgrad_body(const float *__restrict__ H, const float *__restrict__ dz, int B,
+                                                int F, int A, int R, float *__restrict__ gc, float *__restrict__ ga,
+                                                float *__restrict__ gr, int bx, int o, float *dzs) {
+  // dzs: [B] column o, then [4][64] partials
+  const int O = 1 + A + R;
   for (int i = threadIdx.x; i < B; i += 256) dzs[i] = dz[(size_t)i * O + o];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int f = blockIdx.x * 64 + lane;  // f == F is the bias row
+  const int f = bx * 64 + lane;  // f == F is the bias row
   const int q = (B + 3) / 4, b0 = w * q, b1 = min(B, b0 + q);
   float a[4] = {0.f, 0.f, 0.f, 0.f};
   if (f <= F) {
@@ -623,6 +725,19 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const float *__restrict
     gr[(size_t)f * R + (o - 1 - A)] = acc;
 }
 
+// The head weight gradient as a job of a grouped launch: block (f chunk of 64, output o).
+struct HeadWgradJob {
+  const float *H, *dz;
+  int B, F, A, R;
+  float *gc, *ga, *gr;
+  __host__ __device__ int gx() const { return (F + 1 + 63) / 64; }
+  __host__ __device__ int blocks() const { return gx() * (1 + A + R); }
+  size_t lds() const { return sizeof(float) * ((size_t)B + 4 * 64); }
+  __device__ __forceinline__ void run(int id, float *smem) const {
+    head_wgrad_body(H, dz, B, F, A, R, gc, ga, gr, id % gx(), id / gx(), smem);
+  }
+};
+
 // ---------------------------------------------------------------------------------------------
 // Layer drivers
 // ---------------------------------------------------------------------------------------------
@@ -636,38 +751,39 @@ static int conv_forward(const void *X, const float *Wt, const float *bias, float
   return launch_gemm<T>(la, lb, ep, B * G::OH * G::OW, G::COUT, G::KK, 1, s);
 }
 
-// dW (+db) of a conv: [im2col(X), 1]^T . dY  -> grad[(KK+1) x COUT] (weights then biases).
+// dW (+db) of a conv: [im2col(X), 1]^T . dY  -> grad[(KK+1) x COUT] (weights then biases), as a
+// GEMM job into K-split slabs (one split: straight into gwb, [M][COUT] = the S = 1 slab layout)
+// and the slab-sum job that finishes it (no job when unsplit).
 template <class G, bool U8>
-static int conv_wgrad(const void *X, const float *dY, float *slab, float *gwb, int B,
-                      hipStream_t s) {
+struct WgradJobs {
+  GemmJob<TileConvWgrad<G>, LdIm2colT<G, U8>, LdColMajor, EpSlab> gemm;
+  SlabJob sum;
+};
+template <class G, bool U8>
+static WgradJobs<G, U8> conv_wgrad_jobs(const void *X, const float *dY, float *slab, float *gwb, int B) {
   using T = TileConvWgrad<G>;
   const int M = G::KK + 1, K = B * G::OH * G::OW;
   const int S = conv_wgrad_splits<G>(B);
   LdIm2colT<G, U8> la{reinterpret_cast<const typename InElem<U8>::T *>(X)};
   LdColMajor lb{dY, G::COUT, -1};
-  if (S == 1) return launch_gemm<T>(la, lb, EpStore{gwb, G::COUT}, M, G::COUT, K, 1, s);
-  int rc = launch_gemm<T>(la, lb, EpSlab{slab, M, G::COUT}, M, G::COUT, K, S, s);
-  if (rc) return rc;
-  return sum_slabs(slab, S, (size_t)M * G::COUT, gwb, s);
+  if (S == 1) return {gemm_job<T>(la, lb, EpSlab{gwb, M, G::COUT}, M, G::COUT, K, 1), SlabJob{}};
+  return {gemm_job<T>(la, lb, EpSlab{slab, M, G::COUT}, M, G::COUT, K, S), SlabJob{slab, S, (size_t)M * G::COUT, gwb}};
 }
 
-// dX of a conv (transposed-conv gather), masked by the activation derivative of X.
+// dX of a conv (transposed-conv gather), masked by the activation derivative of X, as a GEMM job.
 template <class G>
-static int conv_dgrad(const float *dY, const float *Wt, const float *Xact, float *dX, int B,
-                      int act, float alpha, hipStream_t s) {
+static auto conv_dgrad_job(const float *dY, const float *Wt, const float *Xact, float *dX, int B, int act,
+                           float alpha) {
   using T = TileConvDgrad<G>;
   if constexpr (PhaseGeom<G>::OK) {  // stride phases: K / (S*S), no multiplications by holes
     constexpr int S2 = G::S * G::S;
     const int mp = cdiv(B * PhaseGeom<G>::HQ * PhaseGeom<G>::WQ, T::BM) * T::BM;
-    LdConvBwdAPhase<G> la{dY, mp, B};
-    LdConvBwdBPhase<G> lb{Wt, mp / T::BM};
-    EpMaskedPhase<G> ep{dX, Xact, mp, B, act, alpha};
-    return launch_gemm<T>(la, lb, ep, S2 * mp, G::CIN, PhaseGeom<G>::KP, 1, s);
+    return gemm_job<T>(LdConvBwdAPhase<G>{dY, mp, B}, LdConvBwdBPhase<G>{Wt, mp / T::BM},
+                       EpMaskedPhase<G>{dX, Xact, mp, B, act, alpha}, S2 * mp, G::CIN, PhaseGeom<G>::KP, 1);
+  } else {
+    return gemm_job<T>(LdConvBwdA<G>{dY}, LdConvBwdB<G>{Wt}, EpMasked{dX, Xact, G::CIN, act, alpha},
+                       B * G::H * G::W, G::CIN, G::KH * G::KW * G::COUT, 1);
   }
-  LdConvBwdA<G> la{dY};
-  LdConvBwdB<G> lb{Wt};
-  EpMasked ep{dX, Xact, G::CIN, act, alpha};
-  return launch_gemm<T>(la, lb, ep, B * G::H * G::W, G::CIN, G::KH * G::KW * G::COUT, 1, s);
 }
 
 #define MT_TRY(x)              \
@@ -772,27 +888,59 @@ static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, 
 // Backward through conv layer I given the gradient w.r.t. its post-activation output, already
 // masked (ws + L.dact[I]): weight gradient, then (I > 0) the masked gradient of its input,
 // routed through the previous layer's pool when there is one.
+// Conv layers I .. 0 of the backward, top down: one grouped launch per layer — its dX (the
+// critical path, first), its dW GEMM and `pending` (the slab sum of layer I+1's dW) — then
+// conv1's slab sum. Layer I's slabs live in region I % 2 (wslab / wslab2), so the slab sum of
+// layer I+1 reads the other region while layer I's dW GEMM writes its own.
+// Optional global-norm partials of the whole gradient written by the backward's last launch
+// (world == 1: no all-reduce between the backward and the clip, so mt_grad_sumsq is not needed).
+struct NormOut {
+  float *partials = nullptr;  // [MT_NORM_PARTIALS]
+  size_t n = 0;               // gradient floats
+};
+
 template <class Ar, int I>
 static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
-                          const WsLayout &L, float *grad, hipStream_t s) {
+                          const WsLayout &L, float *grad, hipStream_t s, SlabJob pending = SlabJob{},
+                          const NormOut &no = NormOut{}) {
   using G = LayerG<Ar, I>;
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
   const void *x = I == 0 ? (const void *)obs : (const void *)layer_out<Ar, (I > 0 ? I - 1 : 0)>(ws, L);
-  MT_TRY((conv_wgrad<G, I == 0>(x, ws + L.dact[I], ws + L.wslab, grad + n->off_conv[I], B, s)));
+  const auto wg = conv_wgrad_jobs<G, I == 0>(x, ws + L.dact[I], ws + (I % 2 ? L.wslab2 : L.wslab),
+                                             grad + n->off_conv[I], B);
   if constexpr (I > 0) {
     constexpr int J = I - 1;
     using GJ = LayerG<Ar, J>;
     if constexpr (pooled<Ar, J>()) {
-      MT_TRY((conv_dgrad<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J], ws + L.dpool[J], B, act, al, s)));
+      MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J], ws + L.dpool[J], B,
+                                               act, al),
+                          wg.gemm, pending));
       MT_TRY(maxpool_bwd(ws + L.act[J], ws + L.pool[J], ws + L.dpool[J], B, GJ::OH, GJ::OW, GJ::COUT,
                          ws + L.dact[J], s));
     } else {
-      MT_TRY((conv_dgrad<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B, act, al, s)));
+      MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
+                                               act, al),
+                          wg.gemm, pending));
     }
-    return trunk_backward<Ar, J>(n, P, obs, B, ws, L, grad, s);
+    return trunk_backward<Ar, J>(n, P, obs, B, ws, L, grad, s, wg.sum, no);
+  } else {
+    MT_TRY(launch_group(s, wg.gemm, pending));
+    SlabJob last = wg.sum;
+    if (no.partials && last.blocks() <= MT_NORM_PARTIALS / 2) {
+      // conv1's slab sum writes the norm partials of its region, the rest of the gradient (complete
+      // since the previous launches) is summed beside it: partials [0, slab blocks) + the rest
+      last.sq = no.partials;
+      const size_t b0 = n->off_conv[0], b1 = b0 + last.n;
+      SumsqJob rest{grad, no.n, last.blocks() ? b0 : 0, last.blocks() ? b1 : 0, no.partials + last.blocks(),
+                    MT_NORM_PARTIALS - last.blocks()};
+      return launch_group(s, last, rest);
+    }
+    MT_TRY(launch_group(s, last));
+    if (no.partials)  // (no room for the fused form: all partials from the complete gradient)
+      return launch_group(s, SumsqJob{grad, no.n, 0, 0, no.partials, MT_NORM_PARTIALS});
+    return MT_OK;
   }
-  return MT_OK;
 }
 
 // Per-row conv buffers of a layout moved to start at row `row0` (the dense/head buffers stay).
@@ -885,66 +1033,80 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
 // overwritten by the backward (no accumulation), so grad is not cleared: its alignment padding
 // must be zero once (include/manette_hip.h, mt_loss_backward).
 template <class Ar>
-static int heads_backward(const mt_net *n, const float *P, int B, float *ws, const WsLayout &L, const float *pi,
-                          const float *rep, const float *v, const int32_t *a_idx, const int32_t *r_idx,
-                          const float *y, const float *adv, float beta, float *grad, float *loss_terms,
-                          hipStream_t s) {
-  const int act = n->cfg.activation;
-  const float al = n->cfg.alpha_leaky;
+static int loss_bwd_launch(const mt_net *n, const float *P, int B, float *ws, const WsLayout &L, const float *pi,
+                           const float *rep, const float *v, const int32_t *a_idx, const int32_t *r_idx,
+                           const float *y, const float *adv, float beta, float *loss_terms, hipStream_t s,
+                           const ReturnsSrc &rs = ReturnsSrc{}) {
   // loss scaling 5.0 and the batch mean (policy_v_network.py:70-74): scale = 5/B.
   const float scale = 5.0f / (float)B;
   HeadParams hp = head_params(n, P);
-  hipLaunchKernelGGL(loss_bwd_kernel, dim3(B), dim3(256), 0, s, hp, ws + L.H, pi, rep, v, a_idx,
-                     r_idx, y, adv, beta, scale, n->cfg.softmax_temp, act, al, ws + L.dz, ws + L.dH,
-                     loss_terms);
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3(B), dim3(256), 0, s, hp, ws + L.H, pi, rep, v, a_idx, r_idx, y, adv,
+                     beta, scale, n->cfg.softmax_temp, n->cfg.activation, n->cfg.alpha_leaky, ws + L.dz, ws + L.dH,
+                     loss_terms, rs);
   MT_LAUNCHED();
-  {
-    static bool wg_attr = false;
-    if (!wg_attr) {
-      MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&head_wgrad_kernel),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      wg_attr = true;
-    }
-    const size_t lds = sizeof(float) * ((size_t)B + 4 * 64);
-    if (lds > 160 * 1024) {
-      set_error("batch %d exceeds the head-gradient LDS stage", B);
-      return MT_ERR_ARG;
-    }
-    hipLaunchKernelGGL(head_wgrad_kernel, dim3(cdiv(Ar::F + 1, 64), n->O), dim3(256), lds, s, ws + L.H, ws + L.dz,
-                       B, Ar::F, n->cfg.num_actions, n->cfg.num_reps, grad + n->off_critic, grad + n->off_actor,
-                       grad + n->off_rep);
-    MT_LAUNCHED();
-  }
   return MT_OK;
 }
 
 template <class Ar>
+static HeadWgradJob head_wgrad_job(const mt_net *n, int B, float *ws, const WsLayout &L, float *grad) {
+  return HeadWgradJob{ws + L.H, ws + L.dz, B, Ar::F, n->cfg.num_actions, n->cfg.num_reps,
+                      grad + n->off_critic, grad + n->off_actor, grad + n->off_rep};
+}
+
+template <class Ar>
+static int heads_backward(const mt_net *n, const float *P, int B, float *ws, const WsLayout &L, const float *pi,
+                          const float *rep, const float *v, const int32_t *a_idx, const int32_t *r_idx,
+                          const float *y, const float *adv, float beta, float *grad, float *loss_terms,
+                          hipStream_t s) {
+  if (sizeof(float) * ((size_t)B + 4 * 64) > 160 * 1024) {
+    set_error("batch %d exceeds the head-gradient LDS stage", B);
+    return MT_ERR_ARG;
+  }
+  MT_TRY(loss_bwd_launch<Ar>(n, P, B, ws, L, pi, rep, v, a_idx, r_idx, y, adv, beta, loss_terms, s));
+  return launch_group(s, head_wgrad_job<Ar>(n, B, ws, L, grad));
+}
+
+// Backward of the non-LSTM archs as grouped launches (gemm.h, launch_group): each launch runs
+// every product whose inputs the previous one completed — loss | dense dX + dense dW + head dW |
+// per conv layer I (top down): conv dX + conv dW + the slab sum of layer I+1's dW | conv1's slab
+// sum — 2 + NCONV launches (+ max-pool backward kernels) instead of two or three per layer.
+template <class Ar>
 static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
                          const float *pi, const float *rep, const float *v, const int32_t *a_idx,
                          const int32_t *r_idx, const float *y, const float *adv, float beta,
-                         float *grad, float *loss_terms, hipStream_t s) {
+                         float *grad, float *loss_terms, hipStream_t s, const ReturnsSrc &rs = ReturnsSrc{},
+                         const NormOut &no = NormOut{}) {
   const WsLayout L = ws_layout<Ar>(n, B);
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
-  MT_TRY(heads_backward<Ar>(n, P, B, ws, L, pi, rep, v, a_idx, r_idx, y, adv, beta, grad, loss_terms, s));
+  if (sizeof(float) * ((size_t)B + 4 * 64) > 160 * 1024) {
+    set_error("batch %d exceeds the head-gradient LDS stage", B);
+    return MT_ERR_ARG;
+  }
+  MT_TRY(loss_bwd_launch<Ar>(n, P, B, ws, L, pi, rep, v, a_idx, r_idx, y, adv, beta, loss_terms, s, rs));
   constexpr int K = Ar::NCONV - 1;
   const float *flat = layer_out<Ar, K>(ws, L);
   const float *Wfc = P + n->off_fc;
   // dense dW, db: [flat, 1]^T . dH -> grad[(FLAT+1) x F]
-  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
-                                  EpStore{grad + n->off_fc, Ar::F}, Ar::FLAT + 1, Ar::F, B, 1, s)));
+  const auto dw = gemm_job<TileDenseW>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
+                                       EpStore{grad + n->off_fc, Ar::F}, Ar::FLAT + 1, Ar::F, B, 1);
+  const HeadWgradJob hw = head_wgrad_job<Ar>(n, B, ws, L, grad);
   // dense dX: dH . W^T, masked by the last conv's (pooled) activation, then through its pool
   if constexpr (pooled<Ar, K>()) {
     using GK = LayerG<Ar, K>;
-    MT_TRY((launch_gemm<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
-                                    EpMasked{ws + L.dpool[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1, s)));
+    MT_TRY(launch_group(s, gemm_job<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+                                                EpMasked{ws + L.dpool[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT,
+                                                Ar::F, 1),
+                        dw, hw));
     MT_TRY(maxpool_bwd(ws + L.act[K], ws + L.pool[K], ws + L.dpool[K], B, GK::OH, GK::OW, GK::COUT,
                        ws + L.dact[K], s));
   } else {
-    MT_TRY((launch_gemm<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
-                                    EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1, s)));
+    MT_TRY(launch_group(s, gemm_job<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+                                                EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT,
+                                                Ar::F, 1),
+                        dw, hw));
   }
-  return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s);
+  return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s, SlabJob{}, no);
 }
 
 }  // namespace mt
@@ -1171,6 +1333,46 @@ extern "C" int mt_loss_backward(const mt_net *net, const float *params, const ui
     else
       return backward_impl<Ar>(net, params, obs, batch, (float *)ws, pi, rep, v, a_idx, r_idx, y, adv,
                                entropy_beta, grad, loss_terms, (hipStream_t)stream);
+  });
+  return MT_OK;
+}
+
+extern "C" int mt_returns_loss_backward(const mt_net *net, const float *params, const uint8_t *obs, int T, int E,
+                                        void *ws, size_t ws_bytes, const float *pi, const float *rep,
+                                        const float *values, const int32_t *a_idx, const int32_t *r_idx,
+                                        const float *rewards, const float *masks, const float *v_boot, double gamma,
+                                        float *y, float *adv, float entropy_beta, float *grad, float *loss_terms,
+                                        float *norm_partials, mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && obs && ws && pi && rep && values && a_idx && r_idx && rewards && masks && v_boot &&
+                   y && adv && grad,
+               "null argument");
+  MT_CHECK_ARG(T >= 1 && E >= 1 && T <= kMaxScan, "T=%d (<= %d) and E=%d must be >= 1", T, kMaxScan, E);
+  const int batch = T * E;
+  MT_ARCH_SWITCH(net, {
+    if constexpr (Ar::LSTM) {
+      set_error("mt_returns_loss_backward: the LSTM arch trains through mt_lstm_frames_backward");
+      return MT_ERR_UNSUPPORTED;
+    } else {
+      const WsLayout L = ws_layout<Ar>(net, batch);
+      if (ws_bytes < L.total * sizeof(float)) {
+        set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
+        return MT_ERR_WORKSPACE;
+      }
+      ReturnsSrc rs;
+      rs.r = rewards;
+      rs.mask = masks;
+      rs.VT = v_boot;
+      rs.gamma = gamma;
+      rs.T = T;
+      rs.E = E;
+      rs.y_out = y;
+      rs.adv_out = adv;
+      NormOut no;
+      no.partials = norm_partials;
+      no.n = net->nparams;
+      return backward_impl<Ar>(net, params, obs, batch, (float *)ws, pi, rep, values, a_idx, r_idx, y, adv,
+                               entropy_beta, grad, loss_terms, (hipStream_t)stream, rs, no);
+    }
   });
   return MT_OK;
 }

@@ -32,6 +32,7 @@ struct mt_rollout {
   uint32_t *seq_dev, *status_dev;
   uint32_t *ready_dev = nullptr;  // [E] pair-ready flags (device address of b.ready_host)
   uint32_t fwd_seq = 0;           // sequence number of the last enqueued forward + draw
+  int64_t rollouts = 0;           // completed rollouts (calls with t = T-1)
   // stack_fwd: per-env ready words the emulator threads store (mh_runner_set_ready) and the
   // tagged (a, r) words the heads kernel stores (SampleArgs::packed); pinned, device-mapped
   uint32_t *env_ready_host = nullptr, *env_ready_dev = nullptr;
@@ -244,11 +245,15 @@ namespace {
 // indices land in idx[.][t] and the [2][E] pair; ev[t & 1] marks the pair ready.
 // stacked: state slot t is built from slot t-1 + step t-1's pushes inside the forward's conv
 // kernel (fused mt_preprocess_resized; ro->stack_fwd).
+// t == 0 && stacked: slot 0 <- slot T of the previous rollout inside the forward (the copy of
+// paac.py's states carrying over, otherwise a separate copy on the update's critical path).
 int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, bool stacked = false) {
   const mt_rollout_buffers &b = ro->b;
   const int E = ro->E, T = ro->T;
   const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
-  const StackSrc st{b.states + (size_t)(t - 1) * slot, ro->frames_hbm, ro->count_hbm, b.states + (size_t)t * slot};
+  const StackSrc st = t > 0 ? StackSrc{b.states + (size_t)(t - 1) * slot, ro->frames_hbm, ro->count_hbm,
+                                       b.states + (size_t)t * slot}
+                            : StackSrc{b.states + (size_t)T * slot, nullptr, nullptr, b.states};
   int32_t *a_d = b.idx + (size_t)t * E, *r_d = b.idx + (size_t)T * E + (size_t)t * E;
   SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
   smp.ready = ro->ready_dev;
@@ -347,7 +352,8 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   // 1. forward + draw of step t, unless a previous call already enqueued it
   if (t == 0 || !ro->pipelined) ro->armed_upto = -1;  // a new rollout (parameters changed)
   if (ro->armed_upto < t) {
-    MT_TRY_(enqueue_forward(ro, params, t, s));
+    // stack_fwd: after a completed rollout, slot 0 is taken from slot T inside this forward
+    MT_TRY_(enqueue_forward(ro, params, t, s, t == 0 && ro->stack_fwd && ro->rollouts > 0));
     ro->armed_upto = t;
   }
   // 2. pipelined: arm steps up to t + depth (at most T) while the GPU works on step t, so the
@@ -441,7 +447,14 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   ro->acc[2] += t3 - t2;
   ro->acc[3] += t4 - t3;
   ro->acc[4] += 1;
+  if (rc == MT_OK && t == T - 1) ro->rollouts += 1;
   return rc;
+}
+
+extern "C" int mt_rollout_run(mt_rollout *ro, const float *params, int64_t *global_step, mt_stream_t stream) {
+  MT_CHECK_ARG(ro, "null argument");
+  for (int t = 0; t < ro->T; ++t) MT_TRY_(mt_rollout_step(ro, params, t, global_step, stream));
+  return MT_OK;
 }
 
 extern "C" int mt_rollout_stats(mt_rollout *ro, double *out5, int reset) {

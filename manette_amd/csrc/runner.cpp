@@ -83,11 +83,6 @@ struct mh_runner {
   int chunk_base[kMaxChunks];
   int nchunks = 0;
 
-  // FramePool max + nearest resize of one push into its 84x84xdepth staging frame
-  // (atari_emulator.py:79-88 + the imresize of :113-124): rows[q] / cols[x] are the LUTs. Per
-  // output row: SSE max of the two source rows into a buffer, then each 16-byte output chunk is
-  // OR-ed from pshufb of up to 3 source vectors (gray and RGB alike); the next row's source lines
-  // are prefetched while this one is gathered.
   // d (16-byte aligned, n a multiple of 16 — a final frame: 7056 * depth) <- s with streaming
   // stores; the caller fences (sfence) before publishing d
   static void stream_copy(uint8_t *d, const uint8_t *s, size_t n) {
@@ -95,19 +90,27 @@ struct mh_runner {
       _mm_stream_si128(reinterpret_cast<__m128i *>(d + x), _mm_load_si128(reinterpret_cast<const __m128i *>(s + x)));
   }
 
+  // FramePool max + nearest resize of one push into its 84x84xdepth staging frame
+  // (atari_emulator.py:79-88 + the imresize of :113-124): rows[q] / cols[x] are the LUTs. Per
+  // output row: SSE max of the two source rows into a buffer, then each 16-byte output chunk is
+  // OR-ed from pshufb of up to 3 source vectors (gray and RGB alike); the source lines of the row
+  // PD rows ahead are prefetched while this one is gathered.
   void resize_push(uint8_t *d, const uint8_t *s0, const uint8_t *s1) const {
     const int rb = (int)row_bytes, ob = 84 * depth;
     alignas(16) uint8_t m[480 + 64];
     for (int x = rb; x < rb + 64; x += 16) _mm_store_si128(reinterpret_cast<__m128i *>(m + x), _mm_setzero_si128());
+    constexpr int PD = 1;  // rows prefetched ahead
+    auto prefetch_row = [&](int q) {
+      const uint8_t *na = s0 + (size_t)rows[q] * row_bytes, *nb = s1 + (size_t)rows[q] * row_bytes;
+      for (int x = 0; x < rb; x += 64) {
+        _mm_prefetch(reinterpret_cast<const char *>(na + x), _MM_HINT_T0);
+        _mm_prefetch(reinterpret_cast<const char *>(nb + x), _MM_HINT_T0);
+      }
+    };
+    for (int q = 0; q < PD; ++q) prefetch_row(q);
     for (int q = 0; q < 84; ++q) {
       const uint8_t *a = s0 + (size_t)rows[q] * row_bytes, *b = s1 + (size_t)rows[q] * row_bytes;
-      if (q + 1 < 84) {
-        const uint8_t *na = s0 + (size_t)rows[q + 1] * row_bytes, *nb = s1 + (size_t)rows[q + 1] * row_bytes;
-        for (int x = 0; x < rb; x += 64) {
-          _mm_prefetch(reinterpret_cast<const char *>(na + x), _MM_HINT_T0);
-          _mm_prefetch(reinterpret_cast<const char *>(nb + x), _MM_HINT_T0);
-        }
-      }
+      if (q + PD < 84) prefetch_row(q + PD);
       for (int x = 0; x < rb; x += 16)
         _mm_store_si128(reinterpret_cast<__m128i *>(m + x),
                         _mm_max_epu8(_mm_loadu_si128(reinterpret_cast<const __m128i *>(a + x)),

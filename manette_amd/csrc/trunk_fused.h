@@ -92,14 +92,16 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
       for (int q = threadIdx.x; q < Fz::IN_BYTES / 16; q += 256) dst[q] = src[q];
     }
     // one round trip for the common case: the push count and push 0's rows with the prev rows
-    if (threadIdx.x == 0) s_p = st.count[e];
-    {
+    // (count == NULL: no pushes, the new state is a copy of prev — slot 0 <- slot T of the
+    // previous rollout, mt_rollout_step)
+    if (threadIdx.x == 0) s_p = st.count ? st.count[e] : 0;
+    if (st.count) {
       const size_t f0 = ((size_t)4 * e * 84 + 8 * i) * 84 * Fz::D;  // push 0 = slot 4e
       const uint4 *fs = reinterpret_cast<const uint4 *>(st.frames + f0);
       for (int q = threadIdx.x; q < Fz::FR_BYTES / 16; q += 256) reinterpret_cast<uint4 *>(fr)[q] = fs[q];
     }
     __syncthreads();
-    const int p = min(max(s_p, 1), 4);
+    const int p = st.count ? min(max(s_p, 1), 4) : 0;
     if (p > 1) {  // FiGAR repeats: pushes 1..p-1 (slots 4e+1..)
       for (int q = threadIdx.x; q < (p - 1) * (Fz::FR_BYTES / 16); q += 256) {
         const int j = 1 + q / (Fz::FR_BYTES / 16), qq = q - (j - 1) * (Fz::FR_BYTES / 16);

@@ -219,18 +219,36 @@ class DeviceNetwork(object):
             _ptr(loss_terms), _stream()), 'mt_loss_backward')
         return self.grad
 
+    def returns_loss_backward(self, obs, T, E, pi, rep, values, a_idx, r_idx, rewards, masks, v_boot, gamma, y, adv,
+                              loss_terms=None, ws_key=None, norm_partials=False):
+        """mt_returns + mt_loss_backward in one call (rows t*E + e): the n-step scan of paac.py:219-231
+        runs inside the loss kernel. rewards / masks: [T][E] device tensors or device addresses.
+        norm_partials: the backward also leaves the global-norm partials in self.partials, so the
+        following apply_gradients(partials_ready=True) skips mt_grad_sumsq (single process only)."""
+        B = T * E
+        ws = self.workspace(B, ws_key)
+        addr = lambda x: C.c_void_p(x) if isinstance(x, int) else _ptr(x)
+        check(_lib.hip().mt_returns_loss_backward(
+            self._h, _ptr(self.params), _ptr(obs), int(T), int(E), _ptr(ws), ws.numel(), _ptr(pi), _ptr(rep),
+            _ptr(values), _ptr(a_idx), _ptr(r_idx), addr(rewards), addr(masks), _ptr(v_boot), float(gamma), _ptr(y),
+            _ptr(adv), self.beta, _ptr(self.grad), _ptr(loss_terms), _ptr(self.partials if norm_partials else None),
+            _stream()), 'mt_returns_loss_backward')
+        return self.grad
+
     def set_lr(self, lr):
         """The LR of the next apply_gradients: written into pinned host memory that the RMSProp
         kernel reads in place (no copy; a captured graph also picks up the schedule)."""
         self._lr_host[0] = float(lr)
 
-    def apply_gradients(self, inv_scale=1.0):
+    def apply_gradients(self, inv_scale=1.0, partials_ready=False):
         """clip_by_global_norm + ApplyRMSProp on self.grad (actor_learner.py:47-74).
-        inv_scale folds the 1/world of a data-parallel gradient sum."""
+        inv_scale folds the 1/world of a data-parallel gradient sum. partials_ready: the backward
+        already wrote the norm partials (returns_loss_backward(norm_partials=True), inv_scale 1)."""
         lib = _lib.hip()
         s = _stream()
-        check(lib.mt_grad_sumsq(_ptr(self.grad), self.nparams, float(inv_scale), _ptr(self.partials), s),
-              'mt_grad_sumsq')
+        if not partials_ready:
+            check(lib.mt_grad_sumsq(_ptr(self.grad), self.nparams, float(inv_scale), _ptr(self.partials), s),
+                  'mt_grad_sumsq')
         check(lib.mt_clip_rmsprop(_ptr(self.params), _ptr(self.ms), _ptr(self.mom), _ptr(self.grad),
                                   self.nparams, _ptr(self.partials), C.c_void_p(self._lr_dev_addr), self.decay, 0.0,
                                   self.eps, self.clip_norm, self.clip_type, float(inv_scale),

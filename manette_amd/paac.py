@@ -1,6 +1,6 @@
 """PAACLearner: the PAAC+FiGAR rollout/update loop (paac.py:15-301) on one MI355X per process.
 
-train() = init_network; loop { for t in range(T): step(t); update(); log; save_vars }; cleanup
+train() = init_network; loop { rollout() (= step(t) for t in range(T)); update(); log; save_vars }; cleanup
 (the reference has no step()/update(); these are the decomposition of paac.py:140-205 and
 :219-256). Data stays in HBM: the (T+1, E, 84, 84, C) uint8 rollout state ring, values,
 action/repetition indices, y/adv. Per macro-step only the sampled indices go device->host and
@@ -108,6 +108,7 @@ class PAACLearner(ActorLearner):
         self.book = NativeBook(E, self.num_actions, self.tab_rep)
         self.native_step = None  # mt_rollout handle (native runner + device sampling)
         self.boot_in_rollout = False
+        self.slot0_in_rollout = False
         self.runners = None
         self.profile = None      # name -> [(start_event, end_event)] when profiling (bench.py)
         self.sample_seed = (self.seed * 1000003 + self.rank * 7919 + 1) & 0xffffffffffff
@@ -199,6 +200,10 @@ class PAACLearner(ActorLearner):
                                                 C.c_uint64(self.sample_seed), C.byref(h)), 'mt_rollout_create')
         self.native_step = h
         self.boot_in_rollout = self.pipeline  # the last step's chain runs the bootstrap forward
+        # the rollout's stacking NIPS forward (pipelined, resized staging) also carries slot T over
+        # into slot 0 at the next step 0 (mt_rollout_step): the update does not copy it
+        self.slot0_in_rollout = self.pipeline and self.staging == 'resized' and self.network.arch == 'NIPS' \
+            and not self.lstm_bool
         self._gs = C.c_int64(0)
 
     def _upload_pushes(self, total, out, prev):
@@ -233,6 +238,19 @@ class PAACLearner(ActorLearner):
         return ev[1]
 
     # ------------------------------------------------------------------------------------------
+    def rollout(self):
+        """The T macro-steps of one rollout (paac.py:140-205): one native call (mt_rollout_run)
+        with the native step, else step(t) for t in 0..T-1."""
+        if self.native_step is not None:
+            from . import _lib
+            self._gs.value = self.global_step
+            _lib.check(_lib.hip().mt_rollout_run(self.native_step, devnet._ptr(self.network.params),
+                                                 self._lib_ref(self._gs), devnet._stream()), 'mt_rollout_run')
+            self.global_step = self._gs.value
+            return
+        for t in range(self.max_local_steps):
+            self.step(t)
+
     def step(self, t):
         """One rollout macro-step (paac.py:140-205)."""
         net = self.network
@@ -346,10 +364,20 @@ class PAACLearner(ActorLearner):
             self._lstm_forward(T, self.v_boot)
         elif not (self.boot_in_rollout and self.native_step is not None):  # (else queued behind the last step)
             net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout', infer=True)
-        devnet.returns(self.rm_h_dev, self.rm_h_dev + 4 * T * E, self.values, self.v_boot, self.gamma, self.y,
-                       self.adv)
-        end = self._mark('train_pass')
-        self.train_backward()
+        if self.lstm_bool:
+            devnet.returns(self.rm_h_dev, self.rm_h_dev + 4 * T * E, self.values, self.v_boot, self.gamma, self.y,
+                           self.adv)
+            end = self._mark('train_pass')
+            self.train_backward()
+        else:
+            # n-step scan (paac.py:219-231) inside the loss kernel: one launch fewer
+            end = self._mark('train_pass')
+            N = E * T
+            net.returns_loss_backward(self.states[:T].reshape(N, 84, 84, self.C), T, E, self.pi_all[:T].reshape(N, -1),
+                                      self.rep_all[:T].reshape(N, -1), self.values, self.idx[0].view(N),
+                                      self.idx[1].view(N), self.rm_h_dev, self.rm_h_dev + 4 * T * E, self.v_boot,
+                                      self.gamma, self.y, self.adv, loss_terms=self.loss_terms, ws_key='train',
+                                      norm_partials=self.world == 1)
         if end is not None:
             end.record()
 
@@ -374,11 +402,12 @@ class PAACLearner(ActorLearner):
 
     def _update_apply(self):
         T = self.max_local_steps
-        self.network.apply_gradients(1.0 / self.world if self.world > 1 else 1.0)
+        self.network.apply_gradients(1.0 / self.world if self.world > 1 else 1.0,
+                                     partials_ready=self.world == 1 and not self.lstm_bool)
         if self.lstm_bool:  # the next rollout's slots 0..4 = s_{T-4} .. s_T; windows carry over
             self.slots[0:5].copy_(self.slots[T:T + 5].clone())
             self.nz_h.numpy()[0] = self.nz_h.numpy()[T]
-        else:
+        elif not (self.native_step is not None and self.slot0_in_rollout):
             self.states[0].copy_(self.states[T])
 
     def _capture_update(self):
@@ -448,8 +477,7 @@ class PAACLearner(ActorLearner):
             while self.global_step < self.max_global_steps:
                 loop_start_time = time.time()
                 self.book.new_update()
-                for t in range(self.max_local_steps):
-                    self.step(t)
+                self.rollout()
                 self.update()
                 counter += 1
                 if counter % max(1, 2048 // self.emulator_counts) == 0:

@@ -176,6 +176,43 @@ def test_returns_bit_exact(T, E):
     np.testing.assert_array_equal(adv.cpu().numpy(), adv0.astype(np.float32))
 
 
+@pytest.mark.parametrize('arch,depth,A,R', [('NIPS', 1, 6, 1), ('NATURE', 1, 4, 11), ('PWYX', 1, 4, 11)])
+@pytest.mark.parametrize('T,E', [(5, 8), (3, 5)])
+def test_returns_loss_backward_fused(arch, depth, A, R, T, E):
+    """mt_returns_loss_backward (the n-step scan inside the loss kernel) == mt_returns followed by
+    mt_loss_backward: y, adv, loss terms and every gradient bit for bit; the scan reads rewards /
+    masks from pinned host memory in place, as the learner does."""
+    from manette_amd.network import returns as dev_returns, host_device_pointer
+    net = _net(arch, depth, A, R, seed=T + E)
+    rs = np.random.RandomState(100 * T + E)
+    N = T * E
+    obs = torch.from_numpy(rs.randint(0, 256, size=(N, 84, 84, 4 * depth)).astype(np.uint8)).cuda()
+    v, pi, rep = [t.clone() for t in net.forward(obs)]
+    a_idx = torch.from_numpy(rs.randint(0, A, N).astype(np.int32)).cuda()
+    r_idx = torch.from_numpy(rs.randint(0, R, N).astype(np.int32)).cuda()
+    rm = torch.zeros(2, T, E, dtype=torch.float32).pin_memory()
+    rm[0] = torch.from_numpy(rs.choice([-1.0, 0.0, 1.0], size=(T, E)).astype(np.float32))
+    rm[1] = torch.from_numpy((rs.rand(T, E) > 0.2).astype(np.float32))
+    rm_dev = host_device_pointer(rm)
+    VT = torch.from_numpy(rs.randn(E).astype(np.float32)).cuda()
+    y0, adv0 = torch.empty(T, E, device='cuda'), torch.empty(T, E, device='cuda')
+    lt0, lt1 = torch.empty(N, 4, device='cuda'), torch.empty(N, 4, device='cuda')
+    dev_returns(rm_dev, rm_dev + 4 * N, v.view(T, E), VT, 0.99, y0, adv0)
+    net.loss_backward(obs, N, v, pi, rep, a_idx, r_idx, y0.view(N), adv0.view(N), loss_terms=lt0)
+    g0 = net.grad.clone()
+    y1, adv1 = torch.empty(T, E, device='cuda'), torch.empty(T, E, device='cuda')
+    net.grad.zero_()
+    net.returns_loss_backward(obs, T, E, pi, rep, v, a_idx, r_idx, rm_dev, rm_dev + 4 * N, VT, 0.99, y1, adv1,
+                              loss_terms=lt1, norm_partials=True)
+    torch.cuda.synchronize()
+    for a, b, k in ((y0, y1, 'y'), (adv0, adv1, 'adv'), (lt0, lt1, 'loss_terms'), (g0, net.grad, 'grad')):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=k)
+    # the fused norm partials add up to the global norm of the gradient (oracle: float64)
+    norm = float(np.sqrt(net.partials.double().sum().item()))
+    ref = optim.global_norm([g0.cpu().numpy()])
+    assert abs(norm - ref) <= 1e-5 * ref, (norm, ref)
+
+
 @pytest.mark.parametrize('clip_type', ['global', 'ignore'])
 @pytest.mark.parametrize('gscale', [1e-3, 10.0])
 def test_clip_rmsprop(clip_type, gscale):
