@@ -90,11 +90,12 @@ int mt_forward(const mt_net *net, const float *params, const uint8_t *obs, int b
 
 /* ---- inference forward (rollout steps, bootstrap V(s_T)) -----------------------------------
  * Same outputs as mt_forward (paac.py:144-146, :219-224) but keeps no activations for a backward
- * pass, so the NIPS arch runs its fused trunk (conv1 -> conv2 -> dense partials in one launch,
- * manette_amd/csrc/trunk_fused.h) followed by the heads kernel; other arches take mt_forward's
- * layered path. Same workspace size as mt_forward. (A one-launch variant whose last block per
- * env finished the heads measured 25 us vs 12.7 + 6.1 us: the release/acquire fences and the
- * serial tail cost more than the second launch.) */
+ * pass, so the NIPS arch runs its rollout trunk (manette_amd/csrc/trunk_fused.h: one conv kernel,
+ * conv1 -> conv2 per (env, conv2 row) block, then the dense layer as its own MFMA GEMM kernel
+ * writing 9 split-K slabs) followed by the heads kernel; other arches take mt_forward's layered
+ * path. Same workspace size as mt_forward. (A one-launch variant whose last block per env
+ * finished the heads measured 25 us vs 12.7 + 6.1 us: the release/acquire fences and the serial
+ * tail cost more than the second launch.) */
 int mt_forward_infer(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                      size_t ws_bytes, float *v, float *pi, float *rep, mt_stream_t stream);
 
@@ -110,7 +111,7 @@ int mt_forward_rows(const mt_net *net, const float *params, const uint8_t *obs, 
                     float *pi, float *rep, mt_stream_t stream);
 
 /* Trunk half of mt_forward_infer alone (roofline timing / diagnostics): the convs and the dense
- * layer's partial products, left in `ws` (NIPS: the one fused-trunk launch). */
+ * layer's partial products, left in `ws` (NIPS: the conv kernel + the dense kernel). */
 int mt_forward_trunk(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                      size_t ws_bytes, mt_stream_t stream);
 
@@ -276,7 +277,14 @@ int mt_memory_push(uint8_t *memory, uint8_t *whole_t, const uint8_t *fresh, cons
 /* flags & MT_ROLLOUT_PIPELINED (needs ZERO_COPY or IN_PLACE): each call enqueues step t+1's chain
  * (a bounded device wait on sync_host[0], preprocess, forward + draw) before it waits for step t's
  * indices, and after the emulators only stores the step word — no launch on the critical path.
- * sync_host = [2] uint32 pinned + mapped: [0] host step word, [1] device wait timeout status. */
+ * sync_host = [2] uint32 pinned + mapped: [0] host step word, [1] device wait timeout status.
+ * PIPELINED + RESIZED + the NIPS arch ("stacking" rollout): the chain of step t+1 is a pull kernel
+ * (per env, it waits for the word the emulator thread stores once the env is staged,
+ * mh_runner_set_ready, and copies its frames into HBM while the other envs are still emulated),
+ * the conv kernel that stacks state slot t+1 from slot t and those frames itself (no preprocess
+ * launch), the dense kernel and the heads kernel, which writes each env's (a, r) as one tagged
+ * 8-byte word into host memory (no fence); chains are armed two steps ahead, and step 0's forward
+ * takes slot 0 from slot T of the previous rollout (the update then needs no copy). */
 #define MT_ROLLOUT_PIPELINED 8
 /* flags & MT_ROLLOUT_RESIZED: the runner stages each push's final 84x84 frame (MH_RUNNER_RESIZED,
  * staging [4E][84*84*depth]) and the preprocess is mt_preprocess_resized (row/col LUTs unused). */

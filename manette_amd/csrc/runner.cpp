@@ -27,6 +27,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -146,6 +147,7 @@ struct mh_runner {
   uint32_t *ready = nullptr;
   uint32_t ready_value = 0;
   bool busy = false;  // mh_runner_step_begin dispatched, mh_runner_step_end not yet called
+  bool nt_stores = true;  // resized frames: streaming stores (plain stores measured the same on the box)
 
   int block_begin(int w) const { return (int)((int64_t)E * w / W); }
   int block_end(int w) const { return (int)((int64_t)E * (w + 1) / W); }
@@ -231,9 +233,14 @@ struct mh_runner {
         // resized into an L1-resident buffer, then streamed to the staging with non-temporal
         // stores: the lines never sit modified in this core's cache, so the GPU reading them
         // over PCIe (while this thread works on the next env) does not snoop them out of it
+        uint8_t *dst = staging + (size_t)(push_offset[i] + j) * sfb;
+        if (!nt_stores) {
+          resize_push(dst, e.screens + (size_t)((2 * kk) % ring) * fb, e.screens + (size_t)((2 * kk + 1) % ring) * fb);
+          continue;
+        }
         alignas(64) uint8_t buf[84 * 84 * 3 + 64];
         resize_push(buf, e.screens + (size_t)((2 * kk) % ring) * fb, e.screens + (size_t)((2 * kk + 1) % ring) * fb);
-        stream_copy(staging + (size_t)(push_offset[i] + j) * sfb, buf, sfb);
+        stream_copy(dst, buf, sfb);
         continue;
       }
       if (pooled) {  // FramePool max (atari_emulator.py:79-88) of the staged rows, on the host
