@@ -22,9 +22,10 @@ struct mt_rollout {
   uint64_t seed;
   hipEvent_t ev2[4];  // pair of step t ready: ev2[t & 3]
   bool zero_copy, in_place, pooled, resized, pipelined;
-  bool stack_fwd;     // pipelined + resized + NIPS: the forward's conv kernel stacks (no preprocess)
+  bool pull;          // pipelined + resized: per-env ready words, pull kernel into HBM, tagged pairs
+  bool stack_fwd;     // pull + NIPS: the forward's conv kernel stacks (no preprocess launch)
   int armed_upto = -1;  // pipelined: last step whose chain (forward) is already enqueued
-  int ahead = 1;        // pipelined: steps armed ahead (2 with stack_fwd)
+  int ahead = 1;        // pipelined: steps armed ahead (2 with pull)
   std::vector<uint32_t> fwd_of;  // [T] draw sequence number of step t's forward
   uint32_t seq = 0;   // host step sequence word value last stored
   uint8_t *staging_dev;  // device addresses of the host-mapped buffers (zero-copy mode)
@@ -33,7 +34,7 @@ struct mt_rollout {
   uint32_t *ready_dev = nullptr;  // [E] pair-ready flags (device address of b.ready_host)
   uint32_t fwd_seq = 0;           // sequence number of the last enqueued forward + draw
   int64_t rollouts = 0;           // completed rollouts (calls with t = T-1)
-  // stack_fwd: per-env ready words the emulator threads store (mh_runner_set_ready) and the
+  // pull: per-env ready words the emulator threads store (mh_runner_set_ready) and the
   // tagged (a, r) words the heads kernel stores (SampleArgs::packed); pinned, device-mapped
   uint32_t *env_ready_host = nullptr, *env_ready_dev = nullptr;
   uint64_t *packed_host = nullptr, *packed_dev = nullptr;
@@ -109,7 +110,8 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->pooled = po;
   ro->resized = rz;
   ro->pipelined = pl;
-  ro->stack_fwd = pl && rz && cfg.arch == MT_ARCH_NIPS;
+  ro->pull = pl && rz;
+  ro->stack_fwd = ro->pull && cfg.arch == MT_ARCH_NIPS;
   ro->frames_dev = (int32_t *)frames_dev;
   ro->ready_dev = (uint32_t *)ready_dev;
   ro->seq_dev = (uint32_t *)sync_dev;
@@ -117,13 +119,18 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->staging_dev = (uint8_t *)staging_dev;
   ro->meta_dev = (int32_t *)meta_dev;
   ro->pair_dev = (int32_t *)pair_dev;
-  if (ro->stack_fwd) {
+  if (ro->pull) {
     hipError_t e = hipHostMalloc((void **)&ro->env_ready_host, sizeof(uint32_t) * E, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostMalloc((void **)&ro->packed_host, sizeof(uint64_t) * E, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&ro->env_ready_dev, ro->env_ready_host, 0);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&ro->packed_dev, ro->packed_host, 0);
     if (e == hipSuccess) e = hipMalloc((void **)&ro->frames_hbm, (size_t)4 * E * 84 * 84 * cfg.depth);
-    if (e == hipSuccess) e = hipMalloc((void **)&ro->count_hbm, sizeof(int32_t) * E);
+    if (e == hipSuccess) e = hipMalloc((void **)&ro->count_hbm, sizeof(int32_t) * 2 * E);  // counts; offsets 4e
+    if (e == hipSuccess) {
+      std::vector<int32_t> offs(E);
+      for (int i = 0; i < E; ++i) offs[i] = 4 * i;
+      e = hipMemcpy(ro->count_hbm + E, offs.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
       if (ro->env_ready_host) (void)hipHostFree(ro->env_ready_host);
       if (ro->packed_host) (void)hipHostFree(ro->packed_host);
@@ -136,7 +143,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
     std::memset(ro->env_ready_host, 0, sizeof(uint32_t) * E);
     std::memset(ro->packed_host, 0, sizeof(uint64_t) * E);
   }
-  ro->ahead = ro->stack_fwd ? 2 : 1;
+  ro->ahead = ro->pull ? 2 : 1;
   ro->fwd_of.assign(T, 0);
   for (int i = 0; i < 4; ++i) {
     hipError_t e = hipEventCreateWithFlags(&ro->ev2[i], hipEventDisableTiming);
@@ -154,7 +161,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
 extern "C" void mt_rollout_destroy(mt_rollout *ro) {
   if (!ro) return;
   for (int i = 0; i < 4; ++i) (void)hipEventDestroy(ro->ev2[i]);
-  if (ro->stack_fwd) {
+  if (ro->pull) {
     (void)mh_runner_set_ready(ro->runner, nullptr, 0);
     (void)hipHostFree(ro->env_ready_host);
     (void)hipHostFree(ro->packed_host);
@@ -186,7 +193,7 @@ __global__ void wait_seq_kernel(const uint32_t *seq_word, uint32_t seq, uint32_t
   }
 }
 
-// Pull kernel (stack_fwd): copies each env's pushes from the pinned staging into HBM as soon as
+// Pull kernel (pull mode: pipelined + resized): copies each env's pushes from the pinned staging into HBM as soon as
 // its emulator thread has published it (ready[e] = (step << 3) | push count,
 // mh_runner_set_ready), so the PCIe transfer of a step's frames overlaps the emulation of the
 // other envs and the stacking conv kernel reads HBM only. Block = kPullEnvs consecutive envs
@@ -306,14 +313,20 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
   const mt_rollout_buffers &b = ro->b;
   const int E = ro->E, T = ro->T;
   const uint32_t want = ro->seq + (uint32_t)ahead;
-  // stack_fwd: the pull kernel waits per env and copies the pushes into HBM; the preprocess
-  // of step k-1 runs inside step k's forward conv kernel
+  // pull: the pull kernel waits per env and copies the pushes into HBM; the preprocess of step
+  // k-1 then reads them there — inside step k's forward conv kernel (stack_fwd, NIPS), else as
+  // mt_preprocess_resized
   const bool stk = ro->stack_fwd && (k < T || b.v_boot);
-  if (stk) {
+  if (ro->pull) {
     hipLaunchKernelGGL(pull_frames_kernel, dim3((E + kPullEnvs - 1) / kPullEnvs), dim3(256), 0, s,
                        reinterpret_cast<const uint4 *>(ro->staging_dev), ro->env_ready_dev, want, ro->status_dev, E,
                        (int)(84 * 84 * ro->depth / 16), reinterpret_cast<uint4 *>(ro->frames_hbm), ro->count_hbm);
     MT_LAUNCHED();
+    if (!stk) {
+      const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
+      MT_TRY_(mt_preprocess_resized(ro->frames_hbm, ro->count_hbm + E, ro->count_hbm, E, ro->depth,
+                                    b.states + (size_t)(k - 1) * slot, b.states + (size_t)k * slot, (mt_stream_t)s));
+    }
   } else {
     hipLaunchKernelGGL(wait_seq_kernel, dim3(1), dim3(64), 0, s, ro->seq_dev, want, ro->status_dev);
     MT_LAUNCHED();
@@ -414,7 +427,7 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   const double t1 = now_us();
   // 4. emulators (runners.py:44-50 / emulator_runner.py:24-41) + bookkeeping (paac.py:176-205)
   int total = 0;
-  if (ro->stack_fwd && mh_runner_set_ready(ro->runner, ro->env_ready_host, ro->seq + 1) != 0) {
+  if (ro->pull && mh_runner_set_ready(ro->runner, ro->env_ready_host, ro->seq + 1) != 0) {
     set_error("mh_runner_set_ready: %s", mh_last_error());
     return MT_ERR_ARG;
   }
