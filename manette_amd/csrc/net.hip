@@ -748,7 +748,14 @@ static int conv_forward(const void *X, const float *Wt, const float *bias, float
   LdIm2col<G, U8> la{reinterpret_cast<const typename InElem<U8>::T *>(X)};
   LdColMajor lb{Wt, G::COUT, -1};
   EpBiasAct ep{Y, bias, G::COUT, act, alpha};
-  return launch_gemm<T>(la, lb, ep, B * G::OH * G::OW, G::COUT, G::KK, 1, s);
+  const int M = B * G::OH * G::OW;
+  if constexpr (G::COUT % 32 == 0) {
+    // small batches (a rollout step): a grid of under two workgroups per CU leaves most CUs idle
+    // and each wave a long MFMA chain — 32 x 32 tiles, one 16 x 16 accumulator per wave
+    using TS = Tile<32, 32, 2, 2, conv_bk<G::KK>()>;
+    if (cdiv(M, T::BM) * cdiv(G::COUT, T::BN) < 512) return launch_gemm<TS>(la, lb, ep, M, G::COUT, G::KK, 1, s);
+  }
+  return launch_gemm<T>(la, lb, ep, M, G::COUT, G::KK, 1, s);
 }
 
 // dW (+db) of a conv: [im2col(X), 1]^T . dY  -> grad[(KK+1) x COUT] (weights then biases), as a
@@ -885,9 +892,6 @@ static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, 
   return MT_OK;
 }
 
-// Backward through conv layer I given the gradient w.r.t. its post-activation output, already
-// masked (ws + L.dact[I]): weight gradient, then (I > 0) the masked gradient of its input,
-// routed through the previous layer's pool when there is one.
 // Conv layers I .. 0 of the backward, top down: one grouped launch per layer — its dX (the
 // critical path, first), its dW GEMM and `pending` (the slab sum of layer I+1's dW) — then
 // conv1's slab sum. Layer I's slabs live in region I % 2 (wslab / wslab2), so the slab sum of
