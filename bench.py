@@ -200,6 +200,8 @@ def main():
                     help='disable MT_ROLLOUT_PIPELINED (on by default)')
     ap.add_argument('--no_update_graph', dest='update_graph', action='store_false',
                     help='launch the update eagerly instead of replaying it as a hipGraph')
+    ap.add_argument('--trunk_sweep', default='256,1024,4096',
+                    help='extra batch sizes the trunk kernel is timed at after the run ("" = none)')
     a = ap.parse_args()
 
     import torch
@@ -308,6 +310,25 @@ def main():
     torch.cuda.synchronize()
     prof['rollout_forward'] = [s_ev_.elapsed_time(e_ev_) for (s_ev_, e_ev_) in fw[5:]]
     prof['rollout_trunk'] = [s_ev.elapsed_time(e_ev) / 40.0]
+    # the same trunk launch at larger batches (supplementary: how far the kernel is from its
+    # bounds once the grid fills the chip; the workload's own batch is E = ec above)
+    sweep = []
+    if not learner.lstm_bool and a.trunk_sweep:
+        depth_ = 3 if cfg['rgb'] else 1
+        g = torch.Generator(device='cuda').manual_seed(7)
+        for Eb in [int(x) for x in a.trunk_sweep.split(',')]:
+            obs_b = torch.randint(0, 256, (Eb, 84, 84, 4 * depth_), dtype=torch.uint8, device='cuda', generator=g)
+            for _ in range(3):
+                net.forward_trunk(obs_b, Eb, ws_key=('sweep', Eb))
+            s_b, e_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_b.record()
+            for _ in range(10):
+                net.forward_trunk(obs_b, Eb, ws_key=('sweep', Eb))
+            e_b.record()
+            torch.cuda.synchronize()
+            sweep.append((Eb, s_b.elapsed_time(e_b) / 10.0))
+            del obs_b
+            net._ws.pop(('sweep', Eb), None)
     ec = cfg['ec']
     value = world * ec * T * a.steps / elapsed
 
@@ -364,6 +385,17 @@ def main():
                                 'hbm_gbs': round(fwd_bytes / (rf_ms * 1e-3) / 1e9, 1),
                                 'hbm_frac': round(fwd_bytes / (rf_ms * 1e-3) / 1e9 / MI355X_HBM_GBS, 4)},
         }
+        if sweep:
+            per_env_bytes = 84 * 84 * 4 * depth + 4 * out_floats
+            w_bytes = 4 * sum(l[2] for l in trunk)
+            per_env_flops = sum(l[1] for l in trunk)
+            line['trunk_batch_sweep'] = [
+                {'envs': Eb, 'us_per_launch': round(ms * 1e3, 2),
+                 'hbm_gbs': round((Eb * per_env_bytes + w_bytes) / (ms * 1e-3) / 1e9, 1),
+                 'hbm_frac': round((Eb * per_env_bytes + w_bytes) / (ms * 1e-3) / 1e9 / MI355X_HBM_GBS, 4),
+                 'tflops': round(Eb * per_env_flops / (ms * 1e-3) / 1e12, 2),
+                 'flop_frac': round(Eb * per_env_flops / (ms * 1e-3) / 1e12 / MI355X_FP32_TFLOPS, 4)}
+                for Eb, ms in sweep]
         if step_phases:
             line['macro_step_host_us'] = step_phases
         if world == 1 and not a.no_cpu_baseline:

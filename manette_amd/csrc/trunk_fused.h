@@ -23,9 +23,13 @@
 // partial accumulators are added in wave order through LDS (deterministic). Input scaling
 // x = u8 * (1/255) in fp32 as networks.py:155 (same expression as LdIm2col's loader).
 //
-// blockIdx -> (i, e) of the conv kernel is XCD-aware: blocks are dealt round-robin over the 8
+// blockIdx -> (e, i) of the conv kernel is XCD-aware: blocks are dealt round-robin over the 8
 // XCDs, so the linear index L = (bid % 8) * (grid / 8) + bid / 8 gives each XCD a contiguous run
-// of L, i.e. 1-2 conv2 rows (speed only; any placement computes the same values).
+// of L, env-major (L = 9 e + i): the 9 blocks of an env, whose 20-row input windows overlap by
+// 12 rows, share one XCD's L2, so each frame crosses the fabric once, not 2.5 times. The fc
+// kernel deals its (16-column, row i) blocks the same way, i-major: an XCD holds the 16 column
+// blocks of 1-2 rows, so each 128-byte weight line (two 16-column halves) and each act2 row
+// chunk is fetched by one XCD (speed only; any placement computes the same values).
 #pragma once
 #include "gemm.h"
 
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(256) void nips_conv_kernel(const uint8_t *__restric
   const int bid = blockIdx.x;
   MT_PROBE_AT(0, bid, 0);
   const int L = (nb % 8 == 0) ? (bid % 8) * (nb / 8) + bid / 8 : bid;
-  const int i = L / B, e = L - i * B;
+  const int e = L / Fz::ROWS2, i = L - e * Fz::ROWS2;  // env-major: an env's 9 blocks share an XCD
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
 
@@ -259,8 +263,11 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
                                                       const float *__restrict__ Wfc, float *__restrict__ slabs) {
   using Fz = FusedNips<C>;
   __shared__ __attribute__((aligned(16))) float red[4][Fz::FC_BM][Fz::FC_BN];
-  const int n0 = blockIdx.x * Fz::FC_BN, i = blockIdx.y, e0 = blockIdx.z * Fz::FC_BM;
   const int pb = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  const int nbk = gridDim.x * gridDim.y * gridDim.z;
+  const int L = (nbk % 8 == 0) ? (pb % 8) * (nbk / 8) + pb / 8 : pb;  // XCD-aware (see the top)
+  const int xb = L % gridDim.x, yz = L / gridDim.x;
+  const int n0 = xb * Fz::FC_BN, i = yz % gridDim.y, e0 = (yz / gridDim.y) * Fz::FC_BM;
   MT_PROBE_AT(1, pb, 0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;

@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 cd /tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $C -d $R/gpurun_out/$NAME/$C -o run --output-format csv -- \
-    python3 $R/bench.py --steps 10 --warmup 3 --no_cpu_baseline "$@" > $R/gpurun_out/$NAME.$C.log 2>&1
+    python3 $R/bench.py --steps 10 --warmup 3 --no_cpu_baseline --trunk_sweep= "$@" > $R/gpurun_out/$NAME.$C.log 2>&1
   rc=$?
   echo "pmc $C rc=$rc"
   [ $rc -ne 0 ] && exit $rc
