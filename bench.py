@@ -370,13 +370,21 @@ def main():
             'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step, %s staging%s' % (
                 a.config, ec, cfg['ew'], T, a.sampling, a.step_impl, a.staging, ', pipelined' if a.pipeline else ''), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
                 'global_emulators': ec * world, 'parallelism': 'dp%d' % world},
-            'roofline': {'bound': 'hbm', 'kernel': ' + '.join(TRUNK_KERNELS.get(cfg['arch'], ['mt_forward_trunk (layered)'])),
-                         'achieved': round(tk_gbs, 1), 'peak': MI355X_HBM_GBS, 'unit': 'GB/s',
-                         'frac': round(tk_gbs / MI355X_HBM_GBS, 4),
-                         'traffic': pmc['hbm_bytes'] if pmc else None,
-                         'algorithmic_bytes_per_launch': tk_bytes, 'us_per_launch': round(tk_ms * 1e3, 2),
-                         'tflops': round(tk_flops / (tk_ms * 1e-3) / 1e12, 3),
-                         'traffic_source': pmc['source'] if pmc else None},
+            # bound = the resource the trunk's arithmetic intensity binds on the roofline (fp32 ridge
+            # 157.3 TFLOP/s / 8 TB/s = 19.7 FLOP/B; NIPS E=32: 52 FLOP/B -> mfma); both fractions kept
+            'roofline': dict(
+                (('bound', 'mfma'), ('achieved', round(tk_flops / (tk_ms * 1e-3) / 1e12, 3)), ('peak', MI355X_FP32_TFLOPS),
+                 ('unit', 'TFLOP/s'), ('frac', round(tk_flops / (tk_ms * 1e-3) / 1e12 / MI355X_FP32_TFLOPS, 4)))
+                if tk_flops / tk_bytes > MI355X_FP32_TFLOPS * 1e12 / (MI355X_HBM_GBS * 1e9) else
+                (('bound', 'hbm'), ('achieved', round(tk_gbs, 1)), ('peak', MI355X_HBM_GBS), ('unit', 'GB/s'),
+                 ('frac', round(tk_gbs / MI355X_HBM_GBS, 4))),
+                kernel=' + '.join(TRUNK_KERNELS.get(cfg['arch'], ['mt_forward_trunk (layered)'])),
+                traffic=pmc['hbm_bytes'] if pmc else None,
+                algorithmic_bytes_per_launch=tk_bytes, algorithmic_flop_per_launch=tk_flops,
+                us_per_launch=round(tk_ms * 1e3, 2), hbm_gbs=round(tk_gbs, 1),
+                hbm_frac=round(tk_gbs / MI355X_HBM_GBS, 4),
+                flop_frac=round(tk_flops / (tk_ms * 1e-3) / 1e12 / MI355X_FP32_TFLOPS, 4),
+                traffic_source=pmc['source'] if pmc else None),
             'train_pass': {'bound': 'mfma', 'kernels': ('backward of %d windows over %d distinct frames (forward reused from the rollout)' % (N, 1 + (T + 4) * ec)) if lstm else 'forward + fused loss backward, %d rows' % N,
                            'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',
                            'frac': round(achieved / MI355X_FP32_TFLOPS, 4),

@@ -78,13 +78,34 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float *__restrict__ g,
 //   mom  = mom * momentum + (grad * lr) / sqrt(ms + epsilon)
 //   var -= mom
 // clip_by_global_norm: scale = clip * min(1/norm, 1/clip) (both factors fp32).
+// One float4 of (w, ms, mom, g) per thread (VEC; else one float), its four loads issued before
+// the block reduces the norm partials so their latency overlaps that reduction.
+template <bool VEC>
 __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
     float *__restrict__ w, float *__restrict__ ms, float *__restrict__ mom,
     const float *__restrict__ g, size_t n, const float *__restrict__ partials,
     const float *__restrict__ lr_dev, float decay, float momentum, float eps, float clip,
     int clip_type, float s, float *__restrict__ norm_out) {
 #pragma clang fp contract(off)  // TF's operation-by-operation rounding, no fused multiply-add
+  constexpr int V = VEC ? 4 : 1;
   __shared__ float sh_scale;
+  const size_t i0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * V;
+  const bool full = i0 + V <= n;
+  f32x4 gv{0.f, 0.f, 0.f, 0.f}, mv{0.f, 0.f, 0.f, 0.f}, ov{0.f, 0.f, 0.f, 0.f}, wv{0.f, 0.f, 0.f, 0.f};
+  if (VEC && full) {
+    gv = *reinterpret_cast<const f32x4 *>(g + i0);
+    mv = *reinterpret_cast<const f32x4 *>(ms + i0);
+    ov = *reinterpret_cast<const f32x4 *>(mom + i0);
+    wv = *reinterpret_cast<const f32x4 *>(w + i0);
+  } else {
+    for (int k = 0; k < V; ++k)
+      if (i0 + k < n) {
+        gv[k] = g[i0 + k];
+        mv[k] = ms[i0 + k];
+        ov[k] = mom[i0 + k];
+        wv[k] = w[i0 + k];
+      }
+  }
   if (threadIdx.x < 64) {
     double acc = 0.0;
     for (int i = threadIdx.x; i < MT_NORM_PARTIALS; i += 64) acc += (double)partials[i];
@@ -104,16 +125,28 @@ __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
   const float scale = sh_scale;
   const float lr = *lr_dev;
   const float one_m_rho = 1.0f - decay;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
     // with s != 1 (data parallel), g is the SUM over ranks: scale folds 1/world and the clip.
-    const float gi = (clip_type == MT_CLIP_GLOBAL) ? g[i] * scale : g[i] * s;
-    float m = ms[i];
+    const float gi = (clip_type == MT_CLIP_GLOBAL) ? gv[k] * scale : gv[k] * s;
+    float m = mv[k];
     m = m + (gi * gi - m) * one_m_rho;
-    const float mo = mom[i] * momentum + (gi * lr) / sqrtf(m + eps);
-    ms[i] = m;
-    mom[i] = mo;
-    w[i] = w[i] - mo;
+    const float mo = ov[k] * momentum + (gi * lr) / sqrtf(m + eps);
+    mv[k] = m;
+    ov[k] = mo;
+    wv[k] = wv[k] - mo;
+  }
+  if (VEC && full) {
+    *reinterpret_cast<f32x4 *>(ms + i0) = mv;
+    *reinterpret_cast<f32x4 *>(mom + i0) = ov;
+    *reinterpret_cast<f32x4 *>(w + i0) = wv;
+  } else {
+    for (int k = 0; k < V; ++k)
+      if (i0 + k < n) {
+        ms[i0 + k] = mv[k];
+        mom[i0 + k] = ov[k];
+        w[i0 + k] = wv[k];
+      }
   }
 }
 
@@ -276,11 +309,17 @@ extern "C" int mt_clip_rmsprop(float *w, float *ms, float *mom, const float *g, 
                "clip_type %d not supported (reference 'local' is broken: actor_learner.py:66-67)",
                clip_type);
   MT_CHECK_ARG(clip_type != MT_CLIP_GLOBAL || clip > 0.f, "clip must be > 0");
-  int blocks = (int)std::min<size_t>((n + 255) / 256, 1024);
+  MT_CHECK_ARG(n <= ((size_t)1 << 36), "n too large");
+  const bool vec = ((((uintptr_t)w) | ((uintptr_t)ms) | ((uintptr_t)mom) | ((uintptr_t)g)) & 15) == 0;
+  const size_t per_thread = vec ? 4 : 1;
+  int blocks = (int)((n + 256 * per_thread - 1) / (256 * per_thread));
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(clip_rmsprop_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, ms,
-                     mom, g, n, partials, lr_dev, decay, momentum, eps, clip, clip_type, inv_scale,
-                     norm_out);
+  if (vec)
+    hipLaunchKernelGGL(clip_rmsprop_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, ms, mom, g, n,
+                       partials, lr_dev, decay, momentum, eps, clip, clip_type, inv_scale, norm_out);
+  else
+    hipLaunchKernelGGL(clip_rmsprop_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, ms, mom, g, n,
+                       partials, lr_dev, decay, momentum, eps, clip, clip_type, inv_scale, norm_out);
   MT_LAUNCHED();
   return MT_OK;
 }
