@@ -134,12 +134,32 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
   const int q = g / NH;  // 0 i, 1 j, 2 f, 3 o
   float c = 0.f;
   if (g < NH) hs[g] = 0.f;
+  // the x-product slab sums of all STEPS positions first (they do not depend on h): 8 slabs x
+  // STEPS loads in flight per batch instead of one load latency per slab; adds in slab order
+  float zx[STEPS];
+  size_t xoff[STEPS];
+#pragma unroll
+  for (int t = 0; t < STEPS; ++t) {
+    zx[t] = 0.f;
+    xoff[t] = (size_t)map(b, t) * G4 + g;
+  }
+  for (int s0 = 0; s0 < S; s0 += 8) {
+    float v[STEPS][8];
+#pragma unroll
+    for (int t = 0; t < STEPS; ++t)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[t][u] = xg[(size_t)min(s0 + u, S - 1) * rows * G4 + xoff[t]];
+#pragma unroll
+    for (int t = 0; t < STEPS; ++t)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (s0 + u < S) zx[t] += v[t][u];
+  }
   __syncthreads();
+#pragma unroll
   for (int t = 0; t < STEPS; ++t) {
     const int row = b * STEPS + t;
-    const int xr = map(b, t);
-    float z = 0.f;
-    for (int s = 0; s < S; ++s) z += xg[((size_t)s * rows + xr) * G4 + g];
+    float z = zx[t];
     float hz = 0.f;
 #pragma unroll
     for (int k = 0; k < NH; ++k) hz += hs[k] * wcol[k];

@@ -318,15 +318,16 @@ __device__ __forceinline__ void sum_slabs_body(const float *__restrict__ P, int 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (c < n4) {
     const f32x4 *p = reinterpret_cast<const f32x4 *>(P) + c;
-    int z = sub;
-    for (; z + 16 * 15 < S; z += 256) {
+    // batches of up to 16 predicated loads, all issued before the first add (a plain remainder
+    // loop would wait out one load latency per slab); the adds stay in slab order
+    for (int z = sub; z < S; z += 256) {
       f32x4 v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = p[(size_t)(z + 16 * u) * n4];
+      for (int u = 0; u < 16; ++u) v[u] = p[(size_t)min(z + 16 * u, S - 1) * n4];  // clamped: no branches
 #pragma unroll
-      for (int u = 0; u < 16; ++u) acc += v[u];
+      for (int u = 0; u < 16; ++u)
+        if (z + 16 * u < S) acc += v[u];
     }
-    for (; z < S; z += 16) acc += p[(size_t)z * n4];
   }
   part[sub * kSlabCols + col] = acc;
   __syncthreads();
@@ -491,15 +492,16 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
     const float *p = slabs + (size_t)b * F + f;
     const size_t zs_stride = (size_t)B * F;
     float acc = 0.f;
-    int z = 0;
-    for (; z + 7 < S; z += 8) {
-      float t[8];
+    // up to 16 predicated loads in flight (S = 9 for the NIPS trunk: one round trip), adds in
+    // slab order
+    for (int z = 0; z < S; z += 16) {
+      float t[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = p[(size_t)(z + u) * zs_stride];
+      for (int u = 0; u < 16; ++u) t[u] = p[(size_t)min(z + u, S - 1) * zs_stride];  // clamped: no branches
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += t[u];
+      for (int u = 0; u < 16; ++u)
+        if (z + u < S) acc += t[u];
     }
-    for (; z < S; ++z) acc += p[(size_t)z * zs_stride];
     const float h = act_fwd(acc + fc_b[f], act, alpha);
     hs[f] = h;
     H[(size_t)b * F + f] = h;
