@@ -160,7 +160,7 @@ def cpu_baseline(cfg, T, seconds, rank):
         pass
 
     loop = Timed(emus, net, tab, A, max_local_steps=T, workers=ew, record=False, lstm=cfg['arch'] == 'LSTM')
-    # warm up one update, then time whole updates until `seconds` elapse (at most 200)
+    # warm up one update, then time whole updates until `seconds` elapse (at most 2000)
     steps_per_update = ec * T
     t_start = [None]
     n_upd = [0]
@@ -171,7 +171,7 @@ def cpu_baseline(cfg, T, seconds, rank):
         n_upd[0] += 1
         if n_upd[0] == 1:
             t_start[0] = time.perf_counter()
-        elif time.perf_counter() - t_start[0] > seconds or n_upd[0] >= 201:
+        elif time.perf_counter() - t_start[0] > seconds or n_upd[0] >= 2001:
             loop.global_step = 1 << 62  # stop after this update
     net.train = train_hook
     loop.run(1 << 61)
