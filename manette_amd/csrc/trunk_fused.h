@@ -65,11 +65,15 @@ struct FusedNips {
   static constexpr int M1 = ROWS1 * OW1;  // 80 conv1 pixels
   static constexpr int MT1 = (M1 + 15) / 16;  // 5 m-tiles
   static constexpr int KC1 = KK1 / 16, KC2 = KK2 / 16;
-  static_assert(KC1 % 4 == 0 && KC2 % 4 == 0, "K chunks split over 4 waves");
+  // conv kernel waves: 8 for gray frames (two waves per SIMD hide each other's LDS/convert
+  // latency in conv1), 4 for RGB (whose 3x input rows would not fit 64 KB of LDS beside 8 waves'
+  // partials)
+  static constexpr int NW = C == 4 ? 8 : 4, NT = 64 * NW;
+  static_assert(KC1 % NW == 0 && KC2 % NW == 0, "K chunks split over the waves");
   static constexpr int IN_BYTES = RIN * 84 * C;
   static constexpr int FR_BYTES = RIN * 84 * D;  // the block's rows of one new frame
   // LDS (floats unless noted)
-  static constexpr int RED_FLOATS = 4 * MT1 * 16 * CO1;  // >= 4*16*32 (conv2)
+  static constexpr int RED_FLOATS = NW * MT1 * 16 * CO1;  // >= NW*16*32 (conv2)
   static_assert(4 * FR_BYTES <= RED_FLOATS * 4, "staged frames alias the reduction buffer");
   static constexpr size_t LDS_BYTES = IN_BYTES + sizeof(float) * (RED_FLOATS + M1 * A1S);
   // fc kernel
@@ -86,14 +90,14 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
   if constexpr (!STACK) {
     const uint4 *src = reinterpret_cast<const uint4 *>(obs + row0);
     uint4 *dst = reinterpret_cast<uint4 *>(xin);
-    for (int q = threadIdx.x; q < Fz::IN_BYTES / 16; q += 256) dst[q] = src[q];
+    for (int q = threadIdx.x; q < Fz::IN_BYTES / 16; q += Fz::NT) dst[q] = src[q];
     return;
   } else {
     __shared__ int s_p;
     {  // the previous state's rows
       const uint4 *src = reinterpret_cast<const uint4 *>(st.prev + row0);
       uint4 *dst = reinterpret_cast<uint4 *>(xin);
-      for (int q = threadIdx.x; q < Fz::IN_BYTES / 16; q += 256) dst[q] = src[q];
+      for (int q = threadIdx.x; q < Fz::IN_BYTES / 16; q += Fz::NT) dst[q] = src[q];
     }
     // one round trip for the common case: the push count and push 0's rows with the prev rows
     // (count == NULL: no pushes, the new state is a copy of prev — slot 0 <- slot T of the
@@ -102,12 +106,12 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
     if (st.count) {
       const size_t f0 = ((size_t)4 * e * 84 + 8 * i) * 84 * Fz::D;  // push 0 = slot 4e
       const uint4 *fs = reinterpret_cast<const uint4 *>(st.frames + f0);
-      for (int q = threadIdx.x; q < Fz::FR_BYTES / 16; q += 256) reinterpret_cast<uint4 *>(fr)[q] = fs[q];
+      for (int q = threadIdx.x; q < Fz::FR_BYTES / 16; q += Fz::NT) reinterpret_cast<uint4 *>(fr)[q] = fs[q];
     }
     __syncthreads();
     const int p = st.count ? min(max(s_p, 1), 4) : 0;
     if (p > 1) {  // FiGAR repeats: pushes 1..p-1 (slots 4e+1..)
-      for (int q = threadIdx.x; q < (p - 1) * (Fz::FR_BYTES / 16); q += 256) {
+      for (int q = threadIdx.x; q < (p - 1) * (Fz::FR_BYTES / 16); q += Fz::NT) {
         const int j = 1 + q / (Fz::FR_BYTES / 16), qq = q - (j - 1) * (Fz::FR_BYTES / 16);
         const size_t fj = (((size_t)4 * e + j) * 84 + 8 * i) * 84 * Fz::D;
         reinterpret_cast<uint4 *>(fr + j * Fz::FR_BYTES)[qq] = reinterpret_cast<const uint4 *>(st.frames + fj)[qq];
@@ -119,7 +123,7 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
     uint32_t *xw = reinterpret_cast<uint32_t *>(xin);
     uint32_t *ow = reinterpret_cast<uint32_t *>(st.out + row0);
     const int own = (i == Fz::ROWS2 - 1 ? Fz::RIN : 8) * 84 * Fz::D;  // words this block writes
-    for (int w = threadIdx.x; w < Fz::RIN * 84 * Fz::D; w += 256) {
+    for (int w = threadIdx.x; w < Fz::RIN * 84 * Fz::D; w += Fz::NT) {
       uint32_t v = p < 4 ? xw[w] >> (8 * p) : 0u;
       for (int j = 0; j < p; ++j) v |= (uint32_t)fr[j * Fz::FR_BYTES + w] << (8 * (4 - p + j));
       xw[w] = v;
@@ -133,7 +137,7 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
 // block (e, i) writes conv1 rows 2i, 2i+1 (the last block also 18, 19), so each value is written
 // once.
 template <int C, bool STACK>
-__global__ __launch_bounds__(256) void nips_conv_kernel(const uint8_t *__restrict__ obs, StackSrc st, int B,
+__global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8_t *__restrict__ obs, StackSrc st, int B,
                                                         const float *__restrict__ W1, const float *__restrict__ W2,
                                                         int act, float alpha, float *__restrict__ act2,
                                                         float *__restrict__ act1) {
@@ -152,12 +156,13 @@ __global__ __launch_bounds__(256) void nips_conv_kernel(const uint8_t *__restric
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
 
-  // conv1 weight fragments of this wave's K chunks (c = w + 4j): B[k][n] = W1[k*16 + n]
-  constexpr int J1 = Fz::KC1 / 4;
+  // conv1 weight fragments of this wave's K chunks (c = w + NW j): B[k][n] = W1[k*16 + n]
+  constexpr int NW = Fz::NW;
+  constexpr int J1 = Fz::KC1 / NW;
   float b1f[J1][4];
 #pragma unroll
   for (int j = 0; j < J1; ++j) {
-    const int k0 = 16 * (w + 4 * j) + 4 * g;
+    const int k0 = 16 * (w + NW * j) + 4 * g;
 #pragma unroll
     for (int s = 0; s < 4; ++s) b1f[j][s] = W1[(size_t)(k0 + s) * Fz::CO1 + r];
   }
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(256) void nips_conv_kernel(const uint8_t *__restric
     const float sc = 1.0f / 255.0f;
 #pragma unroll
     for (int j = 0; j < J1; ++j) {
-      const int k0 = 16 * (w + 4 * j) + 4 * g;
+      const int k0 = 16 * (w + NW * j) + 4 * g;
       const int kpos = k0 / C, ci = k0 - kpos * C;
       const int ky = kpos >> 3, kx = kpos & 7;
       f32x4 a[Fz::MT1];
@@ -196,11 +201,11 @@ __global__ __launch_bounds__(256) void nips_conv_kernel(const uint8_t *__restric
       for (int q = 0; q < 4; ++q) red[(w * Fz::MT1 * 16 + t * 16 + g * 4 + q) * Fz::CO1 + r] = acc[t][q];
   }
   // conv2 weight fragments (issued before the barrier so their latency overlaps the reduction)
-  constexpr int J2 = Fz::KC2 / 4;
+  constexpr int J2 = Fz::KC2 / NW;
   float b2f[J2][2][4];
 #pragma unroll
   for (int j = 0; j < J2; ++j) {
-    const int k0 = 16 * (w + 4 * j) + 4 * g;
+    const int k0 = 16 * (w + NW * j) + 4 * g;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
@@ -210,9 +215,11 @@ __global__ __launch_bounds__(256) void nips_conv_kernel(const uint8_t *__restric
   {
     const float *b1 = W1 + (size_t)Fz::KK1 * Fz::CO1;
     constexpr int P = Fz::MT1 * 16 * Fz::CO1;  // stride of one wave's partials
-    for (int idx = threadIdx.x; idx < Fz::M1 * Fz::CO1; idx += 256) {
+    for (int idx = threadIdx.x; idx < Fz::M1 * Fz::CO1; idx += Fz::NT) {
       const int m = idx / Fz::CO1, n = idx - m * Fz::CO1;
-      const float s = ((red[idx] + red[P + idx]) + red[2 * P + idx]) + red[3 * P + idx];
+      float s = red[idx];
+#pragma unroll
+      for (int v = 1; v < NW; ++v) s += red[v * P + idx];  // wave order
       const float y = act_fwd(s + b1[n], act, alpha);
       a1[m * Fz::A1S + n] = y;
       if (act1 && (m < 2 * Fz::OW1 || i == Fz::ROWS2 - 1))  // conv1 rows 2i, 2i+1 (+ 18, 19)
@@ -228,7 +235,7 @@ __global__ __launch_bounds__(256) void nips_conv_kernel(const uint8_t *__restric
     const int ox = min(r, Fz::OW2 - 1);
 #pragma unroll
     for (int j = 0; j < J2; ++j) {
-      const int c = w + 4 * j;  // (ky, kx) = (c / 4, c % 4), channels 4g..4g+3
+      const int c = w + NW * j;  // (ky, kx) = (c / 4, c % 4), channels 4g..4g+3
       const int ky = c >> 2, kx = c & 3;
       const f32x4 a = *reinterpret_cast<const f32x4 *>(a1 + (ky * Fz::OW1 + 2 * ox + kx) * Fz::A1S + 4 * g);
 #pragma unroll
@@ -246,9 +253,11 @@ __global__ __launch_bounds__(256) void nips_conv_kernel(const uint8_t *__restric
   {
     const float *b2 = W2 + (size_t)Fz::KK2 * Fz::CO2;
     constexpr int P = 16 * Fz::CO2;
-    for (int idx = threadIdx.x; idx < Fz::FEAT; idx += 256) {
+    for (int idx = threadIdx.x; idx < Fz::FEAT; idx += Fz::NT) {
       const int n = idx & (Fz::CO2 - 1);
-      const float s = ((red[idx] + red[P + idx]) + red[2 * P + idx]) + red[3 * P + idx];
+      float s = red[idx];
+#pragma unroll
+      for (int v = 1; v < NW; ++v) s += red[v * P + idx];  // wave order
       act2[((size_t)e * Fz::ROWS2 + i) * Fz::FEAT + idx] = act_fwd(s + b2[n], act, alpha);
     }
   }
@@ -316,10 +325,10 @@ static inline int launch_nips_trunk(const uint8_t *obs, const StackSrc *st, int 
   using Fz = FusedNips<C>;
   static_assert(Fz::LDS_BYTES <= 64 * 1024, "conv kernel LDS fits the default limit");
   if (st) {
-    hipLaunchKernelGGL((nips_conv_kernel<C, true>), dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, st->out, *st,
+    hipLaunchKernelGGL((nips_conv_kernel<C, true>), dim3(Fz::ROWS2 * B), dim3(Fz::NT), Fz::LDS_BYTES, s, st->out, *st,
                        B, W1, W2, act, alpha, act2, act1);
   } else {
-    hipLaunchKernelGGL((nips_conv_kernel<C, false>), dim3(Fz::ROWS2 * B), dim3(256), Fz::LDS_BYTES, s, obs,
+    hipLaunchKernelGGL((nips_conv_kernel<C, false>), dim3(Fz::ROWS2 * B), dim3(Fz::NT), Fz::LDS_BYTES, s, obs,
                        StackSrc{}, B, W1, W2, act, alpha, act2, act1);
   }
   hipLaunchKernelGGL(nips_fc_kernel<C>, dim3(Fz::F / Fz::FC_BN, Fz::ROWS2, (B + Fz::FC_BM - 1) / Fz::FC_BM),
