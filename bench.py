@@ -39,9 +39,6 @@ CONFIGS = {
 }
 MI355X_FP32_TFLOPS = 157.3   # dense fp32 (vector = MFMA), MI355X_MICROARCH.md
 MI355X_HBM_GBS = 8000.0      # HBM3E peak, MI355X_MICROARCH.md
-# the kernels one mt_forward_trunk call launches (rocprof names, template arguments for gray
-# frames), per arch where the trunk has dedicated kernels: NIPS conv (no stacking) + fc
-TRUNK_KERNELS = {'NIPS': ['nips_conv_kernel<4, false>', 'nips_fc_kernel<4>']}
 
 
 def load_pmc(config, kernels):
@@ -106,18 +103,19 @@ FRAME_LAYERS = ('conv', 'lstm_x')
 
 
 def train_pass_flops(layers, N, frame_rows=None):
-    """forward + backward (dW everywhere, dX everywhere except the input conv). LSTM frame
-    store: the rollout already ran the forward, so the train pass is the backward of the
-    frame_rows distinct frames (2x their forward, minus conv1's dX) + that of the N windows."""
-    if frame_rows is None:
+    """FLOPs the update's train pass executes: the rollout already ran the forward of every row
+    (mt_forward_rows / the LSTM frame store), so it is the backward only — dW of every layer and
+    dX of every layer except the input conv (2x the forward minus conv1's forward), per row; LSTM:
+    that of the frame_rows distinct frames + the N windows' cell / dense / heads."""
+    if frame_rows is None:  # the forward is the rollout's: backward only (dW all, dX all but conv1)
         fwd = sum(l[1] for l in layers)
-        return N * (3 * fwd - layers[0][1])
+        return N * (2 * fwd - layers[0][1])
     per_frame = sum(l[1] for l in layers if l[0] in FRAME_LAYERS)
     per_win = sum(l[1] for l in layers if l[0] not in FRAME_LAYERS)
     return frame_rows * (2 * per_frame - layers[0][1]) + N * 2 * per_win
 
 
-def build_args(cfg, T, sampling, seed):
+def build_args(cfg, T, sampling, seed, debugging_folder=None):
     import train as train_cli
     a = train_cli.get_arg_parser().parse_args([])
     a.game = cfg['game']
@@ -133,8 +131,34 @@ def build_args(cfg, T, sampling, seed):
     a.sampling = sampling
     a.runner = 'native'
     a.seed = seed
-    a.debugging_folder = tempfile.mkdtemp(prefix='manette_bench_')
+    a.debugging_folder = debugging_folder or tempfile.mkdtemp(prefix='manette_bench_')
     return a
+
+
+def make_learner(config, T=5, sampling='device', seed=0, staging='resized', pipeline=True, update_graph=True,
+                 rank=0, debugging_folder=None, episode_len=None):
+    """The benchmarked learner of `config` (BASELINE.json configs[1..4]; tests/test_e2e_gpu.py
+    checks exactly this path against the oracle). episode_len: a shorter synthetic episode (tests
+    exercise resets); None = the synthetic default."""
+    from manette_amd.exploration_policy import ExplorationPolicy
+    from manette_amd.paac import PAACLearner
+    import train as train_cli
+    cfg = CONFIGS[config]
+    args = build_args(cfg, T, sampling, seed, debugging_folder)
+    args.env_id_offset = rank * cfg['ec']
+    args.staging = staging
+    args.pipeline = pipeline
+    args.update_graph = update_graph
+    np.random.seed(1234 + rank)
+    explo = ExplorationPolicy(args)
+    net_creator, env_creator = train_cli.get_network_and_environment_creator(args, explo)
+    if episode_len is not None:
+        from manette_amd.synthetic import SyntheticBank
+        env_creator.create_bank = lambda first, n: SyntheticBank(env_creator.rank_offset + first, n, rgb=cfg['rgb'],
+                                                                 episode_len=episode_len)
+    learner = PAACLearner(net_creator, env_creator, explo, args)
+    learner.is_chief = False  # no checkpoint writes from the benchmark
+    return learner, args
 
 
 def cpu_baseline(cfg, T, seconds, rank):
@@ -159,6 +183,16 @@ def cpu_baseline(cfg, T, seconds, rank):
     class Timed(host_loop.HostLoop):
         pass
 
+    net_s = [0.0]
+    orig_fwd = net.forward
+
+    def fwd_hook(*a, **k):
+        t = time.perf_counter()
+        r = orig_fwd(*a, **k)
+        if t_start[0] is not None:
+            net_s[0] += time.perf_counter() - t
+        return r
+    net.forward = fwd_hook
     loop = Timed(emus, net, tab, A, max_local_steps=T, workers=ew, record=False, lstm=cfg['arch'] == 'LSTM')
     # warm up one update, then time whole updates until `seconds` elapse (at most 2000)
     steps_per_update = ec * T
@@ -167,7 +201,10 @@ def cpu_baseline(cfg, T, seconds, rank):
     orig_train = net.train
 
     def train_hook(*a, **k):
+        t = time.perf_counter()
         orig_train(*a, **k)
+        if t_start[0] is not None:
+            net_s[0] += time.perf_counter() - t
         n_upd[0] += 1
         if n_upd[0] == 1:
             t_start[0] = time.perf_counter()
@@ -178,6 +215,7 @@ def cpu_baseline(cfg, T, seconds, rank):
     elapsed = time.perf_counter() - t_start[0]
     timed = n_upd[0] - 1
     return dict(value=timed * steps_per_update / elapsed, unit='env-steps/s', cores=cores, kind='port',
+                _net_ms_per_update=1e3 * net_s[0] / max(timed, 1),
                 sample='%d PAAC updates (ec=%d, t_max=%d, %s) after 1 warm-up, %d emulator worker '
                        'processes, torch-CPU fp32 network on %d threads, %.1f s' % (timed, ec, T, cfg['arch'], ew, cores, elapsed))
 
@@ -200,6 +238,8 @@ def main():
                     help='disable MT_ROLLOUT_PIPELINED (on by default)')
     ap.add_argument('--no_update_graph', dest='update_graph', action='store_false',
                     help='launch the update eagerly instead of replaying it as a hipGraph')
+    ap.add_argument('--measure_updates', type=int, default=20,
+                    help='updates after the timed region during which the rollout times its trunk kernels in place')
     ap.add_argument('--trunk_sweep', default='256,1024,4096',
                     help='extra batch sizes the trunk kernel is timed at after the run ("" = none)')
     a = ap.parse_args()
@@ -210,24 +250,11 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    if world > 1:  # control channel (barriers, max-over-ranks time, RCCL unique id); data: mt_allreduce
+        dist.init_process_group('gloo')
     cfg = CONFIGS[a.config]
     T = a.t_max
-    args = build_args(cfg, T, a.sampling, a.seed)
-    args.env_id_offset = rank * cfg['ec']
-    args.staging = a.staging
-    args.pipeline = a.pipeline
-    args.update_graph = a.update_graph
-
-    from manette_amd.exploration_policy import ExplorationPolicy
-    from manette_amd.paac import PAACLearner
-    import train as train_cli
-    np.random.seed(1234 + rank)
-    explo = ExplorationPolicy(args)
-    net_creator, env_creator = train_cli.get_network_and_environment_creator(args, explo)
-    learner = PAACLearner(net_creator, env_creator, explo, args)
-    learner.is_chief = False  # no checkpoint writes from the benchmark
+    learner, args = make_learner(a.config, T, a.sampling, a.seed, a.staging, a.pipeline, a.update_graph, rank)
     learner.start()
     if a.step_impl == 'python' and learner.native_step is not None:
         from manette_amd import _lib
@@ -265,12 +292,30 @@ def main():
     else:
         step_phases = None
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    # the update's train pass (backward of the last rollout) alone: 20 launches back to back
-    # between one event pair, after the timed region (which runs the update as a hipGraph)
+    # ---- measurements after the timed region (none of them is part of `value`) ----------------
     prof = {}
+    # (1) roofline kernels where the timed loop runs them: the native rollout records an event
+    #     pair around every step forward's trunk launches (NIPS: the stacking conv kernel + the
+    #     dense kernel, between the pull and heads kernels of the pipelined chain) over
+    #     --measure_updates more updates (mt_rollout_trunk_timing)
+    inloop_us = None
+    if learner.native_step is not None and a.measure_updates > 0:
+        import ctypes as C
+        from manette_amd import _lib
+        lib = _lib.hip()
+        tot, cnt = C.c_double(), C.c_int64()
+        _lib.check(lib.mt_rollout_trunk_timing(learner.native_step, 1, C.byref(tot), C.byref(cnt)))
+        for _ in range(a.measure_updates):
+            one_update()
+        torch.cuda.synchronize()
+        _lib.check(lib.mt_rollout_trunk_timing(learner.native_step, 0, C.byref(tot), C.byref(cnt)))
+        if cnt.value:
+            inloop_us = tot.value / cnt.value
+    # (2) the update's train pass (backward of the last rollout) alone: 20 launches back to back
+    #     between one event pair (the timed region replays it inside the update's hipGraph)
     learner.train_backward()
     s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s_ev.record()
@@ -279,9 +324,9 @@ def main():
     e_ev.record()
     torch.cuda.synchronize()
     prof['train_pass'] = [s_ev.elapsed_time(e_ev) / 20.0]
-    # rollout-batch forward (E rows) and its trunk half alone (the roofline kernel: mt_forward_trunk,
-    # one launch of the fused NIPS trunk), each timed with HIP events on the stream they are
-    # launched on (torch's current stream, passed to every C-ABI call), back to back
+    # (3) supplementary, isolated: the rollout-batch forward (E rows) and its trunk half
+    #     (mt_forward_trunk: NIPS = the non-stacking conv kernel + the dense kernel) back to back,
+    #     HIP events on the stream they are launched on (torch's current stream)
     E = cfg['ec']
     net = learner.network
     if learner.lstm_bool:  # a step's new frames (trunk + cell x-product), + its E windows
@@ -298,8 +343,6 @@ def main():
         roll_fwd()
         e_ev.record()
         fw.append((s_ev, e_ev))
-    # trunk: 5 warm launches, then 40 launches back to back between one event pair (the GPU
-    # stays busy, so the per-launch average is the kernel's duration, as rocprof reports it)
     for _ in range(5):
         roll_trunk()
     s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -310,6 +353,14 @@ def main():
     torch.cuda.synchronize()
     prof['rollout_forward'] = [s_ev_.elapsed_time(e_ev_) for (s_ev_, e_ev_) in fw[5:]]
     prof['rollout_trunk'] = [s_ev.elapsed_time(e_ev) / 40.0]
+    # (4) data parallel: the replicas must hold identical parameters after the run
+    replicas = None
+    if world > 1:
+        pf = learner.network.params.double()
+        ck = torch.stack([pf.sum(), (pf * torch.arange(pf.numel(), device=pf.device, dtype=torch.float64)).sum()]).cpu()
+        allck = [torch.zeros_like(ck) for _ in range(world)]
+        dist.all_gather(allck, ck)
+        replicas = all(torch.equal(x, allck[0]) for x in allck)
     # the same trunk launch at larger batches (supplementary: how far the kernel is from its
     # bounds once the grid fills the chip; the workload's own batch is E = ec above)
     sweep = []
@@ -341,18 +392,35 @@ def main():
         tp_ms = float(np.mean(prof['train_pass']))
         tp_flops = train_pass_flops(layers, N, 1 + (T + 4) * ec if lstm else None)
         rf_ms = float(np.mean(prof['rollout_forward']))
-        tk_ms = float(np.mean(prof['rollout_trunk']))
+        iso_ms = float(np.mean(prof['rollout_trunk']))
         # one rollout step: E new frames (trunk) + E windows (LSTM) / E states
         fwd_flops = ec * sum(l[1] for l in layers)
         fwd_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in layers) + 4 * ec * sum(l[3] for l in layers)
-        # trunk (roofline kernel): algorithmic bytes = the frames read once + the trunk weights
-        # read once + the dense layer's pre-activation output written once
+        # trunk (roofline kernels): algorithmic bytes = the E states read once + the trunk weights
+        # read once + the dense layer's pre-activation output written once; FLOP = E x (convs + dense)
+        # 
         trunk = [l for l in layers if l[0] in ('conv', 'fc', 'lstm_x')]
         out_floats = trunk[-1][3]
         tk_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in trunk) + 4 * ec * out_floats
         tk_flops = ec * sum(l[1] for l in trunk)
+        C_in = 4 * depth
+        stacking = learner is not None and getattr(learner, 'slot0_in_rollout', False)
+        if inloop_us is not None:
+            tk_ms = inloop_us * 1e-3
+            kern = ('nips_conv_kernel<%d, true> + nips_fc_kernel<%d> (stacking rollout chain)' % (C_in, C_in)
+                    if stacking else 'trunk kernels of the rollout forward (implicit-GEMM convs + split-K dense)')
+            timing = 'in the timed loop: HIP event pair around each macro-step forward\'s trunk launches ' \
+                     '(mt_rollout_trunk_timing), %d updates after the timed region' % a.measure_updates
+            pmc_kernels = (['nips_conv_kernel<%d, true>' % C_in, 'nips_fc_kernel<%d>' % C_in]
+                           if stacking else None)
+        else:
+            tk_ms = iso_ms
+            kern = 'mt_forward_trunk (%s)' % ('LSTM frame trunk + cell x-product' if lstm else 'layered')
+            timing = 'isolated: 40 mt_forward_trunk calls back to back between one HIP event pair'
+            pmc_kernels = None
         tk_gbs = tk_bytes / (tk_ms * 1e-3) / 1e9
-        pmc = load_pmc(a.config, TRUNK_KERNELS.get(cfg['arch']) if not cfg['rgb'] else None)
+        tk_tf = tk_flops / (tk_ms * 1e-3) / 1e12
+        pmc = load_pmc(a.config, pmc_kernels)
         achieved = tp_flops / (tp_ms * 1e-3) / 1e12
         line = {
             'metric': 'env-steps/sec (ec x t_max frames per update)',
@@ -366,26 +434,31 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'fp32',
-            'data': 'synthetic (seeded 210x160 screens, native emulator threads, GPU preprocess)',
+            'data': 'synthetic emulators (seeded 210x160 screen rings, manette_amd/synthetic.py; no ALE): host '
+                    'emulator threads pool + resize each push to 84x84, the GPU stacks the 4-frame states and runs '
+                    'forward, sampling, returns, backward and RMSProp; random-init weights. The emulators are '
+                    'near-free, so this is an upper bound for real ALE games (learner_only isolates the GPU side)',
             'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step, %s staging%s' % (
                 a.config, ec, cfg['ew'], T, a.sampling, a.step_impl, a.staging, ', pipelined' if a.pipeline else ''), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
                 'global_emulators': ec * world, 'parallelism': 'dp%d' % world},
             # bound = the resource the trunk's arithmetic intensity binds on the roofline (fp32 ridge
             # 157.3 TFLOP/s / 8 TB/s = 19.7 FLOP/B; NIPS E=32: 52 FLOP/B -> mfma); both fractions kept
             'roofline': dict(
-                (('bound', 'mfma'), ('achieved', round(tk_flops / (tk_ms * 1e-3) / 1e12, 3)), ('peak', MI355X_FP32_TFLOPS),
-                 ('unit', 'TFLOP/s'), ('frac', round(tk_flops / (tk_ms * 1e-3) / 1e12 / MI355X_FP32_TFLOPS, 4)))
+                (('bound', 'mfma'), ('achieved', round(tk_tf, 3)), ('peak', MI355X_FP32_TFLOPS),
+                 ('unit', 'TFLOP/s'), ('frac', round(tk_tf / MI355X_FP32_TFLOPS, 4)))
                 if tk_flops / tk_bytes > MI355X_FP32_TFLOPS * 1e12 / (MI355X_HBM_GBS * 1e9) else
                 (('bound', 'hbm'), ('achieved', round(tk_gbs, 1)), ('peak', MI355X_HBM_GBS), ('unit', 'GB/s'),
                  ('frac', round(tk_gbs / MI355X_HBM_GBS, 4))),
-                kernel=' + '.join(TRUNK_KERNELS.get(cfg['arch'], ['mt_forward_trunk (layered)'])),
+                kernel=kern, timing=timing,
                 traffic=pmc['hbm_bytes'] if pmc else None,
                 algorithmic_bytes_per_launch=tk_bytes, algorithmic_flop_per_launch=tk_flops,
                 us_per_launch=round(tk_ms * 1e3, 2), hbm_gbs=round(tk_gbs, 1),
-                hbm_frac=round(tk_gbs / MI355X_HBM_GBS, 4),
-                flop_frac=round(tk_flops / (tk_ms * 1e-3) / 1e12 / MI355X_FP32_TFLOPS, 4),
+                hbm_frac=round(tk_gbs / MI355X_HBM_GBS, 4), flop_frac=round(tk_tf / MI355X_FP32_TFLOPS, 4),
                 traffic_source=pmc['source'] if pmc else None),
-            'train_pass': {'bound': 'mfma', 'kernels': ('backward of %d windows over %d distinct frames (forward reused from the rollout)' % (N, 1 + (T + 4) * ec)) if lstm else 'forward + fused loss backward, %d rows' % N,
+            'trunk_isolated': {'kernel': 'mt_forward_trunk, back to back', 'us_per_launch': round(iso_ms * 1e3, 2),
+                               'tflops': round(tk_flops / (iso_ms * 1e-3) / 1e12, 3)},
+            'train_pass': {'bound': 'mfma', 'kernels': ('backward of %d windows over %d distinct frames (forward reused from the rollout)' % (N, 1 + (T + 4) * ec)) if lstm else 'fused returns + loss + backward of %d rows (forward reused from the rollout)' % N,
+                           'flop_count': 'executed backward: dW of every layer + dX of every layer but conv1',
                            'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',
                            'frac': round(achieved / MI355X_FP32_TFLOPS, 4),
                            'ms_per_launch': round(tp_ms, 4), 'flop_per_launch': tp_flops},
@@ -393,6 +466,8 @@ def main():
                                 'hbm_gbs': round(fwd_bytes / (rf_ms * 1e-3) / 1e9, 1),
                                 'hbm_frac': round(fwd_bytes / (rf_ms * 1e-3) / 1e9 / MI355X_HBM_GBS, 4)},
         }
+        if replicas is not None:
+            line['replicas_identical'] = replicas
         if sweep:
             per_env_bytes = 84 * 84 * 4 * depth + 4 * out_floats
             w_bytes = 4 * sum(l[2] for l in trunk)
@@ -410,6 +485,15 @@ def main():
             learner.cleanup()
             learner = None
             line['cpu_baseline'] = cpu_baseline(cfg, T, a.cpu_seconds, rank)
+            # learner-only: the network work of one update on each side (GPU: T + 1 rollout
+            # forwards of E rows + the train pass; CPU port: its T + 1 forwards + train step)
+            cpu_net = line['cpu_baseline'].pop('_net_ms_per_update')
+            gpu_net = (T + 1) * rf_ms + tp_ms
+            line['learner_only'] = {'gpu_ms_per_update': round(gpu_net, 4), 'cpu_ms_per_update': round(cpu_net, 3),
+                                    'ratio': round(cpu_net / gpu_net, 1),
+                                    'note': 'network work only (no emulators, no host loop): GPU = (T+1) isolated '
+                                            'rollout forwards + the train pass; CPU = the port\'s torch-CPU forwards '
+                                            '+ train step inside the cpu_baseline sample'}
         print(json.dumps(line), flush=True)
     if learner is not None:
         learner.cleanup()

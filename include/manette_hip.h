@@ -145,12 +145,14 @@ int mt_lstm_frames_backward(const mt_net *net, const float *params, const uint8_
  * Replaces ExplorationPolicy.multinomial_choose (exploration_policy.py:108-116) with an
  * inverse-CDF draw on (p - float32 epsneg), the last category taking the remainder — the
  * distribution numpy's multinomial(1, p - epsneg) draws from. Uniforms come from a
- * counter-based hash of (seed, row, counters[row]); counters (device, one uint64 per row) are
- * incremented by the call, so a captured graph draws fresh numbers on every replay.
+ * counter-based hash of (seed, row0 + row, counters[row]); row0 = the global env id of row 0
+ * (a data-parallel rank's env offset, runners.py:17-18 shard), so every env draws the same
+ * stream whichever rank owns it. counters (device, one uint64 per row) are incremented by the
+ * call, so a captured graph draws fresh numbers on every replay.
  * Writes int32 indices a_idx [batch], r_idx [batch], and (if pair != NULL) both again into
  * pair [2][batch] so one copy moves them to the host. */
 int mt_sample(const float *pi, const float *rep, int batch, int num_actions, int num_reps,
-              uint64_t seed, uint64_t *counters, int32_t *a_idx, int32_t *r_idx, int32_t *pair,
+              uint64_t seed, int row0, uint64_t *counters, int32_t *a_idx, int32_t *r_idx, int32_t *pair,
               mt_stream_t stream);
 
 /* ---- n-step return / advantage scan (A9) ---------------------------------------------------
@@ -324,6 +326,7 @@ typedef struct mt_rollout_buffers {
                                   env after writing its pair; the host polls these instead of an event
                                   (NULL: hipEventQuery) */
   int32_t flags;               /* MT_ROLLOUT_* */
+  int32_t env_offset;          /* global env id of env 0 (data-parallel shard offset): the draw's row0 */
 } mt_rollout_buffers;
 int mt_rollout_create(const mt_net *net, int E, int T, void *runner, void *book,
                       const mt_rollout_buffers *buffers, uint64_t seed, mt_rollout **out);
@@ -337,6 +340,33 @@ int mt_rollout_run(mt_rollout *ro, const float *params, int64_t *global_step, mt
  * for the sampled indices, [1] emulator step, [2] bookkeeping, [3] upload + preprocess
  * enqueue, [4] number of steps. reset != 0 zeroes the counters. */
 int mt_rollout_stats(mt_rollout *ro, double *out5, int reset);
+/* Live timing of the trunk kernels the rollout runs (roofline measurement, bench.py): enable != 0
+ * records an event pair around each step forward's trunk launches (NIPS: the stacking conv kernel
+ * + the dense kernel); a call with enable == 0 waits for them and returns their summed duration
+ * in microseconds and their count, then stops. Any call returns (and forgets) what was recorded. */
+int mt_rollout_trunk_timing(mt_rollout *ro, int enable, double *sum_us, int64_t *count);
+
+/* ---- data-parallel communicator (RCCL over xGMI; manette_amd/csrc/comm.hip) ----------------
+ * The reference has no collective: its only shard unit is the contiguous env split of
+ * runners.py:17-18 (np.split over workers). This build splits envs over ranks the same way (rank r
+ * owns global envs [r*ec, (r+1)*ec)) and exchanges exactly one thing per update: the flat fp32
+ * gradient, summed in place (mt_allreduce) between mt_returns_loss_backward and mt_clip_rmsprop
+ * (inv_scale = 1/world), i.e. the union batch's mean gradient of actor_learner.py:49 before the
+ * global-norm clip of :59-63. mt_broadcast copies rank 0's parameters / RMSProp slots at start
+ * (and on resume). Both are stream-ordered and capturable into a hipGraph.
+ * Bootstrap: rank 0 calls mt_comm_unique_id, ships the MT_COMM_UID_BYTES bytes to every rank over
+ * any control channel (the learner uses torch.distributed's gloo store), then every rank calls
+ * mt_comm_init(uid, rank, world, device) collectively. */
+#define MT_COMM_UID_BYTES 128
+typedef struct mt_comm mt_comm;
+int mt_comm_unique_id(char *uid /* [MT_COMM_UID_BYTES] */);
+int mt_comm_init(const char *uid, int rank, int world, int device, mt_comm **out);
+void mt_comm_destroy(mt_comm *comm);
+int mt_comm_info(const mt_comm *comm, int *rank, int *world);
+/* In-place sum over ranks of n fp32 values (ncclAllReduce, ncclSum). */
+int mt_allreduce(mt_comm *comm, float *buf, size_t n, mt_stream_t stream);
+/* In-place broadcast of `bytes` bytes from rank `root`. */
+int mt_broadcast(mt_comm *comm, void *buf, size_t bytes, int root, mt_stream_t stream);
 
 /* ---- small helpers ----------------------------------------------------------------------- */
 /* out[i] = sum_z parts[z*n + i] (deterministic order); used for split reductions. */

@@ -111,6 +111,13 @@ int mh_book_create(int n_envs, int num_actions, const int32_t *tab_rep, int n_re
 void mh_book_destroy(mh_book *b);
 int mh_book_step(mh_book *b, int64_t *global_step, const int32_t *a_idx, const int32_t *r_idx,
                  const float *reward, const float *over, float *rewards_out, float *masks_out);
+/* Data-parallel shard (runners.py:17-18 split over ranks): this book's envs are global envs
+ * [env_offset, env_offset + n_envs) of a learner stepping envs_total envs per macro-step. Then
+ * global_step advances by envs_total per macro-step (paac.py:184 counts every env the learner
+ * trains on, identical on every rank) and env e's episode record carries
+ * global_step_before + env_offset + e + 1, as a single process owning all envs would log it.
+ * Default: env_offset 0, envs_total n_envs. */
+int mh_book_set_shard(mh_book *b, int64_t env_offset, int64_t envs_total);
 /* Start a new update: clears the action/repetition histogram and nb_actions (paac.py:135-136). */
 int mh_book_new_update(mh_book *b);
 /* hist [A][R] int64 of the current update, nb_actions (may be NULL). */

@@ -14,6 +14,7 @@ MT_ARCH = {'NIPS': 0, 'NATURE': 1, 'PWYX': 2, 'LSTM': 3}
 MT_ACT = {'relu': 0, 'leaky_relu': 1}
 MT_CLIP = {'ignore': 0, 'global': 1}
 MT_NORM_PARTIALS = 512
+MT_COMM_UID_BYTES = 128
 
 
 class MTError(RuntimeError):
@@ -27,7 +28,8 @@ class mt_rollout_buffers(C.Structure):
                [(n, C.c_void_p) for n in ('pair', 'pair_host', 'meta', 'row_lut', 'col_lut', 'idx_host',
                                           'staging_host', 'meta_host', 'reward_host', 'over_host',
                                           'rm_host', 'frames_host', 'sync_host', 'train_ws')] + \
-               [('train_ws_bytes', C.c_size_t), ('v_boot', C.c_void_p), ('ready_host', C.c_void_p), ('flags', C.c_int32)]
+               [('train_ws_bytes', C.c_size_t), ('v_boot', C.c_void_p), ('ready_host', C.c_void_p), ('flags', C.c_int32),
+                                                                       ('env_offset', C.c_int32)]
 
 
 MT_ROLLOUT_ZERO_COPY = 1
@@ -70,7 +72,7 @@ _HIP_SIGS = {
     'mt_forward_rows': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _SZ, _I, _I, _P, _P, _P, _P]),
     'mt_forward_trunk': (_I, [_P, _P, _P, _I, _P, _SZ, _P]),
     'mt_forward_infer': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P]),
-    'mt_sample': (_I, [_P, _P, _I, _I, _I, C.c_uint64, _P, _P, _P, _P, _P]),
+    'mt_sample': (_I, [_P, _P, _I, _I, _I, C.c_uint64, _I, _P, _P, _P, _P, _P]),
     'mt_returns': (_I, [_P, _P, _P, _P, C.c_double, _I, _I, _P, _P, _P]),
     'mt_loss_backward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
     'mt_returns_loss_backward': (_I, [_P, _P, _P, _I, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _P, C.c_double, _P, _P,
@@ -90,6 +92,13 @@ _HIP_SIGS = {
     'mt_rollout_step': (_I, [_P, _P, _I, C.POINTER(C.c_int64), _P]),
     'mt_rollout_run': (_I, [_P, _P, C.POINTER(C.c_int64), _P]),
     'mt_rollout_stats': (_I, [_P, C.POINTER(C.c_double), _I]),
+    'mt_rollout_trunk_timing': (_I, [_P, _I, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    'mt_comm_unique_id': (_I, [C.c_char_p]),
+    'mt_comm_init': (_I, [C.c_char_p, _I, _I, _I, C.POINTER(_P)]),
+    'mt_comm_destroy': (None, [_P]),
+    'mt_comm_info': (_I, [_P, C.POINTER(_I), C.POINTER(_I)]),
+    'mt_allreduce': (_I, [_P, _P, _SZ, _P]),
+    'mt_broadcast': (_I, [_P, _P, _SZ, _I, _P]),
     'mt_graph_begin': (_I, [_P]),
     'mt_graph_end': (_I, [_P, C.POINTER(_P)]),
     'mt_graph_launch': (_I, [_P, _P]),
@@ -114,6 +123,7 @@ _HOST_SIGS = {
     'mh_book_destroy': (None, [_P]),
     'mh_book_step': (_I, [_P, C.POINTER(C.c_int64), _P, _P, _P, _P, _P, _P]),
     'mh_book_new_update': (_I, [_P]),
+    'mh_book_set_shard': (_I, [_P, C.c_int64, C.c_int64]),
     'mh_book_histogram': (_I, [_P, _P, C.POINTER(C.c_int64)]),
     'mh_book_pop_episodes': (_I, [_P, _P, _P, _P, _I, C.POINTER(_I)]),
 }

@@ -8,6 +8,9 @@ Exact integer semantics of the reference loop:
   total_action_rep[a_e][r_e] += 1; nb_actions += r_e + 1     (:157, :187-189)
   on over: log (global_step at env e, total reward, emulator_steps), reset both   (:191-201)
 Total episode rewards accumulate in float32 (the shared reward array is float32).
+Data parallel (set_shard): a rank's envs are global envs [env_offset, env_offset + E) of a learner
+stepping envs_total envs per macro-step; global_step then advances by envs_total (the same on
+every rank) and episode records carry the global env's position, as one process would log them.
 """
 import numpy as np
 
@@ -23,7 +26,12 @@ class Bookkeeper(object):
         self.total_rewards = []
         self.total_steps = []
         self.episodes = []   # (global_step, reward, length)
+        self.env_offset, self.envs_total = 0, n_envs
         self.new_update()
+
+    def set_shard(self, env_offset, envs_total):
+        assert 0 <= env_offset and env_offset + self.E <= envs_total
+        self.env_offset, self.envs_total = int(env_offset), int(envs_total)
 
     def new_update(self):
         self.total_action_rep = np.zeros((self.A, self.R), dtype=np.int64)
@@ -45,11 +53,11 @@ class Bookkeeper(object):
         for e in ended:
             self.total_rewards.append(float(self.total_episode_rewards[e]))
             self.total_steps.append(int(self.emulator_steps[e]))
-            self.episodes.append((global_step + int(e) + 1, float(self.total_episode_rewards[e]),
+            self.episodes.append((global_step + self.env_offset + int(e) + 1, float(self.total_episode_rewards[e]),
                                   int(self.emulator_steps[e])))
         self.total_episode_rewards[ended] = 0
         self.emulator_steps[ended] = 0
-        return global_step + self.E
+        return global_step + self.envs_total
 
     def histograms(self):
         """paac.py:269-275: the values log_histogram would receive."""
@@ -80,6 +88,10 @@ class NativeBook(object):
         self.total_rewards = []
         self.total_steps = []
         self.episodes = []
+
+    def set_shard(self, env_offset, envs_total):
+        self._lib.check_host(self._lib.host().mh_book_set_shard(self._h, int(env_offset), int(envs_total)),
+                             'mh_book_set_shard')
 
     @property
     def handle(self):

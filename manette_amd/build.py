@@ -10,7 +10,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
-HIP_SOURCES = ['net.hip', 'misc.hip', 'rollout.hip']
+HIP_SOURCES = ['net.hip', 'misc.hip', 'rollout.hip', 'comm.hip']
 HIP_HEADERS = ['common.h', 'gemm.h', 'trunk_fused.h', 'lstm.h']
 HOST_SOURCES = ['runner.cpp', 'crc32c.cpp']
 HIP_LIB = os.path.join(HERE, 'libmanette_hip.so')
@@ -44,7 +44,8 @@ def build_hip(force=False, verbose=False, out=None, defines=()):
     tmp = target + '.tmp'
     cmd = [_hipcc(), '--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
            '-Wno-unused-result'] + ['-D' + d for d in defines] + ['-o', tmp] + srcs + [
-               '-L' + HERE, '-lmanette_host', '-Wl,-rpath,$ORIGIN']
+               '-L' + HERE, '-lmanette_host', '-Wl,-rpath,$ORIGIN', '-L/opt/rocm/lib', '-lrccl',
+               '-Wl,-rpath,/opt/rocm/lib']
     if verbose:
         print(' '.join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)

@@ -1,0 +1,93 @@
+"""Data-parallel communicators of the learner.
+
+The reference has no collective: its only shard unit is the contiguous env split of
+runners.py:17-18. This build shards envs over ranks the same way and exchanges one thing per
+update, the flat fp32 gradient (sum all-reduce), plus rank 0's parameters / RMSProp slots at start.
+
+RcclComm   the product path: an RCCL communicator behind the C ABI (mt_comm_*, manette_amd/csrc/
+           comm.hip), called on the learner's stream, capturable into the update's hipGraph.
+           torch.distributed (gloo) is only the control channel that ships rank 0's unique id.
+TorchComm  torch.distributed collectives on the existing process group: for topologies RCCL does
+           not support, i.e. several ranks sharing one GPU (the world-2 tests on a 1-GPU box).
+"""
+import ctypes as C
+
+import torch
+
+from . import _lib
+from ._lib import check
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class RcclComm(object):
+    capturable = True
+    kind = 'rccl'
+
+    def __init__(self, rank, world, device_index):
+        import torch.distributed as dist
+        lib = _lib.hip()
+        uid = C.create_string_buffer(_lib.MT_COMM_UID_BYTES)
+        if rank == 0:
+            check(lib.mt_comm_unique_id(uid), 'mt_comm_unique_id')
+        if world > 1:
+            box = [uid.raw if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            C.memmove(uid, box[0], _lib.MT_COMM_UID_BYTES)
+        h = C.c_void_p()
+        check(lib.mt_comm_init(uid, int(rank), int(world), int(device_index), C.byref(h)), 'mt_comm_init')
+        self._h = h
+        self.rank, self.world = rank, world
+
+    def allreduce(self, t):
+        """In-place sum of a contiguous fp32 device tensor over the ranks (mt_allreduce)."""
+        assert t.dtype == torch.float32 and t.is_cuda and t.is_contiguous()
+        check(_lib.hip().mt_allreduce(self._h, C.c_void_p(t.data_ptr()), t.numel(), _stream()), 'mt_allreduce')
+
+    def broadcast(self, t, root=0):
+        assert t.is_cuda and t.is_contiguous()
+        check(_lib.hip().mt_broadcast(self._h, C.c_void_p(t.data_ptr()), t.numel() * t.element_size(), int(root),
+                                      _stream()), 'mt_broadcast')
+
+    def close(self):
+        if getattr(self, '_h', None):
+            _lib.hip().mt_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class TorchComm(object):
+    capturable = False
+    kind = 'torch'
+
+    def __init__(self, rank, world, device_index=None):
+        self.rank, self.world = rank, world
+
+    def allreduce(self, t):
+        torch.distributed.all_reduce(t)
+
+    def broadcast(self, t, root=0):
+        torch.distributed.broadcast(t, root)
+
+    def close(self):
+        pass
+
+
+def make(kind, rank, world, device_index):
+    if kind == 'rccl':
+        return RcclComm(rank, world, device_index)
+    if kind == 'torch':
+        return TorchComm(rank, world, device_index)
+    raise ValueError('comm must be rccl or torch, not %r' % kind)
+
+
+def broadcast_scalars(values, rank, src=0):
+    """Host integers from rank `src` (control channel: torch.distributed, e.g. gloo)."""
+    import torch.distributed as dist
+    box = [list(values) if rank == src else None]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]

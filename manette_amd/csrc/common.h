@@ -37,6 +37,13 @@ void set_error(const char *fmt, ...);
 
 __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// Load of a value the HOST writes between launches (pinned, device-mapped memory: the rollout's
+// rewards / masks, the LR): a system-scope load bypasses the GPU's non-coherent cache lines, so
+// a line cached by an earlier launch can never be returned stale. Works on device memory too.
+__device__ __forceinline__ float host_ld(const float *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Wave-wide (64 lanes) sum via butterfly shuffles.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -54,9 +61,11 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// A3 perf mode sampler: counter-based uniforms (splitmix64 of seed, row, per-row counter),
+// A3 perf mode sampler: counter-based uniforms (splitmix64 of seed, GLOBAL row, per-row counter),
 // inverse CDF over (p - epsneg(float32)) accumulated in double — the standalone sample kernel
-// and the fused rollout heads kernel share it so both draw identical indices.
+// and the fused rollout heads kernel share it so both draw identical indices. The row is the
+// global env id (local row + row0 = the rank's env offset), so a data-parallel rank draws exactly
+// what a single process owning all envs would draw for the same env.
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
@@ -81,11 +90,11 @@ __device__ __forceinline__ int draw_index(const float *p, int n, double u) {
 }
 
 __device__ __forceinline__ void sample_row(const float *pa, int A, const float *pr, int R, uint64_t seed,
-                                           int b, uint64_t *counters, int *a, int *r) {
+                                           int b, int row0, uint64_t *counters, int *a, int *r) {
   const uint64_t c = counters[b];
   counters[b] = c + 1;
   double ua, ur;
-  row_uniforms(seed, b, c, &ua, &ur);
+  row_uniforms(seed, b + row0, c, &ua, &ur);
   *a = draw_index(pa, A, ua);
   *r = draw_index(pr, R, ur);
 }
@@ -104,6 +113,7 @@ struct SampleArgs {
   // lo = (seq16 << 16) | a, hi = (seq16 << 16) | r (seq16 = seq & 0xffff): both halves carry the
   // tag, so a host that sees the tag in both has the pair, with no fence on the device side
   uint64_t *packed = nullptr;
+  int32_t row0 = 0;  // global env id of row 0 (the rank's env offset): the uniforms hash row0 + b
 };
 
 }  // namespace mt
@@ -130,7 +140,10 @@ struct StackSrc {
 // forward (mt_forward) with the A3 draw fused into the heads kernel; smp, tr and st may be null.
 // st (NIPS inference only): the conv kernel first stacks the new state st->out (== obs) from
 // st->prev and the pushed frames (mt_preprocess_resized's op, fused into the forward).
+// marks (optional, two events): recorded around the trunk launches (convs + dense layer; not the
+// heads), so a caller can time the trunk kernels where they really run (mt_rollout_trunk_timing).
 int forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                    size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp, bool infer,
-                   hipStream_t stream, const TrainRows *tr = nullptr, const StackSrc *st = nullptr);
+                   hipStream_t stream, const TrainRows *tr = nullptr, const StackSrc *st = nullptr,
+                   const hipEvent_t *marks = nullptr);
 }  // namespace mt

@@ -37,13 +37,13 @@ __global__ void returns_kernel(const float *__restrict__ r, const float *__restr
   if (e >= E) return;
   // t = T-1: float32 product gamma*R_T, then float64 with the mask and reward.
   const float g32 = __fmul_rn((float)gamma, VT[e]);
-  double R = (double)r[(size_t)(T - 1) * E + e] + (double)g32 * (double)mask[(size_t)(T - 1) * E + e];
+  double R = (double)host_ld(r + (size_t)(T - 1) * E + e) + (double)g32 * (double)host_ld(mask + (size_t)(T - 1) * E + e);
   y[(size_t)(T - 1) * E + e] = (float)R;
   adv[(size_t)(T - 1) * E + e] = (float)(R - (double)V[(size_t)(T - 1) * E + e]);
   const double gd = gamma;  // python float (float64)
   for (int t = T - 2; t >= 0; --t) {
     const size_t i = (size_t)t * E + e;
-    R = (double)r[i] + (gd * R) * (double)mask[i];
+    R = (double)host_ld(r + i) + (gd * R) * (double)host_ld(mask + i);
     y[i] = (float)R;
     adv[i] = (float)(R - (double)V[i]);
   }
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
   }
   __syncthreads();
   const float scale = sh_scale;
-  const float lr = *lr_dev;
+  const float lr = host_ld(lr_dev);
   const float one_m_rho = 1.0f - decay;
 #pragma unroll
   for (int k = 0; k < V; ++k) {
@@ -257,13 +257,13 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
 // A3 perf mode: counter-based uniforms, inverse CDF over (p - epsneg(float32)).
 // ---------------------------------------------------------------------------------------------
 __global__ void sample_kernel(const float *__restrict__ pi, const float *__restrict__ rep, int B,
-                              int A, int R, uint64_t seed, uint64_t *__restrict__ counters,
+                              int A, int R, uint64_t seed, int row0, uint64_t *__restrict__ counters,
                               int32_t *__restrict__ a_idx, int32_t *__restrict__ r_idx,
                               int32_t *__restrict__ pair) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   int a, r;
-  sample_row(pi + (size_t)b * A, A, rep + (size_t)b * R, R, seed, b, counters, &a, &r);
+  sample_row(pi + (size_t)b * A, A, rep + (size_t)b * R, R, seed, b, row0, counters, &a, &r);
   a_idx[b] = a;
   r_idx[b] = r;
   if (pair) {
@@ -424,12 +424,12 @@ extern "C" int mt_host_device_pointer(void *host, void **dev) {
 }
 
 extern "C" int mt_sample(const float *pi, const float *rep, int batch, int num_actions,
-                         int num_reps, uint64_t seed, uint64_t *counters, int32_t *a_idx,
+                         int num_reps, uint64_t seed, int row0, uint64_t *counters, int32_t *a_idx,
                          int32_t *r_idx, int32_t *pair, mt_stream_t stream) {
   MT_CHECK_ARG(pi && rep && counters && a_idx && r_idx, "null argument");
-  MT_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_reps >= 1, "bad sizes");
+  MT_CHECK_ARG(batch >= 1 && num_actions >= 1 && num_reps >= 1 && row0 >= 0, "bad sizes");
   hipLaunchKernelGGL(sample_kernel, dim3(cdiv(batch, 64)), dim3(64), 0, (hipStream_t)stream, pi,
-                     rep, batch, num_actions, num_reps, seed, counters, a_idx, r_idx, pair);
+                     rep, batch, num_actions, num_reps, seed, row0, counters, a_idx, r_idx, pair);
   MT_LAUNCHED();
   return MT_OK;
 }

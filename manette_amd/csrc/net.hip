@@ -541,7 +541,7 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   if (smp.counters) {
     const uint64_t c = cnt;
     double ua, ur;
-    row_uniforms(smp.seed, b, c, &ua, &ur);
+    row_uniforms(smp.seed, b + smp.row0, c, &ua, &ur);
     const int a = wave_draw(pa, hp.A, ua), r = wave_draw(pr, hp.R, ur);
     if (lane == 0) {
       smp.counters[b] = c + 1;
@@ -622,8 +622,8 @@ __device__ __forceinline__ void row_return(const ReturnsSrc &rs, const float *__
   const int T = rs.T, E = rs.E;
   const int t = b / E, e = b - t * E, n = T - t;  // steps t .. T-1
   for (int k = threadIdx.x; k < n; k += 256) {
-    buf[2 * k] = rs.r[(size_t)(t + k) * E + e];
-    buf[2 * k + 1] = rs.mask[(size_t)(t + k) * E + e];
+    buf[2 * k] = host_ld(rs.r + (size_t)(t + k) * E + e);
+    buf[2 * k + 1] = host_ld(rs.mask + (size_t)(t + k) * E + e);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -985,15 +985,17 @@ static ActRows act_rows(const mt_net *n, float *ws, const WsLayout &L, const Tra
 template <class Ar>
 static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
                         float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s,
-                        const TrainRows *tr = nullptr) {
+                        const TrainRows *tr = nullptr, const hipEvent_t *marks = nullptr) {
   const WsLayout L = ws_layout<Ar>(n, B);
   const ActRows A = act_rows<Ar>(n, ws, L, tr);
+  if (marks) MT_HIP(hipEventRecord(marks[0], s));
   MT_TRY((trunk_forward<Ar>(n, P, obs, B, A.base, A.L, s)));
   const float *flat = layer_out<Ar, Ar::NCONV - 1>(A.base, A.L);
   // dense layer (networks.py:57-70), split-K partial slabs; heads kernel finishes bias + act.
   const float *Wfc = P + n->off_fc;
   MT_TRY((launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1},
                               EpSlab{ws + L.fcslab, B, Ar::F}, B, Ar::F, Ar::FLAT, L.fc_splits, s)));
+  if (marks) MT_HIP(hipEventRecord(marks[1], s));
   HeadParams hp = head_params(n, P);
   hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, L.fc_splits, B,
                      Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp,
@@ -1008,17 +1010,20 @@ static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int
 template <class Ar>
 static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
                               float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s,
-                              const TrainRows *tr = nullptr, const StackSrc *st = nullptr) {
+                              const TrainRows *tr = nullptr, const StackSrc *st = nullptr,
+                              const hipEvent_t *marks = nullptr) {
   if constexpr (Ar::FUSED_SLABS > 0) {
     constexpr int C = LayerG<Ar, 0>::CIN;
     using Fz = FusedNips<C>;
     const WsLayout L = ws_layout<Ar>(n, B);
     const ActRows A = act_rows<Ar>(n, ws, L, tr);
     const float *Wfc = P + n->off_fc;
+    if (marks) MT_HIP(hipEventRecord(marks[0], s));
     MT_TRY((launch_nips_trunk<C>(obs, st, B, P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation,
                                  n->cfg.alpha_leaky, A.base + A.L.act[1], tr ? A.base + A.L.act[0] : nullptr,
                                  ws + L.fcslab, s)));
     MT_LAUNCHED();
+    if (marks) MT_HIP(hipEventRecord(marks[1], s));
     HeadParams hp = head_params(n, P);
     hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, Fz::ROWS2, B,
                        Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp,
@@ -1030,7 +1035,7 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
       set_error("stacking forward is built for the NIPS arch only");
       return MT_ERR_ARG;
     }
-    return forward_impl<Ar>(n, P, obs, B, ws, v, pi, rep, smp, s, tr);
+    return forward_impl<Ar>(n, P, obs, B, ws, v, pi, rep, smp, s, tr, marks);
   }
 }
 
@@ -1288,7 +1293,8 @@ extern "C" int mt_forward_infer(const mt_net *net, const float *params, const ui
 
 int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch,
                        void *ws, size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp,
-                       bool infer, hipStream_t stream, const TrainRows *tr, const StackSrc *st) {
+                       bool infer, hipStream_t stream, const TrainRows *tr, const StackSrc *st,
+                       const hipEvent_t *marks) {
   MT_CHECK_ARG(net && params && obs && ws && v && pi && rep, "null argument");
   MT_CHECK_ARG(!smp || (smp->counters && smp->a_idx && smp->r_idx), "null sample buffer");
   MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
@@ -1312,8 +1318,9 @@ int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *ob
       return lstm_forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream);
     else
       MT_CHECK_ARG(!st || infer, "stacking forward is an inference forward");
-      return infer ? forward_infer_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream, tr, st)
-                   : forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream, tr);
+      return infer ? forward_infer_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream, tr, st,
+                                            marks)
+                   : forward_impl<Ar>(net, params, obs, batch, (float *)ws, v, pi, rep, smp, stream, tr, marks);
   });
   return MT_OK;
 }

@@ -41,6 +41,10 @@ struct mt_rollout {
   uint8_t *frames_hbm = nullptr;   // [4E][84*84*depth] HBM copy of the pushes (pull kernel)
   int32_t *count_hbm = nullptr;    // [E] push counts
   double acc[5];  // host wall us: launch+wait for indices, runner, book, upload+preprocess enqueue; steps
+  // mt_rollout_trunk_timing: event pairs recorded around each step forward's trunk launches
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> marks;
+  size_t marks_used = 0;
 };
 
 using namespace mt;
@@ -60,6 +64,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
                             MT_ROLLOUT_RESIZED)) == 0,
                "unknown rollout flags %d", b.flags);
   MT_CHECK_ARG(!ip || b.frames_host, "in-place rollout needs frames_host");
+  MT_CHECK_ARG(b.env_offset >= 0, "env_offset must be >= 0");
   MT_CHECK_ARG((int)ip + (int)po + (int)rz <= 1, "in-place, pooled and resized staging are exclusive");
   MT_CHECK_ARG(!pl || (zc && b.sync_host), "pipelined rollout needs zero-copy or in-place screens and sync_host");
   MT_CHECK_ARG(b.states && b.values && b.idx && b.pi && b.rep && b.ws && b.counters &&
@@ -161,6 +166,10 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
 extern "C" void mt_rollout_destroy(mt_rollout *ro) {
   if (!ro) return;
   for (int i = 0; i < 4; ++i) (void)hipEventDestroy(ro->ev2[i]);
+  for (auto &m : ro->marks) {
+    (void)hipEventDestroy(m.first);
+    (void)hipEventDestroy(m.second);
+  }
   if (ro->pull) {
     (void)mh_runner_set_ready(ro->runner, nullptr, 0);
     (void)hipHostFree(ro->env_ready_host);
@@ -191,15 +200,28 @@ __global__ void wait_seq_kernel(const uint32_t *seq_word, uint32_t seq, uint32_t
       return;
     }
   }
+  // the preprocess that follows in the stream reads the staging in place: a new dispatch, whose
+  // system-scope acquire drops any line cached before the host wrote it
 }
 
 // Pull kernel (pull mode: pipelined + resized): copies each env's pushes from the pinned staging into HBM as soon as
-// its emulator thread has published it (ready[e] = (step << 3) | push count,
-// mh_runner_set_ready), so the PCIe transfer of a step's frames overlaps the emulation of the
-// other envs and the stacking conv kernel reads HBM only. Block = kPullEnvs consecutive envs
-// (one runner worker's share at E = 32, ew = 8; a worker steps its envs in index order, so lane 0
-// polls only the next one: one PCIe read in flight per block, s_sleep between polls). Bounded
-// like wait_seq_kernel: after ~2 s it records the failure in status and returns.
+// its emulator thread has published it (ready[e] = (step << 3) | push count, mh_runner_set_ready),
+// so the PCIe transfer of a step's frames overlaps the emulation of the other envs and the
+// stacking conv kernel reads HBM only. Block = kPullEnvs consecutive envs (one runner worker's
+// share at E = 32, ew = 8; a worker steps its envs in index order, so lane 0 polls only the next
+// one: one PCIe read in flight per block, s_sleep between polls). Bounded like wait_seq_kernel:
+// after ~2 s it records the failure in status and returns.
+// Memory ordering. The host writes env e's frames, then `sfence` + a release store of ready[e]
+// (runner.cpp). Lane 0 sees the word with a system-scope load (it bypasses the non-coherent
+// caches); the block barrier orders every data load after it (a GPU issues no load ahead of a
+// barrier). The staging is non-coherent pinned memory, so a data load may hit a cache line
+// fetched EARLIER — within one launch that can only be a line another env's copy fetched: env
+// slot groups are 4 x 7,056 B, so an env's first and last 128-B lines may hold bytes of its
+// neighbours, which can be published later than the line was fetched. Those edge chunks are read
+// with system-scope loads (never served from, nor trusted in, those caches); every other line of
+// env e's range holds env e's bytes only and is first touched after ready[e]. (Lines fetched in an
+// earlier launch do not survive: each dispatch starts with a system-scope acquire.) No cache
+// invalidation is issued: a device-wide invalidate would also drop the trunk weights from L2.
 constexpr int kPullEnvs = 4;
 #ifdef MT_PROBE  // experiment builds: per env, when its word was seen and its copy done (tools/probe.py)
 static __device__ unsigned long long mt_probe_ro[512 * 4];
@@ -212,6 +234,17 @@ extern "C" int mt_probe_read_rollout(unsigned long long *out, size_t n) {
 #else
 #define MT_PROBE_RO(e, p)
 #endif
+// a 16-B chunk whose 128-B line also holds bytes outside [lo, hi) (byte offsets): read it with
+// two system-scope 8-byte loads
+__device__ __forceinline__ uint4 pull_chunk(const uint4 *staging, size_t q, size_t lo, size_t hi) {
+  const size_t a = q * 16, line = a & ~(size_t)127;
+  if (line >= lo && line + 128 <= hi) return staging[q];
+  const uint64_t *p = reinterpret_cast<const uint64_t *>(staging + q);
+  const uint64_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+}
+
 __global__ __launch_bounds__(256) void pull_frames_kernel(const uint4 *__restrict__ staging, const uint32_t *ready,
                                                           uint32_t want, uint32_t *status, int E, int frame16,
                                                           uint4 *__restrict__ frames, int32_t *__restrict__ count) {
@@ -240,7 +273,8 @@ __global__ __launch_bounds__(256) void pull_frames_kernel(const uint4 *__restric
     if (p0 < 0) return;  // timed out (uniform over the block)
     const int p = min(max(p0, 1), 4);
     const size_t base = (size_t)4 * e * frame16;  // slots 4e .. 4e + p - 1 are contiguous
-    for (int q = threadIdx.x; q < p * frame16; q += 256) frames[base + q] = staging[base + q];
+    const size_t lo = base * 16, hi = (base + (size_t)4 * frame16) * 16;  // env e's slot group (bytes)
+    for (int q = threadIdx.x; q < p * frame16; q += 256) frames[base + q] = pull_chunk(staging, base + q, lo, hi);
     if (threadIdx.x == 0) count[e] = p;
     __syncthreads();  // s_p is rewritten by the next round
     if (threadIdx.x == 0) MT_PROBE_RO(e, 1);
@@ -248,6 +282,24 @@ __global__ __launch_bounds__(256) void pull_frames_kernel(const uint4 *__restric
 }
 
 namespace {
+// the next event pair of the trunk timing (mt_rollout_trunk_timing), or null when it is off
+int next_marks(mt_rollout *ro, const hipEvent_t **out) {
+  *out = nullptr;
+  if (!ro->timing) return MT_OK;
+  if (ro->marks_used == ro->marks.size()) {
+    hipEvent_t a, b;
+    MT_HIP(hipEventCreate(&a));
+    if (hipEventCreate(&b) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      set_error("hipEventCreate failed");
+      return MT_ERR_HIP;
+    }
+    ro->marks.emplace_back(a, b);
+  }
+  *out = &ro->marks[ro->marks_used++].first;
+  return MT_OK;
+}
+
 // forward of state slot t with the A3 draw fused into its heads kernel (paac.py:144-147); the
 // indices land in idx[.][t] and the [2][E] pair; ev[t & 1] marks the pair ready.
 // stacked: state slot t is built from slot t-1 + step t-1's pushes inside the forward's conv
@@ -267,12 +319,15 @@ int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, b
   smp.seq = ++ro->fwd_seq;
   ro->fwd_of[t] = smp.seq;
   smp.packed = ro->packed_dev;
+  smp.row0 = b.env_offset;
   // with a train workspace: activations into its rows t*E.., per-step pi / rep (mt_forward_rows)
   const TrainRows tr{(float *)b.train_ws, b.train_ws_bytes, T * E, t * E};
   const size_t po = b.train_ws ? (size_t)t * E : 0;
+  const hipEvent_t *marks;
+  MT_TRY_(next_marks(ro, &marks));
   MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)t * slot, E, b.ws, b.ws_bytes,
                          b.values + (size_t)t * E, b.pi + po * ro->A, b.rep + po * ro->R, &smp, true, s,
-                         b.train_ws ? &tr : nullptr, stacked ? &st : nullptr));
+                         b.train_ws ? &tr : nullptr, stacked ? &st : nullptr, marks));
   if (!ro->zero_copy)
     MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
   MT_HIP(hipEventRecord(ro->ev2[t & 3], s));
@@ -475,5 +530,26 @@ extern "C" int mt_rollout_stats(mt_rollout *ro, double *out5, int reset) {
   for (int i = 0; i < 5; ++i) out5[i] = ro->acc[i];
   if (reset)
     for (int i = 0; i < 5; ++i) ro->acc[i] = 0;
+  return MT_OK;
+}
+
+// Trunk timing of the macro-steps' forwards, in place (the kernels the rollout runs, as it runs
+// them): enable != 0 starts recording an event pair around every step forward's trunk launches;
+// enable == 0 stops, waits for the recorded events and returns their summed duration (us) and
+// count, then forgets them. Each pair spans the trunk kernels of one forward (NIPS: the stacking
+// conv kernel + the dense kernel) and the boundary between them.
+extern "C" int mt_rollout_trunk_timing(mt_rollout *ro, int enable, double *sum_us, int64_t *count) {
+  MT_CHECK_ARG(ro, "null argument");
+  double total = 0.0;
+  for (size_t i = 0; i < ro->marks_used; ++i) {
+    MT_HIP(hipEventSynchronize(ro->marks[i].second));
+    float ms = 0.f;
+    MT_HIP(hipEventElapsedTime(&ms, ro->marks[i].first, ro->marks[i].second));
+    total += 1e3 * (double)ms;
+  }
+  if (sum_us) *sum_us = total;
+  if (count) *count = (int64_t)ro->marks_used;
+  ro->marks_used = 0;
+  ro->timing = enable != 0;
   return MT_OK;
 }

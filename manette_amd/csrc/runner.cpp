@@ -616,6 +616,7 @@ struct mh_book {
   std::vector<float> total_reward;
   std::vector<int64_t> hist;  // [A][R]
   int64_t nb_actions = 0;
+  int64_t env_offset = 0, envs_total = 0;  // data-parallel shard (mh_book_set_shard)
   struct Episode {
     int64_t step;
     float reward;
@@ -639,6 +640,7 @@ extern "C" int mh_book_create(int n_envs, int num_actions, const int32_t *tab_re
   b->emulator_steps.assign(n_envs, 0);
   b->total_reward.assign(n_envs, 0.f);
   b->hist.assign((size_t)num_actions * n_reps, 0);
+  b->envs_total = n_envs;
   *out = b;
   return 0;
 }
@@ -670,12 +672,22 @@ extern "C" int mh_book_step(mh_book *b, int64_t *global_step, const int32_t *a_i
     b->hist[(size_t)a * b->R + r] += 1;
     b->nb_actions += r + 1;
     if (over[e] != 0.f) {
-      b->episodes.push_back({gs0 + e + 1, b->total_reward[e], b->emulator_steps[e]});
+      b->episodes.push_back({gs0 + b->env_offset + e + 1, b->total_reward[e], b->emulator_steps[e]});
       b->total_reward[e] = 0.f;
       b->emulator_steps[e] = 0;
     }
   }
-  *global_step = gs0 + b->E;
+  *global_step = gs0 + b->envs_total;
+  return 0;
+}
+
+extern "C" int mh_book_set_shard(mh_book *b, int64_t env_offset, int64_t envs_total) {
+  if (!b || env_offset < 0 || envs_total < env_offset + b->E) {
+    set_error("bad shard (offset %lld, total %lld)", (long long)env_offset, (long long)envs_total);
+    return 1;
+  }
+  b->env_offset = env_offset;
+  b->envs_total = envs_total;
   return 0;
 }
 

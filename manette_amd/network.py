@@ -255,11 +255,12 @@ class DeviceNetwork(object):
                                   _ptr(self.norm_dev), s), 'mt_clip_rmsprop')
 
 
-def sample(pi, rep, seed, counters, a_idx, r_idx, pair=None):
-    """Device multinomial draw (perf mode of exploration_policy.py:108-116)."""
+def sample(pi, rep, seed, counters, a_idx, r_idx, pair=None, row0=0):
+    """Device multinomial draw (perf mode of exploration_policy.py:108-116); row0 = the global env
+    id of row 0 (the uniforms hash the global env id, so a DP shard draws as the union would)."""
     B, A = pi.shape
     R = rep.shape[1]
-    check(_lib.hip().mt_sample(_ptr(pi), _ptr(rep), B, A, R, C.c_uint64(seed), _ptr(counters),
+    check(_lib.hip().mt_sample(_ptr(pi), _ptr(rep), B, A, R, C.c_uint64(seed), int(row0), _ptr(counters),
                                _ptr(a_idx), _ptr(r_idx), _ptr(pair), _stream()), 'mt_sample')
 
 

@@ -13,10 +13,15 @@ Paths (args.runner):
             84x84xC observations go H2D.
 Sampling (args.sampling): 'host' = the reference's numpy multinomial stream (parity mode),
 'device' = mt_sample (perf mode, same distribution).
-Data parallel: one process per GPU (torch.distributed, RCCL); env ids are offset by rank
-(rank r owns global envs [r*ec, (r+1)*ec)), each rank rolls out its own shard and the flat
-gradient is summed by ONE all_reduce per update; 1/world is folded into mt_clip_rmsprop, so
-clip + RMSProp see the global-batch mean gradient and the replicas stay identical.
+Data parallel: one process per GPU; env ids are offset by rank (rank r owns global envs
+[r*ec, (r+1)*ec), the runners.py:17-18 split over ranks), each rank rolls out its own shard and
+the flat gradient is summed by ONE all-reduce per update (RCCL behind the C ABI, mt_allreduce,
+inside the update's hipGraph; manette_amd/comm.py); 1/world is folded into mt_clip_rmsprop, so
+clip + RMSProp see the global-batch mean gradient and the replicas stay identical. The device
+draw hashes the global env id and global_step counts every env of the job (mh_book_set_shard),
+so a W-rank run takes the same trajectory and LR schedule as one process owning all W*ec envs.
+torch.distributed (gloo) is the control channel only: the RCCL unique id and, at start / resume,
+rank 0's global_step.
 """
 import logging
 import time
@@ -58,6 +63,13 @@ class PAACLearner(ActorLearner):
         self.world = torch.distributed.get_world_size() if self.dist else 1
         self.rank = torch.distributed.get_rank() if self.dist else 0
         self.is_chief = self.rank == 0
+        # global env id of env 0 (train.py: rank * ec); the device draw hashes global env ids
+        self.env_offset = int(getattr(args, 'env_id_offset', self.rank * self.emulator_counts))
+        self.comm_kind = getattr(args, 'comm', 'rccl')
+        self.comm = None
+        if self.sampling == 'device' and getattr(args, 'egreedy', False):
+            # the device draw is the multinomial of exploration_policy.py:108-116 only
+            raise ValueError('--egreedy needs --sampling host (the device sampler draws multinomially)')
         self.dev = self.network.device
         E, T, C = self.emulator_counts, self.max_local_steps, self.C
         dev = self.dev
@@ -106,12 +118,14 @@ class PAACLearner(ActorLearner):
         self.col_lut = torch.from_numpy(COL_LUT.astype(np.int32)).to(dev)
         self.event = torch.cuda.Event()
         self.book = NativeBook(E, self.num_actions, self.tab_rep)
+        if self.world > 1:  # global_step counts every env of the job, as one process would
+            self.book.set_shard(self.env_offset, E * self.world)
         self.native_step = None  # mt_rollout handle (native runner + device sampling)
         self.boot_in_rollout = False
         self.slot0_in_rollout = False
         self.runners = None
         self.profile = None      # name -> [(start_event, end_event)] when profiling (bench.py)
-        self.sample_seed = (self.seed * 1000003 + self.rank * 7919 + 1) & 0xffffffffffff
+        self.sample_seed = (self.seed * 1000003 + 1) & 0xffffffffffff  # rank-independent: rows are global
         # replay the update as hipGraph(s) from the second update on (native pipelined step)
         self.use_update_graph = bool(getattr(args, 'update_graph', True))
         self._graphs = None
@@ -193,7 +207,7 @@ class PAACLearner(ActorLearner):
             p(rows), p(self.col_lut), p(self.idx_h), p(staging), p(r.push_meta), p(r.reward),
             p(r.over), p(self.rm_h), p(frames), p(self.sync_h), p(self.train_ws),
             0 if self.train_ws is None else self.train_ws.numel(),
-            p(self.v_boot if self.pipeline else None), p(self.ready_h), flags)
+            p(self.v_boot if self.pipeline else None), p(self.ready_h), flags, self.env_offset)
         h = C.c_void_p()
         _lib.check(_lib.hip().mt_rollout_create(net._h, self.emulator_counts, self.max_local_steps, r._h,
                                                 self.book.handle, C.byref(self._bufs),
@@ -271,7 +285,7 @@ class PAACLearner(ActorLearner):
         if end is not None:
             end.record()
         if self.sampling == 'device':
-            devnet.sample(pi, rep, self.sample_seed, self.counters, self.a_idx[t], self.r_idx[t])
+            devnet.sample(pi, rep, self.sample_seed, self.counters, self.a_idx[t], self.r_idx[t], row0=self.env_offset)
             self.a_h[t].copy_(self.a_idx[t], non_blocking=True)
             self.r_h[t].copy_(self.r_idx[t], non_blocking=True)
             self.event.record()
@@ -342,14 +356,14 @@ class PAACLearner(ActorLearner):
             if self._graphs is not None:
                 s = devnet._stream()
                 self._launch_graph(self._graphs[0], s)
-                if self.world > 1:
-                    torch.distributed.all_reduce(self.network.grad)
+                if len(self._graphs) > 1:  # the all-reduce could not be captured
+                    self.comm.allreduce(self.network.grad)
                     self._launch_graph(self._graphs[1], s)
                 return lr
         self._eager_updates += 1
         self._update_backward()
         if self.world > 1:
-            torch.distributed.all_reduce(self.network.grad)
+            self.comm.allreduce(self.network.grad)
         self._update_apply()
         return lr
 
@@ -419,21 +433,40 @@ class PAACLearner(ActorLearner):
         side = torch.cuda.Stream()
         side.wait_stream(cur)
         torch.cuda.synchronize()
-        parts = [self._update_backward, self._update_apply]
-        if self.world == 1:
-            parts = [lambda: (self._update_backward(), self._update_apply())]
-        graphs = []
-        with torch.cuda.stream(side):
-            sp = devnet._stream()
-            for fn in parts:
-                _lib.check(lib.mt_graph_begin(sp), 'mt_graph_begin')
-                try:
-                    fn()
-                finally:
-                    g = C.c_void_p()
-                    rc = lib.mt_graph_end(sp, C.byref(g))
-                _lib.check(rc, 'mt_graph_end')
-                graphs.append(g)
+        def whole():
+            self._update_backward()
+            if self.world > 1:
+                self.comm.allreduce(self.network.grad)
+            self._update_apply()
+
+        def capture(parts):
+            graphs = []
+            with torch.cuda.stream(side):
+                sp = devnet._stream()
+                for fn in parts:
+                    _lib.check(lib.mt_graph_begin(sp), 'mt_graph_begin')
+                    try:
+                        fn()
+                    finally:
+                        g = C.c_void_p()
+                        rc = lib.mt_graph_end(sp, C.byref(g))
+                    if rc != 0:
+                        for h in graphs:
+                            lib.mt_graph_destroy(h)
+                    _lib.check(rc, 'mt_graph_end')
+                    graphs.append(g)
+            return graphs
+
+        graphs = None
+        if self.world == 1 or self.comm.capturable:
+            try:  # one graph, the RCCL all-reduce inside it
+                graphs = capture([whole])
+            except _lib.MTError:
+                if self.world == 1:
+                    raise
+                graphs = None
+        if graphs is None:  # split around the all-reduce, which then runs eagerly
+            graphs = capture([self._update_backward, self._update_apply])
         self._graphs = graphs
         self._graph_stream = side  # keep the capture stream alive with the graphs
 
@@ -459,9 +492,14 @@ class PAACLearner(ActorLearner):
     def start(self):
         self.global_step = self.init_network()
         if self.world > 1:
-            torch.distributed.broadcast(self.network.params, 0)
-            torch.distributed.broadcast(self.network.ms, 0)
-            torch.distributed.broadcast(self.network.mom, 0)
+            from . import comm
+            self.comm = comm.make(self.comm_kind, self.rank, self.world, torch.cuda.current_device())
+            # rank 0's run is the run: its checkpoint step (resume) and its parameters / slots
+            self.global_step, self.last_saving_step = comm.broadcast_scalars(
+                [self.global_step, self.last_saving_step], self.rank)
+            for t in (self.network.params, self.network.ms, self.network.mom):
+                self.comm.broadcast(t, 0)
+            torch.cuda.current_stream().synchronize()
         self.global_step_start = self.global_step
         self._start_runners()
         if self.lstm_bool:  # memory = zeros except memory[:, -1] = initial state (paac.py:109-112)
@@ -506,3 +544,6 @@ class PAACLearner(ActorLearner):
             if self.runners is not None:
                 self.runners.stop()
                 self.runners = None
+            if self.comm is not None:
+                self.comm.close()
+                self.comm = None

@@ -12,7 +12,46 @@ from ctypes import c_float, c_uint8
 
 import numpy as np
 
-from . import nets, optim, policy, returns
+from . import nets, optim, policy, preprocess, returns
+
+
+class SyntheticEmulator(object):
+    """The synthetic ALE stand-in of SURVEY §8(d) restated on the oracle's preprocess (test data
+    for replays): per global env id, np.random.RandomState(1000 + id) draws a ring of 64 uniform
+    210x160 screens, then 4096 rewards in {-1, 0, +1} with p = (0.05, 0.90, 0.05). Push k pools
+    screens 2k, 2k+1 (mod 64) and resizes them (atari_emulator.py:79-100); next() returns reward k
+    (mod 4096) and pushes; an episode ends after episode_len next() calls; get_initial_state()
+    makes 4 pushes (environment.py / atari_emulator.py:102-124 contract)."""
+    RING, REWARD_LEN = 64, 4096
+
+    def __init__(self, global_env_id, depth=1, episode_len=997):
+        rs = np.random.RandomState(1000 + int(global_env_id))
+        self.screens = rs.randint(0, 256, size=(self.RING, 210, 160, depth), dtype=np.uint8)
+        self.rewards = rs.choice(np.array([-1.0, 0.0, 1.0]), p=[0.05, 0.90, 0.05],
+                                 size=self.REWARD_LEN).astype(np.float32)
+        self.depth = depth
+        self.episode_len = episode_len
+        self.stack = preprocess.ObservationStack(depth)
+        self.k = 0
+        self.steps = 0
+
+    def _push(self):
+        f0 = self.screens[(2 * self.k) % self.RING]
+        f1 = self.screens[(2 * self.k + 1) % self.RING]
+        self.stack.push(preprocess.pool_and_resize(f0, f1))
+        self.k += 1
+
+    def get_initial_state(self):
+        for _ in range(4):
+            self._push()
+        self.steps = 0
+        return self.stack.stacked()
+
+    def next(self, action):
+        reward = float(self.rewards[self.k % self.REWARD_LEN])
+        self._push()
+        self.steps += 1
+        return self.stack.stacked(), reward, self.steps >= self.episode_len
 
 
 def emulator_runner_step(tab_rep, emulators, states, rewards, over, a_idx, r_idx):

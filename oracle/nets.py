@@ -205,13 +205,11 @@ def lstm_backward(spec, P, lc, dout, dtype, G):
     return dX.reshape(B * T, nin)
 
 
-def forward(spec, P, obs, act='relu', alpha=0.1, temp=1.0, dtype=np.float64):
-    """P: dict name -> array. obs uint8 [B,84,84,C] (LSTM: [B,5,84,84,C], the memory window of
-    paac.py:79-83). Returns (v, pi, rep, cache)."""
-    if spec.get('lstm'):
-        obs = obs.reshape((-1,) + obs.shape[2:])
+def trunk_forward(spec, P, obs, act='relu', alpha=0.1, dtype=np.float64):
+    """Input scale (networks.py:155) + the conv layers (+ pools) of one frame batch obs uint8
+    [B,84,84,C]: returns (flat [B, spec['flat']] in NHWC order, layer caches)."""
     x = obs.astype(dtype) * dtype(1.0 / 255.0)  # networks.py:155
-    cache = dict(layers=[])
+    layers = []
     for (name, k, s, cin, cout, pad, pool) in spec['convs']:
         W = P['Network/%s/%s_weights' % (name, name)].astype(dtype)
         b = P['Network/%s/%s_biases' % (name, name)].astype(dtype)
@@ -222,11 +220,37 @@ def forward(spec, P, obs, act='relu', alpha=0.1, temp=1.0, dtype=np.float64):
             y2 = maxpool2(y)
             entry['yp'] = y2
             y = y2
-        cache['layers'].append(entry)
+        layers.append(entry)
         x = y
-    B = x.shape[0]
-    flat = x.reshape(B, -1)
-    cache.update(flat=flat)
+    return x.reshape(x.shape[0], -1), layers
+
+
+def trunk_backward(spec, P, layers, dflat, G, act='relu', alpha=0.1, dtype=np.float64):
+    """Gradient of trunk_forward for dflat [B, flat]: conv weight / bias gradients ADDED into G
+    (so chunks of frames accumulate), TF's Conv2DBackprop* / ReluGrad / MaxPoolGrad."""
+    last = layers[-1]
+    dx = dflat.reshape(last['yp'].shape if last['pool'] else last['y'].shape)
+    for li in range(len(layers) - 1, -1, -1):
+        L = layers[li]
+        if L['pool']:
+            dx = maxpool2_bwd(L['y'], L['yp'], dx)
+        dy = dx * act_bwd(L['y'], act, alpha)
+        cols, _ = im2col(L['x'], L['k'], L['s'], L['pad'])
+        dy2 = dy.reshape(-1, L['cout'])
+        name = L['name']
+        W = P['Network/%s/%s_weights' % (name, name)].astype(dtype)
+        for key, val in (('Network/%s/%s_weights' % (name, name), (cols.T @ dy2).reshape(W.shape)),
+                         ('Network/%s/%s_biases' % (name, name), dy2.sum(0))):
+            G[key] = G[key] + val if key in G else val
+        if li > 0:
+            dcols = dy2 @ W.reshape(-1, L['cout']).T
+            dx = col2im(dcols, L['x'].shape, L['k'], L['s'], L['pad'])
+
+
+def heads_forward(spec, P, flat, act='relu', alpha=0.1, temp=1.0, dtype=np.float64):
+    """[LSTM cell over the 5 window positions] + dense layer + the three heads, from the trunk
+    features flat ([B, flat]; LSTM: [B*5, flat], window-major). Returns (v, pi, rep, cache)."""
+    cache = dict(flat=flat)
     fc_in = flat
     if spec.get('lstm'):
         fc_in, cache['lstm'] = lstm_forward(spec, P, flat, dtype)
@@ -247,10 +271,21 @@ def forward(spec, P, obs, act='relu', alpha=0.1, temp=1.0, dtype=np.float64):
     return v, pi, rep, cache
 
 
-def loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1, temp=1.0,
-                   dtype=np.float64):
-    """Loss of policy_v_network.py:25-74 and its gradient for every variable (dict)."""
-    v, pi, rep, c = forward(spec, P, obs, act, alpha, temp, dtype)
+def forward(spec, P, obs, act='relu', alpha=0.1, temp=1.0, dtype=np.float64):
+    """P: dict name -> array. obs uint8 [B,84,84,C] (LSTM: [B,5,84,84,C], the memory window of
+    paac.py:79-83). Returns (v, pi, rep, cache)."""
+    if spec.get('lstm'):
+        obs = obs.reshape((-1,) + obs.shape[2:])
+    flat, layers = trunk_forward(spec, P, obs, act, alpha, dtype)
+    v, pi, rep, cache = heads_forward(spec, P, flat, act, alpha, temp, dtype)
+    cache['layers'] = layers
+    return v, pi, rep, cache
+
+
+def heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1, temp=1.0,
+                         dtype=np.float64):
+    """Loss of policy_v_network.py:25-74 from heads_forward's outputs; gradients of the head,
+    dense [and LSTM] variables into a new dict G. Returns (loss, G, dflat, aux)."""
     B = len(v)
     y = np.asarray(y, dtype)
     adv = np.asarray(adv, dtype)
@@ -297,25 +332,41 @@ def loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0
     dflat = dh @ Wf.T
     if spec.get('lstm'):
         dflat = lstm_backward(spec, P, c['lstm'], dflat, dtype, G)
-    layers = c['layers']
-    last = layers[-1]
-    dx = dflat.reshape(last['yp'].shape if last['pool'] else last['y'].shape)
-    for li in range(len(layers) - 1, -1, -1):
-        L = layers[li]
-        if L['pool']:
-            dx = maxpool2_bwd(L['y'], L['yp'], dx)
-        dy = dx * act_bwd(L['y'], act, alpha)
-        cols, _ = im2col(L['x'], L['k'], L['s'], L['pad'])
-        dy2 = dy.reshape(-1, L['cout'])
-        name = L['name']
-        W = P['Network/%s/%s_weights' % (name, name)].astype(dtype)
-        G['Network/%s/%s_weights' % (name, name)] = (cols.T @ dy2).reshape(W.shape)
-        G['Network/%s/%s_biases' % (name, name)] = dy2.sum(0)
-        if li > 0:
-            dcols = dy2 @ W.reshape(-1, L['cout']).T
-            dx = col2im(dcols, L['x'].shape, L['k'], L['s'], L['pad'])
     terms = np.stack([critic, -((sel_pi + sel_rep) * adv), ent_pi, ent_rep], axis=1)
-    return loss, G, dict(v=v, pi=pi, rep=rep, terms=terms)
+    return loss, G, dflat, dict(v=v, pi=pi, rep=rep, terms=terms)
+
+
+def loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1, temp=1.0,
+                   dtype=np.float64):
+    """Loss of policy_v_network.py:25-74 and its gradient for every variable (dict)."""
+    v, pi, rep, c = forward(spec, P, obs, act, alpha, temp, dtype)
+    loss, G, dflat, aux = heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act, alpha,
+                                               temp, dtype)
+    trunk_backward(spec, P, c['layers'], dflat, G, act, alpha, dtype)
+    return loss, G, aux
+
+
+def window_frames_loss_and_grads(spec, P, frames, win, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1,
+                                 temp=1.0, dtype=np.float64, chunk=32):
+    """loss_and_grads of LSTM windows given as indices into distinct frames: window b's position k
+    is frames[win[b, k]] (the reference builds each window as an explicit [5][84][84][C] slice of
+    whole_memory, paac.py:79-83, :233-234; zeroed positions after an episode end are a zero frame).
+    Every distinct frame goes through the trunk once (forward in chunks, features gathered per
+    window position), and the trunk gradient is that of each frame's summed feature gradient —
+    the same sums, by linearity, as the explicit windows' loss_and_grads (tests/test_oracle_torch.py
+    pins the two against each other). frames: uint8 [F,84,84,C]; win: int [B,5]."""
+    F = len(frames)
+    flat = np.concatenate([trunk_forward(spec, P, frames[c0:c0 + chunk], act, alpha, dtype)[0]
+                           for c0 in range(0, F, chunk)])
+    v, pi, rep, c = heads_forward(spec, P, flat[np.asarray(win).reshape(-1)], act, alpha, temp, dtype)
+    loss, G, dflat_w, aux = heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act, alpha,
+                                                 temp, dtype)
+    dflat = np.zeros_like(flat)
+    np.add.at(dflat, np.asarray(win).reshape(-1), dflat_w)
+    for c0 in range(0, F, chunk):
+        _, layers = trunk_forward(spec, P, frames[c0:c0 + chunk], act, alpha, dtype)
+        trunk_backward(spec, P, layers, dflat[c0:c0 + chunk], G, act, alpha, dtype)
+    return loss, G, aux
 
 
 def init_params(spec, seed):

@@ -1,7 +1,14 @@
-"""One rank of the data-parallel tests (launched by tests with WORLD_SIZE/RANK set).
+"""One rank of the data-parallel tests (launched by tests with WORLD_SIZE/RANK set, or alone for
+the single-process reference run).
 
-gpu: PAACLearner on cuda:0 with torch.distributed (gloo), rank r owns global envs
-     [r*ec, (r+1)*ec); after 3 updates the rank's flat parameters are saved.
+gpu: PAACLearner on cuda:0 over the benchmarked path (native step, device sampling, resized
+     staging, pipelined, update replayed as a hipGraph from the second update on). The job has
+     ENVS global envs; rank r owns [r*ENVS/W, (r+1)*ENVS/W) (the runners.py:17-18 split over
+     ranks), the gradient is summed by the learner's comm (torch.distributed on the gloo group:
+     the ranks share one GPU, which RCCL does not allow) once per update. After every update
+     the rank saves its parameters, its envs' states, global_step and episode records, so the
+     test can compare a W-rank run with the single process that owns all ENVS envs.
+resume: a W-rank run is stopped (rank 0 checkpoints) and resumed from rank 0's checkpoint.
 cpu: the DP update protocol on the oracle (no GPU): each rank takes half of a fixed batch, the
      flat gradient is summed by all_reduce, scaled by 1/world, clipped by its global norm and
      applied with TF1 RMSProp (manette_amd.paac.PAACLearner.update's order).
@@ -16,32 +23,84 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+ENVS = 16
+UPDATES = 4
 
-def gpu_rank(out_dir):
+
+def _learner(out_dir, rank, world, comm='torch'):
     import train as cli
     from manette_amd.exploration_policy import ExplorationPolicy
     from manette_amd.paac import PAACLearner
-    rank = dist.get_rank()
+    from manette_amd.synthetic import SyntheticBank
     a = cli.get_arg_parser().parse_args([])
-    a.game, a.arch, a.emulator_counts, a.emulator_workers = 'pong', 'NIPS', 8, 2
-    a.runner, a.sampling, a.seed = 'native', 'device', 0
-    a.debugging_folder = os.path.join(out_dir, 'r%d' % rank) + '/'
+    ec = ENVS // world
+    a.game, a.arch, a.emulator_counts, a.emulator_workers = 'breakout', 'NIPS', ec, 2
+    a.max_repetition, a.nb_choices = 10, 11
+    a.runner, a.sampling, a.seed, a.staging, a.pipeline = 'native', 'device', 0, 'resized', True
+    a.comm = comm
+    a.debugging_folder = os.path.join(out_dir, 'w%d_r%d' % (world, rank)) + '/'
     a.max_global_steps = 1 << 40
     a.checkpoint_interval = 1 << 40
-    a.env_id_offset = rank * a.emulator_counts
+    a.env_id_offset = rank * ec
     explo = ExplorationPolicy(a)
     nc, ecr = cli.get_network_and_environment_creator(a, explo)
+    # short episodes, so resets (and their global_step records) happen inside the run
+    ecr.create_bank = lambda first, n: SyntheticBank(ecr.rank_offset + first, n, episode_len=23)
     L = PAACLearner(nc, ecr, explo, a)
-    assert L.world == 2
+    assert L.world == world
     L.start()
-    for _ in range(3):
-        L.book.new_update()
-        for t in range(L.max_local_steps):
-            L.step(t)
-        L.update()
-    torch.cuda.synchronize()
-    np.save(os.path.join(out_dir, 'rank%d.npy' % rank), L.network.params.cpu().numpy())
-    L.cleanup()
+    return L
+
+
+def gpu_rank(out_dir, rank, world):
+    L = _learner(out_dir, rank, world)
+    rec = dict(params=[], states=[], gs=[])
+    params0 = L.network.params.cpu().numpy().copy()
+    try:
+        for _ in range(UPDATES):
+            L.book.new_update()
+            L.rollout()
+            L.update()
+            torch.cuda.synchronize()
+            rec['params'].append(L.network.params.cpu().numpy().copy())
+            rec['states'].append(L.states[1:].cpu().numpy().copy())
+            rec['gs'].append(L.global_step)
+        L.book.drain()
+        assert L._graphs is not None  # the graph path ran
+        np.savez(os.path.join(out_dir, 'w%d_r%d.npz' % (world, rank)), params0=params0, params=np.stack(rec['params']),
+                 states=np.stack(rec['states']), gs=np.array(rec['gs']),
+                 episodes=np.array(L.book.episodes, dtype=np.float64).reshape(-1, 3))
+    finally:
+        L.cleanup()
+
+
+def resume_rank(out_dir, rank, world):
+    """a W-rank run resumed from rank 0's checkpoint (the other ranks' folders have
+    none, as train.py gives them rank<r>/ folders) continues from rank 0's step on every rank with
+    rank 0's parameters, and the replicas stay identical."""
+    L = _learner(out_dir, rank, world)
+    try:
+        for _ in range(2):
+            L.book.new_update()
+            L.rollout()
+            L.update()
+        saved = L.global_step
+    finally:
+        L.cleanup()  # rank 0 writes its checkpoint (save_vars(True))
+    dist.barrier()
+    L = _learner(out_dir, rank, world)
+    try:
+        start = L.global_step
+        p_start = L.network.params.cpu().numpy().copy()
+        for _ in range(2):
+            L.book.new_update()
+            L.rollout()
+            L.update()
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, 'resume_r%d.npz' % rank), saved=saved, start=start, end=L.global_step,
+                 p_start=p_start, params=L.network.params.cpu().numpy())
+    finally:
+        L.cleanup()
 
 
 def cpu_batch():
@@ -81,10 +140,19 @@ def cpu_rank(out_dir):
 
 if __name__ == '__main__':
     out_dir, mode = sys.argv[1], sys.argv[2]
-    if mode == 'gpu':
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if mode in ('gpu', 'resume'):
         torch.cuda.set_device(0)
+    if world == 1 and mode == 'gpu':  # the single process owning every env
+        gpu_rank(out_dir, 0, 1)
+        sys.exit(0)
     dist.init_process_group('gloo')
     try:
-        gpu_rank(out_dir) if mode == 'gpu' else cpu_rank(out_dir)
+        if mode == 'gpu':
+            gpu_rank(out_dir, dist.get_rank(), world)
+        elif mode == 'resume':
+            resume_rank(out_dir, dist.get_rank(), world)
+        else:
+            cpu_rank(out_dir)
     finally:
         dist.destroy_process_group()

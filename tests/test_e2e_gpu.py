@@ -1,0 +1,182 @@
+"""End-to-end oracle parity of the BENCHMARKED path at every 1-GPU config size.
+
+The learner is bench.make_learner(config) — the exact object bench.py times: native emulator
+threads, device sampling fused into the heads kernel, resized staging, the pipelined native
+macro-step (NIPS: pull kernel + stacking conv kernel), the update replayed as a hipGraph from the
+second update on; LSTM: the frame-store path. U updates run; the last one (a graph replay) is
+checked against the oracle on everything it consumed and produced:
+
+  trajectory  every state slot 0..T and the clipped rewards / masks == a replay of the oracle's
+              synthetic emulators (oracle/host_loop.py: emulator_runner.py:24-41 + the
+              atari_emulator.py preprocess) under the recorded action / repetition indices of
+              every rollout so far (A1, A2, A4, A8)                              bit-exact
+  forward     v / pi / rep of every rollout row and V(s_T) == oracle forward      2e-5 relative
+  returns     y / adv == oracle.returns.nstep_returns (paac.py:219-231)          bit-exact
+  gradient    every variable == oracle.nets.loss_and_grads of the T*E rows        2e-4 rel. L2
+              (LSTM: of the T*E windows over the distinct frames)
+  loss terms  per row == oracle                                                   1e-4 relative
+  optimizer   lr == get_lr(global_step); norm == ||grad|| (1e-5); params / ms / mom after the
+              update == oracle.optim clip + TF1 RMSProp on the device gradient    bit-exact
+Reference: paac.py:140-256, actor_learner.py:43-74, policy_v_network.py:25-74.
+Synthetic episodes are shortened (episode_len) so episode ends and resets happen inside the run.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import host_loop, nets, optim, policy, returns
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+UPDATES = 4
+EPISODE_LEN = 13
+
+
+def _replay(cfg, E, A, idx_all, T):
+    """Oracle emulators stepped with the recorded indices: states [U][T+1][E], rewards / masks [U][T][E]."""
+    depth = 3 if cfg['rgb'] else 1
+    tab = policy.tab_repetitions(cfg['max_repetition'], cfg['nb_choices'])
+    emus = [host_loop.SyntheticEmulator(e, depth, EPISODE_LEN) for e in range(E)]
+    s = np.stack([em.get_initial_state() for em in emus])
+    rew = np.zeros(E, np.float32)
+    over = np.zeros(E, np.float32)
+    out = []
+    for idx in idx_all:
+        states, rr, mm = [s.copy()], [], []
+        for t in range(T):
+            host_loop.emulator_runner_step(tab, emus, s, rew, over, idx[0, t], idx[1, t])
+            states.append(s.copy())
+            rr.append(np.clip(rew, -1.0, 1.0).astype(np.float32))
+            mm.append((1.0 - over).astype(np.float32))
+        out.append((np.stack(states), np.stack(rr), np.stack(mm)))
+    return out
+
+
+def _run(config, tmp_path):
+    import bench
+    L, args = bench.make_learner(config, debugging_folder=str(tmp_path) + '/', episode_len=EPISODE_LEN)
+    L.start()
+    return L, args, bench.CONFIGS[config]
+
+
+def _window_rows(nz, t, E):
+    """Frame-store rows of the windows of step t: position k < nz reads the zero frame (row 0),
+    else slot t + k (row 1 + (t + k) * E + e) — the reference's memory window (paac.py:79-83)."""
+    w = np.zeros((E, 5), np.int64)
+    for e in range(E):
+        for k in range(5):
+            w[e, k] = 0 if k < nz[e] else 1 + (t + k) * E + e
+    return w
+
+
+@pytest.mark.parametrize('config', ['pong-nips', 'breakout-nature-figar', 'seaquest-nature', 'mspacman-lstm-figar'])
+def test_benchmarked_path_matches_oracle(config, tmp_path):
+    import parity_util
+    L, args, cfg = _run(config, tmp_path)
+    try:
+        lstm = L.lstm_bool
+        if not lstm:
+            assert L.native_step is not None and L.boot_in_rollout and L._graph_ok()
+        E, T, A, R = L.emulator_counts, L.max_local_steps, L.num_actions, L.total_repetitions
+        N = E * T
+        idx_all = []
+        for u in range(UPDATES - 1):
+            L.book.new_update()
+            L.rollout()
+            idx_all.append(L.idx_h.numpy().copy())
+            L.update()
+        if not lstm:
+            assert L._graphs is not None  # the checked update is a graph replay
+        L.book.new_update()
+        L.rollout()
+        torch.cuda.synchronize()
+        idx_all.append(L.idx_h.numpy().copy())
+        c = lambda t: t.detach().cpu().numpy().copy()
+        P = L.network.get_variables()
+        flat_p, ms0, mom0 = c(L.network.params), c(L.network.ms), c(L.network.mom)
+        states = c(L.states)
+        rm = L.rm_h.numpy().copy()
+        values = c(L.values)
+        gs = L.global_step
+        if lstm:  # (the update's apply moves slots T.. to 0.. and nz[T] to nz[0])
+            fstore, nz = c(L.fstore), L.nz_h.numpy().copy()
+        L.update()
+        torch.cuda.synchronize()
+        # V(s_T): the rollout's last chain (pipelined native step) or the update's first forward (LSTM)
+        v_boot, pi_all, rep_all = c(L.v_boot), c(L.pi_all), c(L.rep_all)
+        grad, y, adv = L.network.get_variables('grad'), c(L.y), c(L.adv)
+        grad_flat = c(L.network.grad)
+        w1, ms1, mom1 = c(L.network.params), c(L.network.ms), c(L.network.mom)
+        norm_dev = float(L.network.norm_dev.item())
+        lr_dev = float(L.network._lr_host[0])
+        terms = c(L.loss_terms)
+    finally:
+        L.cleanup()
+
+    # ---- trajectory: states, rewards, masks (bit-exact) --------------------------------------
+    rep_states, rep_r, rep_m = _replay(cfg, E, A, idx_all, T)[-1]
+    for t in range(T + 1):
+        np.testing.assert_array_equal(states[t], rep_states[t], err_msg='state slot %d' % t)
+    np.testing.assert_array_equal(rm[0], rep_r)
+    np.testing.assert_array_equal(rm[1], rep_m)
+    assert gs == UPDATES * T * E
+    assert (idx_all[-1][0] < A).all() and (idx_all[-1][1] < R).all() and (idx_all[-1] >= 0).all()
+
+    # ---- forward of every rollout row + V(s_T) ----------------------------------------------
+    spec = nets.arch_spec(cfg['arch'], 3 if cfg['rgb'] else 1, A, R)
+    if lstm:
+        Fr = 1 + (T + 5) * E
+        feats = np.concatenate([nets.trunk_forward(spec, P, fstore[c0:c0 + 32])[0] for c0 in range(0, Fr, 32)])
+        for t in range(T + 1):
+            rows = _window_rows(nz[t], t, E)
+            v0, pi0, rep0, _ = nets.heads_forward(spec, P, feats[rows.reshape(-1)])
+            v_t = values[t] if t < T else v_boot
+            np.testing.assert_allclose(v_t, v0, rtol=2e-5, atol=2e-5, err_msg='v step %d' % t)
+            np.testing.assert_allclose(pi_all[t], pi0, rtol=2e-5, atol=1e-6, err_msg='pi step %d' % t)
+            np.testing.assert_allclose(rep_all[t], rep0, rtol=2e-5, atol=1e-6, err_msg='rep step %d' % t)
+    else:
+        obs = states[:T + 1].reshape((T + 1) * E, 84, 84, -1)
+        v0, pi0, rep0, _ = nets.forward(spec, P, obs)
+        np.testing.assert_allclose(values.reshape(-1), v0[:N], rtol=2e-5, atol=2e-5)
+        np.testing.assert_allclose(v_boot, v0[N:], rtol=2e-5, atol=2e-5)
+        np.testing.assert_allclose(pi_all[:T].reshape(N, A), pi0[:N], rtol=2e-5, atol=1e-6)
+        np.testing.assert_allclose(rep_all[:T].reshape(N, R), rep0[:N], rtol=2e-5, atol=1e-6)
+
+    # ---- n-step returns (bit-exact with the reference's dtype trail) --------------------------
+    y0, adv0 = returns.nstep_returns(rm[0].astype(np.float64), rm[1].astype(np.float64), values.astype(np.float64),
+                                     v_boot, L.gamma)
+    np.testing.assert_array_equal(y, y0.astype(np.float32))
+    np.testing.assert_array_equal(adv, adv0.astype(np.float32))
+
+    # ---- gradient of the T*E rows / windows ----------------------------------------------------
+    a_idx, r_idx = idx_all[-1][0].reshape(N), idx_all[-1][1].reshape(N)
+    beta = L.network.beta
+    if lstm:
+        win = np.concatenate([_window_rows(nz[t], t, E) for t in range(T)])
+        Fb = 1 + (T + 4) * E
+        _, G, aux = nets.window_frames_loss_and_grads(spec, P, fstore[:Fb], win, a_idx, r_idx, y.reshape(N),
+                                                      adv.reshape(N), beta)
+        loose = parity_util.near_tie_layers_frames(spec, P, fstore[:Fb])
+    else:
+        obs_n = states[:T].reshape(N, 84, 84, -1)
+        _, G, aux = nets.loss_and_grads(spec, P, obs_n, a_idx, r_idx, y.reshape(N), adv.reshape(N), beta)
+        loose = set()
+    parity_util.check_grads(spec, grad, G, loose)
+    np.testing.assert_allclose(terms, aux['terms'], rtol=1e-4, atol=1e-5)
+
+    # ---- global-norm clip + TF1 RMSProp (bit-exact given the device gradient and norm) --------
+    assert np.float32(lr_dev) == np.float32(optim.get_lr(gs, L.initial_lr, L.lr_annealing_steps))
+    ref_norm = optim.global_norm([grad_flat])
+    assert abs(norm_dev - ref_norm) <= 1e-5 * ref_norm, (norm_dev, ref_norm)
+    s = optim.clip_scale(norm_dev, L.network.clip_norm)
+    w, ms, mom = flat_p.copy(), ms0.copy(), mom0.copy()
+    optim.rmsprop_apply(w, ms, mom, grad_flat * s, np.float32(lr_dev), L.network.decay, 0.0, L.network.eps)
+    np.testing.assert_array_equal(ms1, ms)
+    np.testing.assert_array_equal(mom1, mom)
+    np.testing.assert_array_equal(w1, w)

@@ -327,3 +327,35 @@ def test_sample_distribution():
     assert np.abs(freq - p).max() < 0.01
     ah = a.cpu().numpy()
     assert ah.min() >= 0 and ah.max() < A and r.cpu().numpy().max() < R
+
+
+def test_zero_copy_reads_see_host_rewrites_across_launches():
+    """The zero-copy kernels read pinned (non-coherent) host memory with plain loads; a line a
+    launch cached must not serve a later launch after the host rewrote it (each dispatch starts
+    with a system-scope acquire — rollout.hip's pull kernel relies on it). 50 rounds: the host
+    rewrites the staged frames in place, the same kernel reads them again."""
+    from manette_amd.network import preprocess as dev_pre, host_device_pointer
+    E, depth = 8, 1
+    rs = np.random.RandomState(5)
+    frames = torch.zeros(4 * E, 84, 84, depth, dtype=torch.uint8).pin_memory()
+    fdev = host_device_pointer(frames)
+    offs = torch.from_numpy((4 * np.arange(E)).astype(np.int32)).cuda()
+    counts_h = rs.randint(1, 5, E).astype(np.int32)
+    counts = torch.from_numpy(counts_h).cuda()
+    prev = torch.from_numpy(rs.randint(0, 256, size=(E, 84, 84, 4 * depth)).astype(np.uint8)).cuda()
+    out = torch.empty_like(prev)
+    import ctypes as C
+    from manette_amd import _lib
+    for it in range(50):
+        frames.numpy()[...] = rs.randint(0, 256, size=frames.shape).astype(np.uint8)
+        _lib.check(_lib.hip().mt_preprocess_resized(C.c_void_p(fdev), C.c_void_p(offs.data_ptr()),
+                                                    C.c_void_p(counts.data_ptr()), E, depth,
+                                                    C.c_void_p(prev.data_ptr()), C.c_void_p(out.data_ptr()),
+                                                    C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        f = frames.numpy()
+        pv = prev.cpu().numpy()
+        for e in range(E):
+            pushes = [f[4 * e + j] for j in range(counts_h[e])]
+            np.testing.assert_array_equal(got[e], preprocess.stack_update(pv[e], pushes, depth), err_msg='round %d' % it)

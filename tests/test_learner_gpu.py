@@ -158,19 +158,61 @@ def test_eval_cli_restores_training_checkpoint(tmp_path, arch, extra):
     assert any(l.startswith('Mean: ') for l in lines) and any(l.startswith('Std: ') for l in lines)
 
 
-def test_dp_two_ranks_gloo_on_one_gpu(tmp_path):
-    """world_size 2 (gloo over the same GPU): the flat gradient is all-reduced once per update
-    and both replicas stay bit-identical."""
+def _dp_run(tmp_path, world, port, mode='gpu'):
     script = os.path.join(ROOT, 'tests', 'dp_worker.py')
-    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT='29533', WORLD_SIZE='2')
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world))
     procs = []
-    for r in range(2):
+    for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK='0')
-        procs.append(subprocess.Popen([sys.executable, script, str(tmp_path), 'gpu'], env=e,
+        procs.append(subprocess.Popen([sys.executable, script, str(tmp_path), mode], env=e,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=300) for p in procs]
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, o[-2000:] + e[-3000:]
-    p0 = np.load(os.path.join(str(tmp_path), 'rank0.npy'))
-    p1 = np.load(os.path.join(str(tmp_path), 'rank1.npy'))
-    np.testing.assert_array_equal(p0, p1)
+    if mode != 'gpu':
+        return None
+    return [np.load(os.path.join(str(tmp_path), 'w%d_r%d.npz' % (world, r))) for r in range(world)]
+
+
+def test_dp_two_ranks_equal_single_process_union(tmp_path):
+    """W=2 ranks (8 envs each, gradient summed once per update, 1/W folded into the
+    clip) == ONE process owning all 16 envs, through the product's update (graph-replayed from the
+    second update on): the device draw hashes global env ids, so both runs take the same
+    trajectory (states bit-identical per env), global_step advances by all 16 envs per macro-step
+    on every rank (mh_book_set_shard), episodes carry the same global steps, and the parameters
+    after every update agree within the fp32 reduction-order budget (the W=2 gradient is two
+    80-row sums added by the all-reduce instead of one 160-row sum)."""
+    one = _dp_run(tmp_path, 1, 29531)[0]
+    two = _dp_run(tmp_path, 2, 29533)
+    ec = 8
+    p0 = None
+    for r in range(2):
+        np.testing.assert_array_equal(two[r]['gs'], one['gs'])
+        np.testing.assert_array_equal(two[r]['states'], one['states'][:, :, r * ec:(r + 1) * ec],
+                                      err_msg='rank %d trajectory' % r)
+    np.testing.assert_array_equal(two[0]['params'], two[1]['params'])  # replicas identical
+    assert one['gs'][-1] == 4 * 5 * 16
+    ep1 = sorted(map(tuple, one['episodes']))
+    ep2 = sorted(map(tuple, np.concatenate([two[0]['episodes'], two[1]['episodes']])))
+    assert len(ep1) > 0 and ep1 == ep2
+    np.testing.assert_array_equal(two[0]['params0'], one['params0'])
+    # parameter updates: relative L2 of (W2 - W1) against the update itself, per update
+    prev = one['params0'].astype(np.float64)
+    for u in range(one['params'].shape[0]):
+        a, b = one['params'][u].astype(np.float64), two[0]['params'][u].astype(np.float64)
+        step = np.linalg.norm(a - prev)
+        assert step > 0 and np.linalg.norm(a - b) <= 1e-4 * step, (u, np.linalg.norm(a - b), step)
+        prev = a
+
+
+def test_dp_resume_from_rank0_checkpoint(tmp_path):
+    """resuming a 2-rank run — rank 0 restores its checkpoint, rank 1's folder has
+    none — continues from rank 0's global_step on both ranks with rank 0's parameters (broadcast at
+    start), so both ranks follow one LR schedule and the replicas stay bit-identical."""
+    _dp_run(tmp_path, 2, 29541, mode='resume')
+    r0, r1 = [np.load(os.path.join(str(tmp_path), 'resume_r%d.npz' % r)) for r in range(2)]
+    assert int(r0['saved']) == int(r1['saved']) == 2 * 5 * 16
+    assert int(r0['start']) == int(r1['start']) == int(r0['saved'])
+    assert int(r0['end']) == int(r1['end']) == int(r0['saved']) + 2 * 5 * 16
+    np.testing.assert_array_equal(r0['p_start'], r1['p_start'])
+    np.testing.assert_array_equal(r0['params'], r1['params'])

@@ -196,3 +196,22 @@ def test_meta_graph_constants_g5():
     assert [x['padding'] for x in pw['convs']] == ['SAME'] * 4
     assert all(p['padding'] == 'VALID' and p['ksize'] == [1, 2, 2, 1] for p in pw['pools'])
     assert len(m['catcher']['apply_rmsprop']) == 12
+
+
+def test_oracle_synthetic_emulator_equals_product_stream():
+    """oracle/host_loop.SyntheticEmulator (the replay emulator of tests/test_e2e_gpu.py) restates
+    the bench's synthetic stream (manette_amd/synthetic.py) on the oracle's preprocess:
+    identical observations, rewards and terminals over resets, gray and RGB."""
+    from oracle import host_loop
+    from manette_amd.synthetic import SyntheticEmulator
+    for gid, rgb in ((3, False), (17, True)):
+        a = host_loop.SyntheticEmulator(gid, 3 if rgb else 1, episode_len=5)
+        b = SyntheticEmulator(gid, 6, rgb=rgb, episode_len=5)
+        np.testing.assert_array_equal(a.get_initial_state(), b.get_initial_state())
+        for i in range(40):
+            sa, ra, ta = a.next(0)
+            sb, rb, tb = b.next(0)
+            np.testing.assert_array_equal(sa, sb)
+            assert ra == rb and ta == tb
+            if ta:
+                np.testing.assert_array_equal(a.get_initial_state(), b.get_initial_state())

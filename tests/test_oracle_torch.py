@@ -104,3 +104,25 @@ def test_cpu_baseline_network_matches_oracle(arch, A, R):
     np.testing.assert_allclose(v, v0, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(pi, pi0, rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(rep, rep0, rtol=1e-4, atol=1e-6)
+
+
+def test_window_frames_oracle_equals_explicit_windows():
+    """nets.window_frames_loss_and_grads (each distinct frame through the trunk once, windows as
+    frame indices, the zero frame included) == nets.loss_and_grads on the explicit [B][5] windows
+    the reference feeds (paac.py:79-83, :233-234)."""
+    spec = nets.arch_spec('LSTM', 1, 5, 3)
+    P = nets.init_params(spec, 3)
+    P['rnn/basic_lstm_cell/bias'] = np.random.RandomState(1).uniform(-0.5, 0.5, 128).astype(np.float32)
+    rs = np.random.RandomState(4)
+    F, B = 6, 4
+    frames = rs.randint(0, 256, size=(F, 84, 84, 4)).astype(np.uint8)
+    frames[0] = 0
+    win = np.array([[0, 0, 1, 2, 3], [1, 2, 3, 4, 5], [0, 0, 0, 0, 5], [2, 3, 4, 5, 1]])
+    a, r = rs.randint(0, 5, B), rs.randint(0, 3, B)
+    y, adv = rs.randn(B), rs.randn(B)
+    l0, G0, aux0 = nets.loss_and_grads(spec, P, frames[win], a, r, y, adv, 0.02)
+    l1, G1, aux1 = nets.window_frames_loss_and_grads(spec, P, frames, win, a, r, y, adv, 0.02, chunk=4)
+    assert abs(l0 - l1) <= 1e-12 * abs(l0)
+    np.testing.assert_allclose(aux1['terms'], aux0['terms'], rtol=1e-12)
+    for k in G0:
+        np.testing.assert_allclose(G1[k], G0[k], rtol=1e-9, atol=1e-14, err_msg=k)

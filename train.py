@@ -4,7 +4,8 @@
 Extra flags (this build only): --runner {native,python}, --sampling {host,device},
 --staging {resized,in_place,zero_copy,copy,pooled}, --no_pipeline, --seed.
 Multi-GPU: launch one process per GPU with torch.distributed.run; each rank trains
--ec emulators of its own (global env ids offset by rank) and gradients are all-reduced.
+-ec emulators of its own (global env ids offset by rank) and gradients are all-reduced by RCCL
+behind the C ABI (--comm rccl; torch.distributed runs on gloo as the control channel only).
 """
 import argparse
 import copy
@@ -41,7 +42,8 @@ def _setup_distributed(args):
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     if world > 1 and not torch.distributed.is_initialized():
-        torch.distributed.init_process_group('nccl' if torch.cuda.is_available() else 'gloo')
+        # control channel only (RCCL unique id, resume step); the gradient goes over mt_allreduce
+        torch.distributed.init_process_group('gloo')
     rank = torch.distributed.get_rank() if world > 1 else 0
     args.env_id_offset = rank * args.emulator_counts
     if rank != 0:
@@ -140,6 +142,9 @@ def get_arg_parser():
                         '(MT_ROLLOUT_PIPELINED, on by default)', dest='pipeline')
     parser.add_argument('--sampling', default='host', choices=['host', 'device'], help='host: numpy multinomial (reference stream); device: mt_sample', dest='sampling')
     parser.add_argument('--seed', default=0, type=int, help='parameter init / device sampling seed', dest='seed')
+    parser.add_argument('--comm', default='rccl', choices=['rccl', 'torch'], help='data-parallel gradient all-reduce: '
+                        'rccl = RCCL behind the C ABI (mt_allreduce, one GPU per rank); torch = torch.distributed on '
+                        'the process group (ranks sharing a GPU, tests)', dest='comm')
     return parser
 
 
