@@ -37,13 +37,6 @@ void set_error(const char *fmt, ...);
 
 __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-// Load of a value the HOST writes between launches (pinned, device-mapped memory: the rollout's
-// rewards / masks, the LR): a system-scope load bypasses the GPU's non-coherent cache lines, so
-// a line cached by an earlier launch can never be returned stale. Works on device memory too.
-__device__ __forceinline__ float host_ld(const float *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // Wave-wide (64 lanes) sum via butterfly shuffles.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -37,13 +37,13 @@ __global__ void returns_kernel(const float *__restrict__ r, const float *__restr
   if (e >= E) return;
   // t = T-1: float32 product gamma*R_T, then float64 with the mask and reward.
   const float g32 = __fmul_rn((float)gamma, VT[e]);
-  double R = (double)host_ld(r + (size_t)(T - 1) * E + e) + (double)g32 * (double)host_ld(mask + (size_t)(T - 1) * E + e);
+  double R = (double)r[(size_t)(T - 1) * E + e] + (double)g32 * (double)mask[(size_t)(T - 1) * E + e];
   y[(size_t)(T - 1) * E + e] = (float)R;
   adv[(size_t)(T - 1) * E + e] = (float)(R - (double)V[(size_t)(T - 1) * E + e]);
   const double gd = gamma;  // python float (float64)
   for (int t = T - 2; t >= 0; --t) {
     const size_t i = (size_t)t * E + e;
-    R = (double)host_ld(r + i) + (gd * R) * (double)host_ld(mask + i);
+    R = (double)r[i] + (gd * R) * (double)mask[i];
     y[i] = (float)R;
     adv[i] = (float)(R - (double)V[i]);
   }
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
   }
   __syncthreads();
   const float scale = sh_scale;
-  const float lr = host_ld(lr_dev);
+  const float lr = *lr_dev;  // host-written between launches: each dispatch's acquire makes it visible
   const float one_m_rho = 1.0f - decay;
 #pragma unroll
   for (int k = 0; k < V; ++k) {

@@ -622,8 +622,8 @@ __device__ __forceinline__ void row_return(const ReturnsSrc &rs, const float *__
   const int T = rs.T, E = rs.E;
   const int t = b / E, e = b - t * E, n = T - t;  // steps t .. T-1
   for (int k = threadIdx.x; k < n; k += 256) {
-    buf[2 * k] = host_ld(rs.r + (size_t)(t + k) * E + e);
-    buf[2 * k + 1] = host_ld(rs.mask + (size_t)(t + k) * E + e);
+    buf[2 * k] = rs.r[(size_t)(t + k) * E + e];
+    buf[2 * k + 1] = rs.mask[(size_t)(t + k) * E + e];
   }
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -130,6 +130,8 @@ class PAACLearner(ActorLearner):
         self.use_update_graph = bool(getattr(args, 'update_graph', True))
         self._graphs = None
         self._eager_updates = 0
+        self.summaries = None  # TensorBoard event files of the chief (manette_amd/summary.py)
+        self._logged_episodes = 0
 
     # ------------------------------------------------------------------------------------------
     def _start_runners(self):
@@ -505,6 +507,23 @@ class PAACLearner(ActorLearner):
         if self.lstm_bool:  # memory = zeros except memory[:, -1] = initial state (paac.py:109-112)
             self.nz_h.numpy()[0] = 4
 
+    def write_summaries(self):
+        """The reference's TensorBoard scalars of the last rollout + update (chief only):
+        rl/reward and rl/episode_length per finished episode (paac.py:191-199), then
+        rewards_per_episode/* and steps_per_episode/* (paac.py:65-77, :265-266)."""
+        if self.summaries is None:
+            if not self.is_chief:
+                return
+            from .summary import LearnerSummaries
+            self.summaries = LearnerSummaries(self.debugging_folder)
+        self.book.drain()
+        eps = self.book.episodes
+        self.summaries.episodes(eps[self._logged_episodes:])
+        self._logged_episodes = len(eps)
+        self.summaries.log_values(self.book.total_rewards, 'rewards_per_episode', self.global_step)
+        self.summaries.log_values(self.book.total_steps, 'steps_per_episode', self.global_step)
+        self.summaries.flush()
+
     def train(self):
         """Main actor learner loop (paac.py:86-297)."""
         self.start()
@@ -517,6 +536,7 @@ class PAACLearner(ActorLearner):
                 self.book.new_update()
                 self.rollout()
                 self.update()
+                self.write_summaries()
                 counter += 1
                 if counter % max(1, 2048 // self.emulator_counts) == 0:
                     torch.cuda.synchronize()
@@ -547,3 +567,6 @@ class PAACLearner(ActorLearner):
             if self.comm is not None:
                 self.comm.close()
                 self.comm = None
+            if self.summaries is not None:
+                self.summaries.close()
+                self.summaries = None

@@ -307,26 +307,123 @@ def test_preprocess_resized_bit_exact(depth):
         np.testing.assert_array_equal(got[e], preprocess.stack_update(prev[e], pushes, depth))
 
 
-def test_sample_distribution():
+EPSNEG = float(np.finfo(np.float32).epsneg)
+
+
+def _draw_probs(p):
+    """Distribution of the device draw (common.h draw_index): inverse CDF over (p_j - epsneg) for
+    j < n-1, the last category taking the remainder. With every p_j >= epsneg it is numpy's
+    multinomial(1, p - epsneg) of exploration_policy.py:108-116; a category below epsneg (where
+    the reference's numpy raises 'pvals < 0') gets no mass and eats into the next one's interval."""
+    p = np.asarray(p, np.float32)
+    cum = np.cumsum([np.float64(np.float32(x) - np.float32(EPSNEG)) for x in p[:-1]])
+    out = np.zeros(len(p))
+    m = 0.0
+    for j, c in enumerate(cum):
+        out[j] = max(0.0, min(c, 1.0) - m)
+        m = max(m, min(c, 1.0))
+    out[-1] = max(0.0, 1.0 - m)
+    return out
+
+
+def _chi2_ok(counts, probs, alpha=1e-4):
+    from scipy.stats import chi2
+    nz = probs > 0
+    assert counts[~nz].sum() == 0, 'a zero-probability category was drawn'
+    n = counts.sum()
+    exp = probs[nz] * n
+    stat = float(((counts[nz] - exp) ** 2 / exp).sum())
+    pval = chi2.sf(stat, max(int(nz.sum()) - 1, 1))
+    assert pval > alpha, (stat, pval, counts, exp)
+
+
+def _sample(pi, rep, seed, ctr, row0=0):
     from manette_amd.network import sample
-    B, A, R = 4096, 6, 3
-    rs = np.random.RandomState(0)
+    B = pi.shape[0]
+    a = torch.empty(B, dtype=torch.int32, device='cuda')
+    r = torch.empty(B, dtype=torch.int32, device='cuda')
+    sample(pi, rep, seed, ctr, a, r, row0=row0)
+    return a, r
+
+
+@pytest.mark.parametrize('A,R', [(6, 1), (18, 11), (9, 11)])
+def test_sample_chi_square_both_heads(A, R):
+    """Chi-square goodness of fit of both heads (A = 18 Seaquest, R = 11 FiGAR10) against the
+    reference's multinomial(1, p - epsneg) over 8 x 4096 draws; counters advance by one per call."""
+    B, K = 4096, 8
+    rs = np.random.RandomState(A * 100 + R)
     p = rs.dirichlet(np.ones(A)).astype(np.float32)
     q = rs.dirichlet(np.ones(R)).astype(np.float32)
     pi = torch.from_numpy(np.tile(p, (B, 1))).cuda()
     rep = torch.from_numpy(np.tile(q, (B, 1))).cuda()
     ctr = torch.zeros(B, dtype=torch.int64, device='cuda')
-    a = torch.empty(B, dtype=torch.int32, device='cuda')
-    r = torch.empty(B, dtype=torch.int32, device='cuda')
-    counts = np.zeros(A)
-    for _ in range(8):
-        sample(pi, rep, 1234, ctr, a, r)
-        counts += np.bincount(a.cpu().numpy(), minlength=A)
-    assert (ctr.cpu().numpy() == 8).all()
-    freq = counts / counts.sum()
-    assert np.abs(freq - p).max() < 0.01
-    ah = a.cpu().numpy()
-    assert ah.min() >= 0 and ah.max() < A and r.cpu().numpy().max() < R
+    ca, cr = np.zeros(A), np.zeros(R)
+    for _ in range(K):
+        a, r = _sample(pi, rep, 1234, ctr)
+        ca += np.bincount(a.cpu().numpy(), minlength=A)
+        cr += np.bincount(r.cpu().numpy(), minlength=R)
+    assert (ctr.cpu().numpy() == K).all()
+    _chi2_ok(ca, _draw_probs(p))
+    if R > 1:
+        _chi2_ok(cr, _draw_probs(q))
+    else:
+        assert cr[0] == B * K
+
+
+def test_sample_epsneg_and_last_category_remainder():
+    """Entries below float32 epsneg are never drawn (the reference's numpy raises on them); the
+    last category takes the remainder 1 - sum_{j<n-1}(p_j - epsneg), including the epsneg mass
+    the others give up; a near-one-hot row always draws its category."""
+    B, K = 4096, 8
+    p = np.array([0.5, 1e-9, 0.25, 0.0, 0.25 - 1e-9], np.float32)
+    p = p / p.sum()
+    q = np.array([1e-12, 1e-12, 1.0], np.float32)
+    pi = torch.from_numpy(np.tile(p, (B, 1))).cuda()
+    rep = torch.from_numpy(np.tile(q, (B, 1))).cuda()
+    ctr = torch.zeros(B, dtype=torch.int64, device='cuda')
+    ca = np.zeros(5)
+    for _ in range(K):
+        a, r = _sample(pi, rep, 77, ctr)
+        ca += np.bincount(a.cpu().numpy(), minlength=5)
+        assert (r.cpu().numpy() == 2).all()
+    probs = _draw_probs(p)
+    assert probs[1] == 0 and probs[3] == 0
+    _chi2_ok(ca, probs)
+    # a one-hot row: p = (1, 0, ..., 0) -> always category 0 (1 - epsneg > u for u < 1 - 2^-24)
+    oh = np.zeros((B, 6), np.float32)
+    oh[:, 0] = 1.0
+    a, _ = _sample(torch.from_numpy(oh).cuda(), rep, 5, torch.zeros(B, dtype=torch.int64, device='cuda'))
+    assert (a.cpu().numpy() == 0).mean() > 0.9999
+
+
+def test_sample_rows_independent_and_global_row_ids():
+    """Rows with the same pi draw independent streams (pairwise agreement = sum p^2); the draw is a
+    pure function of (seed, global row, counter): rows [8, 16) of a 16-row call with row0 = 0 ==
+    an 8-row call with row0 = 8 (a data-parallel rank's shard), and replaying the counters
+    reproduces the draws."""
+    A, R, B = 6, 11, 16
+    rs = np.random.RandomState(3)
+    p = rs.dirichlet(np.ones(A)).astype(np.float32)
+    q = rs.dirichlet(np.ones(R)).astype(np.float32)
+    pi = torch.from_numpy(np.tile(p, (B, 1))).cuda()
+    rep = torch.from_numpy(np.tile(q, (B, 1))).cuda()
+    ctr = torch.zeros(B, dtype=torch.int64, device='cuda')
+    full = [tuple(t.cpu().numpy() for t in _sample(pi, rep, 9, ctr)) for _ in range(300)]
+    ctr8 = torch.zeros(8, dtype=torch.int64, device='cuda')
+    half = [tuple(t.cpu().numpy() for t in _sample(pi[8:].contiguous(), rep[8:].contiguous(), 9, ctr8, row0=8))
+            for _ in range(300)]
+    for (fa, fr), (ha, hr) in zip(full, half):
+        np.testing.assert_array_equal(fa[8:], ha)
+        np.testing.assert_array_equal(fr[8:], hr)
+    ctr.zero_()
+    again = [tuple(t.cpu().numpy() for t in _sample(pi, rep, 9, ctr)) for _ in range(300)]
+    for (fa, fr), (ga, gr) in zip(full, again):
+        np.testing.assert_array_equal(fa, ga)
+        np.testing.assert_array_equal(fr, gr)
+    acts = np.stack([f[0] for f in full])  # [300][16]
+    agree = np.mean([np.mean(acts[:, i] == acts[:, j]) for i in range(B) for j in range(i + 1, B)])
+    expect = float((_draw_probs(p) ** 2).sum())
+    assert abs(agree - expect) < 0.02, (agree, expect)
 
 
 def test_zero_copy_reads_see_host_rewrites_across_launches():

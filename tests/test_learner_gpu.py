@@ -131,6 +131,12 @@ def test_train_cli_checkpoint_resume(tmp_path):
     assert 'Network/fc4/fc4_weights/OptimizerVariables' in o and 'Network/fc4/fc4_weights' not in o
     np.testing.assert_array_equal(o['Network/fc4/fc4_weights/OptimizerVariables'],
                                   z['Network/fc4/fc4_weights/OptimizerVariables'])
+    # TensorBoard event file of the run (actor_learner.py:82, paac.py:23-31): args text at step 0
+    from manette_amd import summary
+    evf = [f for f in os.listdir(df + 'tf') if f.startswith('events.out.tfevents.')]
+    assert evf
+    ev = summary.read_events(df + 'tf/' + evf[0])
+    assert ev[0][2] == {'file_version': 'brain.Event:2'} and '"arch": "NATURE"' in ev[1][2]['text']
     # resume: starts from step 200 and continues to 280
     cmd[cmd.index('--max_global_steps') + 1] = '280'
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
