@@ -115,6 +115,17 @@ int mt_forward_rows(const mt_net *net, const float *params, const uint8_t *obs, 
 int mt_forward_trunk(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                      size_t ws_bytes, mt_stream_t stream);
 
+/* The rollout chain's stacking trunk alone (roofline timing, parity tests): the NIPS conv kernel
+ * in its in-kernel-pull form — per env, wait until ready[e * MH_READY_STRIDE] >> 3 == tag (one
+ * 128-B line per env, manette_host.h), stack out = prev shifted by the push count (its low 3 bits)
+ * + that many final frames (frames = [4*batch][84][84][depth],
+ * env e's pushes at slots 4e..; host-mapped pinned staging or device memory) — then the dense
+ * layer's split-K partials, left in ws. With every ready word already set nothing waits: the
+ * kernels' own duration. NIPS only (MT_ERR_UNSUPPORTED otherwise). */
+int mt_forward_trunk_stacking(const mt_net *net, const float *params, const uint8_t *prev, const uint8_t *frames,
+                              const uint32_t *ready, uint32_t tag, uint8_t *out, int batch, void *ws, size_t ws_bytes,
+                              mt_stream_t stream);
+
 /* ---- LSTM frame-store mode (the learner's LSTM path; manette_amd/csrc/lstm.h) -------------
  * The reference feeds each step's memory window [E][5][84][84][C] (paac.py:79-83) and the train
  * step the T*E windows of whole_memory (paac.py:233-234); consecutive windows share 4 frames.

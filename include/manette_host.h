@@ -81,10 +81,13 @@ int mh_runner_step_end(mh_runner *r, int *total_pushes);
 
 /* Per-env ready words (fixed + resized staging only; ready = NULL turns them off): during the
  * following mh_runner_step calls, the worker that steps env e stages e's pushes and its push count
- * and then stores ready[e] = (value << 3) | push_count[e] (release), so a consumer polling ready[e]
- * (a GPU kernel reading pinned, device-mapped memory: mt_rollout_step's pull kernel) can take env
- * e while the other envs are still being emulated. Call before every step with that step's value
- * (compared modulo 2^29). */
+ * and then stores ready[e * MH_READY_STRIDE] = (value << 3) | push_count[e] (release), so a
+ * consumer polling that word (GPU kernels reading pinned, device-mapped memory: mt_rollout_step's
+ * conv / pull kernels) can take env e while the other envs are still being emulated. Call before
+ * every step with that step's value (compared modulo 2^29). Each env's word has a 128-B line of
+ * its own (ready holds E * MH_READY_STRIDE words): a line the emulator threads keep writing while
+ * hundreds of GPU pollers read it would bounce between the CPU caches and PCIe. */
+#define MH_READY_STRIDE 32
 int mh_runner_set_ready(mh_runner *r, uint32_t *ready, uint32_t value);
 
 /* In-place frames: the same macro-step (and reset), but no screen is copied. Per env e,

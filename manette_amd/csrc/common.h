@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "../../include/manette_hip.h"
+#include "../../include/manette_host.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -126,10 +127,51 @@ struct TrainRows {
 // mt_rollout_step's pull kernel).
 struct StackSrc {
   const uint8_t *prev;    // state slot t [B][84][84][C] (HBM)
-  const uint8_t *frames;  // device address of the pinned staging
-  const int32_t *count;   // push_count [B]; NULL: no pushes (out = a copy of prev)
+  const uint8_t *frames;  // the pushes' final frames: HBM, or the device address of the pinned staging
+  const int32_t *count;   // push_count [B]; NULL (and no ready words): no pushes (out = a copy of prev)
   uint8_t *out;           // state slot t + 1 (the forward's input)
+  // in-kernel pull (mt_rollout_step's stacking chain): env e's frames are read from the pinned
+  // staging itself once its emulator thread has published it, ready[e * MH_READY_STRIDE] =
+  // (tag << 3) | push count
+  // (device address of the host-mapped words, mh_runner_set_ready); bounded wait, status <- 1 on
+  // timeout. count is then unused.
+  const uint32_t *ready = nullptr;
+  uint32_t tag = 0;
+  uint32_t *status = nullptr;
 };
+
+// 16 bytes at byte offset `off` of a host-published buffer, where [lo, hi) is the byte range
+// published together with them: a chunk whose 128-B cache line also holds bytes outside that
+// range (published at another time, possibly after the line was fetched) is read with two
+// system-scope 8-byte loads, never served from a non-coherent cached line; any other chunk with a
+// plain 16-B load (its line is first touched after the publication; lines cached by an earlier
+// launch are dropped by each dispatch's system-scope acquire).
+__device__ __forceinline__ uint4 ld_published16(const uint8_t *base, size_t off, size_t lo, size_t hi) {
+  const size_t line = off & ~(size_t)127;
+  if (line >= lo && line + 128 <= hi) return *reinterpret_cast<const uint4 *>(base + off);
+  const uint64_t *p = reinterpret_cast<const uint64_t *>(base + off);
+  const uint64_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+}
+
+// Lane 0: wait (bounded, ~2 s of s_memrealtime at 100 MHz) for ready[e * MH_READY_STRIDE] >> 3 == tag
+// (one 128-B line per env, include/manette_host.h); returns the
+// push count (ready & 7), or -1 after recording a timeout in *status. System-scope relaxed polls
+// (they bypass the non-coherent caches) with s_sleep between them.
+__device__ __forceinline__ int wait_published(const uint32_t *ready, int e, uint32_t tag, uint32_t *status) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t v;
+  while (((v = __hip_atomic_load(ready + (size_t)e * MH_READY_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> 3) !=
+         tag) {
+    __builtin_amdgcn_s_sleep(8);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+      if (status) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return -1;
+    }
+  }
+  return (int)(v & 7u);
+}
 // forward (mt_forward) with the A3 draw fused into the heads kernel; smp, tr and st may be null.
 // st (NIPS inference only): the conv kernel first stacks the new state st->out (== obs) from
 // st->prev and the pushed frames (mt_preprocess_resized's op, fused into the forward).

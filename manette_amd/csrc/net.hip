@@ -1233,7 +1233,8 @@ extern "C" int mt_forward(const mt_net *net, const float *params, const uint8_t 
 // dense layer's partial slabs that heads_fwd_kernel finishes — the fused NIPS trunk, else the
 // layered convs + split-K fc (LSTM: the 5B-frame trunk + the cell's x-product slabs).
 template <class Ar>
-static int trunk_infer_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws, hipStream_t s) {
+static int trunk_infer_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws, hipStream_t s,
+                            const StackSrc *st = nullptr) {
   if constexpr (Ar::LSTM) {
     LstmWs X;
     const WsLayout L = lstm_ws_layout<Ar>(n, B, &X);
@@ -1247,11 +1248,15 @@ static int trunk_infer_impl(const mt_net *n, const float *P, const uint8_t *obs,
     const float *Wfc = P + n->off_fc;
     if constexpr (Ar::FUSED_SLABS > 0) {
       constexpr int C = LayerG<Ar, 0>::CIN;
-      MT_TRY((launch_nips_trunk<C>(obs, nullptr, B, P + n->off_conv[0], P + n->off_conv[1], Wfc,
+      MT_TRY((launch_nips_trunk<C>(obs, st, B, P + n->off_conv[0], P + n->off_conv[1], Wfc,
                                    n->cfg.activation, n->cfg.alpha_leaky, ws + L.act[1], nullptr, ws + L.fcslab, s)));
       MT_LAUNCHED();
       return MT_OK;
     } else {
+      if (st) {
+        set_error("stacking trunk is built for the NIPS arch only");
+        return MT_ERR_UNSUPPORTED;
+      }
       MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s)));
       return launch_gemm<TileFc>(LdRowMajor{layer_out<Ar, Ar::NCONV - 1>(ws, L), Ar::FLAT},
                                  LdColMajor{Wfc, Ar::F, -1}, EpSlab{ws + L.fcslab, B, Ar::F}, B, Ar::F, Ar::FLAT,
@@ -1271,6 +1276,30 @@ extern "C" int mt_forward_trunk(const mt_net *net, const float *params, const ui
       return MT_ERR_WORKSPACE;
     }
     return trunk_infer_impl<Ar>(net, params, obs, batch, (float *)ws, (hipStream_t)stream);
+  });
+  return MT_OK;
+}
+
+extern "C" int mt_forward_trunk_stacking(const mt_net *net, const float *params, const uint8_t *prev,
+                                         const uint8_t *frames, const uint32_t *ready, uint32_t tag, uint8_t *out,
+                                         int batch, void *ws, size_t ws_bytes, mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && prev && frames && ready && out && ws, "null argument");
+  MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
+  StackSrc st{prev, frames, nullptr, out};
+  st.ready = ready;
+  st.tag = tag & 0x1fffffffu;
+  MT_ARCH_SWITCH(net, {
+    const WsLayout L = ws_layout<Ar>(net, batch);
+    if (ws_bytes < L.total * sizeof(float)) {
+      set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
+      return MT_ERR_WORKSPACE;
+    }
+    if constexpr (Ar::LSTM) {
+      set_error("stacking trunk is built for the NIPS arch only");
+      return MT_ERR_UNSUPPORTED;
+    } else {
+      return trunk_infer_impl<Ar>(net, params, out, batch, (float *)ws, (hipStream_t)stream, &st);
+    }
   });
   return MT_OK;
 }

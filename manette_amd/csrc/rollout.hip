@@ -125,7 +125,8 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->meta_dev = (int32_t *)meta_dev;
   ro->pair_dev = (int32_t *)pair_dev;
   if (ro->pull) {
-    hipError_t e = hipHostMalloc((void **)&ro->env_ready_host, sizeof(uint32_t) * E, hipHostMallocMapped);
+    hipError_t e = hipHostMalloc((void **)&ro->env_ready_host, sizeof(uint32_t) * E * MH_READY_STRIDE,
+                                 hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostMalloc((void **)&ro->packed_host, sizeof(uint64_t) * E, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&ro->env_ready_dev, ro->env_ready_host, 0);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&ro->packed_dev, ro->packed_host, 0);
@@ -145,7 +146,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
       set_error("pinned step words: %s", hipGetErrorString(e));
       return MT_ERR_HIP;
     }
-    std::memset(ro->env_ready_host, 0, sizeof(uint32_t) * E);
+    std::memset(ro->env_ready_host, 0, sizeof(uint32_t) * E * MH_READY_STRIDE);
     std::memset(ro->packed_host, 0, sizeof(uint64_t) * E);
   }
   ro->ahead = ro->pull ? 2 : 1;
@@ -257,7 +258,8 @@ __global__ __launch_bounds__(256) void pull_frames_kernel(const uint4 *__restric
     if (threadIdx.x == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t v;
-      while (((v = __hip_atomic_load(ready + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> 3) != tag) {
+      while (((v = __hip_atomic_load(ready + (size_t)e * MH_READY_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >>
+              3) != tag) {
         __builtin_amdgcn_s_sleep(8);
         if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
           __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -306,13 +308,19 @@ int next_marks(mt_rollout *ro, const hipEvent_t **out) {
 // kernel (fused mt_preprocess_resized; ro->stack_fwd).
 // t == 0 && stacked: slot 0 <- slot T of the previous rollout inside the forward (the copy of
 // paac.py's states carrying over, otherwise a separate copy on the update's critical path).
-int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, bool stacked = false) {
+int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, bool stacked = false,
+                    uint32_t want = 0) {
   const mt_rollout_buffers &b = ro->b;
   const int E = ro->E, T = ro->T;
   const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
-  const StackSrc st = t > 0 ? StackSrc{b.states + (size_t)(t - 1) * slot, ro->frames_hbm, ro->count_hbm,
-                                       b.states + (size_t)t * slot}
-                            : StackSrc{b.states + (size_t)T * slot, nullptr, nullptr, b.states};
+  // t > 0: the conv kernel pulls step t-1's pushes itself (ready words tagged `want`)
+  StackSrc st = t > 0 ? StackSrc{b.states + (size_t)(t - 1) * slot, ro->staging_dev, nullptr, b.states + (size_t)t * slot}
+                      : StackSrc{b.states + (size_t)T * slot, nullptr, nullptr, b.states};
+  if (t > 0) {
+    st.ready = ro->env_ready_dev;
+    st.tag = want & 0x1fffffffu;
+    st.status = ro->status_dev;
+  }
   int32_t *a_d = b.idx + (size_t)t * E, *r_d = b.idx + (size_t)T * E + (size_t)t * E;
   SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
   smp.ready = ro->ready_dev;
@@ -373,11 +381,11 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
   // mt_preprocess_resized
   const bool stk = ro->stack_fwd && (k < T || b.v_boot);
   if (ro->pull) {
-    hipLaunchKernelGGL(pull_frames_kernel, dim3((E + kPullEnvs - 1) / kPullEnvs), dim3(256), 0, s,
-                       reinterpret_cast<const uint4 *>(ro->staging_dev), ro->env_ready_dev, want, ro->status_dev, E,
-                       (int)(84 * 84 * ro->depth / 16), reinterpret_cast<uint4 *>(ro->frames_hbm), ro->count_hbm);
-    MT_LAUNCHED();
-    if (!stk) {
+    if (!stk) {  // (the stacking conv kernel pulls each env itself)
+      hipLaunchKernelGGL(pull_frames_kernel, dim3((E + kPullEnvs - 1) / kPullEnvs), dim3(256), 0, s,
+                         reinterpret_cast<const uint4 *>(ro->staging_dev), ro->env_ready_dev, want, ro->status_dev, E,
+                         (int)(84 * 84 * ro->depth / 16), reinterpret_cast<uint4 *>(ro->frames_hbm), ro->count_hbm);
+      MT_LAUNCHED();
       const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
       MT_TRY_(mt_preprocess_resized(ro->frames_hbm, ro->count_hbm + E, ro->count_hbm, E, ro->depth,
                                     b.states + (size_t)(k - 1) * slot, b.states + (size_t)k * slot, (mt_stream_t)s));
@@ -388,11 +396,14 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
     MT_TRY_(enqueue_preprocess(ro, k - 1, 4 * E, s));
   }
   if (k < T) {
-    MT_TRY_(enqueue_forward(ro, params, k, s, stk));
+    MT_TRY_(enqueue_forward(ro, params, k, s, stk, want));
   } else if (b.v_boot) {  // bootstrap V(s_T), no draw, no train rows
     const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
     const size_t po = b.train_ws ? (size_t)T * E : 0;
-    const StackSrc st{b.states + (size_t)(T - 1) * slot, ro->frames_hbm, ro->count_hbm, b.states + (size_t)T * slot};
+    StackSrc st{b.states + (size_t)(T - 1) * slot, ro->staging_dev, nullptr, b.states + (size_t)T * slot};
+    st.ready = ro->env_ready_dev;
+    st.tag = want & 0x1fffffffu;
+    st.status = ro->status_dev;
     MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)T * slot, E, b.ws, b.ws_bytes, b.v_boot,
                            b.pi + po * ro->A, b.rep + po * ro->R, nullptr, true, s, nullptr, stk ? &st : nullptr));
   }

@@ -142,7 +142,7 @@ struct mh_runner {
   int32_t *frame_idx = nullptr;  // in-place mode: [E][8] bank frame indices (else null)
   float *reward = nullptr, *over = nullptr;
   // per-env ready words (fixed slots): env i's staging + push count are complete once
-  // ready[i] == (ready_value << 3) | push count (mh_runner_set_ready); the GPU pulls env i while
+  // ready[i * MH_READY_STRIDE] == (ready_value << 3) | push count (mh_runner_set_ready); the GPU pulls env i while
   // the others are still being emulated
   uint32_t *ready = nullptr;
   uint32_t ready_value = 0;
@@ -200,7 +200,8 @@ struct mh_runner {
         if (per_env) {  // stage env i now and publish it (sfence: the streaming stores first)
           stage_env(i);
           _mm_sfence();
-          __atomic_store_n(ready + i, (ready_value << 3) | (uint32_t)std::min(e.npush, 4), __ATOMIC_RELEASE);
+          __atomic_store_n(ready + (size_t)i * MH_READY_STRIDE, (ready_value << 3) | (uint32_t)std::min(e.npush, 4),
+                           __ATOMIC_RELEASE);
         }
       }
       if (per_env) return;

@@ -10,10 +10,12 @@
 //    writes those 288 activations to act2 [B][2592] (NHWC flatten order).
 //    STACK variant (the pipelined rollout, resized staging): the block also does the A2 stacking
 //    of mt_preprocess_resized (atari_emulator.py:79-124, environment.py:42-80) for its rows — the
-//    previous state's rows from HBM and the env's p new final frames read in place from pinned
-//    host staging (fixed slots 4e + j), stacked in LDS, the block's own rows (8i..8i+7; the last
-//    block 64..83) written to the new state slot — so no separate preprocess launch sits on the
-//    step's critical path.
+//    previous state's rows from HBM and the env's p new final frames, stacked in LDS, the block's
+//    own rows (8i..8i+7; the last block 64..83) written to the new state slot — so no separate
+//    preprocess launch sits on the step's critical path. With ready words (in-kernel pull, the
+//    rollout chain) each block waits for ITS env's publication by the emulator thread and reads
+//    the frames from the pinned staging itself: an env's convs run while the later envs are still
+//    being emulated, with no pull kernel and no kernel boundary in front of them.
 // 2. nips_fc_kernel — the dense layer as a real GEMM: block = (16 output columns, conv2 row i,
 //    32 envs); slab[i][e][n] = sum_{f < 288} act2[e][288 i + f] Wfc[288 i + f][n] on MFMA. Each
 //    fc weight is read once per 32 envs (the former one-launch trunk streamed the row's 295 KB
@@ -99,24 +101,41 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
       uint4 *dst = reinterpret_cast<uint4 *>(xin);
       for (int q = threadIdx.x; q < Fz::IN_BYTES / 16; q += Fz::NT) dst[q] = src[q];
     }
-    // one round trip for the common case: the push count and push 0's rows with the prev rows
-    // (count == NULL: no pushes, the new state is a copy of prev — slot 0 <- slot T of the
-    // previous rollout, mt_rollout_step)
-    if (threadIdx.x == 0) s_p = st.count ? st.count[e] : 0;
-    if (st.count) {
-      const size_t f0 = ((size_t)4 * e * 84 + 8 * i) * 84 * Fz::D;  // push 0 = slot 4e
-      const uint4 *fs = reinterpret_cast<const uint4 *>(st.frames + f0);
-      for (int q = threadIdx.x; q < Fz::FR_BYTES / 16; q += Fz::NT) reinterpret_cast<uint4 *>(fr)[q] = fs[q];
-    }
-    __syncthreads();
-    const int p = st.count ? min(max(s_p, 1), 4) : 0;
-    if (p > 1) {  // FiGAR repeats: pushes 1..p-1 (slots 4e+1..)
-      for (int q = threadIdx.x; q < (p - 1) * (Fz::FR_BYTES / 16); q += Fz::NT) {
-        const int j = 1 + q / (Fz::FR_BYTES / 16), qq = q - (j - 1) * (Fz::FR_BYTES / 16);
-        const size_t fj = (((size_t)4 * e + j) * 84 + 8 * i) * 84 * Fz::D;
-        reinterpret_cast<uint4 *>(fr + j * Fz::FR_BYTES)[qq] = reinterpret_cast<const uint4 *>(st.frames + fj)[qq];
+    int p;
+    if (st.ready) {
+      // in-kernel pull: wait for env e's publication, then read its p pushes' rows 8i..8i+19
+      // from the pinned staging (slots 4e + j) in one round trip; the edge lines of env e's slot
+      // group are read with system-scope loads (ld_published16)
+      if (threadIdx.x == 0) s_p = wait_published(st.ready, e, st.tag, st.status);
+      __syncthreads();
+      p = min(max(s_p, 0), 4);  // (a timeout stacks no frame; the host reports the error)
+      const size_t F = (size_t)84 * 84 * Fz::D, lo = 4 * e * F, hi = lo + 4 * F;
+      for (int q = threadIdx.x; q < p * (Fz::FR_BYTES / 16); q += Fz::NT) {
+        const int j = q / (Fz::FR_BYTES / 16), qq = q - j * (Fz::FR_BYTES / 16);
+        const size_t off = (((size_t)4 * e + j) * 84 + 8 * i) * 84 * Fz::D + 16 * (size_t)qq;
+        reinterpret_cast<uint4 *>(fr + j * Fz::FR_BYTES)[qq] = ld_published16(st.frames, off, lo, hi);
       }
       __syncthreads();
+    } else {
+      // one round trip for the common case: the push count and push 0's rows with the prev rows
+      // (count == NULL: no pushes, the new state is a copy of prev — slot 0 <- slot T of the
+      // previous rollout, mt_rollout_step)
+      if (threadIdx.x == 0) s_p = st.count ? st.count[e] : 0;
+      if (st.count) {
+        const size_t f0 = ((size_t)4 * e * 84 + 8 * i) * 84 * Fz::D;  // push 0 = slot 4e
+        const uint4 *fs = reinterpret_cast<const uint4 *>(st.frames + f0);
+        for (int q = threadIdx.x; q < Fz::FR_BYTES / 16; q += Fz::NT) reinterpret_cast<uint4 *>(fr)[q] = fs[q];
+      }
+      __syncthreads();
+      p = st.count ? min(max(s_p, 1), 4) : 0;
+      if (p > 1) {  // FiGAR repeats: pushes 1..p-1 (slots 4e+1..)
+        for (int q = threadIdx.x; q < (p - 1) * (Fz::FR_BYTES / 16); q += Fz::NT) {
+          const int j = 1 + q / (Fz::FR_BYTES / 16), qq = q - (j - 1) * (Fz::FR_BYTES / 16);
+          const size_t fj = (((size_t)4 * e + j) * 84 + 8 * i) * 84 * Fz::D;
+          reinterpret_cast<uint4 *>(fr + j * Fz::FR_BYTES)[qq] = reinterpret_cast<const uint4 *>(st.frames + fj)[qq];
+        }
+        __syncthreads();
+      }
     }
     // word w of the rows = channels 4c..4c+3 of pixel (r, x), c < D: byte offset 4w in the state
     // rows and byte w in each frame's rows (C = 4D). Same op as preprocess_kernel<D, kSrcFinal>.

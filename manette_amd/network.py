@@ -171,6 +171,16 @@ class DeviceNetwork(object):
         check(_lib.hip().mt_forward_trunk(self._h, _ptr(self.params), _ptr(obs), int(batch), _ptr(ws), ws.numel(),
                                           _stream()), 'mt_forward_trunk')
 
+    def forward_trunk_stacking(self, prev, frames, ready, tag, out, batch, ws_key=None):
+        """mt_forward_trunk_stacking: the rollout chain's stacking trunk (in-kernel pull of each
+        env's frames behind its ready word), diagnostics / parity / roofline timing."""
+        ws = self.workspace(batch, ws_key)
+        addr = lambda x: x if isinstance(x, C.c_void_p) else _ptr(x)
+        check(_lib.hip().mt_forward_trunk_stacking(self._h, _ptr(self.params), _ptr(prev), addr(frames), addr(ready),
+                                                   C.c_uint32(tag), _ptr(out), int(batch), _ptr(ws), ws.numel(),
+                                                   _stream()), 'mt_forward_trunk_stacking')
+        return ws
+
     # ---- LSTM frame-store mode (include/manette_hip.h, mt_lstm_*) -------------------------------
     def lstm_workspace(self, E, T):
         n = C.c_size_t()

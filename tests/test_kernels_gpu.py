@@ -456,3 +456,40 @@ def test_zero_copy_reads_see_host_rewrites_across_launches():
         for e in range(E):
             pushes = [f[4 * e + j] for j in range(counts_h[e])]
             np.testing.assert_array_equal(got[e], preprocess.stack_update(pv[e], pushes, depth), err_msg='round %d' % it)
+
+
+@pytest.mark.parametrize('E,depth', [(7, 1), (32, 1), (5, 3)])
+def test_stacking_trunk_in_kernel_pull(E, depth):
+    """mt_forward_trunk_stacking — the rollout chain's conv kernel pulling each env's frames from
+    pinned host staging behind its ready word (edge cache lines read with system-scope loads):
+    the stacked state == the A2 oracle (bit-exact), and the trunk outputs (act2 + dense partial
+    slabs) == mt_forward_trunk on that state, bit for bit."""
+    from manette_amd.network import host_device_pointer
+    import ctypes as C
+    net = _net('NIPS', depth, 6, 11, seed=E)
+    rs = np.random.RandomState(30 + E + depth)
+    counts = rs.randint(1, 5, E).astype(np.int32)
+    counts[:2] = 4  # full slot groups: their last line borders the next env's first
+    frames = torch.zeros(4 * E, 84, 84, depth, dtype=torch.uint8).pin_memory()
+    frames.numpy()[...] = rs.randint(0, 256, size=frames.shape).astype(np.uint8)
+    tag = 12345
+    ready = torch.zeros(E, 32, dtype=torch.int32).pin_memory()  # MH_READY_STRIDE words per env
+    ready.numpy()[:, 0] = (tag << 3) | counts
+    prev_h = rs.randint(0, 256, size=(E, 84, 84, 4 * depth)).astype(np.uint8)
+    prev = torch.from_numpy(prev_h).cuda()
+    out = torch.zeros_like(prev)
+    ws = net.workspace(E, 'stk')
+    ws.zero_()
+    net.forward_trunk_stacking(prev, C.c_void_p(host_device_pointer(frames)), C.c_void_p(host_device_pointer(ready)),
+                               tag, out, E, ws_key='stk')
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    f = frames.numpy()
+    for e in range(E):
+        pushes = [f[4 * e + j] for j in range(counts[e])]
+        np.testing.assert_array_equal(got[e], preprocess.stack_update(prev_h[e], pushes, depth), err_msg='env %d' % e)
+    ws2 = net.workspace(E, 'plain')
+    ws2.zero_()
+    net.forward_trunk(out, E, ws_key='plain')
+    torch.cuda.synchronize()
+    assert torch.equal(ws[:ws2.numel()], ws2)
