@@ -41,13 +41,14 @@ MI355X_FP32_TFLOPS = 157.3   # dense fp32 (vector = MFMA), MI355X_MICROARCH.md
 MI355X_HBM_GBS = 8000.0      # HBM3E peak, MI355X_MICROARCH.md
 
 
-def load_pmc(config, kernels):
-    """HBM bytes per mt_forward_trunk call (the sum over its kernels of bytes per launch) from the
-    committed PMC summary of this workload (profiles/pmc_<config>.json, written by tools/pmc.sh +
-    tools/pmc_summary.py), or None when a kernel is missing from it."""
+def load_pmc(config, kernels, name='pmc_trunk_%s.json'):
+    """HBM bytes per roofline launch (the sum over its kernels of bytes per launch) from the
+    committed PMC summary of this workload's roofline launch (profiles/pmc_trunk_<config>.json,
+    written by tools/pmc_trunk.sh + tools/pmc_summary.py on tools/trunk_only.py: the same
+    kernels, grid and inputs bench.py times), or None when a kernel is missing from it."""
     if not kernels:
         return None
-    path = os.path.join(ROOT, 'profiles', 'pmc_%s.json' % config)
+    path = os.path.join(ROOT, 'profiles', name % config)
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
@@ -57,7 +58,7 @@ def load_pmc(config, kernels):
         if not hit:
             return None
         total += hit[0]['hbm_bytes']
-    return dict(hbm_bytes=total, source='profiles/pmc_%s.json' % config)
+    return dict(hbm_bytes=total, source='profiles/' + name % config)
 
 
 def conv_out(h, k, s):
@@ -324,14 +325,32 @@ def main():
     e_ev.record()
     torch.cuda.synchronize()
     prof['train_pass'] = [s_ev.elapsed_time(e_ev) / 20.0]
-    # (3) supplementary, isolated: the rollout-batch forward (E rows) and its trunk half
-    #     (mt_forward_trunk: NIPS = the non-stacking conv kernel + the dense kernel) back to back,
-    #     HIP events on the stream they are launched on (torch's current stream)
+    # (3) the trunk kernels back to back, HIP events on the stream they are launched on (torch's
+    #     current stream), 40 launches between one event pair: the stacking rollout chain's kernels
+    #     (NIPS: mt_forward_trunk_stacking = the in-kernel-pull conv kernel + the dense kernel, with
+    #     every env's ready word already set and its pushes resident in HBM, so nothing waits),
+    #     else mt_forward_trunk; and the whole rollout-batch forward (E rows, with the heads)
     E = cfg['ec']
     net = learner.network
+    stacking = getattr(learner, 'slot0_in_rollout', False)
     if learner.lstm_bool:  # a step's new frames (trunk + cell x-product), + its E windows
         roll_fwd = lambda: learner._lstm_forward(1, learner.v_boot)
         roll_trunk = lambda: net.lstm_frames_forward(learner.fstore, 1 + 5 * E, E, E, T)
+    elif stacking:
+        depth_ = 3 if cfg['rgb'] else 1
+        gen = torch.Generator(device='cuda').manual_seed(11)
+        pushes = torch.randint(0, 256, (4 * E, 84, 84, depth_), dtype=torch.uint8, device='cuda', generator=gen)
+        counts = torch.ones(E, dtype=torch.int32) if cfg['max_repetition'] == 0 else \
+            torch.from_numpy(np.random.RandomState(5).randint(1, 5, E).astype(np.int32))
+        ready = torch.zeros(E, 32, dtype=torch.int32)  # MH_READY_STRIDE words per env
+        ready[:, 0] = (7 << 3) | counts
+        stack_pushes = int(counts.sum())
+        ready = ready.cuda()
+        stk_out = torch.empty_like(learner.states[0])
+        roll_fwd = lambda: net.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
+                                       ws_key='rollout', infer=True)
+        roll_trunk = lambda: net.forward_trunk_stacking(learner.states[0], pushes, ready, 7, stk_out, E,
+                                                        ws_key='rollout')
     else:
         roll_fwd = lambda: net.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
                                        ws_key='rollout', infer=True)
@@ -404,15 +423,23 @@ def main():
         tk_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in trunk) + 4 * ec * out_floats
         tk_flops = ec * sum(l[1] for l in trunk)
         C_in = 4 * depth
-        stacking = learner is not None and getattr(learner, 'slot0_in_rollout', False)
-        if inloop_us is not None:
+        if stacking:  # + the fused A2 stacking: the pushes read and the new state written
+            tk_bytes += int(stack_pushes) * 84 * 84 * depth + ec * 84 * 84 * 4 * depth
+            # the rollout chain's own kernels; in the loop each conv block also waits for its env's
+            # emulator (in-kernel pull), so the roofline times them with every env published
+            tk_ms = iso_ms
+            kern = 'nips_conv_kernel<%d, true> (in-kernel pull) + nips_fc_kernel<%d>: the stacking rollout chain' % (
+                C_in, C_in)
+            timing = ('40 mt_forward_trunk_stacking calls back to back between one HIP event pair, every env '
+                      'published and its pushes in HBM (the kernels the timed loop runs; there the conv blocks '
+                      'also wait for their env: trunk_in_loop)')
+            pmc_kernels = ['nips_conv_kernel<%d, true>' % C_in, 'nips_fc_kernel<%d>' % C_in]
+        elif inloop_us is not None:
             tk_ms = inloop_us * 1e-3
-            kern = ('nips_conv_kernel<%d, true> + nips_fc_kernel<%d> (stacking rollout chain)' % (C_in, C_in)
-                    if stacking else 'trunk kernels of the rollout forward (implicit-GEMM convs + split-K dense)')
+            kern = 'trunk kernels of the rollout forward (implicit-GEMM convs + split-K dense)'
             timing = 'in the timed loop: HIP event pair around each macro-step forward\'s trunk launches ' \
                      '(mt_rollout_trunk_timing), %d updates after the timed region' % a.measure_updates
-            pmc_kernels = (['nips_conv_kernel<%d, true>' % C_in, 'nips_fc_kernel<%d>' % C_in]
-                           if stacking else None)
+            pmc_kernels = None
         else:
             tk_ms = iso_ms
             kern = 'mt_forward_trunk (%s)' % ('LSTM frame trunk + cell x-product' if lstm else 'layered')
@@ -455,8 +482,12 @@ def main():
                 us_per_launch=round(tk_ms * 1e3, 2), hbm_gbs=round(tk_gbs, 1),
                 hbm_frac=round(tk_gbs / MI355X_HBM_GBS, 4), flop_frac=round(tk_tf / MI355X_FP32_TFLOPS, 4),
                 traffic_source=pmc['source'] if pmc else None),
-            'trunk_isolated': {'kernel': 'mt_forward_trunk, back to back', 'us_per_launch': round(iso_ms * 1e3, 2),
-                               'tflops': round(tk_flops / (iso_ms * 1e-3) / 1e12, 3)},
+            'trunk_in_loop': None if inloop_us is None else {
+                'us_per_forward': round(inloop_us, 2),
+                'note': 'event pair around each macro-step forward\'s trunk launches in the timed loop '
+                        '(mt_rollout_trunk_timing, %d updates after the timed region)%s' % (
+                            a.measure_updates, '; includes the conv blocks\' wait for their env\'s emulator '
+                            '(in-kernel pull)' if stacking else '')},
             'train_pass': {'bound': 'mfma', 'kernels': ('backward of %d windows over %d distinct frames (forward reused from the rollout)' % (N, 1 + (T + 4) * ec)) if lstm else 'fused returns + loss + backward of %d rows (forward reused from the rollout)' % N,
                            'flop_count': 'executed backward: dW of every layer + dX of every layer but conv1',
                            'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',

@@ -230,7 +230,10 @@ static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
 // at most kWgradChunks BK-chunks (each chunk is one load latency: with only M x N / 1024 MFMA
 // tiles per wave the chunk chain, not the MFMA, sets a block's time), capped so the partial slabs
 // stay <= kSlabFloats.
-constexpr int kWgradChunks = 4;
+#ifndef MT_WGRAD_CHUNKS
+#define MT_WGRAD_CHUNKS 4
+#endif
+constexpr int kWgradChunks = MT_WGRAD_CHUNKS;
 constexpr size_t kSlabFloats = (size_t)4 << 20;
 template <class G>
 static int conv_wgrad_splits(int B) {

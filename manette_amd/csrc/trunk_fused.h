@@ -107,6 +107,7 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
       // from the pinned staging (slots 4e + j) in one round trip; the edge lines of env e's slot
       // group are read with system-scope loads (ld_published16)
       if (threadIdx.x == 0) s_p = wait_published(st.ready, e, st.tag, st.status);
+      MT_PROBE_AT(0, blockIdx.x, 5);  // env e seen published
       __syncthreads();
       p = min(max(s_p, 0), 4);  // (a timeout stacks no frame; the host reports the error)
       const size_t F = (size_t)84 * 84 * Fz::D, lo = 4 * e * F, hi = lo + 4 * F;

@@ -20,7 +20,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PHASES = {0: ('conv', ['stage', 'conv1', 'conv2', 'act2']),
+PHASES = {0: ('conv', ['stage (incl. wait)', 'conv1', 'conv2', 'act2']),
           1: ('fc', ['load+mfma', 'reduce+store']),
           2: ('heads', ['slab sum', 'heads gemv', 'softmax+draw+flag'])}
 
@@ -69,13 +69,20 @@ def main():
     nblocks = {0: 9 * E, 1: 16 * 9 * ((E + 31) // 32), 2: E}
     t0 = P[0, :nblocks[0], 0].min()
     us = lambda x: x * 0.01  # 100 MHz ticks
-    seen, done = R[:, 0] - t0, R[:, 1] - t0
-    pstart = R[::4, 2] - t0
-    print('pull   per env: seen / done (us):', ' '.join('%d:%.1f/%.1f' % (e, us(seen[e]), us(done[e])) for e in range(E)))
-    print('pull   start %+7.2f us (after the previous heads kernel), env words seen %+7.2f..%+7.2f us '
-          '(median %+7.2f), copies done ..%+7.2f us, copy med %.2f us' % (
-              us(pstart.min()), us(seen.min()), us(seen.max()), us(np.median(seen)), us(done.max()),
-              us(np.median(done - seen))))
+    if R[:, 0].any():  # a pull kernel ran (non-stacking chains)
+        seen, done = R[:, 0] - t0, R[:, 1] - t0
+        pstart = R[::4, 2] - t0
+        print('pull   per env: seen / done (us):', ' '.join('%d:%.1f/%.1f' % (e, us(seen[e]), us(done[e])) for e in range(E)))
+        print('pull   start %+7.2f us (after the previous heads kernel), env words seen %+7.2f..%+7.2f us '
+              '(median %+7.2f), copies done ..%+7.2f us, copy med %.2f us' % (
+                  us(pstart.min()), us(seen.min()), us(seen.max()), us(np.median(seen)), us(done.max()),
+                  us(np.median(done - seen))))
+    pub = P[0, :nblocks[0], 5]
+    if pub.any():  # in-kernel pull: when each conv block saw its env published (blockIdx order)
+        pub = pub - t0
+        print('conv   env published seen (us, per block): min %+7.2f median %+7.2f max %+7.2f; '
+              'last block end - last seen %.2f us' % (us(pub.min()), us(np.median(pub)), us(pub.max()),
+                                                     us(P[0, :nblocks[0], 4].max() - t0 - pub.max())))
     prev_end = None
     for k in (0, 1, 2):
         name, ph = PHASES[k]
