@@ -80,10 +80,26 @@ __device__ __forceinline__ void lds_put(float *L, int rr, int kk, f32x4 v) {
 }
 
 // Stage of one operand: registers for one chunk.
+// A thread's items keep their row (or row quad) for the whole K walk, only k advances, so each
+// loader splits its address math into a per-row context (the row -> (image, pixel) or
+// (tap, channel) decomposition, computed once per tile in init) and the per-k remainder
+// (fetch_ctx): the integer divisions of an implicit im2col run once, not once per chunk.
 template <class LD, int ROWS, int BK>
 struct Stage {
   using S = LdsShape<LD::KMAJOR, ROWS, BK>;
   f32x4 r[S::ITEMS];
+  typename LD::Ctx cx[S::ITEMS];
+  __device__ __forceinline__ void init(const LD &ld, int row0) {
+#pragma unroll
+    for (int i = 0; i < S::ITEMS; ++i) {
+      const int it = threadIdx.x + i * 256;
+      if (S::QUADS % 256 == 0 || it < S::QUADS) {
+        int rr, kk;
+        item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
+        cx[i] = ld.ctx(row0 + rr);
+      }
+    }
+  }
   // Interior tiles (uniform per workgroup) take the branch-free fetch: every load of the chunk
   // is issued back to back and waited for once (a per-element guarded load would make hipcc
   // wait vmcnt(0) per element — cdna_hip_programming.md §5 trap (c)).
@@ -95,7 +111,7 @@ struct Stage {
         if (S::QUADS % 256 == 0 || it < S::QUADS) {
           int rr, kk;
           item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
-          r[i] = ld.fetch_fast(row0 + rr, k0 + kk);
+          r[i] = ld.fetch_ctx(cx[i], k0 + kk);
         }
       }
     } else {
@@ -150,6 +166,8 @@ __device__ __forceinline__ void gemm_body(const LA &la, const LB &lb, const EP &
 
   Stage<LA, T::BM, T::BK> sa;
   Stage<LB, T::BN, T::BK> sb;
+  sa.init(la, m0);
+  sb.init(lb, n0);
   if (kb < ke) {
     sa.load(la, m0, kb, ke, M);
     sb.load(lb, n0, kb, ke, N);
@@ -321,7 +339,8 @@ inline int launch_group(hipStream_t s, const J1 &j1, const J2 &j2 = NoJob{}, con
 // ------------------------------------------------------------------------------------------
 // Loaders: fetch(row0, rr, k0, kk, ke, nrows) returns the 4 values of item (row0+rr, k0+kk)
 // — 4 consecutive k (KMAJOR) or 4 consecutive rows (!KMAJOR) — zero outside
-// [0, nrows) x [.., ke).
+// [0, nrows) x [.., ke); interior tiles use ctx(row) once per tile and fetch_ctx(ctx, k) per
+// chunk (Stage).
 // ------------------------------------------------------------------------------------------
 
 // Dense row-major operand X[row][k] (k contiguous, leading dim ld), fp32. KMAJOR.
@@ -332,8 +351,12 @@ struct LdRowMajor {
   __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
     return row0 + rows <= nrows && k0 + bk <= ke;
   }
-  __device__ __forceinline__ f32x4 fetch_fast(int row, int k) const {
-    return *reinterpret_cast<const f32x4 *>(X + (size_t)row * ld + k);
+  struct Ctx {
+    const float *p;
+  };
+  __device__ __forceinline__ Ctx ctx(int row) const { return {X + (size_t)row * ld}; }
+  __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int k) const {
+    return *reinterpret_cast<const f32x4 *>(c.p + k);
   }
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
     const int row = row0 + rr, k = k0 + kk;
@@ -365,8 +388,12 @@ struct LdColMajor {
     const int nx = ones_row >= 0 ? ones_row : nrows;
     return row0 + rows <= nx && k0 + bk <= ke && (ld & 3) == 0;
   }
-  __device__ __forceinline__ f32x4 fetch_fast(int row, int k) const {
-    return *reinterpret_cast<const f32x4 *>(X + (size_t)k * ld + row);
+  struct Ctx {
+    const float *p;
+  };
+  __device__ __forceinline__ Ctx ctx(int row) const { return {X + row}; }
+  __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int k) const {
+    return *reinterpret_cast<const f32x4 *>(c.p + (size_t)k * ld);
   }
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
     const int row = row0 + rr, k = k0 + kk;
@@ -429,28 +456,36 @@ template <class G, bool U8>
 struct LdIm2col {
   static constexpr bool KMAJOR = true;
   const typename InElem<U8>::T *X;
-  // k >= KK (a BK that does not divide KK) is zeroed inside fetch_fast, so only the rows decide.
+  // k >= KK (a BK that does not divide KK) is zeroed inside fetch_ctx, so only the rows decide.
   __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
     return row0 + rows <= nrows && (k0 + bk <= ke || ke == G::KK);
   }
-  // Padding (SAME) and the k tail handled branch-free: clamped address, zero by select.
-  __device__ __forceinline__ f32x4 fetch_fast(int m, int k) const {
-    const bool kok = k < G::KK;
-    k = kok ? k : 0;
+  // Row context: the image of output pixel m and its window's top-left input pixel.
+  struct Ctx {
+    const typename InElem<U8>::T *img;
+    int iy0, ix0;
+  };
+  __device__ __forceinline__ Ctx ctx(int m) const {
     const int b = m / (G::OH * G::OW);
     const int rem = m - b * (G::OH * G::OW);
     const int oy = rem / G::OW, ox = rem - oy * G::OW;
+    return {X + (size_t)b * G::H * G::W * G::CIN, oy * G::S - G::PT, ox * G::S - G::PL};
+  }
+  // Padding (SAME) and the k tail handled branch-free: clamped address, zero by select.
+  __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int k) const {
+    const bool kok = k < G::KK;
+    k = kok ? k : 0;
     const int ky = k / (G::KW * G::CIN);
     const int r2 = k - ky * (G::KW * G::CIN);
     const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
-    const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
+    const int iy = c.iy0 + ky, ix = c.ix0 + kx;
     if constexpr (G::SAME) {
       const bool ok = kok && iy >= 0 && iy < G::H && ix >= 0 && ix < G::W;
       const int iyc = min(max(iy, 0), G::H - 1), ixc = min(max(ix, 0), G::W - 1);
-      const f32x4 v = InElem<U8>::load4(X + (((size_t)b * G::H + iyc) * G::W + ixc) * G::CIN + ci);
+      const f32x4 v = InElem<U8>::load4(c.img + ((size_t)iyc * G::W + ixc) * G::CIN + ci);
       return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     } else {
-      const f32x4 v = InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
+      const f32x4 v = InElem<U8>::load4(c.img + ((size_t)iy * G::W + ix) * G::CIN + ci);
       return kok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
@@ -480,21 +515,28 @@ struct LdIm2colT {
   __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
     return row0 + rows <= G::KK && k0 + bk <= ke;  // the bias-row tile takes the guarded path
   }
-  __device__ __forceinline__ f32x4 fetch_fast(int kr, int m) const {
+  // Row context: the tap (ky - PT, kx - PL) and channel of weight row quad kr.
+  struct Ctx {
+    int dy, dx, ci;
+  };
+  __device__ __forceinline__ Ctx ctx(int kr) const {
+    const int ky = kr / (G::KW * G::CIN);
+    const int r2 = kr - ky * (G::KW * G::CIN);
+    const int kx = r2 / G::CIN;
+    return {ky - G::PT, kx - G::PL, r2 - kx * G::CIN};
+  }
+  __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int m) const {
     const int b = m / (G::OH * G::OW);
     const int rem = m - b * (G::OH * G::OW);
     const int oy = rem / G::OW, ox = rem - oy * G::OW;
-    const int ky = kr / (G::KW * G::CIN);
-    const int r2 = kr - ky * (G::KW * G::CIN);
-    const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
-    const int iy = oy * G::S + ky - G::PT, ix = ox * G::S + kx - G::PL;
+    const int iy = oy * G::S + c.dy, ix = ox * G::S + c.dx;
     if constexpr (G::SAME) {
       const bool ok = iy >= 0 && iy < G::H && ix >= 0 && ix < G::W;
       const int iyc = min(max(iy, 0), G::H - 1), ixc = min(max(ix, 0), G::W - 1);
-      const f32x4 v = InElem<U8>::load4(X + (((size_t)b * G::H + iyc) * G::W + ixc) * G::CIN + ci);
+      const f32x4 v = InElem<U8>::load4(X + (((size_t)b * G::H + iyc) * G::W + ixc) * G::CIN + c.ci);
       return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
     } else {
-      return InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + ci);
+      return InElem<U8>::load4(X + (((size_t)b * G::H + iy) * G::W + ix) * G::CIN + c.ci);
     }
   }
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
@@ -528,20 +570,28 @@ struct LdConvBwdA {
   __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
     return row0 + rows <= nrows && k0 + bk <= ke;
   }
-  // The stride-S holes of the transposed conv are data-dependent: clamped address + select.
-  __device__ __forceinline__ f32x4 fetch_fast(int m, int k) const {
+  // Row context: the image of input pixel m and (iy + PT, ix + PL).
+  struct Ctx {
+    const float *img;
+    int ty0, tx0;
+  };
+  __device__ __forceinline__ Ctx ctx(int m) const {
     const int b = m / (G::H * G::W);
     const int rem = m - b * (G::H * G::W);
     const int iy = rem / G::W, ix = rem - iy * G::W;
+    return {dY + (size_t)b * G::OH * G::OW * G::COUT, iy + G::PT, ix + G::PL};
+  }
+  // The stride-S holes of the transposed conv are data-dependent: clamped address + select.
+  __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int k) const {
     const int ky = k / (G::KW * G::COUT);
     const int r2 = k - ky * (G::KW * G::COUT);
     const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
-    const int ty = iy + G::PT - ky, tx = ix + G::PL - kx;
+    const int ty = c.ty0 - ky, tx = c.tx0 - kx;
     const int oy = ty / G::S, ox = tx / G::S;  // only used when ty, tx >= 0
     const bool ok = ty >= 0 && tx >= 0 && (ty - oy * G::S) == 0 && (tx - ox * G::S) == 0 &&
                     oy < G::OH && ox < G::OW;
     const int oyc = min(max(oy, 0), G::OH - 1), oxc = min(max(ox, 0), G::OW - 1);
-    const f32x4 v = *reinterpret_cast<const f32x4 *>(dY + (((size_t)b * G::OH + oyc) * G::OW + oxc) * G::COUT + co);
+    const f32x4 v = *reinterpret_cast<const f32x4 *>(c.img + ((size_t)oyc * G::OW + oxc) * G::COUT + co);
     return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
@@ -573,11 +623,15 @@ struct LdConvBwdB {
   __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
     return row0 + rows <= nrows && k0 + bk <= ke;
   }
-  __device__ __forceinline__ f32x4 fetch_fast(int ci, int k) const {
+  struct Ctx {
+    const float *p;
+  };
+  __device__ __forceinline__ Ctx ctx(int ci) const { return {Wt + (size_t)ci * G::COUT}; }
+  __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int k) const {
     const int ky = k / (G::KW * G::COUT);
     const int r2 = k - ky * (G::KW * G::COUT);
     const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
-    return *reinterpret_cast<const f32x4 *>(Wt + (((size_t)(ky * G::KW + kx) * G::CIN + ci) * G::COUT + co));
+    return *reinterpret_cast<const f32x4 *>(c.p + (size_t)(ky * G::KW + kx) * G::CIN * G::COUT + co);
   }
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
     const int ci = row0 + rr, k = k0 + kk;
@@ -632,7 +686,29 @@ struct LdConvBwdAPhase {
     const f32x4 v = *reinterpret_cast<const f32x4 *>(dY + (((size_t)bc * G::OH + oyc) * G::OW + oxc) * G::COUT + co);
     return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  __device__ __forceinline__ f32x4 fetch_fast(int m, int k) const { return at(m, k); }
+  // Row context: the clamped image of phase row m, its (qy, qx), and whether it is a real row.
+  struct Ctx {
+    const float *img;
+    int qy, qx;
+    bool ok;
+  };
+  __device__ __forceinline__ Ctx ctx(int m) const {
+    const int ph = m / mp, l = m - ph * mp;
+    const int b = l / (P::HQ * P::WQ);
+    const int rem = l - b * (P::HQ * P::WQ);
+    const int qy = rem / P::WQ;
+    return {dY + (size_t)min(b, B - 1) * G::OH * G::OW * G::COUT, qy, rem - qy * P::WQ, b < B};
+  }
+  __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int k) const {
+    const int a = k / (P::KB * G::COUT);
+    const int r2 = k - a * (P::KB * G::COUT);
+    const int bb = r2 / G::COUT, co = r2 - bb * G::COUT;
+    const int oy = c.qy - a, ox = c.qx - bb;
+    const bool ok = c.ok && oy >= 0 && ox >= 0 && oy < G::OH && ox < G::OW;
+    const int oyc = min(max(oy, 0), G::OH - 1), oxc = min(max(ox, 0), G::OW - 1);
+    const f32x4 v = *reinterpret_cast<const f32x4 *>(c.img + ((size_t)oyc * G::OW + oxc) * G::COUT + co);
+    return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
     const int m = row0 + rr, k = k0 + kk;
     return (m < nrows && k < ke) ? at(m, k) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -657,7 +733,11 @@ struct LdConvBwdBPhase {
     const int ky = py + G::S * a, kx = px + G::S * bb;
     return *reinterpret_cast<const f32x4 *>(Wt + (((size_t)(ky * G::KW + kx) * G::CIN + ci) * G::COUT + co));
   }
-  __device__ __forceinline__ f32x4 fetch_fast(int ci, int k) const { return at(ci, k); }
+  struct Ctx {
+    int ci;
+  };
+  __device__ __forceinline__ Ctx ctx(int ci) const { return {ci}; }
+  __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int k) const { return at(c.ci, k); }
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
     const int ci = row0 + rr, k = k0 + kk;
     return (ci < nrows && k < ke) ? at(ci, k) : f32x4{0.f, 0.f, 0.f, 0.f};
