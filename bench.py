@@ -434,7 +434,7 @@ def main():
                       'published and its pushes in HBM (the kernels the timed loop runs; there the conv blocks '
                       'also wait for their env: trunk_in_loop)')
             pmc_kernels = ['nips_conv_kernel<%d, true>' % C_in, 'nips_fc_kernel<%d>' % C_in]
-        elif inloop_us is not None:
+        elif inloop_us is not None and not lstm:  # (LSTM: step 0's forward has 1 + 5E rows, the others E)
             tk_ms = inloop_us * 1e-3
             kern = 'trunk kernels of the rollout forward (implicit-GEMM convs + split-K dense)'
             timing = 'in the timed loop: HIP event pair around each macro-step forward\'s trunk launches ' \
@@ -487,7 +487,9 @@ def main():
                 'note': 'event pair around each macro-step forward\'s trunk launches in the timed loop '
                         '(mt_rollout_trunk_timing, %d updates after the timed region)%s' % (
                             a.measure_updates, '; includes the conv blocks\' wait for their env\'s emulator '
-                            '(in-kernel pull)' if stacking else '')},
+                            '(in-kernel pull)' if stacking else
+                            '; LSTM: frame trunk + cell x-product, averaged over step 0 (1 + 5E rows), steps '
+                            '1..T-1 and the bootstrap (E rows each)' if lstm else '')},
             'train_pass': {'bound': 'mfma', 'kernels': ('backward of %d windows over %d distinct frames (forward reused from the rollout)' % (N, 1 + (T + 4) * ec)) if lstm else 'fused returns + loss + backward of %d rows (forward reused from the rollout)' % N,
                            'flop_count': 'executed backward: dW of every layer + dX of every layer but conv1',
                            'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',

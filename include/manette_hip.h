@@ -138,6 +138,11 @@ int mt_forward_trunk_stacking(const mt_net *net, const float *params, const uint
  *    kept in ws (step 0: rows [0, 1+5E) — zero frame + slots 0..4; step t: slot 4+t's E rows);
  *  - mt_lstm_windows_forward: the E windows of step t (t == T: the bootstrap windows) ->
  *    v [E], pi [E][A], rep [E][R] (paac.py:144-152, :219-224), nz_t = nz[t][0..E);
+ *  - mt_lstm_step_forward: one macro-step of the rollout = frames_forward of step t's new rows
+ *    + windows_forward of step t, with nz[t] derived on the device for t > 0 (nz [T+1][E]:
+ *    nz[t][e] = over[e] != 0 ? 5 : max(nz[t-1][e] - 1, 0), `over` = step t-1's episode-end
+ *    flags, device-readable — paac.py:173-174 update_memory, :202-203 the reset); the native
+ *    rollout (mt_rollout_*) runs the same forward with the draw fused into its heads kernel;
  *  - mt_lstm_frames_backward: loss + gradient of the T*E windows of steps 0..T-1 (the train
  *    step of paac.py:254-256) from the rollout's activations (unchanged parameters), with pi,
  *    rep, v [T*E] the rollout outputs; back-propagates through each distinct frame once. */
@@ -146,6 +151,9 @@ int mt_lstm_frames_forward(const mt_net *net, const float *params, const uint8_t
                            int E, int T, void *ws, size_t ws_bytes, mt_stream_t stream);
 int mt_lstm_windows_forward(const mt_net *net, const float *params, const int32_t *nz_t, int t, int E, int T,
                             void *ws, size_t ws_bytes, float *v, float *pi, float *rep, mt_stream_t stream);
+int mt_lstm_step_forward(const mt_net *net, const float *params, const uint8_t *fstore, int t, int E, int T,
+                         int32_t *nz, const float *over, void *ws, size_t ws_bytes, float *v, float *pi,
+                         float *rep, mt_stream_t stream);
 int mt_lstm_frames_backward(const mt_net *net, const float *params, const uint8_t *fstore, const int32_t *nz,
                             int E, int T, void *ws, size_t ws_bytes, const float *pi, const float *rep,
                             const float *v, const int32_t *a_idx, const int32_t *r_idx, const float *y,
@@ -338,6 +346,12 @@ typedef struct mt_rollout_buffers {
                                   (NULL: hipEventQuery) */
   int32_t flags;               /* MT_ROLLOUT_* */
   int32_t env_offset;          /* global env id of env 0 (data-parallel shard offset): the draw's row0 */
+  int32_t *nz;                 /* LSTM arch only (else NULL): [T+1][E] device window zero counts; nz[0]
+                                  is the caller's, step t > 0 derives nz[t] (mt_lstm_step_forward).
+                                  With the LSTM arch `states` is slot 4 of a frame store
+                                  [1 + (T+5)E][84][84][C] (mt_lstm_*), ws is its workspace
+                                  (mt_lstm_frames_workspace_bytes), train_ws is NULL and pi / rep are
+                                  [T+1][E][.] per-step outputs (row T: the bootstrap's) */
 } mt_rollout_buffers;
 int mt_rollout_create(const mt_net *net, int E, int T, void *runner, void *book,
                       const mt_rollout_buffers *buffers, uint64_t seed, mt_rollout **out);

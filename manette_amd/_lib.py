@@ -29,7 +29,7 @@ class mt_rollout_buffers(C.Structure):
                                           'staging_host', 'meta_host', 'reward_host', 'over_host',
                                           'rm_host', 'frames_host', 'sync_host', 'train_ws')] + \
                [('train_ws_bytes', C.c_size_t), ('v_boot', C.c_void_p), ('ready_host', C.c_void_p), ('flags', C.c_int32),
-                                                                       ('env_offset', C.c_int32)]
+                                                                       ('env_offset', C.c_int32), ('nz', C.c_void_p)]
 
 
 MT_ROLLOUT_ZERO_COPY = 1
@@ -68,6 +68,7 @@ _HIP_SIGS = {
     'mt_lstm_frames_workspace_bytes': (_I, [_P, _I, _I, C.POINTER(_SZ)]),
     'mt_lstm_frames_forward': (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),
     'mt_lstm_windows_forward': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P, _P, _P, _P]),
+    'mt_lstm_step_forward': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _SZ, _P, _P, _P, _P]),
     'mt_lstm_frames_backward': (_I, [_P, _P, _P, _P, _I, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
     'mt_forward_rows': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _SZ, _I, _I, _P, _P, _P, _P]),
     'mt_forward_trunk': (_I, [_P, _P, _P, _I, _P, _SZ, _P]),

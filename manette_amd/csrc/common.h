@@ -181,4 +181,8 @@ int forward_sample(const mt_net *net, const float *params, const uint8_t *obs, i
                    size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp, bool infer,
                    hipStream_t stream, const TrainRows *tr = nullptr, const StackSrc *st = nullptr,
                    const hipEvent_t *marks = nullptr);
+// the native rollout's LSTM macro-step forward (lstm.h lstm_step_fwd_impl; mt_lstm_step_forward)
+int lstm_step_forward(const mt_net *net, const float *params, const uint8_t *fstore, int t, int E, int T,
+                      int32_t *nz, const float *over, void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
+                      const SampleArgs *smp, hipStream_t stream, const hipEvent_t *marks = nullptr);
 }  // namespace mt

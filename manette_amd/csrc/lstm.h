@@ -105,12 +105,26 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-
 //  frame-store layout: row 0 is the zero frame, row 1 + slot*E + e is env e's state of frame
 //  slot `slot`; window b = (step t0 + b / E, env b % E) holds nz[b] leading zero frames, then
 //  slots t..t+4 (paac.py:79-83: the window of step t is s_{t-4} .. s_t).
+//  nz_prev != null (the native rollout, one step's E windows): nz[b] is derived here from the
+//  previous step's count and that step's episode-end flag over[b] (host-mapped, written by the
+//  emulator threads before the step's chain runs) — update_memory shifts one frame in, an
+//  episode end zeroes the whole window (paac.py:173-174, :202-203) — and stored to nz[b].
 struct XgRows {
-  const int32_t *nz;
+  int32_t *nz;
   int t0, E;
-  __device__ __forceinline__ int operator()(int b, int k) const {
+  const int32_t *nz_prev = nullptr;
+  const float *over = nullptr;
+  // leading zero frames of window b (thread 0 of the block stores the derived count)
+  __device__ __forceinline__ int zeros(int b) const {
+    if (!nz) return 0;
+    if (!nz_prev) return nz[b];
+    const int z = over[b] != 0.f ? 5 : max(nz_prev[b] - 1, 0);
+    if (threadIdx.x == 0) nz[b] = z;
+    return z;
+  }
+  __device__ __forceinline__ int row(int b, int k, int z) const {
     if (!nz) return b * 5 + k;
-    if (k < nz[b]) return 0;
+    if (k < z) return 0;
     return 1 + (t0 + b / E + k) * E + b % E;
   }
 };
@@ -138,10 +152,11 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
   // STEPS loads in flight per batch instead of one load latency per slab; adds in slab order
   float zx[STEPS];
   size_t xoff[STEPS];
+  const int z = map.zeros(b);
 #pragma unroll
   for (int t = 0; t < STEPS; ++t) {
     zx[t] = 0.f;
-    xoff[t] = (size_t)map(b, t) * G4 + g;
+    xoff[t] = (size_t)map.row(b, t, z) * G4 + g;
   }
   for (int s0 = 0; s0 < S; s0 += 8) {
     float v[STEPS][8];
@@ -438,8 +453,10 @@ static int lstm_frames_fwd_impl(const mt_net *n, const float *P, const uint8_t *
 }
 
 template <class Ar>
-static int lstm_windows_fwd_impl(const mt_net *n, const float *P, const int32_t *nz_t, int t, int E, int T,
-                                 float *ws, float *v, float *pi, float *rep, hipStream_t s) {
+static int lstm_windows_fwd_impl(const mt_net *n, const float *P, int32_t *nz_t, int t, int E, int T,
+                                 float *ws, float *v, float *pi, float *rep, hipStream_t s,
+                                 const SampleArgs *smp = nullptr, const int32_t *nz_prev = nullptr,
+                                 const float *over = nullptr) {
   MT_CHECK_ARG(t >= 0 && t <= T, "step %d outside [0, %d]", t, T);
   const LstmFrameWs X = lstm_frame_layout<Ar>(n, E, T);
   const size_t w0 = (size_t)t * E;
@@ -447,7 +464,7 @@ static int lstm_windows_fwd_impl(const mt_net *n, const float *P, const int32_t 
   const float *Wp = P + n->off_proj;
   const float *W6 = P + n->off_fc;
   hipLaunchKernelGGL((lstm_fwd_kernel<Ar::NH, Ar::STEPS>), dim3(E), dim3(Ar::G4), 0, s, ws + X.xg, X.S, X.R_max,
-                     XgRows{nz_t, t, E}, Kh, Kh + Ar::NH * Ar::G4, Wp, Wp + Ar::NH * Ar::NH, W6, Ar::F, 1.0f,
+                     XgRows{nz_t, t, E, nz_prev, over}, Kh, Kh + Ar::NH * Ar::G4, Wp, Wp + Ar::NH * Ar::NH, W6, Ar::F, 1.0f,
                      ws + X.gates + w0 * Ar::STEPS * Ar::G4, ws + X.cst + w0 * Ar::STEPS * Ar::NH,
                      ws + X.hprev + w0 * Ar::STEPS * Ar::NH, ws + X.h5 + w0 * Ar::NH, ws + X.out32 + w0 * Ar::NH,
                      ws + X.slab6 + w0 * Ar::F);
@@ -455,9 +472,29 @@ static int lstm_windows_fwd_impl(const mt_net *n, const float *P, const int32_t 
   HeadParams hp = head_params(n, P);
   hipLaunchKernelGGL(heads_fwd_kernel, dim3(E), dim3(256), 0, s, ws + X.slab6 + w0 * Ar::F, 1, E,
                      W6 + (size_t)Ar::NH * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp, n->cfg.softmax_temp,
-                     ws + X.L.H + w0 * Ar::F, v, pi, rep, SampleArgs{});
+                     ws + X.L.H + w0 * Ar::F, v, pi, rep, smp ? *smp : SampleArgs{});
   MT_LAUNCHED();
   return MT_OK;
+}
+
+// One macro-step forward of the frame-store LSTM inside the native rollout (rollout.hip): the
+// trunk + x-product of the step's new frame rows (step 0: the zero frame and slots 0..4 again,
+// the parameters having changed; step t > 0: slot 4 + t), then the recurrence of its E windows
+// with the draw fused into the heads kernel (smp; null for the bootstrap, t == T). t > 0: nz[t]
+// is derived on the device from nz[t-1] and step t-1's episode-end flags `over` (XgRows).
+// marks: optional event pair around the trunk launches (mt_rollout_trunk_timing).
+template <class Ar>
+static int lstm_step_fwd_impl(const mt_net *n, const float *P, const uint8_t *fstore, int t, int E, int T,
+                              int32_t *nz, const float *over, float *ws, float *v, float *pi, float *rep,
+                              const SampleArgs *smp, hipStream_t s, const hipEvent_t *marks) {
+  MT_CHECK_ARG(t >= 0 && t <= T, "step %d outside [0, %d]", t, T);
+  MT_CHECK_ARG(t == 0 || over, "steps t > 0 need the episode-end flags");
+  const int row0 = t == 0 ? 0 : 1 + (4 + t) * E, nrows = t == 0 ? 1 + 5 * E : E;
+  if (marks) MT_HIP(hipEventRecord(marks[0], s));
+  MT_TRY((lstm_frames_fwd_impl<Ar>(n, P, fstore, row0, nrows, E, T, ws, s)));
+  if (marks) MT_HIP(hipEventRecord(marks[1], s));
+  return lstm_windows_fwd_impl<Ar>(n, P, nz + (size_t)t * E, t, E, T, ws, v, pi, rep, s, smp,
+                                   t > 0 ? nz + (size_t)(t - 1) * E : nullptr, t > 0 ? over : nullptr);
 }
 
 template <class Ar>

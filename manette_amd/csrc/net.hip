@@ -1465,7 +1465,30 @@ extern "C" int mt_lstm_windows_forward(const mt_net *net, const float *params, c
   MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
   MT_LSTM_ONLY(net, {
     MT_LSTM_WS(E, T);
-    return lstm_windows_fwd_impl<Ar>(net, params, nz_t, t, E, T, (float *)ws, v, pi, rep, (hipStream_t)stream);
+    // (nz_t is only read: no nz_prev)
+    return lstm_windows_fwd_impl<Ar>(net, params, const_cast<int32_t *>(nz_t), t, E, T, (float *)ws, v, pi, rep,
+                                     (hipStream_t)stream);
+  });
+  return MT_OK;
+}
+
+extern "C" int mt_lstm_step_forward(const mt_net *net, const float *params, const uint8_t *fstore, int t, int E,
+                                    int T, int32_t *nz, const float *over, void *ws, size_t ws_bytes, float *v,
+                                    float *pi, float *rep, mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && fstore && nz && ws && v && pi && rep, "null argument");
+  MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
+  return mt::lstm_step_forward(net, params, fstore, t, E, T, nz, over, ws, ws_bytes, v, pi, rep, nullptr,
+                               (hipStream_t)stream);
+}
+
+int mt::lstm_step_forward(const mt_net *net, const float *params, const uint8_t *fstore, int t, int E, int T,
+                          int32_t *nz, const float *over, void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
+                          const SampleArgs *smp, hipStream_t stream, const hipEvent_t *marks) {
+  MT_CHECK_ARG(!smp || (smp->counters && smp->a_idx && smp->r_idx), "null sample buffer");
+  MT_LSTM_ONLY(net, {
+    MT_LSTM_WS(E, T);
+    return lstm_step_fwd_impl<Ar>(net, params, fstore, t, E, T, nz, over, (float *)ws, v, pi, rep, smp, stream,
+                                  marks);
   });
   return MT_OK;
 }

@@ -24,6 +24,9 @@ struct mt_rollout {
   bool zero_copy, in_place, pooled, resized, pipelined;
   bool pull;          // pipelined + resized: per-env ready words, pull kernel into HBM, tagged pairs
   bool stack_fwd;     // pull + NIPS: the forward's conv kernel stacks (no preprocess launch)
+  bool lstm;          // LSTM arch: frame-store forward per step (mt_lstm_step_forward), nz on the device
+  const uint8_t *fstore = nullptr;  // LSTM: the frame store (states = its slot 4)
+  const float *over_dev = nullptr;  // LSTM: device address of the pinned episode-end flags
   int armed_upto = -1;  // pipelined: last step whose chain (forward) is already enqueued
   int ahead = 1;        // pipelined: steps armed ahead (2 with pull)
   std::vector<uint32_t> fwd_of;  // [T] draw sequence number of step t's forward
@@ -92,8 +95,14 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   }
   mt_net_config cfg;
   MT_CHECK_ARG(mt_net_get_config(net, &cfg) == MT_OK, "bad net");
+  const bool lstm = cfg.arch == MT_ARCH_LSTM;
+  MT_CHECK_ARG(lstm == (b.nz != nullptr), "nz is required for (and only for) the LSTM arch");
+  MT_CHECK_ARG(!lstm || !b.train_ws, "the LSTM arch keeps its rows in the frame-store workspace (train_ws NULL)");
+  void *over_dev = nullptr;
+  if (lstm) MT_HIP(hipHostGetDevicePointer(&over_dev, b.over_host, 0));  // read by the windows kernel
   size_t need = 0;
-  if (mt_net_workspace_bytes(net, E, &need) != MT_OK) return MT_ERR_ARG;
+  if ((lstm ? mt_lstm_frames_workspace_bytes(net, E, T, &need) : mt_net_workspace_bytes(net, E, &need)) != MT_OK)
+    return MT_ERR_ARG;
   if (b.ws_bytes < need) {
     set_error("rollout workspace %zu < %zu bytes", b.ws_bytes, need);
     return MT_ERR_WORKSPACE;
@@ -117,6 +126,9 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->pipelined = pl;
   ro->pull = pl && rz;
   ro->stack_fwd = ro->pull && cfg.arch == MT_ARCH_NIPS;
+  ro->lstm = lstm;
+  ro->over_dev = (const float *)over_dev;
+  if (lstm) ro->fstore = b.states - (size_t)(1 + 4 * E) * 84 * 84 * 4 * cfg.depth;
   ro->frames_dev = (int32_t *)frames_dev;
   ro->ready_dev = (uint32_t *)ready_dev;
   ro->seq_dev = (uint32_t *)sync_dev;
@@ -333,9 +345,15 @@ int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, b
   const size_t po = b.train_ws ? (size_t)t * E : 0;
   const hipEvent_t *marks;
   MT_TRY_(next_marks(ro, &marks));
-  MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)t * slot, E, b.ws, b.ws_bytes,
-                         b.values + (size_t)t * E, b.pi + po * ro->A, b.rep + po * ro->R, &smp, true, s,
-                         b.train_ws ? &tr : nullptr, stacked ? &st : nullptr, marks));
+  if (ro->lstm) {  // step t's new frames + its E windows, pi / rep [T+1][E][.]
+    MT_TRY_(lstm_step_forward(ro->net, params, ro->fstore, t, E, T, b.nz, ro->over_dev, b.ws, b.ws_bytes,
+                              b.values + (size_t)t * E, b.pi + (size_t)t * E * ro->A, b.rep + (size_t)t * E * ro->R,
+                              &smp, s, marks));
+  } else {
+    MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)t * slot, E, b.ws, b.ws_bytes,
+                           b.values + (size_t)t * E, b.pi + po * ro->A, b.rep + po * ro->R, &smp, true, s,
+                           b.train_ws ? &tr : nullptr, stacked ? &st : nullptr, marks));
+  }
   if (!ro->zero_copy)
     MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
   MT_HIP(hipEventRecord(ro->ev2[t & 3], s));
@@ -397,6 +415,9 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
   }
   if (k < T) {
     MT_TRY_(enqueue_forward(ro, params, k, s, stk, want));
+  } else if (b.v_boot && ro->lstm) {  // bootstrap V(s_T): slot 4 + T's frames + the windows of step T
+    MT_TRY_(lstm_step_forward(ro->net, params, ro->fstore, T, E, T, b.nz, ro->over_dev, b.ws, b.ws_bytes, b.v_boot,
+                              b.pi + (size_t)T * E * ro->A, b.rep + (size_t)T * E * ro->R, nullptr, s));
   } else if (b.v_boot) {  // bootstrap V(s_T), no draw, no train rows
     const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
     const size_t po = b.train_ws ? (size_t)T * E : 0;

@@ -209,6 +209,19 @@ class DeviceNetwork(object):
               'mt_lstm_windows_forward')
         return v, pi, rep
 
+    def lstm_step_forward(self, fstore, t, E, T, nz, over, out):
+        """One rollout macro-step: step t's new frame rows + its E windows (mt_lstm_step_forward).
+        nz: [T+1][E] int32 (device); t > 0 derives nz[t] from nz[t-1] and `over` (step t-1's
+        episode-end flags: a device tensor, or the device address of pinned host memory)."""
+        ws = self.lstm_workspace(E, T)
+        v, pi, rep = out
+        assert nz.dtype == torch.int32 and nz.is_cuda and nz.numel() == (T + 1) * E
+        over_p = over if isinstance(over, (int, C.c_void_p)) or over is None else _ptr(over)
+        check(_lib.hip().mt_lstm_step_forward(self._h, _ptr(self.params), _ptr(fstore), int(t), int(E), int(T),
+                                              _ptr(nz), over_p, _ptr(ws), ws.numel(), _ptr(v), _ptr(pi), _ptr(rep),
+                                              _stream()), 'mt_lstm_step_forward')
+        return v, pi, rep
+
     def lstm_frames_backward(self, fstore, nz, E, T, pi, rep, v, a_idx, r_idx, y, adv, loss_terms=None):
         """Gradient of the T*E windows of the last rollout into self.grad."""
         ws = self.lstm_workspace(E, T)

@@ -82,8 +82,9 @@ class PAACLearner(ActorLearner):
             self.fstore = torch.zeros(1 + (T + 5) * E, 84, 84, C, dtype=torch.uint8, device=dev)
             self.slots = self.fstore[1:].view(T + 5, E, 84, 84, C)
             self.states = self.slots[4:]
-            self.nz_h = torch.zeros(T + 1, E, dtype=torch.int32, pin_memory=True)
+            self.nz_h = torch.zeros(T + 1, E, dtype=torch.int32, pin_memory=True)  # (Python step only)
             self.nz_d = torch.zeros(T + 1, E, dtype=torch.int32, device=dev)
+            self._slots_tmp = torch.zeros(5, E, 84, 84, C, dtype=torch.uint8, device=dev) if T < 5 else None
         else:
             self.states = torch.zeros(T + 1, E, 84, 84, C, dtype=torch.uint8, device=dev)
         self.values = torch.zeros(T, E, dtype=torch.float32, device=dev)
@@ -164,7 +165,7 @@ class PAACLearner(ActorLearner):
                                          dtype=torch.uint8, device=self.dev)
                 total = self.runners.reset()
                 self._upload_pushes(total, self.states[0], self.states[0].clone())
-            if self.sampling == 'device' and not self.lstm_bool:
+            if self.sampling == 'device':
                 self._make_native_step()
         else:
             emus = [self.environment_creator.create_environment(i) for i in range(E)]
@@ -182,7 +183,10 @@ class PAACLearner(ActorLearner):
         import ctypes as C
         from . import _lib
         net, r = self.network, self.runners
-        ws = net.workspace(self.emulator_counts, 'rollout')
+        E, T = self.emulator_counts, self.max_local_steps
+        # LSTM: the frame store's workspace; each step's forward = its new frame rows + its E
+        # windows (mt_lstm_step_forward), nz[t] derived on the device from the episode-end flags
+        ws = net.lstm_workspace(E, T) if self.lstm_bool else net.workspace(E, 'rollout')
         p = lambda t: C.c_void_p(None if t is None else t.data_ptr())
         if self.in_place:
             flags, staging, frames, src_rows, rows = (_lib.MT_ROLLOUT_IN_PLACE, self.bank.screens_t, r.frames, 210,
@@ -209,12 +213,14 @@ class PAACLearner(ActorLearner):
             p(rows), p(self.col_lut), p(self.idx_h), p(staging), p(r.push_meta), p(r.reward),
             p(r.over), p(self.rm_h), p(frames), p(self.sync_h), p(self.train_ws),
             0 if self.train_ws is None else self.train_ws.numel(),
-            p(self.v_boot if self.pipeline else None), p(self.ready_h), flags, self.env_offset)
+            p(self.v_boot if self.pipeline else None), p(self.ready_h), flags, self.env_offset,
+            p(self.nz_d if self.lstm_bool else None))
         h = C.c_void_p()
         _lib.check(_lib.hip().mt_rollout_create(net._h, self.emulator_counts, self.max_local_steps, r._h,
                                                 self.book.handle, C.byref(self._bufs),
                                                 C.c_uint64(self.sample_seed), C.byref(h)), 'mt_rollout_create')
         self.native_step = h
+        self._over_dev = devnet.host_device_pointer(r.over) if self.lstm_bool else None
         self.boot_in_rollout = self.pipeline  # the last step's chain runs the bootstrap forward
         # the rollout's stacking NIPS forward (pipelined, resized staging) also carries slot T over
         # into slot 0 at the next step 0 (mt_rollout_step): the update does not copy it
@@ -333,6 +339,9 @@ class PAACLearner(ActorLearner):
         changed) through trunk + cell x-product, then the recurrence of the E windows of step t."""
         E, T = self.emulator_counts, self.max_local_steps
         net = self.network
+        if self.native_step is not None:  # nz lives on the device: nz[t] from nz[t-1] + step t-1's over flags
+            return net.lstm_step_forward(self.fstore, t, E, T, self.nz_d, self._over_dev, out=(v_out, self.pi_all[t],
+                                                                                              self.rep_all[t]))
         if t == 0:
             net.lstm_frames_forward(self.fstore, 0, 1 + 5 * E, E, T)
         else:
@@ -370,15 +379,16 @@ class PAACLearner(ActorLearner):
         return lr
 
     def _graph_ok(self):
-        return (self.use_update_graph and self.profile is None and not self.lstm_bool
+        return (self.use_update_graph and self.profile is None
                 and self.native_step is not None and self.boot_in_rollout)
 
     def _update_backward(self):
         net = self.network
         E, T = self.emulator_counts, self.max_local_steps
-        if self.lstm_bool:
+        boot_done = self.boot_in_rollout and self.native_step is not None  # (queued behind the last step)
+        if self.lstm_bool and not boot_done:
             self._lstm_forward(T, self.v_boot)
-        elif not (self.boot_in_rollout and self.native_step is not None):  # (else queued behind the last step)
+        elif not self.lstm_bool and not boot_done:
             net.forward(self.states[T], E, out=(self.v_boot, self.pi_roll, self.rep_roll), ws_key='rollout', infer=True)
         if self.lstm_bool:
             devnet.returns(self.rm_h_dev, self.rm_h_dev + 4 * T * E, self.values, self.v_boot, self.gamma, self.y,
@@ -421,8 +431,15 @@ class PAACLearner(ActorLearner):
         self.network.apply_gradients(1.0 / self.world if self.world > 1 else 1.0,
                                      partials_ready=self.world == 1 and not self.lstm_bool)
         if self.lstm_bool:  # the next rollout's slots 0..4 = s_{T-4} .. s_T; windows carry over
-            self.slots[0:5].copy_(self.slots[T:T + 5].clone())
-            self.nz_h.numpy()[0] = self.nz_h.numpy()[T]
+            if T >= 5:
+                self.slots[0:5].copy_(self.slots[T:T + 5])
+            else:  # overlapping ranges: through a fixed buffer (graph-capturable, no allocation)
+                self._slots_tmp.copy_(self.slots[T:T + 5])
+                self.slots[0:5].copy_(self._slots_tmp)
+            if self.native_step is not None:
+                self.nz_d[0].copy_(self.nz_d[T])
+            else:
+                self.nz_h.numpy()[0] = self.nz_h.numpy()[T]
         elif not (self.native_step is not None and self.slot0_in_rollout):
             self.states[0].copy_(self.states[T])
 
@@ -506,6 +523,7 @@ class PAACLearner(ActorLearner):
         self._start_runners()
         if self.lstm_bool:  # memory = zeros except memory[:, -1] = initial state (paac.py:109-112)
             self.nz_h.numpy()[0] = 4
+            self.nz_d[0].fill_(4)
 
     def write_summaries(self):
         """The reference's TensorBoard scalars of the last rollout + update (chief only):

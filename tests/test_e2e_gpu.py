@@ -3,7 +3,7 @@
 The learner is bench.make_learner(config) — the exact object bench.py times: native emulator
 threads, device sampling fused into the heads kernel, resized staging, the pipelined native
 macro-step (NIPS: pull kernel + stacking conv kernel), the update replayed as a hipGraph from the
-second update on; LSTM: the frame-store path. U updates run; the last one (a graph replay) is
+second update on; LSTM: the native frame-store macro-step. U updates run; the last one (a graph replay) is
 checked against the oracle on everything it consumed and produced:
 
   trajectory  every state slot 0..T and the clipped rewards / masks == a replay of the oracle's
@@ -81,8 +81,7 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
     L, args, cfg = _run(config, tmp_path)
     try:
         lstm = L.lstm_bool
-        if not lstm:
-            assert L.native_step is not None and L.boot_in_rollout and L._graph_ok()
+        assert L.native_step is not None and L.boot_in_rollout and L._graph_ok()
         E, T, A, R = L.emulator_counts, L.max_local_steps, L.num_actions, L.total_repetitions
         N = E * T
         idx_all = []
@@ -91,8 +90,7 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
             L.rollout()
             idx_all.append(L.idx_h.numpy().copy())
             L.update()
-        if not lstm:
-            assert L._graphs is not None  # the checked update is a graph replay
+        assert L._graphs is not None  # the checked update is a graph replay
         L.book.new_update()
         L.rollout()
         torch.cuda.synchronize()
@@ -105,7 +103,7 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
         values = c(L.values)
         gs = L.global_step
         if lstm:  # (the update's apply moves slots T.. to 0.. and nz[T] to nz[0])
-            fstore, nz = c(L.fstore), L.nz_h.numpy().copy()
+            fstore, nz = c(L.fstore), c(L.nz_d)  # (nz derived on the device by the native step)
         L.update()
         torch.cuda.synchronize()
         # V(s_T): the rollout's last chain (pipelined native step) or the update's first forward (LSTM)

@@ -191,11 +191,15 @@ def test_lstm_frame_store_parity(E, T, depth):
     np.testing.assert_allclose(terms.cpu().numpy(), aux['terms'], rtol=1e-4, atol=1e-5)
 
 
-def test_lstm_learner_memory_windows(tmp_path):
+@pytest.mark.parametrize('pipeline', [True, False])
+def test_lstm_learner_memory_windows(tmp_path, pipeline):
     """The learner's LSTM windows (frame store + nz, read at every step and by the train
     step) equal a numpy replay of the reference's memory bookkeeping (paac.py:107-112, :173-174,
     :202-203, :233-234) over the recorded states and episode-end masks, with resets inside the
-    rollout and across updates; the LSTM update runs and changes the parameters."""
+    rollout and across updates; the LSTM update runs and changes the parameters. The learner runs
+    the native macro-step (mt_rollout with the frame-store forward; nz derived on the device from
+    the emulators' episode-end flags), pipelined (bootstrap in the rollout's last chain, update
+    replayed as a hipGraph from the second update on) or not (bootstrap in the update)."""
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -208,6 +212,7 @@ def test_lstm_learner_memory_windows(tmp_path):
     a.game, a.arch, a.emulator_counts, a.emulator_workers = 'ms_pacman', 'LSTM', 6, 2
     a.max_repetition, a.nb_choices = 10, 11
     a.runner, a.sampling, a.seed = 'native', 'device', 0
+    a.pipeline = pipeline
     a.debugging_folder = str(tmp_path) + '/'
     a.max_global_steps = 1 << 40
     a.checkpoint_interval = 1 << 40
@@ -217,7 +222,7 @@ def test_lstm_learner_memory_windows(tmp_path):
     ec.create_bank = lambda first, n: SyntheticBank(first, n, episode_len=9)
     L = PAACLearner(nc, ec, explo, a)
     L.start()
-    assert L.native_step is None  # LSTM takes the Python step
+    assert L.native_step is not None and L.boot_in_rollout == pipeline
     try:
         E, T = 6, L.max_local_steps
         mem = np.zeros((E, 5, 84, 84, 4), np.uint8)
@@ -230,16 +235,22 @@ def test_lstm_learner_memory_windows(tmp_path):
                 L.step(t)
             torch.cuda.synchronize()
             slots = L.slots.cpu().numpy()
-            nz = L.nz_h.numpy().copy()
             masks = L.masks_h.numpy().copy()
             resets += int((masks == 0).sum())
+            nz = L.nz_d.cpu().numpy()
+            L.update()  # (unpipelined: the bootstrap forward derives nz[T] here; then nz[0] <- nz[T])
+            torch.cuda.synchronize()
+            nz_after = L.nz_d.cpu().numpy()
+            if not pipeline:
+                nz[T] = nz_after[T]
+            np.testing.assert_array_equal(nz_after[T], nz[T])
+            np.testing.assert_array_equal(nz_after[0], nz[T])  # carried into the next rollout
             for t in range(T):
                 np.testing.assert_array_equal(_windows_from_store(slots, nz[t], t), mem, err_msg='u%d t%d' % (u, t))
                 _np_memory_push(mem, slots[4 + t + 1], masks[t])
             np.testing.assert_array_equal(_windows_from_store(slots, nz[T], T), mem)  # bootstrap window
-            L.update()
-        torch.cuda.synchronize()
         assert resets > 0
+        assert (L._graphs is not None) == pipeline
         p1 = L.network.params.cpu().numpy()
         assert np.isfinite(p1).all() and not np.array_equal(p0, p1)
     finally:

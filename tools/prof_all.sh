@@ -3,10 +3,10 @@
 set -u
 TAG=${1:-prof}
 for c in ${CONFIGS:-pong-nips breakout-nature-figar seaquest-nature breakout-pwyx-figar-rgb mspacman-lstm-figar}; do
-  bash tools/prof.sh ${TAG}_$c --config $c
+  bash tools/prof.sh ${TAG}_prof_$c --config $c
   rc=$?
-  f=$(ls gpurun_out/${TAG}_$c/*/run_kernel_trace.csv gpurun_out/${TAG}_$c/run_kernel_trace.csv 2>/dev/null | head -1)
-  [ -n "$f" ] && python tools/prof_summary.py $f > gpurun_out/${TAG}_$c.summary.txt
+  f=$(ls gpurun_out/${TAG}_prof_$c/*/run_kernel_trace.csv gpurun_out/${TAG}_prof_$c/run_kernel_trace.csv 2>/dev/null | head -1)
+  [ -n "$f" ] && python tools/prof_summary.py $f > gpurun_out/${TAG}_prof_$c.summary.txt
   [ $rc -ne 0 ] && exit $rc
 done
 exit 0
