@@ -22,6 +22,7 @@
 // 16-chunk is permuted, which a sum does not see).
 #pragma once
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -139,6 +140,14 @@ struct Stage {
   }
 };
 
+// Quad epilogues (EP::QUAD): ep.quad(m, n, z, v) receives the 4 consecutive rows m..m+3 (m % 4
+// == 0) of column n that one lane's accumulator holds — a 2x2 max pool over pool-ordered rows
+// (LdIm2col<G, U8, true>) becomes a register reduction. M must be a multiple of 4.
+template <class E, class = void>
+struct IsQuadEp : std::false_type {};
+template <class E>
+struct IsQuadEp<E, std::void_t<decltype(E::QUAD)>> : std::bool_constant<E::QUAD> {};
+
 // One output tile (bx, by) of K-split bz; smem = the dynamic LDS (gemm_lds_bytes). A device
 // function so grouped launches (GemmJob, group_kernel) can run several products in one grid.
 template <class T, class LA, class LB, class EP>
@@ -207,10 +216,15 @@ __device__ __forceinline__ void gemm_body(const LA &la, const LB &lb, const EP &
 #pragma unroll
     for (int j = 0; j < T::TN; ++j) {
       const int n = n0 + (wn * T::TN + j) * 16 + r;
+      if constexpr (IsQuadEp<EP>::value) {
+        const int m = m0 + (wm * T::TM + i) * 16 + g * 4;
+        if (m < M && n < N) ep.quad(m, n, bz, acc[i][j]);
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = m0 + (wm * T::TM + i) * 16 + g * 4 + q;
-        if (m < M && n < N) ep(m, n, bz, acc[i][j][q]);
+        for (int q = 0; q < 4; ++q) {
+          const int m = m0 + (wm * T::TM + i) * 16 + g * 4 + q;
+          if (m < M && n < N) ep(m, n, bz, acc[i][j][q]);
+        }
       }
     }
 }
@@ -451,8 +465,31 @@ struct InElem<false> {
   }
 };
 
+// Output pixel (b, oy, ox) of GEMM row m of a conv: NHWC order, or (POOL) pool order — m = 4p + q
+// with p = (b, py, px) the 2x2/2 VALID pool output and q = (dy, dx) its window position in
+// (row, col) order, so a lane's 4 accumulator rows are one pool window (the odd last row / column
+// a VALID pool drops are not rows at all).
+template <class G, bool POOL>
+__device__ __forceinline__ void out_pixel(int m, int &b, int &oy, int &ox) {
+  if constexpr (POOL) {
+    constexpr int PH = G::OH / 2, PW = G::OW / 2;
+    const int p = m >> 2, q = m & 3;
+    b = p / (PH * PW);
+    const int rem = p - b * (PH * PW);
+    const int py = rem / PW;
+    oy = 2 * py + (q >> 1);
+    ox = 2 * (rem - py * PW) + (q & 1);
+  } else {
+    b = m / (G::OH * G::OW);
+    const int rem = m - b * (G::OH * G::OW);
+    oy = rem / G::OW;
+    ox = rem - oy * G::OW;
+  }
+}
+
 // Implicit im2col of the forward conv: A(m = (b, oy, ox), k = (ky, kx, ci)). KMAJOR.
-template <class G, bool U8>
+// POOL: rows in pool order (out_pixel), for a pooling epilogue (EpBiasActPool).
+template <class G, bool U8, bool POOL = false>
 struct LdIm2col {
   static constexpr bool KMAJOR = true;
   const typename InElem<U8>::T *X;
@@ -466,9 +503,8 @@ struct LdIm2col {
     int iy0, ix0;
   };
   __device__ __forceinline__ Ctx ctx(int m) const {
-    const int b = m / (G::OH * G::OW);
-    const int rem = m - b * (G::OH * G::OW);
-    const int oy = rem / G::OW, ox = rem - oy * G::OW;
+    int b, oy, ox;
+    out_pixel<G, POOL>(m, b, oy, ox);
     return {X + (size_t)b * G::H * G::W * G::CIN, oy * G::S - G::PT, ox * G::S - G::PL};
   }
   // Padding (SAME) and the k tail handled branch-free: clamped address, zero by select.
@@ -493,9 +529,8 @@ struct LdIm2col {
     const int m = row0 + rr, k = k0 + kk;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (m < nrows && k < ke) {
-      const int b = m / (G::OH * G::OW);
-      const int rem = m - b * (G::OH * G::OW);
-      const int oy = rem / G::OW, ox = rem - oy * G::OW;
+      int b, oy, ox;
+      out_pixel<G, POOL>(m, b, oy, ox);
       const int ky = k / (G::KW * G::CIN);
       const int r2 = k - ky * (G::KW * G::CIN);
       const int kx = r2 / G::CIN, ci = r2 - kx * G::CIN;
@@ -769,6 +804,36 @@ struct EpBiasAct {
   }
 };
 
+// Conv bias + activation + 2x2/2 VALID max pool (networks.py:108-110) over pool-ordered rows
+// (LdIm2col<G, U8, true>): the lane's 4 rows are one window; writes the pooled value and the
+// window position of its first maximum in (row, col) order — the position TF's MaxPoolGrad routes
+// the gradient to — so neither the full-resolution activation nor a pool kernel exists.
+template <class G>
+struct EpBiasActPool {
+  static constexpr bool QUAD = true;
+  float *Y;         // [B][OH/2][OW/2][COUT]
+  uint8_t *arg;     // [B][OH/2][OW/2][COUT] first-max position 0..3
+  const float *bias;
+  int act;
+  float alpha;
+  __device__ __forceinline__ void quad(int m, int n, int, f32x4 v) const {
+    const float bn = bias[n];
+    float mx = act_fwd(v[0] + bn, act, alpha);
+    int a = 0;
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const float y = act_fwd(v[q] + bn, act, alpha);
+      if (y > mx) {
+        mx = y;
+        a = q;
+      }
+    }
+    const size_t i = (size_t)(m >> 2) * G::COUT + n;
+    Y[i] = mx;
+    arg[i] = (uint8_t)a;
+  }
+};
+
 struct EpSlab {
   float *P;
   int M, N;
@@ -802,6 +867,49 @@ struct EpMaskedPhase {
     const int qy = rem / P::WQ, qx = rem - qy * P::WQ;
     const size_t i = (((size_t)b * G::H + G::S * qy + py) * G::W + G::S * qx + px) * G::CIN + n;
     dX[i] = v * act_bwd(Yact[i], act, alpha);
+  }
+};
+
+// MaxPoolGrad fused into the backward-data product of the layer after a pool: row m is pooled
+// pixel (b, py, px) of conv GJ's pooled output P, v its gradient; v * act'(P) goes to the window
+// position arg[m][n] of GJ's full-resolution output gradient dact, zeros to the other three and
+// to the odd last row / column the VALID pool dropped (TF MaxPoolGrad; act'(P) == act' at the max).
+template <class GJ>
+struct EpMaskedUnpool {
+  float *dact;          // [B][OH][OW][COUT] of conv GJ
+  const float *P;       // [B][OH/2][OW/2][COUT]
+  const uint8_t *arg;
+  int act;
+  float alpha;
+  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
+    constexpr int PH = GJ::OH / 2, PW = GJ::OW / 2, C = GJ::COUT;
+    const size_t i = (size_t)m * C + n;
+    const float g = v * act_bwd(P[i], act, alpha);
+    const int a = arg[i];
+    const int b = m / (PH * PW);
+    const int rem = m - b * (PH * PW);
+    const int py = rem / PW, px = rem - py * PW;
+    float *d = dact + (((size_t)b * GJ::OH + 2 * py) * GJ::OW + 2 * px) * C + n;
+    constexpr size_t RW = (size_t)GJ::OW * C;
+    d[0] = a == 0 ? g : 0.f;
+    d[C] = a == 1 ? g : 0.f;
+    d[RW] = a == 2 ? g : 0.f;
+    d[RW + C] = a == 3 ? g : 0.f;
+    if constexpr (GJ::OW & 1) {
+      if (px == PW - 1) {
+        d[2 * C] = 0.f;
+        d[RW + 2 * C] = 0.f;
+      }
+    }
+    if constexpr (GJ::OH & 1) {
+      if (py == PH - 1) {
+        d[2 * RW] = 0.f;
+        d[2 * RW + C] = 0.f;
+        if constexpr (GJ::OW & 1) {
+          if (px == PW - 1) d[2 * RW + 2 * C] = 0.f;
+        }
+      }
+    }
   }
 };
 

@@ -175,9 +175,10 @@ static void build_layout(mt_net *n) {
 // Workspace layout (floats), a pure function of (net, batch).
 // ---------------------------------------------------------------------------------------------
 struct WsLayout {
-  // per conv layer: act = post-activation conv output, pool = pooled output (if pooled),
-  // dact = its gradient (pre-activation after masking), dpool = gradient w.r.t. the pooled output
-  size_t act[4], pool[4], dact[4], dpool[4], fcslab, H, dz, dH, wslab, wslab2, total;
+  // per conv layer: act = post-activation conv output (unpooled layers), pool = pooled output and
+  // parg = its window argmax bytes (pooled layers: the conv epilogue pools, EpBiasActPool), dact =
+  // the gradient of the conv output (pre-activation after masking; full resolution)
+  size_t act[4], pool[4], parg[4], dact[4], fcslab, H, dz, dH, wslab, wslab2, total;
   int fc_splits;
 };
 
@@ -268,10 +269,10 @@ static void ws_layers(WsLayout &L, size_t &off, int B, size_t &wslab) {
     };
     const size_t a = (size_t)B * G::OH * G::OW * G::COUT;
     const size_t p = pooled<Ar, I>() ? (size_t)B * (G::OH / 2) * (G::OW / 2) * G::COUT : 0;
-    L.act[I] = take(a);
+    L.act[I] = take(pooled<Ar, I>() ? 0 : a);
     L.dact[I] = take(a);
     L.pool[I] = take(p);
-    L.dpool[I] = take(p);
+    L.parg[I] = take(p / 4);  // bytes (COUT % 4 == 0)
     wslab = std::max(wslab, conv_wgrad_slab<G>(B));
     ws_layers<Ar, I + 1>(L, off, B, wslab);
   }
@@ -763,6 +764,23 @@ static int conv_forward(const void *X, const float *Wt, const float *bias, float
   return launch_gemm<T>(la, lb, ep, M, G::COUT, G::KK, 1, s);
 }
 
+// Conv + bias + activation + 2x2/2 max pool in one product (pool-ordered rows, EpBiasActPool):
+// Y = the pooled output, arg = the window position of each maximum.
+template <class G, bool U8>
+static int conv_forward_pool(const void *X, const float *Wt, const float *bias, float *Y, uint8_t *arg, int B,
+                             int act, float alpha, hipStream_t s) {
+  using T = TileConvFwd<G>;
+  LdIm2col<G, U8, true> la{reinterpret_cast<const typename InElem<U8>::T *>(X)};
+  LdColMajor lb{Wt, G::COUT, -1};
+  EpBiasActPool<G> ep{Y, arg, bias, act, alpha};
+  const int M = B * (G::OH / 2) * (G::OW / 2) * 4;
+  if constexpr (G::COUT % 32 == 0) {
+    using TS = Tile<32, 32, 2, 2, conv_bk<G::KK>()>;
+    if (cdiv(M, T::BM) * cdiv(G::COUT, T::BN) < 512) return launch_gemm<TS>(la, lb, ep, M, G::COUT, G::KK, 1, s);
+  }
+  return launch_gemm<T>(la, lb, ep, M, G::COUT, G::KK, 1, s);
+}
+
 // dW (+db) of a conv: [im2col(X), 1]^T . dY  -> grad[(KK+1) x COUT] (weights then biases), as a
 // GEMM job into K-split slabs (one split: straight into gwb, [M][COUT] = the S = 1 slab layout)
 // and the slab-sum job that finishes it (no job when unsplit).
@@ -798,84 +816,22 @@ static auto conv_dgrad_job(const float *dY, const float *Wt, const float *Xact, 
   }
 }
 
+// dX of a stride-1 conv whose input is the pooled output of conv GJ: the MaxPoolGrad routing and
+// the activation mask run in the epilogue (EpMaskedUnpool), straight into GJ's full-res gradient.
+template <class G, class GJ>
+static auto conv_dgrad_unpool_job(const float *dY, const float *Wt, const float *Pj, const uint8_t *argj,
+                                  float *dactj, int B, int act, float alpha) {
+  using T = TileConvDgrad<G>;
+  static_assert(!PhaseGeom<G>::OK, "pooled inputs feed stride-1 convs (networks.py:206-225)");
+  return gemm_job<T>(LdConvBwdA<G>{dY}, LdConvBwdB<G>{Wt}, EpMaskedUnpool<GJ>{dactj, Pj, argj, act, alpha},
+                     B * G::H * G::W, G::CIN, G::KH * G::KW * G::COUT, 1);
+}
+
 #define MT_TRY(x)              \
   do {                         \
     int rc_ = (x);             \
     if (rc_ != MT_OK) return rc_; \
   } while (0)
-
-// 2x2/2 VALID max pool over NHWC (networks.py:108-110): one thread per output float4 of channels.
-__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float *__restrict__ X, int B, int H, int W,
-                                                          int C, float *__restrict__ Y) {
-  const int OH = H / 2, OW = W / 2, C4 = C / 4;
-  const size_t total = (size_t)B * OH * OW * C4;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int c4 = (int)(i % C4);
-    size_t r = i / C4;
-    const int ox = (int)(r % OW);
-    r /= OW;
-    const int oy = (int)(r % OH);
-    const int b = (int)(r / OH);
-    const f32x4 *x = reinterpret_cast<const f32x4 *>(X) + (((size_t)b * H + 2 * oy) * W + 2 * ox) * C4 + c4;
-    const f32x4 a = x[0], bq = x[C4], c = x[(size_t)W * C4], d = x[(size_t)W * C4 + C4];
-    f32x4 m;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) m[e] = fmaxf(fmaxf(a[e], bq[e]), fmaxf(c[e], d[e]));
-    reinterpret_cast<f32x4 *>(Y)[i] = m;
-  }
-}
-
-// MaxPoolGrad: the pooled gradient goes to the first maximum of the window in (row, col) order;
-// every other input position (and the dropped odd row/col) gets 0. dP is already masked by the
-// activation derivative (act'(P) == act'(X[argmax])).
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float *__restrict__ X,
-                                                          const float *__restrict__ P,
-                                                          const float *__restrict__ dP, int B, int H,
-                                                          int W, int C, float *__restrict__ dX) {
-  const int OH = H / 2, OW = W / 2, C4 = C / 4;
-  const size_t total = (size_t)B * H * W * C4;  // one thread per input float4
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int c4 = (int)(i % C4);
-    size_t r = i / C4;
-    const int x = (int)(r % W);
-    r /= W;
-    const int y = (int)(r % H);
-    const int b = (int)(r / H);
-    const int oy = y / 2, ox = x / 2;
-    f32x4 g = {0.f, 0.f, 0.f, 0.f};
-    if (oy < OH && ox < OW) {
-      const size_t pi = (((size_t)b * OH + oy) * OW + ox) * C4 + c4;
-      const f32x4 p = reinterpret_cast<const f32x4 *>(P)[pi];
-      const f32x4 dp = reinterpret_cast<const f32x4 *>(dP)[pi];
-      const f32x4 *xw = reinterpret_cast<const f32x4 *>(X) + (((size_t)b * H + 2 * oy) * W + 2 * ox) * C4 + c4;
-      const f32x4 w0 = xw[0], w1 = xw[C4], w2 = xw[(size_t)W * C4], w3 = xw[(size_t)W * C4 + C4];
-      const int pos = (y - 2 * oy) * 2 + (x - 2 * ox);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int first = w0[e] == p[e] ? 0 : (w1[e] == p[e] ? 1 : (w2[e] == p[e] ? 2 : 3));
-        g[e] = first == pos ? dp[e] : 0.f;
-      }
-    }
-    reinterpret_cast<f32x4 *>(dX)[i] = g;
-  }
-}
-
-static int maxpool_fwd(const float *X, int B, int H, int W, int C, float *Y, hipStream_t s) {
-  const size_t total = (size_t)B * (H / 2) * (W / 2) * (C / 4);
-  const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks), dim3(256), 0, s, X, B, H, W, C, Y);
-  MT_LAUNCHED();
-  return MT_OK;
-}
-
-static int maxpool_bwd(const float *X, const float *P, const float *dP, int B, int H, int W, int C,
-                       float *dX, hipStream_t s) {
-  const size_t total = (size_t)B * H * W * (C / 4);
-  const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks), dim3(256), 0, s, X, P, dP, B, H, W, C, dX);
-  MT_LAUNCHED();
-  return MT_OK;
-}
 
 template <class Ar, int I>
 static const float *layer_out(float *ws, const WsLayout &L) {
@@ -888,10 +844,12 @@ static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, 
   if constexpr (I < Ar::NCONV) {
     using G = LayerG<Ar, I>;
     const float *W = P + n->off_conv[I];
-    MT_TRY((conv_forward<G, I == 0>(x, W, W + G::KK * G::COUT, ws + L.act[I], B, n->cfg.activation,
-                                    n->cfg.alpha_leaky, s)));
     if constexpr (pooled<Ar, I>())
-      MT_TRY(maxpool_fwd(ws + L.act[I], B, G::OH, G::OW, G::COUT, ws + L.pool[I], s));
+      MT_TRY((conv_forward_pool<G, I == 0>(x, W, W + G::KK * G::COUT, ws + L.pool[I], (uint8_t *)(ws + L.parg[I]), B,
+                                           n->cfg.activation, n->cfg.alpha_leaky, s)));
+    else
+      MT_TRY((conv_forward<G, I == 0>(x, W, W + G::KK * G::COUT, ws + L.act[I], B, n->cfg.activation,
+                                      n->cfg.alpha_leaky, s)));
     return trunk_forward<Ar, I + 1>(n, P, layer_out<Ar, I>(ws, L), B, ws, L, s);
   }
   return MT_OK;
@@ -922,11 +880,10 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
     constexpr int J = I - 1;
     using GJ = LayerG<Ar, J>;
     if constexpr (pooled<Ar, J>()) {
-      MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J], ws + L.dpool[J], B,
-                                               act, al),
+      MT_TRY(launch_group(s, conv_dgrad_unpool_job<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
+                                                           (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act,
+                                                           al),
                           wg.gemm, pending));
-      MT_TRY(maxpool_bwd(ws + L.act[J], ws + L.pool[J], ws + L.dpool[J], B, GJ::OH, GJ::OW, GJ::COUT,
-                         ws + L.dact[J], s));
     } else {
       MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
                                                act, al),
@@ -963,7 +920,7 @@ static void shift_rows(WsLayout &L, size_t row0) {
     if constexpr (pooled<Ar, I>()) {
       const size_t p = row0 * (G::OH / 2) * (G::OW / 2) * G::COUT;
       L.pool[I] += p;
-      L.dpool[I] += p;
+      L.parg[I] += p / 4;
     }
     shift_rows<Ar, I + 1>(L, row0);
   }
@@ -1083,7 +1040,7 @@ static int heads_backward(const mt_net *n, const float *P, int B, float *ws, con
 // Backward of the non-LSTM archs as grouped launches (gemm.h, launch_group): each launch runs
 // every product whose inputs the previous one completed — loss | dense dX + dense dW + head dW |
 // per conv layer I (top down): conv dX + conv dW + the slab sum of layer I+1's dW | conv1's slab
-// sum — 2 + NCONV launches (+ max-pool backward kernels) instead of two or three per layer.
+// sum — 2 + NCONV launches (the max pools are fused into the conv products) instead of two or three per layer.
 template <class Ar>
 static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
                          const float *pi, const float *rep, const float *v, const int32_t *a_idx,
@@ -1105,21 +1062,12 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
   const auto dw = gemm_job<TileDenseW>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
                                        EpStore{grad + n->off_fc, Ar::F}, Ar::FLAT + 1, Ar::F, B, 1);
   const HeadWgradJob hw = head_wgrad_job<Ar>(n, B, ws, L, grad);
-  // dense dX: dH . W^T, masked by the last conv's (pooled) activation, then through its pool
-  if constexpr (pooled<Ar, K>()) {
-    using GK = LayerG<Ar, K>;
-    MT_TRY(launch_group(s, gemm_job<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
-                                                EpMasked{ws + L.dpool[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT,
-                                                Ar::F, 1),
-                        dw, hw));
-    MT_TRY(maxpool_bwd(ws + L.act[K], ws + L.pool[K], ws + L.dpool[K], B, GK::OH, GK::OW, GK::COUT,
-                       ws + L.dact[K], s));
-  } else {
-    MT_TRY(launch_group(s, gemm_job<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
-                                                EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT,
-                                                Ar::F, 1),
-                        dw, hw));
-  }
+  // dense dX: dH . W^T, masked by the last conv's activation (every trunk ends in an unpooled conv)
+  static_assert(!pooled<Ar, K>(), "the trunk ends in an unpooled conv (networks.py:178-278)");
+  MT_TRY(launch_group(s, gemm_job<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+                                              EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT,
+                                              Ar::F, 1),
+                      dw, hw));
   return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s, SlabJob{}, no);
 }
 
