@@ -70,7 +70,10 @@ struct FusedNips {
   // conv kernel waves: 8 for gray frames (two waves per SIMD hide each other's LDS/convert
   // latency in conv1), 4 for RGB (whose 3x input rows would not fit 64 KB of LDS beside 8 waves'
   // partials)
-  static constexpr int NW = C == 4 ? 8 : 4, NT = 64 * NW;
+#ifndef MT_NIPS_NW_GRAY
+#define MT_NIPS_NW_GRAY 8
+#endif
+  static constexpr int NW = C == 4 ? MT_NIPS_NW_GRAY : 4, NT = 64 * NW;
   static_assert(KC1 % NW == 0 && KC2 % NW == 0, "K chunks split over the waves");
   static constexpr int IN_BYTES = RIN * 84 * C;
   static constexpr int FR_BYTES = RIN * 84 * D;  // the block's rows of one new frame
@@ -215,6 +218,7 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
 #pragma unroll
         for (int t = 0; t < Fz::MT1; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], b1f[j][s], acc[t], 0, 0, 0);
     }
+    MT_PROBE_AT(0, bid, 6);  // (wave 0) conv1 products issued
 #pragma unroll
     for (int t = 0; t < Fz::MT1; ++t)
 #pragma unroll
@@ -232,6 +236,7 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
       for (int s = 0; s < 4; ++s) b2f[j][nt][s] = W2[(size_t)(k0 + s) * Fz::CO2 + nt * 16 + r];
   }
   __syncthreads();
+  MT_PROBE_AT(0, bid, 7);  // every wave's conv1 partials in LDS
   {
     const float *b1 = W1 + (size_t)Fz::KK1 * Fz::CO1;
     constexpr int P = Fz::MT1 * 16 * Fz::CO1;  // stride of one wave's partials

@@ -29,6 +29,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='pong-nips')
     ap.add_argument('--updates', type=int, default=20)
+    ap.add_argument('--isolated', action='store_true',
+                    help='time the roofline launch alone (mt_forward_trunk_stacking, every env published, as '
+                         'bench.py / tools/trunk_only.py) instead of a rollout step')
     a = ap.parse_args()
     import torch
     import bench
@@ -57,6 +60,18 @@ def main():
     for t in range(L.max_local_steps):  # the last chain armed is the bootstrap forward's
         L.step(t)
     torch.cuda.synchronize()
+    if a.isolated:
+        E_ = cfg['ec']
+        depth_ = 3 if cfg['rgb'] else 1
+        g = torch.Generator(device='cuda').manual_seed(11)
+        pushes = torch.randint(0, 256, (4 * E_, 84, 84, depth_), dtype=torch.uint8, device='cuda', generator=g)
+        ready = torch.zeros(E_, 32, dtype=torch.int32)
+        ready[:, 0] = (7 << 3) | 2
+        ready = ready.cuda()
+        out = torch.empty_like(L.states[0])
+        for _ in range(10):
+            L.network.forward_trunk_stacking(L.states[0], pushes, ready, 7, out, E_, ws_key='rollout')
+        torch.cuda.synchronize()
     buf[:] = 0
     _lib.check(lib.mt_probe_read(C.c_void_p(buf.ctypes.data), buf.size), 'mt_probe_read')
     P = buf.reshape(4, 512, 8).astype(np.int64)
@@ -77,6 +92,10 @@ def main():
               '(median %+7.2f), copies done ..%+7.2f us, copy med %.2f us' % (
                   us(pstart.min()), us(seen.min()), us(seen.max()), us(np.median(seen)), us(done.max()),
                   us(np.median(done - seen))))
+    c1 = P[0, :nblocks[0]]
+    if c1[:, 6].any():  # conv1 sub-phases (wave 0): products issued, partials in LDS, reduced
+        print('conv1  sub-phases med: mfma %.2f  partial write+barrier %.2f  reduce+act %.2f us' % (
+            us(np.median(c1[:, 6] - c1[:, 1])), us(np.median(c1[:, 7] - c1[:, 6])), us(np.median(c1[:, 2] - c1[:, 7]))))
     pub = P[0, :nblocks[0], 5]
     if pub.any():  # in-kernel pull: when each conv block saw its env published (blockIdx order)
         pub = pub - t0
@@ -88,6 +107,8 @@ def main():
         name, ph = PHASES[k]
         n = nblocks[k]
         p = P[k, :n, :len(ph) + 1]
+        if a.isolated and k == 2:
+            break
         start, end = p[:, 0], p[:, -1]
         line = '%-6s blocks %4d  start %+7.2f..%+7.2f us  end %+7.2f..%+7.2f us  block dur med %.2f max %.2f' % (
             name, n, us(start.min() - t0), us(start.max() - t0), us(end.min() - t0), us(end.max() - t0),
