@@ -781,12 +781,62 @@ static int conv_forward_pool(const void *X, const float *Wt, const float *bias, 
   return launch_gemm<T>(la, lb, ep, M, G::COUT, G::KK, 1, s);
 }
 
-// dW (+db) of a conv: [im2col(X), 1]^T . dY  -> grad[(KK+1) x COUT] (weights then biases), as a
-// GEMM job into K-split slabs (one split: straight into gwb, [M][COUT] = the S = 1 slab layout)
-// and the slab-sum job that finishes it (no job when unsplit).
+// Bias gradient rows of a split conv weight gradient: block z sums dY over split z's GEMM-K range
+// [z*kchunk, min(K, (z+1)*kchunk)) (pixels) for every channel and writes the sum to row KK of slab
+// z (the slab sum then adds the splits in z order, as for the weight rows). 256 threads = 16 row
+// subsets x 16 channel lanes; subsets summed in fixed order through LDS.
+template <int COUT>
+struct BiasRowJob {
+  const float *dY = nullptr;  // [K][COUT]
+  float *out = nullptr;       // slab row KK of split z at out + z * zstride
+  size_t zstride = 0;
+  int K = 0, kchunk = 0, nz = 0;
+  __host__ __device__ int blocks() const { return nz; }
+  size_t lds() const { return sizeof(float) * 256; }
+  __device__ __forceinline__ void run(int z, float *smem) const {
+    static_assert(COUT % 16 == 0 || COUT < 16, "channel lanes");
+    const int k0 = z * kchunk, k1 = min(K, k0 + kchunk);
+    const int sub = threadIdx.x >> 4, c = threadIdx.x & 15;
+    for (int n0 = 0; n0 < COUT; n0 += 16) {
+      float acc = 0.f;
+      if (n0 + c < COUT)
+        for (int k = k0 + sub; k < k1; k += 16) acc += dY[(size_t)k * COUT + n0 + c];
+      smem[threadIdx.x] = acc;
+      __syncthreads();
+      if (sub == 0 && n0 + c < COUT) {
+        float t = smem[c];
+#pragma unroll
+        for (int u = 1; u < 16; ++u) t += smem[u * 16 + c];
+        out[(size_t)z * zstride + n0 + c] = t;
+      }
+      __syncthreads();
+    }
+  }
+};
+
+// Two jobs as one (blocks of the first, then the second): the dW GEMM and its bias-row sums.
+template <class J1, class J2>
+struct PairJob {
+  J1 a;
+  J2 b;
+  __host__ __device__ int blocks() const { return a.blocks() + b.blocks(); }
+  size_t lds() const { return std::max(a.blocks() ? a.lds() : 0, b.blocks() ? b.lds() : 0); }
+  __device__ __forceinline__ void run(int id, float *smem) const {
+    if (id < a.blocks())
+      a.run(id, smem);
+    else
+      b.run(id - a.blocks(), smem);
+  }
+};
+
+// dW (+db) of a conv -> grad[(KK+1) x COUT] (weights then biases): dW = im2col(X)^T . dY as a GEMM
+// job over the KK weight rows into K-split slabs [S][KK+1][COUT] (one split: straight into gwb),
+// db = the column sums of dY per split into slab row KK (BiasRowJob: a 64-row MFMA tile for the
+// single bias row would be a fifth of the product's work), and the slab-sum job that finishes it
+// (no job when unsplit).
 template <class G, bool U8>
 struct WgradJobs {
-  GemmJob<TileConvWgrad<G>, LdIm2colT<G, U8>, LdColMajor, EpSlab> gemm;
+  PairJob<GemmJob<TileConvWgrad<G>, LdIm2colT<G, U8>, LdColMajor, EpSlab>, BiasRowJob<G::COUT>> gemm;
   SlabJob sum;
 };
 template <class G, bool U8>
@@ -796,8 +846,12 @@ static WgradJobs<G, U8> conv_wgrad_jobs(const void *X, const float *dY, float *s
   const int S = conv_wgrad_splits<G>(B);
   LdIm2colT<G, U8> la{reinterpret_cast<const typename InElem<U8>::T *>(X)};
   LdColMajor lb{dY, G::COUT, -1};
-  if (S == 1) return {gemm_job<T>(la, lb, EpSlab{gwb, M, G::COUT}, M, G::COUT, K, 1), SlabJob{}};
-  return {gemm_job<T>(la, lb, EpSlab{slab, M, G::COUT}, M, G::COUT, K, S), SlabJob{slab, S, (size_t)M * G::COUT, gwb}};
+  float *dst = S == 1 ? gwb : slab;
+  const auto g = gemm_job<T>(la, lb, EpSlab{dst, M, G::COUT}, G::KK, G::COUT, K, S);
+  const BiasRowJob<G::COUT> bias{dY, dst + (size_t)G::KK * G::COUT, (size_t)M * G::COUT, K, g.kchunk, g.gz};
+  WgradJobs<G, U8> j{{g, bias}, SlabJob{}};
+  if (g.gz > 1) j.sum = SlabJob{slab, g.gz, (size_t)M * G::COUT, gwb};
+  return j;
 }
 
 // dX of a conv (transposed-conv gather), masked by the activation derivative of X, as a GEMM job.
