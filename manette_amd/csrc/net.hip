@@ -480,9 +480,9 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   __shared__ float zs[64];
   const int F = hp.F, O = 1 + hp.A + hp.R;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // the head weights of this wave's first two outputs (o = w, w + 4) and the row's draw counter
+  // the head weights of this wave's first PRE outputs (o = w, w + 4, ...) and the row's draw counter
   // do not depend on the slabs: requested before the slab loads so their latency overlaps
-  constexpr int PRE = 2, FMAX = 8;  // F <= 512
+  constexpr int PRE = 6, FMAX = 8;  // F <= 512; 4 * PRE = 24 >= 1 + A + R of every bench config
   float wpre[PRE][FMAX];
 #pragma unroll
   for (int k = 0; k < PRE; ++k)
