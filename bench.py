@@ -276,8 +276,8 @@ def main():
     if learner.native_step is not None:
         import ctypes as C
         from manette_amd import _lib
-        stats = (C.c_double * 5)()
-        _lib.hip().mt_rollout_stats(learner.native_step, stats, 1)
+        stats = (C.c_double * 7)()
+        _lib.hip().mt_rollout_stats_ex(learner.native_step, stats, 7, 1)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         one_update()
@@ -286,10 +286,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if stats is not None:
-        _lib.hip().mt_rollout_stats(learner.native_step, stats, 0)
+        _lib.hip().mt_rollout_stats_ex(learner.native_step, stats, 7, 0)
         n = max(stats[4], 1)
         step_phases = {k: round(stats[i] / n, 2) for i, k in enumerate(
             ['launch_and_wait_us', 'emulators_us', 'bookkeeping_us', 'upload_enqueue_us'])}
+        # launch_and_wait = host launches (this step's forward if not armed + the chains armed
+        # ahead) + the spin for this step's sampled indices
+        step_phases['of_which_enqueue_us'] = round(stats[5] / n, 2)
+        step_phases['of_which_wait_us'] = round(stats[6] / n, 2)
     else:
         step_phases = None
     if world > 1:

@@ -365,6 +365,13 @@ int mt_rollout_run(mt_rollout *ro, const float *params, int64_t *global_step, mt
  * for the sampled indices, [1] emulator step, [2] bookkeeping, [3] upload + preprocess
  * enqueue, [4] number of steps. reset != 0 zeroes the counters. */
 int mt_rollout_stats(mt_rollout *ro, double *out5, int reset);
+/* mt_rollout_stats plus the split of [0]: out[5] = host enqueue (the step's forward and the armed
+ * chains' launches), out[6] = wait for the sampled indices; n = how many of the 7 values to copy. */
+int mt_rollout_stats_ex(mt_rollout *ro, double *out, int n, int reset);
+/* Host timeline of the last min(max_steps, 256) macro-steps, oldest first, 6 doubles each:
+ * t, then host wall microseconds at the call's start, after its launches, when the sampled
+ * indices were seen, after the emulator step, after the bookkeeping (diagnostics). */
+int mt_rollout_host_trace(mt_rollout *ro, double *out, int max_steps, int *n);
 /* Live timing of the trunk kernels the rollout runs (roofline measurement, bench.py): enable != 0
  * records an event pair around each step forward's trunk launches (NIPS: the stacking conv kernel
  * + the dense kernel); a call with enable == 0 waits for them and returns their summed duration

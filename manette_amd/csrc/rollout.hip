@@ -20,7 +20,8 @@ struct mt_rollout {
   mh_book *book;
   mt_rollout_buffers b;
   uint64_t seed;
-  hipEvent_t ev2[4];  // pair of step t ready: ev2[t & 3]
+  std::vector<hipEvent_t> ev;  // [T] pair of step t ready (recorded once per rollout: chains are armed
+                               // up to T steps ahead)
   bool zero_copy, in_place, pooled, resized, pipelined;
   bool pull;          // pipelined + resized: per-env ready words, pull kernel into HBM, tagged pairs
   bool stack_fwd;     // pull + NIPS: the forward's conv kernel stacks (no preprocess launch)
@@ -28,7 +29,7 @@ struct mt_rollout {
   const uint8_t *fstore = nullptr;  // LSTM: the frame store (states = its slot 4)
   const float *over_dev = nullptr;  // LSTM: device address of the pinned episode-end flags
   int armed_upto = -1;  // pipelined: last step whose chain (forward) is already enqueued
-  int ahead = 1;        // pipelined: steps armed ahead (2 with pull)
+  int ahead = 1;        // pipelined: steps armed ahead (T: every chain of the rollout at its step 0)
   std::vector<uint32_t> fwd_of;  // [T] draw sequence number of step t's forward
   uint32_t seq = 0;   // host step sequence word value last stored
   uint8_t *staging_dev;  // device addresses of the host-mapped buffers (zero-copy mode)
@@ -43,7 +44,10 @@ struct mt_rollout {
   uint64_t *packed_host = nullptr, *packed_dev = nullptr;
   uint8_t *frames_hbm = nullptr;   // [4E][84*84*depth] HBM copy of the pushes (pull kernel)
   int32_t *count_hbm = nullptr;    // [E] push counts
-  double acc[5];  // host wall us: launch+wait for indices, runner, book, upload+preprocess enqueue; steps
+  double trace[256][6];  // host timestamps (us) of the last 256 steps: t, start, enqueued, indices, emulated, booked
+  int64_t ntrace = 0;
+  double acc[7];  // host wall us: launch+wait for indices, runner, book, upload+preprocess enqueue; steps;
+                  // then the launch+wait split: enqueue (forward / armed chains), wait for the indices
   // mt_rollout_trunk_timing: event pairs recorded around each step forward's trunk launches
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> marks;
@@ -161,12 +165,17 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
     std::memset(ro->env_ready_host, 0, sizeof(uint32_t) * E * MH_READY_STRIDE);
     std::memset(ro->packed_host, 0, sizeof(uint64_t) * E);
   }
-  ro->ahead = ro->pull ? 2 : 1;
+  // every chain of a rollout is armed by its step 0 call, right behind the step-0 forward: that
+  // call waits for the update + the step-0 chain anyway (~80 us), so the ~11 us of launches per
+  // chain land there instead of in front of the later steps' waits (step 1 was host-bound)
+  ro->ahead = T;
+  if (const char *v = std::getenv("MT_ROLLOUT_AHEAD")) ro->ahead = std::max(1, std::min(T, std::atoi(v)));
   ro->fwd_of.assign(T, 0);
-  for (int i = 0; i < 4; ++i) {
-    hipError_t e = hipEventCreateWithFlags(&ro->ev2[i], hipEventDisableTiming);
+  ro->ev.assign(T, nullptr);
+  for (int i = 0; i < T; ++i) {
+    hipError_t e = hipEventCreateWithFlags(&ro->ev[i], hipEventDisableTiming);
     if (e != hipSuccess) {
-      for (int j = 0; j < i; ++j) (void)hipEventDestroy(ro->ev2[j]);
+      for (int j = 0; j < i; ++j) (void)hipEventDestroy(ro->ev[j]);
       delete ro;
       set_error("hipEventCreate: %s", hipGetErrorString(e));
       return MT_ERR_HIP;
@@ -178,7 +187,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
 
 extern "C" void mt_rollout_destroy(mt_rollout *ro) {
   if (!ro) return;
-  for (int i = 0; i < 4; ++i) (void)hipEventDestroy(ro->ev2[i]);
+  for (hipEvent_t e : ro->ev) (void)hipEventDestroy(e);
   for (auto &m : ro->marks) {
     (void)hipEventDestroy(m.first);
     (void)hipEventDestroy(m.second);
@@ -356,7 +365,7 @@ int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, b
   }
   if (!ro->zero_copy)
     MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
-  MT_HIP(hipEventRecord(ro->ev2[t & 3], s));
+  MT_HIP(hipEventRecord(ro->ev[t], s));
   return MT_OK;
 }
 
@@ -457,10 +466,11 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
     ro->armed_upto = t;
   }
   // 2. pipelined: arm steps up to t + depth (at most T) while the GPU works on step t, so the
-  //    launches are off the critical path (stack_fwd: two steps ahead — the GPU chain after the
+  //    launches are off the critical path (every chain at step 0, see ahead — the GPU chain after the
   //    emulators is shorter than the launches of a chain)
   if (ro->pipelined)
     for (int k = ro->armed_upto + 1; k <= std::min(t + ro->ahead, T); ++k) MT_TRY_(arm_step(ro, params, k, k - t, s));
+  const double t0w = now_us();
   // 3. wait for the indices of step t (spin: a blocking wait sleeps past the chain and pays the
   //    wake-up latency)
   // (with ready flags: poll the E flags the heads kernel stores after each pair — one cached host
@@ -480,7 +490,7 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
       __builtin_ia32_pause();
       if (++spins == 4096) {
         spins = 0;
-        const hipError_t q = hipEventQuery(ro->ev2[t & 3]);
+        const hipError_t q = hipEventQuery(ro->ev[t]);
         if (q != hipSuccess && q != hipErrorNotReady) MT_HIP(q);
       }
     }
@@ -494,13 +504,13 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
       __builtin_ia32_pause();
       if (++spins == 4096) {
         spins = 0;
-        const hipError_t q = hipEventQuery(ro->ev2[t & 3]);
+        const hipError_t q = hipEventQuery(ro->ev[t]);
         if (q != hipSuccess && q != hipErrorNotReady) MT_HIP(q);
       }
     }
   } else {
     hipError_t q;
-    while ((q = hipEventQuery(ro->ev2[t & 3])) == hipErrorNotReady) __builtin_ia32_pause();
+    while ((q = hipEventQuery(ro->ev[t])) == hipErrorNotReady) __builtin_ia32_pause();
     MT_HIP(q);
   }
   if (ro->pipelined && __atomic_load_n(&b.sync_host[1], __ATOMIC_ACQUIRE) != 0) {
@@ -547,6 +557,17 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   ro->acc[2] += t3 - t2;
   ro->acc[3] += t4 - t3;
   ro->acc[4] += 1;
+  {
+    double *tr = ro->trace[ro->ntrace++ & 255];
+    tr[0] = t;
+    tr[1] = t0;
+    tr[2] = t0w;
+    tr[3] = t1;
+    tr[4] = t2;
+    tr[5] = t3;
+  }
+  ro->acc[5] += t0w - t0;
+  ro->acc[6] += t1 - t0w;
   if (rc == MT_OK && t == T - 1) ro->rollouts += 1;
   return rc;
 }
@@ -570,6 +591,25 @@ extern "C" int mt_rollout_stats(mt_rollout *ro, double *out5, int reset) {
 // enable == 0 stops, waits for the recorded events and returns their summed duration (us) and
 // count, then forgets them. Each pair spans the trunk kernels of one forward (NIPS: the stacking
 // conv kernel + the dense kernel) and the boundary between them.
+extern "C" int mt_rollout_stats_ex(mt_rollout *ro, double *out, int n, int reset) {
+  MT_CHECK_ARG(ro && out && n >= 0, "bad argument");
+  for (int i = 0; i < n && i < 7; ++i) out[i] = ro->acc[i];
+  if (reset)
+    for (int i = 0; i < 7; ++i) ro->acc[i] = 0;
+  return MT_OK;
+}
+
+extern "C" int mt_rollout_host_trace(mt_rollout *ro, double *out, int max_steps, int *n) {
+  MT_CHECK_ARG(ro && out && n && max_steps >= 0, "bad argument");
+  const int64_t have = std::min<int64_t>(std::min<int64_t>(ro->ntrace, 256), max_steps);
+  for (int64_t k = 0; k < have; ++k) {
+    const double *tr = ro->trace[(ro->ntrace - have + k) & 255];
+    for (int j = 0; j < 6; ++j) out[k * 6 + j] = tr[j];
+  }
+  *n = (int)have;
+  return MT_OK;
+}
+
 extern "C" int mt_rollout_trunk_timing(mt_rollout *ro, int enable, double *sum_us, int64_t *count) {
   MT_CHECK_ARG(ro, "null argument");
   double total = 0.0;

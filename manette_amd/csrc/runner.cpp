@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <climits>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -270,18 +271,23 @@ struct mh_runner {
     }
   }
 
+  // Idle workers spin for kSpinUs of wall time before sleeping on the generation word: the longest
+  // regular pause between two emulator steps is the update (the learner's backward + RMSProp and
+  // the next rollout's first forward, ~0.1 ms), and a futex wake-up there cost ~10 us on the
+  // critical path of every update (a fixed spin count measured ~85 us of pause on the box).
+  static constexpr int64_t kSpinUs = 2000;
   void worker(int w) {
     uint32_t seen = 0;
     for (;;) {
-      // spin briefly, then sleep on the generation word
+      // spin, then sleep on the generation word
       int spins = 0;
       uint32_t g;
+      auto t0 = std::chrono::steady_clock::now();
       while ((g = gen.load(std::memory_order_acquire)) == seen) {
-        if (++spins < 4000) {
-          cpu_relax();
-        } else {
+        cpu_relax();
+        if ((++spins & 255) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs))
           gen.wait(seen, std::memory_order_acquire);
-        }
       }
       seen = g;
       if (quit.load(std::memory_order_acquire)) return;
