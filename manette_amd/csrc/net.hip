@@ -12,6 +12,7 @@
 
 #include "gemm.h"
 #include "trunk_fused.h"
+#include "wgrad_s4.h"
 
 namespace mt {
 
@@ -248,6 +249,7 @@ static int conv_wgrad_splits(int B) {
 
 template <class G>
 static size_t conv_wgrad_slab(int B) {
+  if constexpr (is_conv1_s4<G>()) return (size_t)B * (G::KK + 1) * G::COUT;  // Conv1S4WgradJob: a slab per image
   const int s = conv_wgrad_splits<G>(B);
   return s > 1 ? (size_t)s * (G::KK + 1) * G::COUT : 0;
 }
@@ -854,6 +856,23 @@ static WgradJobs<G, U8> conv_wgrad_jobs(const void *X, const float *dY, float *s
   return j;
 }
 
+// The input conv of the NIPS / NATURE trunks: phase-major product per image + slab sum (wgrad_s4.h).
+template <class G>
+struct Conv1S4Jobs {
+  Conv1S4WgradJob<G::CIN, G::COUT> gemm;
+  SlabJob sum;
+};
+template <class G>
+static Conv1S4Jobs<G> conv1_s4_wgrad_jobs(const uint8_t *X, const float *dY, float *slab, float *gwb, int B) {
+  Conv1S4Jobs<G> j;
+  j.gemm.X = X;
+  j.gemm.dY = dY;
+  j.gemm.slab = slab;
+  j.gemm.B = B;
+  j.sum = SlabJob{slab, B, (size_t)(G::KK + 1) * G::COUT, gwb};
+  return j;
+}
+
 // dX of a conv (transposed-conv gather), masked by the activation derivative of X, as a GEMM job.
 template <class G>
 static auto conv_dgrad_job(const float *dY, const float *Wt, const float *Xact, float *dX, int B, int act,
@@ -928,8 +947,13 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
   const void *x = I == 0 ? (const void *)obs : (const void *)layer_out<Ar, (I > 0 ? I - 1 : 0)>(ws, L);
-  const auto wg = conv_wgrad_jobs<G, I == 0>(x, ws + L.dact[I], ws + (I % 2 ? L.wslab2 : L.wslab),
-                                             grad + n->off_conv[I], B);
+  const auto wg = [&] {
+    if constexpr (I == 0 && is_conv1_s4<G>())
+      return conv1_s4_wgrad_jobs<G>(obs, ws + L.dact[0], ws + L.wslab, grad + n->off_conv[0], B);
+    else
+      return conv_wgrad_jobs<G, I == 0>(x, ws + L.dact[I], ws + (I % 2 ? L.wslab2 : L.wslab), grad + n->off_conv[I],
+                                        B);
+  }();
   if constexpr (I > 0) {
     constexpr int J = I - 1;
     using GJ = LayerG<Ar, J>;
