@@ -67,18 +67,22 @@ struct FusedNips {
   static constexpr int M1 = ROWS1 * OW1;  // 80 conv1 pixels
   static constexpr int MT1 = (M1 + 15) / 16;  // 5 m-tiles
   static constexpr int KC1 = KK1 / 16, KC2 = KK2 / 16;
-  // conv kernel waves: 8 for gray frames (two waves per SIMD hide each other's LDS/convert
-  // latency in conv1), 4 for RGB (whose 3x input rows would not fit 64 KB of LDS beside 8 waves'
-  // partials)
+  // conv kernel waves. Gray frames: 10 waves = conv1's 5 M-tiles x 2 K-halves ("units": each
+  // output is the sum of 2 partials, conv2 = 2 N-tiles x 4 K-quarters on 8 of them, 4 partials);
+  // the former 8-wave K-split (every wave all 5 tiles over 1/8 of K) spent ~1.1 us per block
+  // writing and reducing 8 partials per output. RGB: 4 waves splitting K (its 3x input rows would
+  // not fit 64 KB of LDS beside more waves' partials).
 #ifndef MT_NIPS_NW_GRAY
-#define MT_NIPS_NW_GRAY 8
+#define MT_NIPS_NW_GRAY 10
 #endif
   static constexpr int NW = C == 4 ? MT_NIPS_NW_GRAY : 4, NT = 64 * NW;
-  static_assert(KC1 % NW == 0 && KC2 % NW == 0, "K chunks split over the waves");
+  static constexpr bool UNITS = NW == 10;
+  static_assert(UNITS ? (C == 4 && KC1 == 16 && KC2 == 16)
+                      : (KC1 % NW == 0 && KC2 % NW == 0), "K chunks split over the waves");
   static constexpr int IN_BYTES = RIN * 84 * C;
   static constexpr int FR_BYTES = RIN * 84 * D;  // the block's rows of one new frame
   // LDS (floats unless noted)
-  static constexpr int RED_FLOATS = NW * MT1 * 16 * CO1;  // >= NW*16*32 (conv2)
+  static constexpr int RED_FLOATS = UNITS ? 10 * 16 * CO1 : NW * MT1 * 16 * CO1;  // >= conv2's partials
   static_assert(4 * FR_BYTES <= RED_FLOATS * 4, "staged frames alias the reduction buffer");
   static constexpr size_t LDS_BYTES = IN_BYTES + sizeof(float) * (RED_FLOATS + M1 * A1S);
   // fc kernel
@@ -179,13 +183,14 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
 
-  // conv1 weight fragments of this wave's K chunks (c = w + NW j): B[k][n] = W1[k*16 + n]
+  // conv1 weight fragments of this wave's K chunks: B[k][n] = W1[k*16 + n]. K-split: chunks
+  // c = w + NW j; units: chunks 8h .. 8h+7 of the wave's K-half h = w & 1
   constexpr int NW = Fz::NW;
-  constexpr int J1 = Fz::KC1 / NW;
+  constexpr int J1 = Fz::UNITS ? 8 : Fz::KC1 / NW;
   float b1f[J1][4];
 #pragma unroll
   for (int j = 0; j < J1; ++j) {
-    const int k0 = 16 * (w + NW * j) + 4 * g;
+    const int k0 = 16 * (Fz::UNITS ? 8 * (w & 1) + j : w + NW * j) + 4 * g;
 #pragma unroll
     for (int s = 0; s < 4; ++s) b1f[j][s] = W1[(size_t)(k0 + s) * Fz::CO1 + r];
   }
@@ -194,7 +199,27 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   MT_PROBE_AT(0, bid, 1);
 
   // ---- conv1 (VALID 8x8 stride 4): M = 80 pixels (4 rows x 20), N = 16, K = 64*C ----
-  {
+  if constexpr (Fz::UNITS) {
+    // unit w: M-tile t = w / 2, K-half h = w % 2 (K chunks 8h .. 8h+7)
+    const int t = w >> 1, h = w & 1;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float sc = 1.0f / 255.0f;
+    const int m = min(t * 16 + r, Fz::M1 - 1);
+    const int orow = m / Fz::OW1, ox = m - orow * Fz::OW1;
+    const uint8_t *xb = xin + ((4 * orow) * 84 + 4 * ox) * C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kpos = 4 * (8 * h + j) + g;  // (ky, kx) of k0 = 16 c + 4 g (C = 4: the 4 channels)
+      const uint32_t u = *reinterpret_cast<const uint32_t *>(xb + ((kpos >> 3) * 84 + (kpos & 7)) * C);
+      const f32x4 a = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc, (float)((u >> 16) & 0xff) * sc,
+                            (float)(u >> 24) * sc};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b1f[j][s], acc, 0, 0, 0);
+    }
+    MT_PROBE_AT(0, bid, 6);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[(w * 16 + g * 4 + q) * Fz::CO1 + r] = acc[q];
+  } else   {
     f32x4 acc[Fz::MT1];
 #pragma unroll
     for (int t = 0; t < Fz::MT1; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -224,27 +249,36 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
 #pragma unroll
       for (int q = 0; q < 4; ++q) red[(w * Fz::MT1 * 16 + t * 16 + g * 4 + q) * Fz::CO1 + r] = acc[t][q];
   }
-  // conv2 weight fragments (issued before the barrier so their latency overlaps the reduction)
-  constexpr int J2 = Fz::KC2 / NW;
-  float b2f[J2][2][4];
+  // conv2 weight fragments (issued before the barrier so their latency overlaps the reduction).
+  // K-split: chunks w + NW j, both N-tiles; units (w < 8): N-tile w & 1, chunks 4 (w >> 1) + j
+  constexpr int J2 = Fz::UNITS ? 4 : Fz::KC2 / NW;
+  constexpr int NT2 = Fz::UNITS ? 1 : 2;
+  float b2f[J2][NT2][4];
 #pragma unroll
   for (int j = 0; j < J2; ++j) {
-    const int k0 = 16 * (w + NW * j) + 4 * g;
+    const int k0 = 16 * (Fz::UNITS ? 4 * ((w >> 1) & 3) + j : w + NW * j) + 4 * g;
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
+    for (int nt = 0; nt < NT2; ++nt)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) b2f[j][nt][s] = W2[(size_t)(k0 + s) * Fz::CO2 + nt * 16 + r];
+      for (int s = 0; s < 4; ++s)
+        b2f[j][nt][s] = W2[(size_t)(k0 + s) * Fz::CO2 + (Fz::UNITS ? (w & 1) : nt) * 16 + r];
   }
   __syncthreads();
   MT_PROBE_AT(0, bid, 7);  // every wave's conv1 partials in LDS
   {
     const float *b1 = W1 + (size_t)Fz::KK1 * Fz::CO1;
-    constexpr int P = Fz::MT1 * 16 * Fz::CO1;  // stride of one wave's partials
+    constexpr int P = Fz::MT1 * 16 * Fz::CO1;  // stride of one wave's partials (K-split)
     for (int idx = threadIdx.x; idx < Fz::M1 * Fz::CO1; idx += Fz::NT) {
       const int m = idx / Fz::CO1, n = idx - m * Fz::CO1;
-      float s = red[idx];
+      float s;
+      if constexpr (Fz::UNITS) {  // units 2t (K-half 0) + 2t+1 of tile t = m / 16
+        const int t = m >> 4, rr = m & 15;
+        s = red[((2 * t) * 16 + rr) * Fz::CO1 + n] + red[((2 * t + 1) * 16 + rr) * Fz::CO1 + n];
+      } else {
+        s = red[idx];
 #pragma unroll
-      for (int v = 1; v < NW; ++v) s += red[v * P + idx];  // wave order
+        for (int v = 1; v < NW; ++v) s += red[v * P + idx];  // wave order
+      }
       const float y = act_fwd(s + b1[n], act, alpha);
       a1[m * Fz::A1S + n] = y;
       if (act1 && (m < 2 * Fz::OW1 || i == Fz::ROWS2 - 1))  // conv1 rows 2i, 2i+1 (+ 18, 19)
@@ -255,7 +289,21 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   MT_PROBE_AT(0, bid, 2);
 
   // ---- conv2 row i (VALID 4x4 stride 2): M = 9 pixels (padded to 16), N = 32, K = 256 ----
-  {
+  if constexpr (Fz::UNITS) {
+    if (w < 8) {  // unit w: N-tile w & 1, K-quarter kq = w >> 1 (chunks 4kq .. 4kq+3: ky = kq, kx = j)
+      const int kq = w >> 1;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int ox = min(r, Fz::OW2 - 1);
+#pragma unroll
+      for (int j = 0; j < J2; ++j) {
+        const f32x4 a = *reinterpret_cast<const f32x4 *>(a1 + (kq * Fz::OW1 + 2 * ox + j) * Fz::A1S + 4 * g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b2f[j][0][s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[(w * 16 + g * 4 + q) * 16 + r] = acc[q];
+    }
+  } else   {
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const int ox = min(r, Fz::OW2 - 1);
 #pragma unroll
@@ -280,9 +328,17 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
     constexpr int P = 16 * Fz::CO2;
     for (int idx = threadIdx.x; idx < Fz::FEAT; idx += Fz::NT) {
       const int n = idx & (Fz::CO2 - 1);
-      float s = red[idx];
+      float s;
+      if constexpr (Fz::UNITS) {  // K-quarters 0..3 (in order) of N-tile n / 16: units 2 kq + n / 16
+        const int m = idx >> 5, nt = n >> 4, c = n & 15;
+        s = red[(nt * 16 + m) * 16 + c];
 #pragma unroll
-      for (int v = 1; v < NW; ++v) s += red[v * P + idx];  // wave order
+        for (int kq = 1; kq < 4; ++kq) s += red[((kq * 2 + nt) * 16 + m) * 16 + c];
+      } else {
+        s = red[idx];
+#pragma unroll
+        for (int v = 1; v < NW; ++v) s += red[v * P + idx];  // wave order
+      }
       act2[((size_t)e * Fz::ROWS2 + i) * Fz::FEAT + idx] = act_fwd(s + b2[n], act, alpha);
     }
   }
@@ -342,6 +398,131 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
   MT_PROBE_AT(1, pb, 2);
 }
 
+// Throughput form of the NIPS conv trunk for large batches (gray frames, E >= kPersistMinEnvs):
+// the latency form above recomputes 1.8x of conv1 so that 9 blocks can work on one env; once the
+// grid fills the chip that recompute is pure cost. Here a persistent block (8 waves, one per CU)
+// stages W1 / W2 transposed in LDS once and walks envs e = blockIdx.x, += gridDim.x: the env's
+// 84x84x4 frame in LDS, conv1 as 25 M-tiles of 16 pixels over the 8 waves (A fragment = one u32 of
+// 4 channels, B fragment = one ds_read_b128 of the transposed weights, shared by the wave's
+// tiles), bias + act into an LDS act1 [400][16], then conv2 as 6 M-tiles x 2 N-tiles (12 units:
+// three per SIMD), act2 to HBM in the same NHWC flatten order. The next env's frame is loaded into
+// registers during conv2. Same fp32 products (k-ordered MFMA chains) as the latency form.
+constexpr int kPersistMinEnvs = 256;
+struct PersistNips {
+  static constexpr int NT = 512;                         // 8 waves
+  static constexpr int XIN = 84 * 84 * 4;                // 28,224 B
+  static constexpr int A1P = 20, A1 = 400 * A1P;         // act1 [400][20] floats
+  static constexpr int WP = 260;                         // transposed weight row (floats)
+  static constexpr size_t LDS = XIN + sizeof(float) * (A1 + 16 * WP + 32 * WP);
+  static constexpr int NQ = (XIN / 16 + NT - 1) / NT;    // uint4 of a frame per thread
+};
+
+// (one 8-wave block per CU by its LDS: 2 waves per SIMD, so up to 256 VGPRs each — tell the
+// compiler, which otherwise spills the frame prefetch registers to keep a 5-wave occupancy)
+__global__ __launch_bounds__(PersistNips::NT) __attribute__((amdgpu_waves_per_eu(1, 2))) void nips_conv_persist_kernel(
+    const uint8_t *__restrict__ obs, int B, const float *__restrict__ W1, const float *__restrict__ W2, int act,
+    float alpha, float *__restrict__ act2, float *__restrict__ act1_out) {
+  using Pz = PersistNips;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint8_t *xin = reinterpret_cast<uint8_t *>(smem);
+  float *a1 = reinterpret_cast<float *>(xin + Pz::XIN);
+  float *w1t = a1 + Pz::A1;
+  float *w2t = w1t + 16 * Pz::WP;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  for (int i = threadIdx.x; i < 256 * 16; i += Pz::NT) w1t[(i & 15) * Pz::WP + (i >> 4)] = W1[i];
+  for (int i = threadIdx.x; i < 256 * 32; i += Pz::NT) w2t[(i & 31) * Pz::WP + (i >> 5)] = W2[i];
+  const float *b1 = W1 + 256 * 16, *b2 = W2 + 256 * 32;
+  const float bias1 = b1[r], bias2a = b2[r], bias2b = b2[16 + r];
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 nx[Pz::NQ];
+  {
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(obs + (size_t)min((int)blockIdx.x, B - 1) * Pz::XIN);
+#pragma unroll
+    for (int u = 0; u < Pz::NQ; ++u) nx[u] = src[min((int)threadIdx.x + Pz::NT * u, Pz::XIN / 16 - 1)];
+  }
+  const float sc = 1.0f / 255.0f;
+  for (int e = blockIdx.x; e < B; e += gridDim.x) {
+#pragma unroll
+    for (int u = 0; u < Pz::NQ; ++u) {
+      const int q = threadIdx.x + Pz::NT * u;
+      if (q < Pz::XIN / 16) reinterpret_cast<u32x4 *>(xin)[q] = nx[u];
+    }
+    __syncthreads();
+    // ---- conv1: tiles w, w+8, w+16, w+24 (< 25) ----
+    {
+      constexpr int TT = 4;
+      f32x4 acc[TT];
+      int base[TT];
+#pragma unroll
+      for (int t = 0; t < TT; ++t) {
+        acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int m = min(16 * (w + 8 * t) + r, 399), oy = m / 20, ox = m - oy * 20;
+        base[t] = (4 * oy * 84 + 4 * ox) * 4;
+      }
+      const bool t3 = w == 0;  // tile w + 24 exists only for w = 0
+#pragma unroll 4
+      for (int kc = 0; kc < 16; ++kc) {
+        const int kpos = 4 * kc + g, off = ((kpos >> 3) * 84 + (kpos & 7)) * 4;
+        const f32x4 bv = *reinterpret_cast<const f32x4 *>(w1t + r * Pz::WP + 16 * kc + 4 * g);
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+          if (t < 3 || t3) {
+            const uint32_t u = *reinterpret_cast<const uint32_t *>(xin + base[t] + off);
+            const f32x4 av = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc,
+                                   (float)((u >> 16) & 0xff) * sc, (float)(u >> 24) * sc};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc[t], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+        if (t < 3 || t3)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int m = 16 * (w + 8 * t) + 4 * g + q;
+            const float y = act_fwd(acc[t][q] + bias1, act, alpha);
+            a1[m * Pz::A1P + r] = y;
+            if (act1_out) act1_out[((size_t)e * 400 + m) * 16 + r] = y;
+          }
+    }
+    __syncthreads();
+    // the next env's frame: loaded now, stored after this env's conv2 (xin is free)
+    {  // (past the end: a harmless reload; unconditional loads keep nx in VGPRs)
+      const u32x4 *src = reinterpret_cast<const u32x4 *>(obs + (size_t)min(e + (int)gridDim.x, B - 1) * Pz::XIN);
+#pragma unroll
+      for (int u = 0; u < Pz::NQ; ++u) nx[u] = src[min((int)threadIdx.x + Pz::NT * u, Pz::XIN / 16 - 1)];
+    }
+    // ---- conv2: units u = w (+ 8 for w < 4): m-tile u / 2, n-tile u % 2 ----
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const int u = w + 8 * k2;
+      if (u < 12) {
+        const int mt = u >> 1, ntile = u & 1;
+        const int mr = min(16 * mt + r, 80), oy = mr / 9, ox = mr - oy * 9;
+        const float *abase = a1 + (2 * oy * 20 + 2 * ox) * Pz::A1P + 4 * g;
+        const float *bbase = w2t + (16 * ntile + r) * Pz::WP + 4 * g;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int kc = 0; kc < 16; ++kc) {
+          const f32x4 av = *reinterpret_cast<const f32x4 *>(abase + ((kc >> 2) * 20 + (kc & 3)) * Pz::A1P);
+          const f32x4 bv = *reinterpret_cast<const f32x4 *>(bbase + 16 * kc);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = 16 * mt + 4 * g + q;
+          if (m < 81)
+            act2[(size_t)e * 2592 + m * 32 + 16 * ntile + r] = act_fwd(acc[q] + (ntile ? bias2b : bias2a), act, alpha);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Launch the two trunk kernels: conv (optionally stacking) -> act2, fc -> slabs.
 template <int C>
 static inline int launch_nips_trunk(const uint8_t *obs, const StackSrc *st, int B, const float *W1, const float *W2,
@@ -352,6 +533,21 @@ static inline int launch_nips_trunk(const uint8_t *obs, const StackSrc *st, int 
   if (st) {
     hipLaunchKernelGGL((nips_conv_kernel<C, true>), dim3(Fz::ROWS2 * B), dim3(Fz::NT), Fz::LDS_BYTES, s, st->out, *st,
                        B, W1, W2, act, alpha, act2, act1);
+  } else if (C == 4 && B >= kPersistMinEnvs) {
+    static int cus = 0;
+    static bool attr = false;
+    if (!cus) {
+      int dev = 0;
+      MT_HIP(hipGetDevice(&dev));
+      MT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    if (!attr) {
+      MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&nips_conv_persist_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)PersistNips::LDS));
+      attr = true;
+    }
+    hipLaunchKernelGGL(nips_conv_persist_kernel, dim3(std::min(B, cus)), dim3(PersistNips::NT), PersistNips::LDS, s,
+                       obs, B, W1, W2, act, alpha, act2, act1);
   } else {
     hipLaunchKernelGGL((nips_conv_kernel<C, false>), dim3(Fz::ROWS2 * B), dim3(Fz::NT), Fz::LDS_BYTES, s, obs,
                        StackSrc{}, B, W1, W2, act, alpha, act2, act1);

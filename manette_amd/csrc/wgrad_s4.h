@@ -33,21 +33,24 @@ struct Conv1S4WgradJob {
   static constexpr int NT = COUT / 16;     // N tiles
   static constexpr int TPW = C / 4;        // M tiles per wave (a quarter = 16C rows = C tiles)
   static constexpr int QXP = 24;           // bytes per staged phase row (21 used)
-  static constexpr int PLANE = 20 * QXP;   // one (py, px, ci) plane: qy = oy in [0, 20)
+  // one (py, px, ci) plane: qy = oy in [0, 20); +4 bytes so the 16 planes a fragment's lanes
+  // read start on distinct LDS banks (a plane of 120 dwords put lanes r, r+4, ... on one bank)
+  static constexpr int PLANE = 20 * QXP + 4;
   static constexpr int XS_BYTES = 2 * 4 * C * PLANE;
   static constexpr int PIXP = 404;         // padded pixel stride of dY^T (floats)
   static constexpr int KK = 64 * C;
-  static_assert(XS_BYTES % 16 == 0, "dY^T stays 16-byte aligned");
+  static constexpr int XS_ALLOC = (XS_BYTES + 15) / 16 * 16;
+  static_assert(XS_ALLOC % 16 == 0, "dY^T stays 16-byte aligned");
   const uint8_t *X = nullptr;  // [B][84][84][C]
   const float *dY = nullptr;   // [B][20][20][COUT]
   float *slab = nullptr;       // [B][KK + 1][COUT]
   int B = 0;
   __host__ __device__ int blocks() const { return 4 * B; }
-  size_t lds() const { return XS_BYTES + sizeof(float) * COUT * PIXP; }
+  size_t lds() const { return XS_ALLOC + sizeof(float) * COUT * PIXP; }
   __device__ __forceinline__ void run(int id, float *smem) const {
     const int b = id >> 2, q = id & 3, a = q >> 1, py0 = (2 * q) & 3;
     uint8_t *xs = reinterpret_cast<uint8_t *>(smem);
-    float *dyt = reinterpret_cast<float *>(xs + XS_BYTES);
+    float *dyt = reinterpret_cast<float *>(xs + XS_ALLOC);
     // ---- stage: input rows y = 4(qy + a) + py0 + pyl (qy < 20, pyl < 2), phase-major bytes, and
     //      dY^T. Every global load of the thread is issued before the first LDS write (a load /
     //      write loop would wait out one load latency per iteration). ----

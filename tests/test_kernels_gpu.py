@@ -68,6 +68,28 @@ def test_forward_infer_parity(arch, depth, A, R, act, B):
     np.testing.assert_allclose(pi.cpu().numpy(), pi1.cpu().numpy(), rtol=2e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize('act', ['relu', 'leaky_relu'])
+def test_forward_infer_large_batch(act):
+    """B >= 256 gray NIPS takes the persistent throughput trunk (trunk_fused.h
+    nips_conv_persist_kernel: no conv1 recompute, 256 blocks walking the envs): vs the oracle and
+    vs the layered GEMM path on the same 300 rows."""
+    B = 300
+    net = _net('NIPS', 1, 6, 1, seed=5, act=act)
+    rs = np.random.RandomState(77)
+    obs = rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)
+    obs_d = torch.from_numpy(obs).cuda()
+    v, pi, rep = [t.clone() for t in net.forward(obs_d, infer=True, ws_key='infer_big')]
+    v1, pi1, rep1 = net.forward(obs_d)
+    torch.cuda.synchronize()
+    spec = nets.arch_spec('NIPS', 1, 6, 1)
+    v0, pi0, rep0, _ = nets.forward(spec, net.get_variables(), obs, act=act, alpha=0.1)
+    np.testing.assert_allclose(v.cpu().numpy(), v0, rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(pi.cpu().numpy(), pi0, rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(rep.cpu().numpy(), rep0, rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(v.cpu().numpy(), v1.cpu().numpy(), rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(pi.cpu().numpy(), pi1.cpu().numpy(), rtol=2e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize('arch,depth,A,R', CONFIGS)
 @pytest.mark.parametrize('B', [5, 40])
 def test_loss_backward_parity(arch, depth, A, R, B):
