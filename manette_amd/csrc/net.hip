@@ -12,7 +12,6 @@
 
 #include "gemm.h"
 #include "trunk_fused.h"
-#include "wgrad_s4.h"
 
 namespace mt {
 
@@ -249,7 +248,6 @@ static int conv_wgrad_splits(int B) {
 
 template <class G>
 static size_t conv_wgrad_slab(int B) {
-  if constexpr (is_conv1_s4<G>()) return (size_t)B * (G::KK + 1) * G::COUT;  // Conv1S4WgradJob: a slab per image
   const int s = conv_wgrad_splits<G>(B);
   return s > 1 ? (size_t)s * (G::KK + 1) * G::COUT : 0;
 }
@@ -656,19 +654,45 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
   __shared__ float buf[2 * kMaxScan];
   const int b = blockIdx.x;
   const int A = hp.A, R = hp.R, O = 1 + A + R, F = hp.F;
+  // Every load that does not depend on the return is issued first, so its latency overlaps the
+  // scan's (the rewards / masks are read over PCIe from pinned memory): the row's head inputs
+  // (threads < 64) and the dH operands H[b][f] and W[f][.] of the thread's features.
+  const int lane = threadIdx.x;
+  float pa = 0.f, pr = 0.f, vb = 0.f, adv_in = 0.f, y_in = 0.f;
+  int ai = 0, ri = 0;
+  if (threadIdx.x < 64) {
+    pa = lane < A ? pi[(size_t)b * A + lane] : 0.f;
+    pr = lane < R ? rep[(size_t)b * R + lane] : 0.f;
+    vb = v[b];
+    ai = a_idx[b];
+    ri = r_idx[b];
+    if (!rs.r) {
+      adv_in = adv[b];
+      y_in = y[b];
+    }
+  }
+  constexpr int FT = 2, KW = 32;  // F <= 512; A + R <= 32 (else the weights are read after the scan)
+  const bool pre = A + R <= KW;
+  float hv[FT], wc[FT], wk[FT][KW];
+#pragma unroll
+  for (int fi = 0; fi < FT; ++fi) {
+    const int f = min((int)threadIdx.x + 256 * fi, F - 1);
+    hv[fi] = H[(size_t)b * F + f];
+    wc[fi] = hp.Wc[f];
+#pragma unroll
+    for (int k = 0; k < KW; ++k)
+      wk[fi][k] = !pre ? 0.f : (k < A ? hp.Wa[(size_t)f * A + k] : (k < A + R ? hp.Wr[(size_t)f * R + (k - A)] : 0.f));
+  }
   if (rs.r) row_return(rs, v, b, ya, buf);
   if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const float ad = rs.r ? ya[1] : adv[b];
-    const float yb = rs.r ? ya[0] : y[b];
-    const float pa = lane < A ? pi[(size_t)b * A + lane] : 0.f;
-    const float pr = lane < R ? rep[(size_t)b * R + lane] : 0.f;
+    const float ad = rs.r ? ya[1] : adv_in;
+    const float yb = rs.r ? ya[0] : y_in;
     float ent_a, ls_a, ent_r, ls_r;
-    const float ga = head_softmax_grad(pa, lane, A, a_idx[b], ad, beta, scale, temp, &ent_a, &ls_a);
-    const float gr = head_softmax_grad(pr, lane, R, r_idx[b], ad, beta, scale, temp, &ent_r, &ls_r);
-    const float diff = yb - v[b];
+    const float ga = head_softmax_grad(pa, lane, A, ai, ad, beta, scale, temp, &ent_a, &ls_a);
+    const float gr = head_softmax_grad(pr, lane, R, ri, ad, beta, scale, temp, &ent_r, &ls_r);
+    const float diff = yb - vb;
     // d/dv of scale * 0.25 * (y - v)^2  (policy_v_network.py:25-26)
-    const float gv = scale * 0.25f * 2.0f * (v[b] - yb);
+    const float gv = scale * 0.25f * 2.0f * (vb - yb);
     if (lane == 0) dzs[0] = gv;
     if (lane < A) dzs[1 + lane] = ga;
     if (lane < R) dzs[1 + A + lane] = gr;
@@ -681,14 +705,31 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
   }
   __syncthreads();
   for (int o = threadIdx.x; o < O; o += 256) dz[(size_t)b * O + o] = dzs[o];
-  for (int f = threadIdx.x; f < F; f += 256) {
+#pragma unroll
+  for (int fi = 0; fi < FT; ++fi) {
+    const int f = threadIdx.x + 256 * fi;
+    if (f >= F) break;
+    float acc = dzs[0] * wc[fi];
+    if (pre) {
+      // same order as below: actor terms, then repetition terms
+#pragma unroll
+      for (int k = 0; k < KW; ++k)
+        if (k < A + R) acc += dzs[1 + k] * wk[fi][k];
+    } else {
+      const float *wa = hp.Wa + (size_t)f * A;
+      for (int k = 0; k < A; ++k) acc += dzs[1 + k] * wa[k];
+      const float *wr = hp.Wr + (size_t)f * R;
+      for (int k = 0; k < R; ++k) acc += dzs[1 + A + k] * wr[k];
+    }
+    dH[(size_t)b * F + f] = acc * act_bwd(hv[fi], act, alpha);
+  }
+  for (int f = threadIdx.x + 256 * FT; f < F; f += 256) {  // (F > 512: not built today)
     float acc = dzs[0] * hp.Wc[f];
     const float *wa = hp.Wa + (size_t)f * A;
     for (int k = 0; k < A; ++k) acc += dzs[1 + k] * wa[k];
     const float *wr = hp.Wr + (size_t)f * R;
     for (int k = 0; k < R; ++k) acc += dzs[1 + A + k] * wr[k];
-    const float h = H[(size_t)b * F + f];
-    dH[(size_t)b * F + f] = acc * act_bwd(h, act, alpha);
+    dH[(size_t)b * F + f] = acc * act_bwd(H[(size_t)b * F + f], act, alpha);
   }
 }
 
@@ -856,23 +897,6 @@ static WgradJobs<G, U8> conv_wgrad_jobs(const void *X, const float *dY, float *s
   return j;
 }
 
-// The input conv of the NIPS / NATURE trunks: phase-major product per image + slab sum (wgrad_s4.h).
-template <class G>
-struct Conv1S4Jobs {
-  Conv1S4WgradJob<G::CIN, G::COUT> gemm;
-  SlabJob sum;
-};
-template <class G>
-static Conv1S4Jobs<G> conv1_s4_wgrad_jobs(const uint8_t *X, const float *dY, float *slab, float *gwb, int B) {
-  Conv1S4Jobs<G> j;
-  j.gemm.X = X;
-  j.gemm.dY = dY;
-  j.gemm.slab = slab;
-  j.gemm.B = B;
-  j.sum = SlabJob{slab, B, (size_t)(G::KK + 1) * G::COUT, gwb};
-  return j;
-}
-
 // dX of a conv (transposed-conv gather), masked by the activation derivative of X, as a GEMM job.
 template <class G>
 static auto conv_dgrad_job(const float *dY, const float *Wt, const float *Xact, float *dX, int B, int act,
@@ -947,13 +971,8 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
   const void *x = I == 0 ? (const void *)obs : (const void *)layer_out<Ar, (I > 0 ? I - 1 : 0)>(ws, L);
-  const auto wg = [&] {
-    if constexpr (I == 0 && is_conv1_s4<G>())
-      return conv1_s4_wgrad_jobs<G>(obs, ws + L.dact[0], ws + L.wslab, grad + n->off_conv[0], B);
-    else
-      return conv_wgrad_jobs<G, I == 0>(x, ws + L.dact[I], ws + (I % 2 ? L.wslab2 : L.wslab), grad + n->off_conv[I],
-                                        B);
-  }();
+  const auto wg = conv_wgrad_jobs<G, I == 0>(x, ws + L.dact[I], ws + (I % 2 ? L.wslab2 : L.wslab),
+                                             grad + n->off_conv[I], B);
   if constexpr (I > 0) {
     constexpr int J = I - 1;
     using GJ = LayerG<Ar, J>;

@@ -84,7 +84,12 @@ struct FusedNips {
   // LDS (floats unless noted)
   static constexpr int RED_FLOATS = UNITS ? 10 * 16 * CO1 : NW * MT1 * 16 * CO1;  // >= conv2's partials
   static_assert(4 * FR_BYTES <= RED_FLOATS * 4, "staged frames alias the reduction buffer");
-  static constexpr size_t LDS_BYTES = IN_BYTES + sizeof(float) * (RED_FLOATS + M1 * A1S);
+  // units (gray): W1 staged transposed in LDS ([16][W1P] floats) once per block with coalesced 16-B
+  // loads, so each lane's B fragment is one ds_read_b128 — per-wave 4-byte fragment loads fetched
+  // every W1 element 5 times (once per M-tile sharing a K-half)
+  static constexpr int W1P = KK1 + 4;
+  static constexpr int W1T_FLOATS = UNITS ? CO1 * W1P : 0;
+  static constexpr size_t LDS_BYTES = IN_BYTES + sizeof(float) * (RED_FLOATS + M1 * A1S + W1T_FLOATS);
   // fc kernel
   static constexpr int FC_BN = 16, FC_BM = 32, FC_KC = FEAT / 16;  // 18 K chunks of 16
 };
@@ -172,7 +177,8 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *red = smem;                              // [4 waves][..] partial accumulators
   float *a1 = red + Fz::RED_FLOATS;               // [80 pixels][A1S] conv1 rows 2i..2i+3
-  uint8_t *xin = reinterpret_cast<uint8_t *>(a1 + Fz::M1 * Fz::A1S);  // [20][84][C] input rows 8i..
+  float *w1t = a1 + Fz::M1 * Fz::A1S;              // units: [16][W1P] W1 transposed
+  uint8_t *xin = reinterpret_cast<uint8_t *>(w1t + Fz::W1T_FLOATS);  // [20][84][C] input rows 8i..
   uint8_t *fr = reinterpret_cast<uint8_t *>(red);  // STACK: [4][20][84][D] new frames (before conv1)
 
   const int nb = gridDim.x;
@@ -186,13 +192,31 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   // conv1 weight fragments of this wave's K chunks: B[k][n] = W1[k*16 + n]. K-split: chunks
   // c = w + NW j; units: chunks 8h .. 8h+7 of the wave's K-half h = w & 1
   constexpr int NW = Fz::NW;
-  constexpr int J1 = Fz::UNITS ? 8 : Fz::KC1 / NW;
+  constexpr int J1 = Fz::UNITS ? 1 : Fz::KC1 / NW;  // (units: fragments read from the staged w1t)
   float b1f[J1][4];
+  if constexpr (Fz::UNITS) {
+    // W1 [KK1][16] as float4 (4 output channels of one k), written transposed into w1t
+    constexpr int NQ = Fz::KK1 * Fz::CO1 / 4;
+    f32x4 wv[(NQ + Fz::NT - 1) / Fz::NT];
 #pragma unroll
-  for (int j = 0; j < J1; ++j) {
-    const int k0 = 16 * (Fz::UNITS ? 8 * (w & 1) + j : w + NW * j) + 4 * g;
+    for (int u = 0; u < (NQ + Fz::NT - 1) / Fz::NT; ++u)
+      wv[u] = reinterpret_cast<const f32x4 *>(W1)[min((int)threadIdx.x + Fz::NT * u, NQ - 1)];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) b1f[j][s] = W1[(size_t)(k0 + s) * Fz::CO1 + r];
+    for (int u = 0; u < (NQ + Fz::NT - 1) / Fz::NT; ++u) {
+      const int q = threadIdx.x + Fz::NT * u;
+      if (q < NQ) {
+        const int k = q >> 2, c4 = (q & 3) * 4;
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) w1t[(c4 + e2) * Fz::W1P + k] = wv[u][e2];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < J1; ++j) {
+      const int k0 = 16 * (w + NW * j) + 4 * g;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) b1f[j][s] = W1[(size_t)(k0 + s) * Fz::CO1 + r];
+    }
   }
   nips_stage_rows<C, STACK>(obs, st, e, i, xin, fr);
   __syncthreads();
@@ -202,21 +226,37 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   if constexpr (Fz::UNITS) {
     // unit w: M-tile t = w / 2, K-half h = w % 2 (K chunks 8h .. 8h+7)
     const int t = w >> 1, h = w & 1;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;  // even / odd chunks: independent MFMA chains
     const float sc = 1.0f / 255.0f;
     const int m = min(t * 16 + r, Fz::M1 - 1);
     const int orow = m / Fz::OW1, ox = m - orow * Fz::OW1;
     const uint8_t *xb = xin + ((4 * orow) * 84 + 4 * ox) * C;
+    // every LDS operand read of the unit first (8 words + 8 weight fragments in flight), then the
+    // converts and the 32 MFMAs: the reads' latency is paid once, not once per chunk
+    uint32_t au[8];
+    f32x4 bw[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int kpos = 4 * (8 * h + j) + g;  // (ky, kx) of k0 = 16 c + 4 g (C = 4: the 4 channels)
-      const uint32_t u = *reinterpret_cast<const uint32_t *>(xb + ((kpos >> 3) * 84 + (kpos & 7)) * C);
+      au[j] = *reinterpret_cast<const uint32_t *>(xb + ((kpos >> 3) * 84 + (kpos & 7)) * C);
+      bw[j] = *reinterpret_cast<const f32x4 *>(w1t + r * Fz::W1P + 16 * (8 * h + j) + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them to save VGPRs)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t u = au[j];
       const f32x4 a = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc, (float)((u >> 16) & 0xff) * sc,
                             (float)(u >> 24) * sc};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b1f[j][s], acc, 0, 0, 0);
+      for (int s = 0; s < 4; ++s) {
+        if (j & 1)
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[j][s], acc1, 0, 0, 0);
+        else
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[j][s], acc0, 0, 0, 0);
+      }
     }
     MT_PROBE_AT(0, bid, 6);
+    const f32x4 acc = acc0 + acc1;
 #pragma unroll
     for (int q = 0; q < 4; ++q) red[(w * 16 + g * 4 + q) * Fz::CO1 + r] = acc[q];
   } else   {
@@ -292,14 +332,20 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   if constexpr (Fz::UNITS) {
     if (w < 8) {  // unit w: N-tile w & 1, K-quarter kq = w >> 1 (chunks 4kq .. 4kq+3: ky = kq, kx = j)
       const int kq = w >> 1;
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
       const int ox = min(r, Fz::OW2 - 1);
 #pragma unroll
       for (int j = 0; j < J2; ++j) {
         const f32x4 a = *reinterpret_cast<const f32x4 *>(a1 + (kq * Fz::OW1 + 2 * ox + j) * Fz::A1S + 4 * g);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b2f[j][0][s], acc, 0, 0, 0);
+        for (int s = 0; s < 4; ++s) {
+          if (j & 1)
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b2f[j][0][s], acc1, 0, 0, 0);
+          else
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b2f[j][0][s], acc0, 0, 0, 0);
+        }
       }
+      const f32x4 acc = acc0 + acc1;
 #pragma unroll
       for (int q = 0; q < 4; ++q) red[(w * 16 + g * 4 + q) * 16 + r] = acc[q];
     }
@@ -465,16 +511,20 @@ __global__ __launch_bounds__(PersistNips::NT) __attribute__((amdgpu_waves_per_eu
       for (int kc = 0; kc < 16; ++kc) {
         const int kpos = 4 * kc + g, off = ((kpos >> 3) * 84 + (kpos & 7)) * 4;
         const f32x4 bv = *reinterpret_cast<const f32x4 *>(w1t + r * Pz::WP + 16 * kc + 4 * g);
+        f32x4 av[TT];
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
-          if (t < 3 || t3) {
-            const uint32_t u = *reinterpret_cast<const uint32_t *>(xin + base[t] + off);
-            const f32x4 av = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc,
-                                   (float)((u >> 16) & 0xff) * sc, (float)(u >> 24) * sc};
-#pragma unroll
-            for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc[t], 0, 0, 0);
-          }
+          const uint32_t u = *reinterpret_cast<const uint32_t *>(xin + base[t] + off);
+          av[t] = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc, (float)((u >> 16) & 0xff) * sc,
+                        (float)(u >> 24) * sc};
         }
+        // s outer, tiles inner: consecutive MFMAs on independent accumulators (a chain on one
+        // accumulator waits out the 40-cycle dependent latency of the 32-cycle issue)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int t = 0; t < TT; ++t)
+            if (t < 3 || t3) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][s], bv[s], acc[t], 0, 0, 0);
       }
 #pragma unroll
       for (int t = 0; t < TT; ++t)
@@ -503,14 +553,22 @@ __global__ __launch_bounds__(PersistNips::NT) __attribute__((amdgpu_waves_per_eu
         const int mr = min(16 * mt + r, 80), oy = mr / 9, ox = mr - oy * 9;
         const float *abase = a1 + (2 * oy * 20 + 2 * ox) * Pz::A1P + 4 * g;
         const float *bbase = w2t + (16 * ntile + r) * Pz::WP + 4 * g;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        // two accumulators (even / odd K chunks, added at the end) so consecutive MFMAs do not
+        // depend on each other
+        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-        for (int kc = 0; kc < 16; ++kc) {
-          const f32x4 av = *reinterpret_cast<const f32x4 *>(abase + ((kc >> 2) * 20 + (kc & 3)) * Pz::A1P);
-          const f32x4 bv = *reinterpret_cast<const f32x4 *>(bbase + 16 * kc);
+        for (int kc = 0; kc < 16; kc += 2) {
+          const f32x4 av0 = *reinterpret_cast<const f32x4 *>(abase + ((kc >> 2) * 20 + (kc & 3)) * Pz::A1P);
+          const f32x4 bv0 = *reinterpret_cast<const f32x4 *>(bbase + 16 * kc);
+          const f32x4 av1 = *reinterpret_cast<const f32x4 *>(abase + (((kc + 1) >> 2) * 20 + ((kc + 1) & 3)) * Pz::A1P);
+          const f32x4 bv1 = *reinterpret_cast<const f32x4 *>(bbase + 16 * (kc + 1));
 #pragma unroll
-          for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+          for (int s = 0; s < 4; ++s) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[s], bv0[s], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[s], bv1[s], acc1, 0, 0, 0);
+          }
         }
+        const f32x4 acc = acc0 + acc1;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int m = 16 * mt + 4 * g + q;
@@ -548,6 +606,11 @@ static inline int launch_nips_trunk(const uint8_t *obs, const StackSrc *st, int 
     }
     hipLaunchKernelGGL(nips_conv_persist_kernel, dim3(std::min(B, cus)), dim3(PersistNips::NT), PersistNips::LDS, s,
                        obs, B, W1, W2, act, alpha, act2, act1);
+    MT_LAUNCHED();
+    // the dense layer as a 64 x 64-tile GEMM in 9 K-splits of 288 (the slab count the heads kernel
+    // sums): nips_fc_kernel's 16-column blocks would re-read act2 16 times at this batch
+    return launch_gemm<Tile<64, 64, 2, 2, 96>>(LdRowMajor{act2, Fz::FLAT}, LdColMajor{Wfc, Fz::F, -1},
+                                               EpSlab{slabs, B, Fz::F}, B, Fz::F, Fz::FLAT, Fz::ROWS2, s);
   } else {
     hipLaunchKernelGGL((nips_conv_kernel<C, false>), dim3(Fz::ROWS2 * B), dim3(Fz::NT), Fz::LDS_BYTES, s, obs,
                        StackSrc{}, B, W1, W2, act, alpha, act2, act1);
