@@ -446,26 +446,28 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
 
 // Throughput form of the NIPS conv trunk for large batches (gray frames, E >= kPersistMinEnvs):
 // the latency form above recomputes 1.8x of conv1 so that 9 blocks can work on one env; once the
-// grid fills the chip that recompute is pure cost. Here a persistent block (8 waves, one per CU)
-// stages W1 / W2 transposed in LDS once and walks envs e = blockIdx.x, += gridDim.x: the env's
-// 84x84x4 frame in LDS, conv1 as 25 M-tiles of 16 pixels over the 8 waves (A fragment = one u32 of
-// 4 channels, B fragment = one ds_read_b128 of the transposed weights, shared by the wave's
-// tiles), bias + act into an LDS act1 [400][16], then conv2 as 6 M-tiles x 2 N-tiles (12 units:
-// three per SIMD), act2 to HBM in the same NHWC flatten order. The next env's frame is loaded into
-// registers during conv2. Same fp32 products (k-ordered MFMA chains) as the latency form.
+// grid fills the chip that recompute is pure cost. Here a persistent block (16 waves, one block
+// per CU) stages W1 / W2 transposed in LDS once and walks envs e = blockIdx.x, += gridDim.x: the
+// env's 84x84x4 frame in LDS; conv1 as 25 M-tiles of 16 pixels — tiles 0..23 two or one per wave
+// (6 per SIMD: waves w, w+4, w+8, w+12 share one), tile 24 split into 4 K-quarters on waves 8..11
+// (one per SIMD, 4 partials added in order) so every SIMD issues 400 MFMAs per env; A fragment =
+// one u32 of 4 channels, B fragment = one ds_read_b128 of the transposed weights; bias + act into
+// an LDS act1 [400][16]; then conv2 as 6 M-tiles x 2 N-tiles on waves 0..11 (3 per SIMD), act2 to
+// HBM in the same NHWC flatten order. The next env's frame is loaded into registers during conv2.
+// Same fp32 products (k-ordered MFMA chains) as the latency form, up to the summation split.
 constexpr int kPersistMinEnvs = 256;
 struct PersistNips {
-  static constexpr int NT = 512;                         // 8 waves
+  static constexpr int NT = 1024;                        // 16 waves
   static constexpr int XIN = 84 * 84 * 4;                // 28,224 B
   static constexpr int A1P = 20, A1 = 400 * A1P;         // act1 [400][20] floats
   static constexpr int WP = 260;                         // transposed weight row (floats)
-  static constexpr size_t LDS = XIN + sizeof(float) * (A1 + 16 * WP + 32 * WP);
-  static constexpr int NQ = (XIN / 16 + NT - 1) / NT;    // uint4 of a frame per thread
+  static constexpr int T24 = 4 * 256;                    // tile 24's 4 K-quarter partials
+  static constexpr size_t LDS = XIN + sizeof(float) * (A1 + 16 * WP + 32 * WP + T24);
+  static constexpr int NQ = (XIN / 16 + NT - 1) / NT;    // 16-B chunks of a frame per thread
 };
 
-// (one 8-wave block per CU by its LDS: 2 waves per SIMD, so up to 256 VGPRs each — tell the
-// compiler, which otherwise spills the frame prefetch registers to keep a 5-wave occupancy)
-__global__ __launch_bounds__(PersistNips::NT) __attribute__((amdgpu_waves_per_eu(1, 2))) void nips_conv_persist_kernel(
+// (one 16-wave block per CU by its LDS: 4 waves per SIMD, up to 128 VGPRs each)
+__global__ __launch_bounds__(PersistNips::NT) void nips_conv_persist_kernel(
     const uint8_t *__restrict__ obs, int B, const float *__restrict__ W1, const float *__restrict__ W2, int act,
     float alpha, float *__restrict__ act2, float *__restrict__ act1_out) {
   using Pz = PersistNips;
@@ -474,6 +476,7 @@ __global__ __launch_bounds__(PersistNips::NT) __attribute__((amdgpu_waves_per_eu
   float *a1 = reinterpret_cast<float *>(xin + Pz::XIN);
   float *w1t = a1 + Pz::A1;
   float *w2t = w1t + 16 * Pz::WP;
+  float *p24 = w2t + 32 * Pz::WP;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   for (int i = threadIdx.x; i < 256 * 16; i += Pz::NT) w1t[(i & 15) * Pz::WP + (i >> 4)] = W1[i];
@@ -488,6 +491,19 @@ __global__ __launch_bounds__(PersistNips::NT) __attribute__((amdgpu_waves_per_eu
     for (int u = 0; u < Pz::NQ; ++u) nx[u] = src[min((int)threadIdx.x + Pz::NT * u, Pz::XIN / 16 - 1)];
   }
   const float sc = 1.0f / 255.0f;
+  // conv1 work of wave w: tiles w and (w < 8) w + 16; waves 8..11 also K-quarter w - 8 of tile 24
+  const bool two = w < 8, quarter = w >= 8 && w < 12;
+  int base[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int m = min(16 * (w + 16 * t) + r, 399), oy = m / 20, ox = m - oy * 20;
+    base[t] = (4 * oy * 84 + 4 * ox) * 4;
+  }
+  int base24;
+  {
+    const int m = 16 * 24 + r, oy = m / 20, ox = m - oy * 20;
+    base24 = (4 * oy * 84 + 4 * ox) * 4;
+  }
   for (int e = blockIdx.x; e < B; e += gridDim.x) {
 #pragma unroll
     for (int u = 0; u < Pz::NQ; ++u) {
@@ -495,86 +511,89 @@ __global__ __launch_bounds__(PersistNips::NT) __attribute__((amdgpu_waves_per_eu
       if (q < Pz::XIN / 16) reinterpret_cast<u32x4 *>(xin)[q] = nx[u];
     }
     __syncthreads();
-    // ---- conv1: tiles w, w+8, w+16, w+24 (< 25) ----
+    // ---- conv1 ----
     {
-      constexpr int TT = 4;
-      f32x4 acc[TT];
-      int base[TT];
-#pragma unroll
-      for (int t = 0; t < TT; ++t) {
-        acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int m = min(16 * (w + 8 * t) + r, 399), oy = m / 20, ox = m - oy * 20;
-        base[t] = (4 * oy * 84 + 4 * ox) * 4;
-      }
-      const bool t3 = w == 0;  // tile w + 24 exists only for w = 0
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      f32x4 acc24 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
       for (int kc = 0; kc < 16; ++kc) {
         const int kpos = 4 * kc + g, off = ((kpos >> 3) * 84 + (kpos & 7)) * 4;
         const f32x4 bv = *reinterpret_cast<const f32x4 *>(w1t + r * Pz::WP + 16 * kc + 4 * g);
-        f32x4 av[TT];
+        f32x4 av[2];
 #pragma unroll
-        for (int t = 0; t < TT; ++t) {
+        for (int t = 0; t < 2; ++t) {
           const uint32_t u = *reinterpret_cast<const uint32_t *>(xin + base[t] + off);
           av[t] = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc, (float)((u >> 16) & 0xff) * sc,
                         (float)(u >> 24) * sc};
         }
-        // s outer, tiles inner: consecutive MFMAs on independent accumulators (a chain on one
-        // accumulator waits out the 40-cycle dependent latency of the 32-cycle issue)
+        // s outer, tiles inner: consecutive MFMAs on independent accumulators
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s) {
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0][s], bv[s], acc[0], 0, 0, 0);
+          if (two) acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1][s], bv[s], acc[1], 0, 0, 0);
+        }
+        if (quarter && (kc >> 2) == w - 8) {  // (wave-uniform)
+          const uint32_t u = *reinterpret_cast<const uint32_t *>(xin + base24 + off);
+          const f32x4 a24 = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc,
+                                  (float)((u >> 16) & 0xff) * sc, (float)(u >> 24) * sc};
 #pragma unroll
-          for (int t = 0; t < TT; ++t)
-            if (t < 3 || t3) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][s], bv[s], acc[t], 0, 0, 0);
+          for (int s = 0; s < 4; ++s) acc24 = __builtin_amdgcn_mfma_f32_16x16x4f32(a24[s], bv[s], acc24, 0, 0, 0);
+        }
       }
 #pragma unroll
-      for (int t = 0; t < TT; ++t)
-        if (t < 3 || t3)
+      for (int t = 0; t < 2; ++t)
+        if (t == 0 || two)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const int m = 16 * (w + 8 * t) + 4 * g + q;
+            const int m = 16 * (w + 16 * t) + 4 * g + q;
             const float y = act_fwd(acc[t][q] + bias1, act, alpha);
             a1[m * Pz::A1P + r] = y;
             if (act1_out) act1_out[((size_t)e * 400 + m) * 16 + r] = y;
           }
+      if (quarter)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p24[(w - 8) * 256 + (4 * g + q) * 16 + r] = acc24[q];
     }
     __syncthreads();
-    // the next env's frame: loaded now, stored after this env's conv2 (xin is free)
-    {  // (past the end: a harmless reload; unconditional loads keep nx in VGPRs)
+    if (threadIdx.x < 256) {  // tile 24: its 4 K-quarters in order, bias + act
+      const int row = threadIdx.x >> 4, c = threadIdx.x & 15, m = 384 + row;
+      const float s = ((p24[row * 16 + c] + p24[256 + row * 16 + c]) + p24[512 + row * 16 + c]) + p24[768 + row * 16 + c];
+      const float y = act_fwd(s + b1[c], act, alpha);
+      a1[m * Pz::A1P + c] = y;
+      if (act1_out) act1_out[((size_t)e * 400 + m) * 16 + c] = y;
+    }
+    __syncthreads();
+    {  // the next env's frame: loaded now, stored after this env's conv2 (xin is free)
       const u32x4 *src = reinterpret_cast<const u32x4 *>(obs + (size_t)min(e + (int)gridDim.x, B - 1) * Pz::XIN);
 #pragma unroll
       for (int u = 0; u < Pz::NQ; ++u) nx[u] = src[min((int)threadIdx.x + Pz::NT * u, Pz::XIN / 16 - 1)];
     }
-    // ---- conv2: units u = w (+ 8 for w < 4): m-tile u / 2, n-tile u % 2 ----
-#pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      const int u = w + 8 * k2;
-      if (u < 12) {
-        const int mt = u >> 1, ntile = u & 1;
-        const int mr = min(16 * mt + r, 80), oy = mr / 9, ox = mr - oy * 9;
-        const float *abase = a1 + (2 * oy * 20 + 2 * ox) * Pz::A1P + 4 * g;
-        const float *bbase = w2t + (16 * ntile + r) * Pz::WP + 4 * g;
-        // two accumulators (even / odd K chunks, added at the end) so consecutive MFMAs do not
-        // depend on each other
-        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    // ---- conv2: waves 0..11, unit w: m-tile w / 2, n-tile w % 2 ----
+    if (w < 12) {
+      const int mt = w >> 1, ntile = w & 1;
+      const int mr = min(16 * mt + r, 80), oy = mr / 9, ox = mr - oy * 9;
+      const float *abase = a1 + (2 * oy * 20 + 2 * ox) * Pz::A1P + 4 * g;
+      const float *bbase = w2t + (16 * ntile + r) * Pz::WP + 4 * g;
+      // two accumulators (even / odd K chunks, added at the end): no dependent MFMA back to back
+      f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-        for (int kc = 0; kc < 16; kc += 2) {
-          const f32x4 av0 = *reinterpret_cast<const f32x4 *>(abase + ((kc >> 2) * 20 + (kc & 3)) * Pz::A1P);
-          const f32x4 bv0 = *reinterpret_cast<const f32x4 *>(bbase + 16 * kc);
-          const f32x4 av1 = *reinterpret_cast<const f32x4 *>(abase + (((kc + 1) >> 2) * 20 + ((kc + 1) & 3)) * Pz::A1P);
-          const f32x4 bv1 = *reinterpret_cast<const f32x4 *>(bbase + 16 * (kc + 1));
+      for (int kc = 0; kc < 16; kc += 2) {
+        const f32x4 av0 = *reinterpret_cast<const f32x4 *>(abase + ((kc >> 2) * 20 + (kc & 3)) * Pz::A1P);
+        const f32x4 bv0 = *reinterpret_cast<const f32x4 *>(bbase + 16 * kc);
+        const f32x4 av1 = *reinterpret_cast<const f32x4 *>(abase + (((kc + 1) >> 2) * 20 + ((kc + 1) & 3)) * Pz::A1P);
+        const f32x4 bv1 = *reinterpret_cast<const f32x4 *>(bbase + 16 * (kc + 1));
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[s], bv0[s], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[s], bv1[s], acc1, 0, 0, 0);
-          }
+        for (int s = 0; s < 4; ++s) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[s], bv0[s], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[s], bv1[s], acc1, 0, 0, 0);
         }
-        const f32x4 acc = acc0 + acc1;
+      }
+      const f32x4 acc = acc0 + acc1;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int m = 16 * mt + 4 * g + q;
-          if (m < 81)
-            act2[(size_t)e * 2592 + m * 32 + 16 * ntile + r] = act_fwd(acc[q] + (ntile ? bias2b : bias2a), act, alpha);
-        }
+      for (int q = 0; q < 4; ++q) {
+        const int m = 16 * mt + 4 * g + q;
+        if (m < 81)
+          act2[(size_t)e * 2592 + m * 32 + 16 * ntile + r] = act_fwd(acc[q] + (ntile ? bias2b : bias2a), act, alpha);
       }
     }
     __syncthreads();
