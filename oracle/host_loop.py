@@ -183,7 +183,7 @@ class HostLoop(object):
             runners = InProcessRunners(self.tab_rep, self.emulators, shared_states, shared_rewards,
                                        shared_over, a_sh, r_sh)
         else:
-            runners = ProcessRunners(self.tab_rep, self.emulators, self.workers, (84, 84, 4))
+            runners = ProcessRunners(self.tab_rep, self.emulators, self.workers, (84, 84, 4 * self.emulators[0].depth))
             shared_states, shared_rewards, shared_over = runners.states, runners.rewards, runners.over
             a_sh, r_sh = runners.a_idx, runners.r_idx
         try:
