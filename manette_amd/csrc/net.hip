@@ -843,7 +843,14 @@ struct BiasRowJob {
     for (int n0 = 0; n0 < COUT; n0 += 16) {
       float acc = 0.f;
       if (n0 + c < COUT)
-        for (int k = k0 + sub; k < k1; k += 16) acc += dY[(size_t)k * COUT + n0 + c];
+        for (int k = k0 + sub; k < k1; k += 16 * 8) {  // 8 loads in flight, added in row order
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = dY[(size_t)min(k + 16 * u, k1 - 1) * COUT + n0 + c];
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (k + 16 * u < k1) acc += v[u];
+        }
       smem[threadIdx.x] = acc;
       __syncthreads();
       if (sub == 0 && n0 + c < COUT) {
@@ -873,10 +880,11 @@ struct PairJob {
 };
 
 // dW (+db) of a conv -> grad[(KK+1) x COUT] (weights then biases): dW = im2col(X)^T . dY as a GEMM
-// job over the KK weight rows into K-split slabs [S][KK+1][COUT] (one split: straight into gwb),
-// db = the column sums of dY per split into slab row KK (BiasRowJob: a 64-row MFMA tile for the
-// single bias row would be a fifth of the product's work), and the slab-sum job that finishes it
-// (no job when unsplit).
+// job into K-split slabs [S][KK+1][COUT] (one split: straight into gwb) and the slab-sum job that
+// finishes it (no job when unsplit). db: when KK fills whole M-tiles (NIPS / NATURE, PWYX conv3),
+// the column sums of dY per split go to slab row KK (BiasRowJob) — a 64-row MFMA tile for the one
+// bias row would add a fifth of the product's work; otherwise the bias is a ones-row of the same
+// GEMM (LdIm2colT), free in the last tile's spare rows.
 template <class G, bool U8>
 struct WgradJobs {
   PairJob<GemmJob<TileConvWgrad<G>, LdIm2colT<G, U8>, LdColMajor, EpSlab>, BiasRowJob<G::COUT>> gemm;
@@ -890,8 +898,10 @@ static WgradJobs<G, U8> conv_wgrad_jobs(const void *X, const float *dY, float *s
   LdIm2colT<G, U8> la{reinterpret_cast<const typename InElem<U8>::T *>(X)};
   LdColMajor lb{dY, G::COUT, -1};
   float *dst = S == 1 ? gwb : slab;
-  const auto g = gemm_job<T>(la, lb, EpSlab{dst, M, G::COUT}, G::KK, G::COUT, K, S);
-  const BiasRowJob<G::COUT> bias{dY, dst + (size_t)G::KK * G::COUT, (size_t)M * G::COUT, K, g.kchunk, g.gz};
+  constexpr bool sep = G::KK % T::BM == 0;
+  const auto g = gemm_job<T>(la, lb, EpSlab{dst, M, G::COUT}, sep ? G::KK : M, G::COUT, K, S);
+  const BiasRowJob<G::COUT> bias{dY, dst + (size_t)G::KK * G::COUT, (size_t)M * G::COUT, K, g.kchunk,
+                                 sep ? g.gz : 0};
   WgradJobs<G, U8> j{{g, bias}, SlabJob{}};
   if (g.gz > 1) j.sum = SlabJob{slab, g.gz, (size_t)M * G::COUT, gwb};
   return j;
