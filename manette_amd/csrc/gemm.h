@@ -80,17 +80,33 @@ __device__ __forceinline__ void lds_put(float *L, int rr, int kk, f32x4 v) {
     *reinterpret_cast<f32x4 *>(L + kk * (ROWS + 4) + rr) = v;
 }
 
+// Optional per-item k state: a loader with `struct KS` gets ks(ctx, k) once at its split's first
+// k, fetch_ks(ctx, ks) on interior chunks and next<BK>(ks) after every load. The chunks of a split
+// are consecutive BK steps, so the per-k index math (the pixel decomposition of an im2col GEMM-K:
+// divisions, quarter-rate integer multiplies) becomes a few adds per chunk.
+template <class L, class = void>
+struct HasKs : std::false_type {
+  struct KS {};
+};
+template <class L>
+struct HasKs<L, std::void_t<typename L::KS>> : std::true_type {
+  using KS = typename L::KS;
+};
+
 // Stage of one operand: registers for one chunk.
 // A thread's items keep their row (or row quad) for the whole K walk, only k advances, so each
 // loader splits its address math into a per-row context (the row -> (image, pixel) or
 // (tap, channel) decomposition, computed once per tile in init) and the per-k remainder
-// (fetch_ctx): the integer divisions of an implicit im2col run once, not once per chunk.
+// (fetch_ctx, or the k state above): the integer divisions of an implicit im2col run once, not
+// once per chunk.
 template <class LD, int ROWS, int BK>
 struct Stage {
   using S = LdsShape<LD::KMAJOR, ROWS, BK>;
+  static constexpr bool KST = HasKs<LD>::value;
   f32x4 r[S::ITEMS];
   typename LD::Ctx cx[S::ITEMS];
-  __device__ __forceinline__ void init(const LD &ld, int row0) {
+  typename HasKs<LD>::KS ks[KST ? S::ITEMS : 1];
+  __device__ __forceinline__ void init(const LD &ld, int row0, int kb) {
 #pragma unroll
     for (int i = 0; i < S::ITEMS; ++i) {
       const int it = threadIdx.x + i * 256;
@@ -98,6 +114,7 @@ struct Stage {
         int rr, kk;
         item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
         cx[i] = ld.ctx(row0 + rr);
+        if constexpr (KST) ks[i] = ld.ks(cx[i], kb + kk);
       }
     }
   }
@@ -112,7 +129,10 @@ struct Stage {
         if (S::QUADS % 256 == 0 || it < S::QUADS) {
           int rr, kk;
           item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
-          r[i] = ld.fetch_ctx(cx[i], k0 + kk);
+          if constexpr (KST)
+            r[i] = ld.fetch_ks(cx[i], ks[i]);
+          else
+            r[i] = ld.fetch_ctx(cx[i], k0 + kk);
         }
       }
     } else {
@@ -125,6 +145,10 @@ struct Stage {
           r[i] = ld.fetch(row0, rr, k0, kk, ke, nrows);
         }
       }
+    }
+    if constexpr (KST) {
+#pragma unroll
+      for (int i = 0; i < S::ITEMS; ++i) ld.template next<BK>(ks[i]);
     }
   }
   __device__ __forceinline__ void store(float *L) const {
@@ -143,6 +167,14 @@ struct Stage {
 // Quad epilogues (EP::QUAD): ep.quad(m, n, z, v) receives the 4 consecutive rows m..m+3 (m % 4
 // == 0) of column n that one lane's accumulator holds — a 2x2 max pool over pool-ordered rows
 // (LdIm2col<G, U8, true>) becomes a register reduction. M must be a multiple of 4.
+// Two-phase epilogues (EP::Pre): ep.pre(m, n) loads the operands of output (m, n) — called for
+// every output of the lane (clamped to the last valid row / column) before any ep(pre, ...) or
+// ep.quad(pre, ...) stores.
+template <class E, class = void>
+struct HasPre : std::false_type {};
+template <class E>
+struct HasPre<E, std::void_t<typename E::Pre>> : std::true_type {};
+
 template <class E, class = void>
 struct IsQuadEp : std::false_type {};
 template <class E>
@@ -150,9 +182,29 @@ struct IsQuadEp<E, std::void_t<decltype(E::QUAD)>> : std::bool_constant<E::QUAD>
 
 // One output tile (bx, by) of K-split bz; smem = the dynamic LDS (gemm_lds_bytes). A device
 // function so grouped launches (GemmJob, group_kernel) can run several products in one grid.
+// B loaders whose operand depends on the output row tile (LdConvBwdBPhase: the stride phase of
+// its rows) provide for_mtile(bx); the others are used as they are.
+template <class L, class = void>
+struct HasForMtile : std::false_type {};
+template <class L>
+struct HasForMtile<L, std::void_t<decltype(std::declval<const L &>().for_mtile(0))>> : std::true_type {};
+
+template <class T, class LA, class LB, class EP>
+__device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP &ep, int M, int N, int K,
+                                            int kchunk, int bx, int by, int bz, float *smem);
+
 template <class T, class LA, class LB, class EP>
 __device__ __forceinline__ void gemm_body(const LA &la, const LB &lb, const EP &ep, int M, int N, int K, int kchunk,
                                           int bx, int by, int bz, float *smem) {
+  if constexpr (HasForMtile<LB>::value)
+    gemm_body_t<T>(la, lb.for_mtile(bx), ep, M, N, K, kchunk, bx, by, bz, smem);
+  else
+    gemm_body_t<T>(la, lb, ep, M, N, K, kchunk, bx, by, bz, smem);
+}
+
+template <class T, class LA, class LB, class EP>
+__device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP &ep, int M, int N, int K,
+                                            int kchunk, int bx, int by, int bz, float *smem) {
   using SA = LdsShape<LA::KMAJOR, T::BM, T::BK>;
   using SB = LdsShape<LB::KMAJOR, T::BN, T::BK>;
   float *As = smem;
@@ -175,8 +227,8 @@ __device__ __forceinline__ void gemm_body(const LA &la, const LB &lb, const EP &
 
   Stage<LA, T::BM, T::BK> sa;
   Stage<LB, T::BN, T::BK> sb;
-  sa.init(la, m0);
-  sb.init(lb, n0);
+  sa.init(la, m0, kb);
+  sb.init(lb, n0, kb);
   if (kb < ke) {
     sa.load(la, m0, kb, ke, M);
     sb.load(lb, n0, kb, ke, N);
@@ -211,6 +263,41 @@ __device__ __forceinline__ void gemm_body(const LA &la, const LB &lb, const EP &
     __syncthreads();
   }
 
+  if constexpr (HasPre<EP>::value) {
+    // Two-phase epilogue: every operand load of the lane's outputs is issued before the first
+    // store (the stores may alias the loaded arrays as far as the compiler knows, so a fused
+    // load-compute-store per element waits one memory latency per element).
+    constexpr int NQ = IsQuadEp<EP>::value ? 1 : 4;
+    typename EP::Pre pre[T::TM][T::TN][NQ];
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j) {
+        const int n = min(n0 + (wn * T::TN + j) * 16 + r, N - 1);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int m = min(m0 + (wm * T::TM + i) * 16 + g * 4 + q, NQ == 1 ? M - 4 : M - 1);
+          pre[i][j][q] = ep.pre(m, n);
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j) {
+        const int n = n0 + (wn * T::TN + j) * 16 + r;
+        if constexpr (IsQuadEp<EP>::value) {
+          const int m = m0 + (wm * T::TM + i) * 16 + g * 4;
+          if (m < M && n < N) ep.quad(pre[i][j][0], m, n, bz, acc[i][j]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int m = m0 + (wm * T::TM + i) * 16 + g * 4 + q;
+            if (m < M && n < N) ep(pre[i][j][q], m, n, bz, acc[i][j][q]);
+          }
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < T::TM; ++i)
 #pragma unroll
@@ -229,11 +316,28 @@ __device__ __forceinline__ void gemm_body(const LA &la, const LB &lb, const EP &
     }
 }
 
+// XCD-aware tile order. Workgroups are dealt to the 8 XCDs round-robin by launch index (each XCD
+// has its own L2), so with the tile index = launch index the M-tiles of one K-split — which read
+// the same B columns and, for an implicit im2col, nearly the same input pixels — land on 8 L2s
+// and each fetches them from HBM (4.6x the algorithmic bytes on the LSTM conv2 weight gradient).
+// The launch indices of one residue class (one XCD) take a contiguous run of tile indices
+// instead; the n % 8 remainder keeps its own index. A bijection on [0, n): only placement moves.
+__device__ __forceinline__ int xcd_tile(int id, int n) {
+  const int per = n >> 3;
+  return id < (per << 3) ? (id & 7) * per + (id >> 3) : id;
+}
+
 template <class T, class LA, class LB, class EP>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EP ep, int M, int N, int K,
                                                        int kchunk) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+#ifdef MT_NO_XCD_TILES
   gemm_body<T>(la, lb, ep, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+#else
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int t = xcd_tile(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  gemm_body<T>(la, lb, ep, M, N, K, kchunk, t % gx, (t / gx) % gy, t / (gx * gy), smem);
+#endif
 }
 
 template <class T, class LA, class LB>
@@ -290,6 +394,9 @@ struct GemmJob {
   __host__ __device__ int blocks() const { return gx * gy * gz; }
   size_t lds() const { return gemm_lds_bytes<T, LA, LB>(); }
   __device__ __forceinline__ void run(int id, float *smem) const {
+#ifndef MT_NO_XCD_TILES
+    id = xcd_tile(id, blocks());  // (a job's offset in its group only renames the residue classes)
+#endif
     const int bx = id % gx, t = id / gx;
     gemm_body<T>(la, lb, ep, M, N, K, kchunk, bx, t % gy, t / gy, smem);
   }
@@ -332,6 +439,14 @@ __global__ __launch_bounds__(256) void group_kernel(J1 j1, J2 j2, J3 j3) {
 // One grid for up to three jobs (blocks in argument order: put the critical path first).
 template <class J1, class J2 = NoJob, class J3 = NoJob>
 inline int launch_group(hipStream_t s, const J1 &j1, const J2 &j2 = NoJob{}, const J3 &j3 = NoJob{}) {
+#ifdef MT_SPLIT_GROUPS  // experiment builds: every job of a group in its own launch (per-job rocprof times)
+  if constexpr (!std::is_same_v<J2, NoJob> || !std::is_same_v<J3, NoJob>) {
+    int rc = launch_group(s, j1);
+    if (rc == MT_OK) rc = launch_group(s, j2);
+    if (rc == MT_OK) rc = launch_group(s, j3);
+    return rc;
+  }
+#endif
   const int nb = j1.blocks() + j2.blocks() + j3.blocks();
   if (nb == 0) return MT_OK;
   const size_t lds = std::max(j1.blocks() ? j1.lds() : 0, std::max(j2.blocks() ? j2.lds() : 0, j3.blocks() ? j3.lds() : 0));
@@ -408,6 +523,17 @@ struct LdColMajor {
   __device__ __forceinline__ Ctx ctx(int row) const { return {X + row}; }
   __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int k) const {
     return *reinterpret_cast<const f32x4 *>(c.p + (size_t)k * ld);
+  }
+  struct KS {
+    const float *p;
+  };
+  __device__ __forceinline__ KS ks(const Ctx &c, int k) const { return {c.p + (size_t)k * ld}; }
+  __device__ __forceinline__ f32x4 fetch_ks(const Ctx &, const KS &s) const {
+    return *reinterpret_cast<const f32x4 *>(s.p);
+  }
+  template <int BK>
+  __device__ __forceinline__ void next(KS &s) const {
+    s.p += (size_t)BK * ld;
   }
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
     const int row = row0 + rr, k = k0 + kk;
@@ -550,15 +676,57 @@ struct LdIm2colT {
   __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
     return row0 + rows <= G::KK && k0 + bk <= ke;  // the bias-row tile takes the guarded path
   }
-  // Row context: the tap (ky - PT, kx - PL) and channel of weight row quad kr.
+  // Row context: the tap (ky - PT, kx - PL) and channel of weight row quad kr, and its element
+  // offset from the window origin.
   struct Ctx {
-    int dy, dx, ci;
+    int dy, dx, ci, toff;
   };
   __device__ __forceinline__ Ctx ctx(int kr) const {
     const int ky = kr / (G::KW * G::CIN);
     const int r2 = kr - ky * (G::KW * G::CIN);
     const int kx = r2 / G::CIN;
-    return {ky - G::PT, kx - G::PL, r2 - kx * G::CIN};
+    const int dy = ky - G::PT, dx = kx - G::PL, ci = r2 - kx * G::CIN;
+    return {dy, dx, ci, (dy * G::W + dx) * G::CIN + ci};
+  }
+  // k state of GEMM-K pixel m = (b, oy, ox): the window origin (sy, sx) = (oy*S, ox*S) and its
+  // element offset pix = ((b*H + sy)*W + sx)*CIN (the host keeps B*H*W*CIN < 2^31), stepped by
+  // BK pixels with carries instead of re-divided per chunk.
+  struct KS {
+    int pix, sy, sx;
+  };
+  __device__ __forceinline__ KS ks(const Ctx &, int m) const {
+    const int b = m / (G::OH * G::OW);
+    const int rem = m - b * (G::OH * G::OW);
+    const int oy = rem / G::OW, ox = rem - oy * G::OW;
+    return {((b * G::H + oy * G::S) * G::W + ox * G::S) * G::CIN, oy * G::S, ox * G::S};
+  }
+  template <int BK>
+  __device__ __forceinline__ void next(KS &s) const {
+    constexpr int DY = BK / G::OW, DX = BK % G::OW, S = G::S;
+    constexpr int CW = G::W * G::CIN;
+    s.pix += (DY * S * G::W + DX * S) * G::CIN;
+    s.sx += DX * S;
+    s.sy += DY * S;
+    const bool cx = s.sx >= G::OW * S;  // row carry: (oy + 1, ox - OW)
+    s.sx -= cx ? G::OW * S : 0;
+    s.sy += cx ? S : 0;
+    s.pix += cx ? (S * CW - G::OW * S * G::CIN) : 0;
+#pragma unroll
+    for (int w = 0; w < 1 + BK / (G::OH * G::OW); ++w) {  // image carries: (b + 1, oy - OH)
+      const bool cy = s.sy >= G::OH * S;
+      s.sy -= cy ? G::OH * S : 0;
+      s.pix += cy ? (G::H - G::OH * S) * CW : 0;
+    }
+  }
+  __device__ __forceinline__ f32x4 fetch_ks(const Ctx &c, const KS &s) const {
+    if constexpr (G::SAME) {
+      const int iy = s.sy + c.dy, ix = s.sx + c.dx;
+      const bool ok = (unsigned)iy < (unsigned)G::H && (unsigned)ix < (unsigned)G::W;
+      const f32x4 v = InElem<U8>::load4(X + (ok ? s.pix + c.toff : s.pix + c.ci));
+      return ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      return InElem<U8>::load4(X + (s.pix + c.toff));
+    }
   }
   __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int m) const {
     const int b = m / (G::OH * G::OW);
@@ -686,7 +854,7 @@ struct LdConvBwdB {
 // phase (py, px) = (iy % S, ix % S), so the dense gather above multiplies (S*S - 1)/(S*S) zeros.
 // Rows are regrouped by phase — row m' = phase * MP + l, l = (b, qy, qx) with iy = S*qy + py —
 // and K shrinks to (KH/S)(KW/S)*COUT. MP (rows per phase, padded to the tile height) keeps every
-// workgroup inside one phase, which the B loader reads from blockIdx.x.
+// workgroup inside one phase, which the B loader takes from the row tile (for_mtile).
 template <class G>
 struct PhaseGeom {
   static constexpr bool OK = G::S > 1 && !G::SAME && G::KH % G::S == 0 && G::KW % G::S == 0 &&
@@ -756,11 +924,16 @@ struct LdConvBwdBPhase {
   using P = PhaseGeom<G>;
   const float *Wt;  // HWIO
   int blocks_per_phase;
+  int ph = 0;  // set per output tile by for_mtile (gemm_body)
+  __device__ __forceinline__ LdConvBwdBPhase for_mtile(int bx) const {
+    LdConvBwdBPhase l = *this;
+    l.ph = bx / blocks_per_phase;
+    return l;
+  }
   __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
     return row0 + rows <= nrows && k0 + bk <= ke;
   }
   __device__ __forceinline__ f32x4 at(int ci, int k) const {
-    const int ph = (int)blockIdx.x / blocks_per_phase;
     const int py = ph / G::S, px = ph - py * G::S;
     const int a = k / (P::KB * G::COUT);
     const int r2 = k - a * (P::KB * G::COUT);
@@ -802,6 +975,13 @@ struct EpBiasAct {
   __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
     Y[(size_t)m * ld + n] = act_fwd(v + bias[n], act, alpha);
   }
+  struct Pre {
+    float b;
+  };
+  __device__ __forceinline__ Pre pre(int, int n) const { return {bias[n]}; }
+  __device__ __forceinline__ void operator()(const Pre &p, int m, int n, int, float v) const {
+    Y[(size_t)m * ld + n] = act_fwd(v + p.b, act, alpha);
+  }
 };
 
 // Conv bias + activation + 2x2/2 VALID max pool (networks.py:108-110) over pool-ordered rows
@@ -816,8 +996,13 @@ struct EpBiasActPool {
   const float *bias;
   int act;
   float alpha;
-  __device__ __forceinline__ void quad(int m, int n, int, f32x4 v) const {
-    const float bn = bias[n];
+  struct Pre {
+    float b;
+  };
+  __device__ __forceinline__ Pre pre(int, int n) const { return {bias[n]}; }
+  __device__ __forceinline__ void quad(int m, int n, int z, f32x4 v) const { quad(pre(m, n), m, n, z, v); }
+  __device__ __forceinline__ void quad(const Pre &p, int m, int n, int, f32x4 v) const {
+    const float bn = p.b;
     float mx = act_fwd(v[0] + bn, act, alpha);
     int a = 0;
 #pragma unroll
@@ -858,15 +1043,30 @@ struct EpMaskedPhase {
   const float *Yact;
   int mp, B, act;
   float alpha;
-  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
+  // element of phase row m, or -1 for the phase padding rows
+  __device__ __forceinline__ long index(int m, int n) const {
     const int ph = m / mp, l = m - ph * mp;
     const int py = ph / G::S, px = ph - py * G::S;
     const int b = l / (P::HQ * P::WQ);
-    if (b >= B) return;  // phase padding rows
+    if (b >= B) return -1;
     const int rem = l - b * (P::HQ * P::WQ);
     const int qy = rem / P::WQ, qx = rem - qy * P::WQ;
-    const size_t i = (((size_t)b * G::H + G::S * qy + py) * G::W + G::S * qx + px) * G::CIN + n;
-    dX[i] = v * act_bwd(Yact[i], act, alpha);
+    return (((long)b * G::H + G::S * qy + py) * G::W + G::S * qx + px) * G::CIN + n;
+  }
+  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
+    const long i = index(m, n);
+    if (i >= 0) dX[i] = v * act_bwd(Yact[i], act, alpha);
+  }
+  struct Pre {
+    long i;
+    float y;
+  };
+  __device__ __forceinline__ Pre pre(int m, int n) const {
+    const long i = index(m, n);
+    return {i, Yact[i < 0 ? 0 : i]};
+  }
+  __device__ __forceinline__ void operator()(const Pre &p, int, int, int, float v) const {
+    if (p.i >= 0) dX[p.i] = v * act_bwd(p.y, act, alpha);
   }
 };
 
@@ -881,11 +1081,19 @@ struct EpMaskedUnpool {
   const uint8_t *arg;
   int act;
   float alpha;
-  __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
+  struct Pre {
+    float p;
+    int a;
+  };
+  __device__ __forceinline__ Pre pre(int m, int n) const {
+    const size_t i = (size_t)m * GJ::COUT + n;
+    return {P[i], arg[i]};
+  }
+  __device__ __forceinline__ void operator()(int m, int n, int z, float v) const { (*this)(pre(m, n), m, n, z, v); }
+  __device__ __forceinline__ void operator()(const Pre &pr, int m, int n, int, float v) const {
     constexpr int PH = GJ::OH / 2, PW = GJ::OW / 2, C = GJ::COUT;
-    const size_t i = (size_t)m * C + n;
-    const float g = v * act_bwd(P[i], act, alpha);
-    const int a = arg[i];
+    const float g = v * act_bwd(pr.p, act, alpha);
+    const int a = pr.a;
     const int b = m / (PH * PW);
     const int rem = m - b * (PH * PW);
     const int py = rem / PW, px = rem - py * PW;
@@ -923,6 +1131,13 @@ struct EpMasked {
   __device__ __forceinline__ void operator()(int m, int n, int, float v) const {
     const size_t i = (size_t)m * ld + n;
     dX[i] = v * act_bwd(Yact[i], act, alpha);
+  }
+  struct Pre {
+    float y;
+  };
+  __device__ __forceinline__ Pre pre(int m, int n) const { return {Yact[(size_t)m * ld + n]}; }
+  __device__ __forceinline__ void operator()(const Pre &p, int m, int n, int, float v) const {
+    dX[(size_t)m * ld + n] = v * act_bwd(p.y, act, alpha);
   }
 };
 

@@ -210,14 +210,23 @@ constexpr int conv_bk() {
 
 template <class G>
 using TileConvFwd = typename TileFor<G::COUT, conv_bk<G::KK>()>::T;
+#ifndef MT_WGRAD_BK
+#define MT_WGRAD_BK 64
+#endif
 template <class G>
-using TileConvWgrad = typename TileFor<G::COUT, 64>::T;
+using TileConvWgrad = typename TileFor<G::COUT, MT_WGRAD_BK>::T;
+#ifndef MT_DGRAD_BK  // 64: half the LDS of 128, twice the resident workgroups (LSTM conv2 dX -5 %, Pong conv2 dX -7 %)
+#define MT_DGRAD_BK 64
+#endif
 template <class G>
-using TileConvDgrad = typename TileFor<G::CIN, 128>::T;
+using TileConvDgrad = typename TileFor<G::CIN, MT_DGRAD_BK>::T;
 
 using TileFc = Tile<32, 64, 2, 2, 64>;       // dense forward, M = batch (small), split-K
-using TileDenseW = Tile<64, 64, 2, 2, 80>;   // dense dW (GEMM-K = batch: 160 = 2 chunks at ec=32)
-using TileDenseX = Tile<32, 64, 2, 2, 128>;  // dense dX (GEMM-K = F; M = batch: 32-row tiles, 2x the blocks)
+// dense dW (GEMM-K = batch: 160 = 2 chunks at ec=32) and dX (GEMM-K = F, M = batch): latency-bound
+// at rollout batches, so small tiles — more workgroups, fewer MFMAs per wave (Pong: dense group
+// 12.1 -> 10.6 us; LSTM dense dW 17.1 -> 13.1 us)
+using TileDenseW = Tile<32, 64, 2, 2, 80>;
+using TileDenseX = Tile<32, 32, 2, 2, 128>;
 
 static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
   int s = target / (grid_mn > 0 ? grid_mn : 1);
@@ -930,8 +939,13 @@ static auto conv_dgrad_unpool_job(const float *dY, const float *Wt, const float 
                                   float *dactj, int B, int act, float alpha) {
   using T = TileConvDgrad<G>;
   static_assert(!PhaseGeom<G>::OK, "pooled inputs feed stride-1 convs (networks.py:206-225)");
+#ifdef MT_EXP_DX_POOLED_EP  // timing experiment only (wrong gradient): the pooled-resolution epilogue
+  return gemm_job<T>(LdConvBwdA<G>{dY}, LdConvBwdB<G>{Wt}, EpMasked{dactj, Pj, G::CIN, act, alpha},
+                     B * G::H * G::W, G::CIN, G::KH * G::KW * G::COUT, 1);
+#else
   return gemm_job<T>(LdConvBwdA<G>{dY}, LdConvBwdB<G>{Wt}, EpMaskedUnpool<GJ>{dactj, Pj, argj, act, alpha},
                      B * G::H * G::W, G::CIN, G::KH * G::KW * G::COUT, 1);
+#endif
 }
 
 #define MT_TRY(x)              \
@@ -981,6 +995,10 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
   const void *x = I == 0 ? (const void *)obs : (const void *)layer_out<Ar, (I > 0 ? I - 1 : 0)>(ws, L);
+  if ((size_t)B * G::H * G::W * G::CIN >= ((size_t)1 << 31)) {  // LdIm2colT's 32-bit pixel offsets
+    set_error("batch %d too large for the conv %d weight gradient", B, I);
+    return MT_ERR_ARG;
+  }
   const auto wg = conv_wgrad_jobs<G, I == 0>(x, ws + L.dact[I], ws + (I % 2 ? L.wslab2 : L.wslab),
                                              grad + n->off_conv[I], B);
   if constexpr (I > 0) {
