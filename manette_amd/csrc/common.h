@@ -122,6 +122,13 @@ struct SampleArgs {
   // tag, so a host that sees the tag in both has the pair, with no fence on the device side
   uint64_t *packed = nullptr;
   int32_t row0 = 0;  // global env id of row 0 (the rank's env offset): the uniforms hash row0 + b
+  // replayed rollout graph (mt_rollout_step): the kernel arguments are fixed at capture, so the
+  // per-rollout sequence numbers live in device memory: seq = *seq_base + seq (read at kernel
+  // start); advance (bootstrap heads, no draw): block 0 adds advance_by to advance[0] and
+  // advance[1] once every reader of this rollout has run (the next replay's bases)
+  const uint32_t *seq_base = nullptr;
+  uint32_t *advance = nullptr;
+  uint32_t advance_by = 0;
 };
 
 }  // namespace mt
@@ -152,6 +159,9 @@ struct StackSrc {
   const uint32_t *ready = nullptr;
   uint32_t tag = 0;
   uint32_t *status = nullptr;
+  // replayed rollout graph: the tag waited for is (*tag_base + tag) & 0x1fffffff (device memory,
+  // advanced by the graph's bootstrap heads kernel, SampleArgs::advance)
+  const uint32_t *tag_base = nullptr;
 };
 
 // 16 bytes at byte offset `off` of a host-published buffer, where [lo, hi) is the byte range

@@ -501,6 +501,11 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
       wpre[k][j] = (o < O && f < F) ? head_w(hp, f, o) : 0.f;
     }
   const uint64_t cnt = smp.counters ? smp.counters[b] : 0;
+  const uint32_t seq = smp.seq_base ? *smp.seq_base + smp.seq : smp.seq;  // (graph replay: device base)
+  if (smp.advance && b == 0 && threadIdx.x == 0) {  // the replayed rollout's last reader has run
+    smp.advance[0] += smp.advance_by;
+    smp.advance[1] += smp.advance_by;
+  }
   for (int f = threadIdx.x; f < F; f += 256) {
     const float *p = slabs + (size_t)b * F + f;
     const size_t zs_stride = (size_t)B * F;
@@ -561,7 +566,7 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
       smp.a_idx[b] = a;
       smp.r_idx[b] = r;
       if (smp.packed) {  // tagged pair, one 8-byte store, no fence (SampleArgs::packed)
-        const uint64_t tag = (uint64_t)(smp.seq & 0xffffu) << 16;
+        const uint64_t tag = (uint64_t)(seq & 0xffffu) << 16;
         const uint64_t word = ((tag | (uint32_t)r) << 32) | tag | (uint32_t)a;
         __hip_atomic_store(smp.packed + b, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       } else if (smp.pair) {
@@ -570,7 +575,7 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
       }
       if (smp.ready && !smp.packed) {  // release: the pair stores are visible to the host before the flag
         __threadfence_system();
-        __hip_atomic_store(smp.ready + b, smp.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(smp.ready + b, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
@@ -1401,7 +1406,8 @@ int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *ob
                        bool infer, hipStream_t stream, const TrainRows *tr, const StackSrc *st,
                        const hipEvent_t *marks) {
   MT_CHECK_ARG(net && params && obs && ws && v && pi && rep, "null argument");
-  MT_CHECK_ARG(!smp || (smp->counters && smp->a_idx && smp->r_idx), "null sample buffer");
+  // (smp without counters: no draw — the replayed rollout graph's bootstrap carries only `advance`)
+  MT_CHECK_ARG(!smp || !smp->counters || (smp->a_idx && smp->r_idx), "null sample buffer");
   MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
   MT_ARCH_SWITCH(net, {
     const WsLayout L = ws_layout<Ar>(net, batch);

@@ -52,6 +52,23 @@ struct mt_rollout {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> marks;
   size_t marks_used = 0;
+  // Replayed rollout graph (NIPS stacking chains): step 0's forward + the chains of steps 1..T
+  // (the bootstrap last) captured once and launched as one hipGraph per rollout — ~6 us of host
+  // time where enqueueing the 6 chains took ~13 us each, on the step-0 critical path. The kernel
+  // arguments are fixed, so the rollout's sequence bases live in device memory: gbase_dev[0] =
+  // the host step word value at step 0 (ready-word tags), gbase_dev[1] = the draw sequence number
+  // before step 0's forward; the bootstrap heads kernel adds T to both. Host mirror: gbase_next.
+  hipGraphExec_t rgraph = nullptr;
+  const float *rgraph_params = nullptr;
+  hipStream_t cap_stream = nullptr;
+  hipEvent_t gev = nullptr;       // recorded after each replay: device-error checks while waiting
+  uint32_t *gbase_dev = nullptr;  // [2]
+  uint32_t gbase_host[2] = {0, 0};  // staging of the (re)initialisation copy
+  uint32_t gbase_next[2] = {0, 0};  // device values after the last replay
+  bool gbase_valid = false;
+  bool capturing = false;  // enqueue_forward / arm_step record offsets + bases
+  bool graph_live = false; // this rollout runs from the replayed graph
+  bool graph_off = false;  // MT_ROLLOUT_GRAPH=0
 };
 
 using namespace mt;
@@ -170,6 +187,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   // chain land there instead of in front of the later steps' waits (step 1 was host-bound)
   ro->ahead = T;
   if (const char *v = std::getenv("MT_ROLLOUT_AHEAD")) ro->ahead = std::max(1, std::min(T, std::atoi(v)));
+  if (const char *v = std::getenv("MT_ROLLOUT_GRAPH")) ro->graph_off = std::atoi(v) == 0;
   ro->fwd_of.assign(T, 0);
   ro->ev.assign(T, nullptr);
   for (int i = 0; i < T; ++i) {
@@ -187,6 +205,10 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
 
 extern "C" void mt_rollout_destroy(mt_rollout *ro) {
   if (!ro) return;
+  if (ro->rgraph) (void)hipGraphExecDestroy(ro->rgraph);
+  if (ro->cap_stream) (void)hipStreamDestroy(ro->cap_stream);
+  if (ro->gev) (void)hipEventDestroy(ro->gev);
+  if (ro->gbase_dev) (void)hipFree(ro->gbase_dev);
   for (hipEvent_t e : ro->ev) (void)hipEventDestroy(e);
   for (auto &m : ro->marks) {
     (void)hipEventDestroy(m.first);
@@ -339,14 +361,20 @@ int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, b
                       : StackSrc{b.states + (size_t)T * slot, nullptr, nullptr, b.states};
   if (t > 0) {
     st.ready = ro->env_ready_dev;
-    st.tag = want & 0x1fffffffu;
+    st.tag = want & 0x1fffffffu;  // (capturing: the offset k of gbase_dev[0])
     st.status = ro->status_dev;
+    if (ro->capturing) st.tag_base = ro->gbase_dev;
   }
   int32_t *a_d = b.idx + (size_t)t * E, *r_d = b.idx + (size_t)T * E + (size_t)t * E;
   SampleArgs smp{ro->seed, b.counters, a_d, r_d, ro->zero_copy ? ro->pair_dev : b.pair};
   smp.ready = ro->ready_dev;
-  smp.seq = ++ro->fwd_seq;
-  ro->fwd_of[t] = smp.seq;
+  if (ro->capturing) {  // draw sequence number gbase_dev[1] + t + 1 (mt_rollout_step sets fwd_of)
+    smp.seq = (uint32_t)t + 1;
+    smp.seq_base = ro->gbase_dev + 1;
+  } else {
+    smp.seq = ++ro->fwd_seq;
+    ro->fwd_of[t] = smp.seq;
+  }
   smp.packed = ro->packed_dev;
   smp.row0 = b.env_offset;
   // with a train workspace: activations into its rows t*E.., per-step pi / rep (mt_forward_rows)
@@ -365,7 +393,7 @@ int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, b
   }
   if (!ro->zero_copy)
     MT_HIP(hipMemcpyAsync(b.pair_host, b.pair, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
-  MT_HIP(hipEventRecord(ro->ev[t], s));
+  if (!ro->capturing) MT_HIP(hipEventRecord(ro->ev[t], s));
   return MT_OK;
 }
 
@@ -402,7 +430,8 @@ int enqueue_preprocess(mt_rollout *ro, int t, int total, hipStream_t s) {
 int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t s) {
   const mt_rollout_buffers &b = ro->b;
   const int E = ro->E, T = ro->T;
-  const uint32_t want = ro->seq + (uint32_t)ahead;
+  // (capturing: the offset k from the rollout's base gbase_dev[0] = the host step word at step 0)
+  const uint32_t want = ro->capturing ? (uint32_t)k : ro->seq + (uint32_t)ahead;
   // pull: the pull kernel waits per env and copies the pushes into HBM; the preprocess of step
   // k-1 then reads them there — inside step k's forward conv kernel (stack_fwd, NIPS), else as
   // mt_preprocess_resized
@@ -434,12 +463,82 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
     st.ready = ro->env_ready_dev;
     st.tag = want & 0x1fffffffu;
     st.status = ro->status_dev;
+    SampleArgs adv{};  // capturing: no draw; the heads kernel advances the replay's bases by T
+    if (ro->capturing) {
+      st.tag_base = ro->gbase_dev;
+      adv.advance = ro->gbase_dev;
+      adv.advance_by = (uint32_t)T;
+    }
     MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)T * slot, E, b.ws, b.ws_bytes, b.v_boot,
-                           b.pi + po * ro->A, b.rep + po * ro->R, nullptr, true, s, nullptr, stk ? &st : nullptr));
+                           b.pi + po * ro->A, b.rep + po * ro->R, ro->capturing ? &adv : nullptr, true, s, nullptr,
+                           stk ? &st : nullptr));
   }
   ro->armed_upto = k;
   return MT_OK;
 }
+
+// The replayed rollout graph applies to the NIPS stacking chains with the bootstrap in the last
+// chain, every chain armed at step 0, after a first eager rollout (step 0's forward then takes
+// slot 0 from slot T), without trunk timing (its events are per launch).
+bool graph_eligible(const mt_rollout *ro) {
+  return !ro->graph_off && ro->pipelined && ro->stack_fwd && !ro->lstm && ro->packed_host && ro->b.v_boot &&
+         ro->zero_copy && ro->ahead == ro->T && !ro->timing && ro->rollouts > 0;
+}
+
+// Step 0 of a rollout from the replayed graph: capture it on first use (or when the parameter
+// buffer moved), bring the device bases in line with the host's counters when an eager rollout ran
+// in between, launch, and set the host's expectations (draw tags, armed steps).
+int replay_rollout_graph(mt_rollout *ro, const float *params, hipStream_t s) {
+  const int T = ro->T;
+  if (!ro->gbase_dev) {
+    MT_HIP(hipMalloc((void **)&ro->gbase_dev, 2 * sizeof(uint32_t)));
+    MT_HIP(hipEventCreateWithFlags(&ro->gev, hipEventDisableTiming));
+    MT_HIP(hipStreamCreateWithFlags(&ro->cap_stream, hipStreamNonBlocking));
+  }
+  if (ro->rgraph && ro->rgraph_params != params) {
+    MT_HIP(hipGraphExecDestroy(ro->rgraph));
+    ro->rgraph = nullptr;
+  }
+  if (!ro->rgraph) {
+    MT_HIP(hipStreamBeginCapture(ro->cap_stream, hipStreamCaptureModeThreadLocal));
+    ro->capturing = true;
+    int rc = enqueue_forward(ro, params, 0, ro->cap_stream, true);
+    for (int k = 1; rc == MT_OK && k <= T; ++k) rc = arm_step(ro, params, k, k, ro->cap_stream);
+    ro->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(ro->cap_stream, &g);
+    if (rc != MT_OK) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    MT_HIP(ec);
+    const hipError_t ei = hipGraphInstantiate(&ro->rgraph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ei != hipSuccess) {
+      ro->rgraph = nullptr;
+      set_error("hipGraphInstantiate (rollout) failed: %s", hipGetErrorString(ei));
+      return MT_ERR_HIP;
+    }
+    ro->rgraph_params = params;
+  }
+  if (!ro->gbase_valid || ro->gbase_next[0] != ro->seq || ro->gbase_next[1] != ro->fwd_seq) {
+    // (stream-ordered after every earlier reader: the previous replay's bootstrap has advanced them)
+    ro->gbase_host[0] = ro->seq;
+    ro->gbase_host[1] = ro->fwd_seq;
+    MT_HIP(hipMemcpyAsync(ro->gbase_dev, ro->gbase_host, sizeof(ro->gbase_host), hipMemcpyHostToDevice, s));
+  }
+  MT_HIP(hipGraphLaunch(ro->rgraph, s));
+  MT_HIP(hipEventRecord(ro->gev, s));
+  for (int t = 0; t < T; ++t) ro->fwd_of[t] = ro->fwd_seq + 1 + (uint32_t)t;
+  ro->fwd_seq += (uint32_t)T;
+  ro->gbase_next[0] = ro->seq + (uint32_t)T;  // (the host step word after this rollout's T steps)
+  ro->gbase_next[1] = ro->fwd_seq;
+  ro->gbase_valid = true;
+  ro->armed_upto = T;
+  ro->graph_live = true;
+  return MT_OK;
+}
+
 }  // namespace
 
 // One macro-step t (paac.py:140-205). Pipelined mode keeps the GPU one step ahead of the host's
@@ -460,6 +559,10 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   int32_t *a_h = b.idx_host + (size_t)t * E, *r_h = b.idx_host + (size_t)T * E + (size_t)t * E;
   // 1. forward + draw of step t, unless a previous call already enqueued it
   if (t == 0 || !ro->pipelined) ro->armed_upto = -1;  // a new rollout (parameters changed)
+  if (t == 0) {
+    ro->graph_live = false;
+    if (graph_eligible(ro)) MT_TRY_(replay_rollout_graph(ro, params, s));
+  }
   if (ro->armed_upto < t) {
     // stack_fwd: after a completed rollout, slot 0 is taken from slot T inside this forward
     MT_TRY_(enqueue_forward(ro, params, t, s, t == 0 && ro->stack_fwd && ro->rollouts > 0));
@@ -476,6 +579,7 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   // (with ready flags: poll the E flags the heads kernel stores after each pair — one cached host
   //  load each — and query the event only now and then, to surface a device error)
   const uint32_t want = ro->fwd_of[t];
+  const hipEvent_t step_ev = ro->graph_live ? ro->gev : ro->ev[t];  // (device-error checks)
   if (ro->packed_host) {  // tagged (a, r) words: both halves carry the step's tag
     const uint32_t tag = want & 0xffffu;
     const volatile uint64_t *pw = ro->packed_host;
@@ -490,7 +594,7 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
       __builtin_ia32_pause();
       if (++spins == 4096) {
         spins = 0;
-        const hipError_t q = hipEventQuery(ro->ev[t]);
+        const hipError_t q = hipEventQuery(step_ev);
         if (q != hipSuccess && q != hipErrorNotReady) MT_HIP(q);
       }
     }
@@ -504,13 +608,13 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
       __builtin_ia32_pause();
       if (++spins == 4096) {
         spins = 0;
-        const hipError_t q = hipEventQuery(ro->ev[t]);
+        const hipError_t q = hipEventQuery(step_ev);
         if (q != hipSuccess && q != hipErrorNotReady) MT_HIP(q);
       }
     }
   } else {
     hipError_t q;
-    while ((q = hipEventQuery(ro->ev[t])) == hipErrorNotReady) __builtin_ia32_pause();
+    while ((q = hipEventQuery(step_ev)) == hipErrorNotReady) __builtin_ia32_pause();
     MT_HIP(q);
   }
   if (ro->pipelined && __atomic_load_n(&b.sync_host[1], __ATOMIC_ACQUIRE) != 0) {
@@ -573,7 +677,7 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
 }
 
 extern "C" int mt_rollout_run(mt_rollout *ro, const float *params, int64_t *global_step, mt_stream_t stream) {
-  MT_CHECK_ARG(ro, "null argument");
+  MT_CHECK_ARG(ro && params && global_step, "null argument");
   for (int t = 0; t < ro->T; ++t) MT_TRY_(mt_rollout_step(ro, params, t, global_step, stream));
   return MT_OK;
 }

@@ -108,6 +108,8 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
     return;
   } else {
     __shared__ int s_p;
+    // (graph replay: the tag's base is requested first; its latency hides under the row copy)
+    const uint32_t tag = st.tag_base ? ((*st.tag_base + st.tag) & 0x1fffffffu) : st.tag;
     {  // the previous state's rows
       const uint4 *src = reinterpret_cast<const uint4 *>(st.prev + row0);
       uint4 *dst = reinterpret_cast<uint4 *>(xin);
@@ -118,7 +120,7 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
       // in-kernel pull: wait for env e's publication, then read its p pushes' rows 8i..8i+19
       // from the pinned staging (slots 4e + j) in one round trip; the edge lines of env e's slot
       // group are read with system-scope loads (ld_published16)
-      if (threadIdx.x == 0) s_p = wait_published(st.ready, e, st.tag, st.status);
+      if (threadIdx.x == 0) s_p = wait_published(st.ready, e, tag, st.status);
       MT_PROBE_AT(0, blockIdx.x, 5);  // env e seen published
       __syncthreads();
       p = min(max(s_p, 0), 4);  // (a timeout stacks no frame; the host reports the error)
