@@ -378,6 +378,17 @@ int mt_rollout_host_trace(mt_rollout *ro, double *out, int max_steps, int *n);
  * in microseconds and their count, then stops. Any call returns (and forgets) what was recorded. */
 int mt_rollout_trunk_timing(mt_rollout *ro, int enable, double *sum_us, int64_t *count);
 
+/* Update launched by the rollout itself (native pipelined step, replayed update graph): once
+ * registered, the last macro-step of every rollout (after its bookkeeping) stores
+ * lr = get_lr(global_step) — actor_learner.py:145-148: initial_lr - global_step * initial_lr /
+ * annealing_steps while global_step <= annealing_steps, else 0, in double, then rounded to float —
+ * into *lr_host (the pinned LR word the RMSProp kernel reads) and launches graph_exec (the update:
+ * loss backward [, all-reduce], clip + RMSProp) on the rollout's stream, right behind the bootstrap
+ * chain: the update then starts with no host round trip after the last emulator step (the caller
+ * must not launch it again). graph_exec NULL unregisters (before destroying the graph). */
+int mt_rollout_set_update(mt_rollout *ro, void *graph_exec, float *lr_host, double initial_lr,
+                          double annealing_steps);
+
 /* ---- data-parallel communicator (RCCL over xGMI; manette_amd/csrc/comm.hip) ----------------
  * The reference has no collective: its only shard unit is the contiguous env split of
  * runners.py:17-18 (np.split over workers). This build splits envs over ranks the same way (rank r

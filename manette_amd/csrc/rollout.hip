@@ -69,6 +69,10 @@ struct mt_rollout {
   bool capturing = false;  // enqueue_forward / arm_step record offsets + bases
   bool graph_live = false; // this rollout runs from the replayed graph
   bool graph_off = false;  // MT_ROLLOUT_GRAPH=0
+  // update launched at the end of the rollout (mt_rollout_set_update)
+  hipGraphExec_t update_graph = nullptr;
+  float *lr_host = nullptr;
+  double initial_lr = 0.0, annealing_steps = 1.0;
 };
 
 using namespace mt;
@@ -655,6 +659,15 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   } else {
     rc = enqueue_preprocess(ro, t, total, s);
   }
+  // 6. the update right behind the bootstrap chain (mt_rollout_set_update): LR of the step reached
+  if (rc == MT_OK && t == T - 1 && ro->update_graph) {
+    const int64_t gs = *global_step;
+    const double lr = (double)gs <= ro->annealing_steps
+                          ? ro->initial_lr - ((double)gs * ro->initial_lr / ro->annealing_steps)
+                          : 0.0;
+    *ro->lr_host = (float)lr;  // (read by the RMSProp kernel when it runs, after this store)
+    MT_HIP(hipGraphLaunch(ro->update_graph, s));
+  }
   const double t4 = now_us();
   ro->acc[0] += t1 - t0;
   ro->acc[1] += t2 - t1;
@@ -679,6 +692,18 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
 extern "C" int mt_rollout_run(mt_rollout *ro, const float *params, int64_t *global_step, mt_stream_t stream) {
   MT_CHECK_ARG(ro && params && global_step, "null argument");
   for (int t = 0; t < ro->T; ++t) MT_TRY_(mt_rollout_step(ro, params, t, global_step, stream));
+  return MT_OK;
+}
+
+extern "C" int mt_rollout_set_update(mt_rollout *ro, void *graph_exec, float *lr_host, double initial_lr,
+                                     double annealing_steps) {
+  MT_CHECK_ARG(ro, "null argument");
+  MT_CHECK_ARG(!graph_exec || (lr_host && annealing_steps > 0.0), "a registered update needs lr_host and annealing_steps > 0");
+  MT_CHECK_ARG(!graph_exec || ro->pipelined, "the rollout launches the update only in pipelined mode");
+  ro->update_graph = (hipGraphExec_t)graph_exec;
+  ro->lr_host = lr_host;
+  ro->initial_lr = initial_lr;
+  ro->annealing_steps = annealing_steps;
   return MT_OK;
 }
 

@@ -24,6 +24,7 @@ torch.distributed (gloo) is the control channel only: the RCCL unique id and, at
 rank 0's global_step.
 """
 import logging
+import os
 import time
 
 import numpy as np
@@ -130,6 +131,7 @@ class PAACLearner(ActorLearner):
         # replay the update as hipGraph(s) from the second update on (native pipelined step)
         self.use_update_graph = bool(getattr(args, 'update_graph', True))
         self._graphs = None
+        self._update_in_rollout = False  # mt_rollout_set_update registered (_register_update)
         self._eager_updates = 0
         self.summaries = None  # TensorBoard event files of the chief (manette_amd/summary.py)
         self._logged_episodes = 0
@@ -360,6 +362,8 @@ class PAACLearner(ActorLearner):
         instead of a dozen, and no host launch gaps between the backward's kernels."""
         self.book.drain()
         lr = self.get_lr()
+        if self._update_in_rollout:  # the rollout's last step stored lr and launched the update graph
+            return lr
         self.network.set_lr(lr)
         if self._graph_ok():
             if self._graphs is None and self._eager_updates >= 1:
@@ -370,6 +374,8 @@ class PAACLearner(ActorLearner):
                 if len(self._graphs) > 1:  # the all-reduce could not be captured
                     self.comm.allreduce(self.network.grad)
                     self._launch_graph(self._graphs[1], s)
+                else:
+                    self._register_update()
                 return lr
         self._eager_updates += 1
         self._update_backward()
@@ -494,7 +500,24 @@ class PAACLearner(ActorLearner):
         from . import _lib
         _lib.check(_lib.hip().mt_graph_launch(g, s), 'mt_graph_launch')
 
+    def _register_update(self):
+        """From the next rollout on, its last macro-step stores the LR and launches the (single)
+        update graph itself, right behind the bootstrap chain (mt_rollout_set_update): no host
+        round trip between the last emulator step and the update. MT_UPDATE_IN_ROLLOUT=0: off."""
+        if os.environ.get('MT_UPDATE_IN_ROLLOUT', '1') == '0' or self.native_step is None or self.lstm_bool:
+            return  # (LSTM: its update also moves the frame-store slots the next rollout starts from)
+        from . import _lib
+        _lib.check(_lib.hip().mt_rollout_set_update(self.native_step, self._graphs[0],
+                                                    self.network._lr_host.data_ptr(),
+                                                    float(self.initial_lr), float(self.lr_annealing_steps)),
+                   'mt_rollout_set_update')
+        self._update_in_rollout = True
+
     def _destroy_graphs(self):
+        if self._update_in_rollout and self.native_step is not None:
+            from . import _lib
+            _lib.hip().mt_rollout_set_update(self.native_step, None, None, 0.0, 1.0)
+        self._update_in_rollout = False
         if getattr(self, '_graphs', None):
             from . import _lib
             for g in self._graphs:

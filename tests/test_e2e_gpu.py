@@ -91,14 +91,20 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
             idx_all.append(L.idx_h.numpy().copy())
             L.update()
         assert L._graphs is not None  # the checked update is a graph replay
+        # the parameters / slots the checked rollout runs with, read before it: from the third update
+        # on, the rollout's last step launches the update itself (mt_rollout_set_update)
+        torch.cuda.synchronize()
+        c = lambda t: t.detach().cpu().numpy().copy()
+        P = L.network.get_variables()
+        flat_p, ms0, mom0 = c(L.network.params), c(L.network.ms), c(L.network.mom)
+        slot0 = c(L.states[0])  # (copied from slot T by the previous update unless slot0_in_rollout)
         L.book.new_update()
         L.rollout()
         torch.cuda.synchronize()
         idx_all.append(L.idx_h.numpy().copy())
-        c = lambda t: t.detach().cpu().numpy().copy()
-        P = L.network.get_variables()
-        flat_p, ms0, mom0 = c(L.network.params), c(L.network.ms), c(L.network.mom)
         states = c(L.states)
+        if L._update_in_rollout and not L.slot0_in_rollout:  # this update's apply has already run
+            states[0] = slot0
         rm = L.rm_h.numpy().copy()
         values = c(L.values)
         gs = L.global_step
@@ -106,6 +112,7 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
             fstore, nz = c(L.fstore), c(L.nz_d)  # (nz derived on the device by the native step)
         L.update()
         torch.cuda.synchronize()
+        assert L._update_in_rollout == (not lstm)  # the benchmarked path: the rollout launched this update
         # V(s_T): the rollout's last chain (pipelined native step) or the update's first forward (LSTM)
         v_boot, pi_all, rep_all = c(L.v_boot), c(L.pi_all), c(L.rep_all)
         grad, y, adv = L.network.get_variables('grad'), c(L.y), c(L.adv)
