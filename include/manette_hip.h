@@ -210,6 +210,17 @@ int mt_returns_loss_backward(const mt_net *net, const float *params, const uint8
                              const float *masks, const float *v_boot, double gamma, float *y, float *adv,
                              float entropy_beta, float *grad, float *loss_terms, float *norm_partials,
                              mt_stream_t stream);
+/* mt_returns_loss_backward with the bootstrap finished here: boot_ws is the rollout's E-row
+ * inference workspace whose dense-layer slabs the last chain left (MT_ROLLOUT_BOOT_SLABS); each
+ * loss block sums env e's slabs in slab order, adds the bias, applies the activation and takes the
+ * critic's dot product (the heads kernel's arithmetic) for V(s_T)[e] = v_boot[e] (written out),
+ * then scans. Same outputs as mt_returns_loss_backward given that v_boot. */
+int mt_returns_loss_backward_boot(const mt_net *net, const float *params, const uint8_t *obs, int T, int E, void *ws,
+                                  size_t ws_bytes, const float *pi, const float *rep, const float *values,
+                                  const int32_t *a_idx, const int32_t *r_idx, const float *rewards,
+                                  const float *masks, const void *boot_ws, size_t boot_ws_bytes, float *v_boot,
+                                  double gamma, float *y, float *adv, float entropy_beta, float *grad,
+                                  float *loss_terms, float *norm_partials, mt_stream_t stream);
 
 /* ---- global-norm clip + TF1 ApplyRMSProp (A11) ----------------------------------------------
  * Replaces clip_by_global_norm (actor_learner.py:59-63) + ApplyRMSProp (actor_learner.py:47-48,74).
@@ -310,6 +321,11 @@ int mt_memory_push(uint8_t *memory, uint8_t *whole_t, const uint8_t *fresh, cons
 /* flags & MT_ROLLOUT_RESIZED: the runner stages each push's final 84x84 frame (MH_RUNNER_RESIZED,
  * staging [4E][84*84*depth]) and the preprocess is mt_preprocess_resized (row/col LUTs unused). */
 #define MT_ROLLOUT_RESIZED 16
+/* flags & MT_ROLLOUT_BOOT_SLABS (pipelined, v_boot set, not LSTM): the last chain's bootstrap
+ * forward stops after the dense layer — its split-K slabs stay in ws — and the update's loss kernel
+ * finishes V(s_T) itself (mt_returns_loss_backward_boot, which writes v_boot): one heads kernel and
+ * one kernel boundary fewer between the last emulator step and the backward. */
+#define MT_ROLLOUT_BOOT_SLABS 32
 typedef struct mt_rollout mt_rollout;
 typedef struct mt_rollout_buffers {
   /* device */

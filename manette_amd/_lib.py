@@ -37,6 +37,7 @@ MT_ROLLOUT_IN_PLACE = 2
 MT_ROLLOUT_POOLED = 4
 MT_ROLLOUT_PIPELINED = 8
 MT_ROLLOUT_RESIZED = 16
+MT_ROLLOUT_BOOT_SLABS = 32
 MH_RUNNER_RESIZED = 4
 MH_RUNNER_FIXED_SLOTS = 1
 MH_RUNNER_POOLED = 2
@@ -79,6 +80,8 @@ _HIP_SIGS = {
     'mt_loss_backward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
     'mt_returns_loss_backward': (_I, [_P, _P, _P, _I, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _P, C.c_double, _P, _P,
                                       _F, _P, _P, _P, _P]),
+    'mt_returns_loss_backward_boot': (_I, [_P, _P, _P, _I, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P,
+                                           C.c_double, _P, _P, _F, _P, _P, _P, _P]),
     'mt_grad_sumsq': (_I, [_P, _SZ, _F, _P, _P]),
     'mt_clip_rmsprop': (_I, [_P, _P, _P, _P, _SZ, _P, _P, _F, _F, _F, _F, _I, _F, _P, _P]),
     'mt_preprocess': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),

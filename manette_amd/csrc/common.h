@@ -205,6 +205,10 @@ int forward_sample(const mt_net *net, const float *params, const uint8_t *obs, i
                    size_t ws_bytes, float *v, float *pi, float *rep, const SampleArgs *smp, bool infer,
                    hipStream_t stream, const TrainRows *tr = nullptr, const StackSrc *st = nullptr,
                    const hipEvent_t *marks = nullptr);
+// the bootstrap forward without heads (net.hip forward_boot_impl): trunk + dense slabs in ws
+int forward_boot(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws, size_t ws_bytes,
+                 hipStream_t stream, const StackSrc *st = nullptr, uint32_t *advance = nullptr,
+                 uint32_t advance_by = 0);
 // the native rollout's LSTM macro-step forward (lstm.h lstm_step_fwd_impl; mt_lstm_step_forward)
 int lstm_step_forward(const mt_net *net, const float *params, const uint8_t *fstore, int t, int E, int T,
                       int32_t *nz, const float *over, void *ws, size_t ws_bytes, float *v, float *pi, float *rep,

@@ -106,6 +106,10 @@ __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
         wv[k] = w[i0 + k];
       }
   }
+  // the LR word lives in pinned host memory (written between launches; each dispatch's acquire
+  // makes it visible): requested with the operands, so its PCIe round trip overlaps the norm
+  // reduction instead of following the barrier
+  const float lr = *lr_dev;
   if (threadIdx.x < 64) {
     double acc = 0.0;
     for (int i = threadIdx.x; i < MT_NORM_PARTIALS; i += 64) acc += (double)partials[i];
@@ -123,7 +127,6 @@ __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
   }
   __syncthreads();
   const float scale = sh_scale;
-  const float lr = *lr_dev;  // host-written between launches: each dispatch's acquire makes it visible
   const float one_m_rho = 1.0f - decay;
 #pragma unroll
   for (int k = 0; k < V; ++k) {

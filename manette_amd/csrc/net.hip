@@ -629,23 +629,68 @@ struct ReturnsSrc {
   double gamma = 0.0;
   int T = 0, E = 0;
   float *y_out = nullptr, *adv_out = nullptr;
+  // bootstrap from the rollout's last chain without its heads kernel (mt_returns_loss_backward_boot):
+  // V(s_T)[e] = [act(sum_z boot_slabs[z][e] + fc_b), 1] . [Wc, bc] computed by the loss block
+  // itself (VT unused), written to vt_out[e] by the blocks of step 0
+  const float *boot_slabs = nullptr, *fc_b = nullptr;
+  int boot_S = 0;
+  float *vt_out = nullptr;
 };
 
+// V(s_T)[e] of the bootstrap (ReturnsSrc::boot_slabs): the dense layer's split-K slabs summed in
+// slab order + bias + act (heads_row's phase 1), then the critic's dot product as heads_row forms
+// it (lanes over features in 64-strides, DPP wave sum, + bias). Called by the whole block; the
+// result is in *vt (LDS) after the call.
+__device__ __forceinline__ void boot_value(const ReturnsSrc &rs, const HeadParams &hp, int e, int act, float alpha,
+                                           float *hsb, float *vt) {
+  const int F = hp.F;
+  for (int f = threadIdx.x; f < F; f += 256) {
+    const float *p = rs.boot_slabs + (size_t)e * F + f;
+    const size_t zs_stride = (size_t)rs.E * F;
+    float acc = 0.f;
+    for (int z = 0; z < rs.boot_S; z += 16) {
+      float t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t[u] = p[(size_t)min(z + u, rs.boot_S - 1) * zs_stride];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (z + u < rs.boot_S) acc += t[u];
+    }
+    hsb[f] = act_fwd(acc + rs.fc_b[f], act, alpha);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (lane + 64 * j < F) acc += hsb[lane + 64 * j] * hp.Wc[lane + 64 * j];
+    acc = wave_sum(acc);
+    if (lane == 0) *vt = acc + hp.bc[0];
+  }
+  __syncthreads();
+}
+
 // returns_kernel's arithmetic for row b = (t, e): R from T-1 down to t, bit-identical to
-// mt_returns. All threads load the rewards / masks of steps t.. (one round trip), thread 0 scans.
-// Called by the whole block.
-__device__ __forceinline__ void row_return(const ReturnsSrc &rs, const float *__restrict__ V, int b, float *ya,
-                                           float *buf) {
+// mt_returns. Thread k < 256 brings step t + k's reward / mask in (rk, mk: requested by the caller
+// before its other work, one round trip), the rest load here; thread 0 scans. Called by the whole
+// block.
+__device__ __forceinline__ void row_return(const ReturnsSrc &rs, const float *__restrict__ V, int b, float vt,
+                                           float rk, float mk, float *ya, float *buf) {
 #pragma clang fp contract(off)
   const int T = rs.T, E = rs.E;
   const int t = b / E, e = b - t * E, n = T - t;  // steps t .. T-1
-  for (int k = threadIdx.x; k < n; k += 256) {
+  if ((int)threadIdx.x < n) {
+    buf[2 * threadIdx.x] = rk;
+    buf[2 * threadIdx.x + 1] = mk;
+  }
+  for (int k = threadIdx.x + 256; k < n; k += 256) {
     buf[2 * k] = rs.r[(size_t)(t + k) * E + e];
     buf[2 * k + 1] = rs.mask[(size_t)(t + k) * E + e];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float g32 = __fmul_rn((float)rs.gamma, rs.VT[e]);
+    const float g32 = __fmul_rn((float)rs.gamma, vt);
     double R = (double)buf[2 * (n - 1)] + (double)g32 * (double)buf[2 * (n - 1) + 1];
     const double gd = rs.gamma;
     for (int k = n - 2; k >= 0; --k) R = (double)buf[2 * k] + (gd * R) * (double)buf[2 * k + 1];
@@ -697,7 +742,29 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
     for (int k = 0; k < KW; ++k)
       wk[fi][k] = !pre ? 0.f : (k < A ? hp.Wa[(size_t)f * A + k] : (k < A + R ? hp.Wr[(size_t)f * R + (k - A)] : 0.f));
   }
-  if (rs.r) row_return(rs, v, b, ya, buf);
+  if (rs.r) {
+    // this row's rewards / masks (pinned host memory, a PCIe round trip) requested first
+    float rk = 0.f, mk = 0.f;
+    {
+      const int t = b / rs.E, e = b - t * rs.E;
+      if ((int)threadIdx.x < rs.T - t) {
+        rk = rs.r[(size_t)(t + threadIdx.x) * rs.E + e];
+        mk = rs.mask[(size_t)(t + threadIdx.x) * rs.E + e];
+      }
+    }
+    float vt;
+    if (rs.boot_slabs) {
+      __shared__ float hsb[512];
+      __shared__ float vts;
+      const int e = b % rs.E;
+      boot_value(rs, hp, e, act, alpha, hsb, &vts);
+      vt = vts;
+      if (rs.vt_out && b < rs.E && threadIdx.x == 0) rs.vt_out[e] = vt;
+    } else {
+      vt = rs.VT[b % rs.E];
+    }
+    row_return(rs, v, b, vt, rk, mk, ya, buf);
+  }
   if (threadIdx.x < 64) {
     const float ad = rs.r ? ya[1] : adv_in;
     const float yb = rs.r ? ya[0] : y_in;
@@ -1129,6 +1196,32 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
   }
 }
 
+// Bootstrap forward without its heads (mt_rollout's last chain with MT_ROLLOUT_BOOT_SLABS): the
+// trunk + the dense layer's split-K slabs left in ws (ws_layout(B).fcslab; NIPS: the fused trunk's
+// ROWS2 slabs, else fc_splits), whose sum, bias, act and critic the update's loss kernel takes
+// (mt_returns_loss_backward_boot). st: the NIPS stacking source; advance: the replayed rollout's
+// sequence bases (the fused dense kernel advances them).
+template <class Ar>
+static int forward_boot_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws, hipStream_t s,
+                             const StackSrc *st, uint32_t *advance, uint32_t advance_by) {
+  const WsLayout L = ws_layout<Ar>(n, B);
+  const float *Wfc = P + n->off_fc;
+  if constexpr (Ar::FUSED_SLABS > 0) {
+    constexpr int C = LayerG<Ar, 0>::CIN;
+    return launch_nips_trunk<C>(obs, st, B, P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation,
+                                n->cfg.alpha_leaky, ws + L.act[1], nullptr, ws + L.fcslab, s, advance, advance_by);
+  } else {
+    if (st || advance) {
+      set_error("stacking / replayed bootstrap is built for the NIPS arch only");
+      return MT_ERR_ARG;
+    }
+    MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s)));
+    const float *flat = layer_out<Ar, Ar::NCONV - 1>(ws, L);
+    return launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1}, EpSlab{ws + L.fcslab, B, Ar::F},
+                               B, Ar::F, Ar::FLAT, L.fc_splits, s);
+  }
+}
+
 // Loss + head gradients (policy_v_network.py:25-74): writes dz, dH (masked by the trunk output's
 // activation derivative) and the three head (w, b) gradients. Every variable's gradient is
 // overwritten by the backward (no accumulation), so grad is not cleared: its alignment padding
@@ -1436,6 +1529,25 @@ int mt::forward_sample(const mt_net *net, const float *params, const uint8_t *ob
   return MT_OK;
 }
 
+int mt::forward_boot(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
+                     size_t ws_bytes, hipStream_t stream, const StackSrc *st, uint32_t *advance, uint32_t advance_by) {
+  MT_CHECK_ARG(net && params && obs && ws && batch >= 1, "bad argument");
+  MT_ARCH_SWITCH(net, {
+    if constexpr (Ar::LSTM) {
+      set_error("the LSTM bootstrap runs through mt_lstm_step_forward");
+      return MT_ERR_UNSUPPORTED;
+    } else {
+      const WsLayout L = ws_layout<Ar>(net, batch);
+      if (ws_bytes < L.total * sizeof(float)) {
+        set_error("workspace %zu < %zu bytes", ws_bytes, L.total * sizeof(float));
+        return MT_ERR_WORKSPACE;
+      }
+      return forward_boot_impl<Ar>(net, params, obs, batch, (float *)ws, stream, st, advance, advance_by);
+    }
+  });
+  return MT_OK;
+}
+
 extern "C" int mt_loss_backward(const mt_net *net, const float *params, const uint8_t *obs,
                                 int batch, void *ws, size_t ws_bytes, const float *pi,
                                 const float *rep, const float *v, const int32_t *a_idx,
@@ -1491,6 +1603,53 @@ extern "C" int mt_returns_loss_backward(const mt_net *net, const float *params, 
       rs.E = E;
       rs.y_out = y;
       rs.adv_out = adv;
+      NormOut no;
+      no.partials = norm_partials;
+      no.n = net->nparams;
+      return backward_impl<Ar>(net, params, obs, batch, (float *)ws, pi, rep, values, a_idx, r_idx, y, adv,
+                               entropy_beta, grad, loss_terms, (hipStream_t)stream, rs, no);
+    }
+  });
+  return MT_OK;
+}
+
+extern "C" int mt_returns_loss_backward_boot(const mt_net *net, const float *params, const uint8_t *obs, int T, int E,
+                                             void *ws, size_t ws_bytes, const float *pi, const float *rep,
+                                             const float *values, const int32_t *a_idx, const int32_t *r_idx,
+                                             const float *rewards, const float *masks, const void *boot_ws,
+                                             size_t boot_ws_bytes, float *v_boot, double gamma, float *y, float *adv,
+                                             float entropy_beta, float *grad, float *loss_terms, float *norm_partials,
+                                             mt_stream_t stream) {
+  MT_CHECK_ARG(net && params && obs && ws && pi && rep && values && a_idx && r_idx && rewards && masks && boot_ws &&
+                   v_boot && y && adv && grad,
+               "null argument");
+  MT_CHECK_ARG(T >= 1 && E >= 1 && T <= kMaxScan, "T=%d (<= %d) and E=%d must be >= 1", T, kMaxScan, E);
+  const int batch = T * E;
+  MT_ARCH_SWITCH(net, {
+    if constexpr (Ar::LSTM) {
+      set_error("mt_returns_loss_backward_boot: the LSTM arch trains through mt_lstm_frames_backward");
+      return MT_ERR_UNSUPPORTED;
+    } else {
+      const WsLayout L = ws_layout<Ar>(net, batch);
+      const WsLayout LB = ws_layout<Ar>(net, E);
+      if (ws_bytes < L.total * sizeof(float) || boot_ws_bytes < LB.total * sizeof(float)) {
+        set_error("workspace %zu / bootstrap workspace %zu < %zu / %zu bytes", ws_bytes, boot_ws_bytes,
+                  L.total * sizeof(float), LB.total * sizeof(float));
+        return MT_ERR_WORKSPACE;
+      }
+      MT_CHECK_ARG(Ar::F <= 512, "F > 512");
+      ReturnsSrc rs;
+      rs.r = rewards;
+      rs.mask = masks;
+      rs.gamma = gamma;
+      rs.T = T;
+      rs.E = E;
+      rs.y_out = y;
+      rs.adv_out = adv;
+      rs.boot_slabs = (const float *)boot_ws + LB.fcslab;
+      rs.boot_S = Ar::FUSED_SLABS > 0 ? Ar::FUSED_SLABS : LB.fc_splits;
+      rs.fc_b = params + net->off_fc + (size_t)Ar::FLAT * Ar::F;
+      rs.vt_out = v_boot;
       NormOut no;
       no.partials = norm_partials;
       no.n = net->nparams;

@@ -26,6 +26,7 @@ struct mt_rollout {
   bool pull;          // pipelined + resized: per-env ready words, pull kernel into HBM, tagged pairs
   bool stack_fwd;     // pull + NIPS: the forward's conv kernel stacks (no preprocess launch)
   bool lstm;          // LSTM arch: frame-store forward per step (mt_lstm_step_forward), nz on the device
+  bool boot_slabs;    // MT_ROLLOUT_BOOT_SLABS: the bootstrap chain ends at the dense slabs (no heads)
   const uint8_t *fstore = nullptr;  // LSTM: the frame store (states = its slot 4)
   const float *over_dev = nullptr;  // LSTM: device address of the pinned episode-end flags
   int armed_upto = -1;  // pipelined: last step whose chain (forward) is already enqueued
@@ -89,8 +90,10 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   const bool po = (b.flags & MT_ROLLOUT_POOLED) != 0;
   const bool rz = (b.flags & MT_ROLLOUT_RESIZED) != 0;
   MT_CHECK_ARG((b.flags & ~(MT_ROLLOUT_ZERO_COPY | MT_ROLLOUT_IN_PLACE | MT_ROLLOUT_POOLED | MT_ROLLOUT_PIPELINED |
-                            MT_ROLLOUT_RESIZED)) == 0,
+                            MT_ROLLOUT_RESIZED | MT_ROLLOUT_BOOT_SLABS)) == 0,
                "unknown rollout flags %d", b.flags);
+  MT_CHECK_ARG(!(b.flags & MT_ROLLOUT_BOOT_SLABS) || (pl && b.v_boot && !b.nz),
+               "MT_ROLLOUT_BOOT_SLABS needs a pipelined, non-LSTM rollout with v_boot");
   MT_CHECK_ARG(!ip || b.frames_host, "in-place rollout needs frames_host");
   MT_CHECK_ARG(b.env_offset >= 0, "env_offset must be >= 0");
   MT_CHECK_ARG((int)ip + (int)po + (int)rz <= 1, "in-place, pooled and resized staging are exclusive");
@@ -152,6 +155,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->pull = pl && rz;
   ro->stack_fwd = ro->pull && cfg.arch == MT_ARCH_NIPS;
   ro->lstm = lstm;
+  ro->boot_slabs = (b.flags & MT_ROLLOUT_BOOT_SLABS) != 0;
   ro->over_dev = (const float *)over_dev;
   if (lstm) ro->fstore = b.states - (size_t)(1 + 4 * E) * 84 * 84 * 4 * cfg.depth;
   ro->frames_dev = (int32_t *)frames_dev;
@@ -467,15 +471,19 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
     st.ready = ro->env_ready_dev;
     st.tag = want & 0x1fffffffu;
     st.status = ro->status_dev;
-    SampleArgs adv{};  // capturing: no draw; the heads kernel advances the replay's bases by T
+    SampleArgs adv{};  // capturing: no draw; the heads (boot_slabs: dense) kernel advances the replay's bases by T
     if (ro->capturing) {
       st.tag_base = ro->gbase_dev;
       adv.advance = ro->gbase_dev;
       adv.advance_by = (uint32_t)T;
     }
-    MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)T * slot, E, b.ws, b.ws_bytes, b.v_boot,
-                           b.pi + po * ro->A, b.rep + po * ro->R, ro->capturing ? &adv : nullptr, true, s, nullptr,
-                           stk ? &st : nullptr));
+    if (ro->boot_slabs)  // trunk + dense slabs only: the update's loss kernel finishes V(s_T)
+      MT_TRY_(forward_boot(ro->net, params, b.states + (size_t)T * slot, E, b.ws, b.ws_bytes, s, stk ? &st : nullptr,
+                           adv.advance, adv.advance_by));
+    else
+      MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)T * slot, E, b.ws, b.ws_bytes, b.v_boot,
+                             b.pi + po * ro->A, b.rep + po * ro->R, ro->capturing ? &adv : nullptr, true, s, nullptr,
+                             stk ? &st : nullptr));
   }
   ro->armed_upto = k;
   return MT_OK;

@@ -396,12 +396,19 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
 // Dense layer partial products: slabs[i][e][n] = sum_{f < 288} act2[e][288 i + f] Wfc[288 i + f][n].
 // Grid (F / 16, 9, ceil(B / 32)); 4 waves split the 18 K chunks of 16 (c = w + 4j), every operand
 // load of a wave issued before its first MFMA; partials added in wave order through LDS.
+// advance (replayed rollout graph whose bootstrap has no heads kernel, SampleArgs::advance): block 0
+// adds advance_by to advance[0] and advance[1] — every reader of those bases in the replay has run.
 template <int C>
 __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ act2, int B,
-                                                      const float *__restrict__ Wfc, float *__restrict__ slabs) {
+                                                      const float *__restrict__ Wfc, float *__restrict__ slabs,
+                                                      uint32_t *advance, uint32_t advance_by) {
   using Fz = FusedNips<C>;
   __shared__ __attribute__((aligned(16))) float red[4][Fz::FC_BM][Fz::FC_BN];
   const int pb = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  if (advance && pb == 0 && threadIdx.x == 0) {
+    advance[0] += advance_by;
+    advance[1] += advance_by;
+  }
   const int nbk = gridDim.x * gridDim.y * gridDim.z;
   const int L = (nbk % 8 == 0) ? (pb % 8) * (nbk / 8) + pb / 8 : pb;  // XCD-aware (see the top)
   const int xb = L % gridDim.x, yz = L / gridDim.x;
@@ -606,13 +613,17 @@ __global__ __launch_bounds__(PersistNips::NT) void nips_conv_persist_kernel(
 template <int C>
 static inline int launch_nips_trunk(const uint8_t *obs, const StackSrc *st, int B, const float *W1, const float *W2,
                                     const float *Wfc, int act, float alpha, float *act2, float *act1, float *slabs,
-                                    hipStream_t s) {
+                                    hipStream_t s, uint32_t *advance = nullptr, uint32_t advance_by = 0) {
   using Fz = FusedNips<C>;
   static_assert(Fz::LDS_BYTES <= 64 * 1024, "conv kernel LDS fits the default limit");
   if (st) {
     hipLaunchKernelGGL((nips_conv_kernel<C, true>), dim3(Fz::ROWS2 * B), dim3(Fz::NT), Fz::LDS_BYTES, s, st->out, *st,
                        B, W1, W2, act, alpha, act2, act1);
   } else if (C == 4 && B >= kPersistMinEnvs) {
+    if (advance) {
+      set_error("sequence-base advance: stacking trunk launches only");
+      return MT_ERR_ARG;
+    }
     static int cus = 0;
     static bool attr = false;
     if (!cus) {
@@ -637,7 +648,7 @@ static inline int launch_nips_trunk(const uint8_t *obs, const StackSrc *st, int 
                        StackSrc{}, B, W1, W2, act, alpha, act2, act1);
   }
   hipLaunchKernelGGL(nips_fc_kernel<C>, dim3(Fz::F / Fz::FC_BN, Fz::ROWS2, (B + Fz::FC_BM - 1) / Fz::FC_BM),
-                     dim3(256), 0, s, act2, B, Wfc, slabs);
+                     dim3(256), 0, s, act2, B, Wfc, slabs, advance, advance_by);
   return MT_OK;
 }
 

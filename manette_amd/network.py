@@ -243,14 +243,24 @@ class DeviceNetwork(object):
         return self.grad
 
     def returns_loss_backward(self, obs, T, E, pi, rep, values, a_idx, r_idx, rewards, masks, v_boot, gamma, y, adv,
-                              loss_terms=None, ws_key=None, norm_partials=False):
+                              loss_terms=None, ws_key=None, norm_partials=False, boot_ws=None):
         """mt_returns + mt_loss_backward in one call (rows t*E + e): the n-step scan of paac.py:219-231
         runs inside the loss kernel. rewards / masks: [T][E] device tensors or device addresses.
         norm_partials: the backward also leaves the global-norm partials in self.partials, so the
-        following apply_gradients(partials_ready=True) skips mt_grad_sumsq (single process only)."""
+        following apply_gradients(partials_ready=True) skips mt_grad_sumsq (single process only).
+        boot_ws: the rollout's E-row workspace holding the bootstrap's dense slabs (a rollout made
+        with MT_ROLLOUT_BOOT_SLABS): V(s_T) is finished in the loss kernel and written to v_boot
+        (mt_returns_loss_backward_boot)."""
         B = T * E
         ws = self.workspace(B, ws_key)
         addr = lambda x: C.c_void_p(x) if isinstance(x, int) else _ptr(x)
+        if boot_ws is not None:
+            check(_lib.hip().mt_returns_loss_backward_boot(
+                self._h, _ptr(self.params), _ptr(obs), int(T), int(E), _ptr(ws), ws.numel(), _ptr(pi), _ptr(rep),
+                _ptr(values), _ptr(a_idx), _ptr(r_idx), addr(rewards), addr(masks), _ptr(boot_ws), boot_ws.numel(),
+                _ptr(v_boot), float(gamma), _ptr(y), _ptr(adv), self.beta, _ptr(self.grad), _ptr(loss_terms),
+                _ptr(self.partials if norm_partials else None), _stream()), 'mt_returns_loss_backward_boot')
+            return self.grad
         check(_lib.hip().mt_returns_loss_backward(
             self._h, _ptr(self.params), _ptr(obs), int(T), int(E), _ptr(ws), ws.numel(), _ptr(pi), _ptr(rep),
             _ptr(values), _ptr(a_idx), _ptr(r_idx), addr(rewards), addr(masks), _ptr(v_boot), float(gamma), _ptr(y),

@@ -132,6 +132,7 @@ class PAACLearner(ActorLearner):
         self.use_update_graph = bool(getattr(args, 'update_graph', True))
         self._graphs = None
         self._update_in_rollout = False  # mt_rollout_set_update registered (_register_update)
+        self._boot_ws = None  # the rollout's workspace whose bootstrap dense slabs the loss kernel finishes
         self._eager_updates = 0
         self.summaries = None  # TensorBoard event files of the chief (manette_amd/summary.py)
         self._logged_episodes = 0
@@ -209,6 +210,11 @@ class PAACLearner(ActorLearner):
                 raise ValueError('pipeline needs in_place, zero_copy or pooled staging')
             flags |= _lib.MT_ROLLOUT_PIPELINED
             self.sync_h = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+            # the bootstrap chain stops at the dense slabs; the update's loss kernel finishes V(s_T)
+            # (mt_returns_loss_backward_boot). MT_BOOT_IN_LOSS=0: the chain runs its heads kernel.
+            if not self.lstm_bool and os.environ.get('MT_BOOT_IN_LOSS', '1') != '0':
+                flags |= _lib.MT_ROLLOUT_BOOT_SLABS
+                self._boot_ws = ws
         self._bufs = _lib.mt_rollout_buffers(
             p(self.states), p(self.values), p(self.idx), p(self.pi_all), p(self.rep_all), p(ws), ws.numel(),
             p(self.counters), p(self.raw_d), src_rows, p(self.pair_d), p(self.pair_h), p(self.meta_d),
@@ -409,7 +415,7 @@ class PAACLearner(ActorLearner):
                                       self.rep_all[:T].reshape(N, -1), self.values, self.idx[0].view(N),
                                       self.idx[1].view(N), self.rm_h_dev, self.rm_h_dev + 4 * T * E, self.v_boot,
                                       self.gamma, self.y, self.adv, loss_terms=self.loss_terms, ws_key='train',
-                                      norm_partials=self.world == 1)
+                                      norm_partials=self.world == 1, boot_ws=self._boot_ws if boot_done else None)
         if end is not None:
             end.record()
 
