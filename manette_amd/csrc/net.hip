@@ -466,7 +466,7 @@ __device__ __forceinline__ int wave_draw(float p, int n, double u) {
   double cum = 0.0;
   int res = n - 1;
   for (int j = 0; j < n - 1; ++j) {
-    const float pj = __shfl(p, j, 64);
+    const float pj = lane_f(p, j);  // (j is wave-uniform: a readlane, not an LDS-routed shuffle)
     cum += (double)(pj - (float)epsneg);
     if (res == n - 1 && u < cum) res = j;
   }
