@@ -310,13 +310,15 @@ int mt_memory_push(uint8_t *memory, uint8_t *whole_t, const uint8_t *fresh, cons
  * (a bounded device wait on sync_host[0], preprocess, forward + draw) before it waits for step t's
  * indices, and after the emulators only stores the step word — no launch on the critical path.
  * sync_host = [2] uint32 pinned + mapped: [0] host step word, [1] device wait timeout status.
- * PIPELINED + RESIZED + the NIPS arch ("stacking" rollout): the chain of step t+1 is a pull kernel
- * (per env, it waits for the word the emulator thread stores once the env is staged,
- * mh_runner_set_ready, and copies its frames into HBM while the other envs are still emulated),
- * the conv kernel that stacks state slot t+1 from slot t and those frames itself (no preprocess
- * launch), the dense kernel and the heads kernel, which writes each env's (a, r) as one tagged
- * 8-byte word into host memory (no fence); chains are armed two steps ahead, and step 0's forward
- * takes slot 0 from slot T of the previous rollout (the update then needs no copy). */
+ * PIPELINED + RESIZED + the NIPS arch ("stacking" rollout): the chain of step t+1 is the conv
+ * kernel — each (env, row) block waits for the word the emulator thread stores once its env is
+ * staged (mh_runner_set_ready), reads that env's frames from the pinned staging and stacks state
+ * slot t+1 from slot t itself (no pull or preprocess launch) — the dense kernel and the heads
+ * kernel, which writes each env's (a, r) as one tagged 8-byte word into host memory (no fence).
+ * Every chain of a rollout is armed at its step 0 (from the second rollout on as one replayed
+ * hipGraph whose sequence tags live in device memory), and step 0's forward takes slot 0 from
+ * slot T of the previous rollout (the update then needs no copy). Other pipelined modes: a pull
+ * kernel per env copies the frames into HBM, then the preprocess kernel, then the forward. */
 #define MT_ROLLOUT_PIPELINED 8
 /* flags & MT_ROLLOUT_RESIZED: the runner stages each push's final 84x84 frame (MH_RUNNER_RESIZED,
  * staging [4E][84*84*depth]) and the preprocess is mt_preprocess_resized (row/col LUTs unused). */

@@ -553,13 +553,13 @@ int replay_rollout_graph(mt_rollout *ro, const float *params, hipStream_t s) {
 
 }  // namespace
 
-// One macro-step t (paac.py:140-205). Pipelined mode keeps the GPU one step ahead of the host's
-// launch calls: before waiting for step t's indices it enqueues step t+1's chain behind a
-// device-side wait on the host sequence word — wait_seq -> preprocess(t -> t+1) -> forward(t+1)
-// — so when the emulators finish, the host only stores the word and the GPU runs the whole
-// chain without a launch on the critical path. Stream order keeps every buffer hand-off safe:
-// the staging of step t is read by preprocess(t) only after the word, and rewritten by the
-// emulators of step t+1 only after forward(t+1)'s indices (which follow preprocess(t)) arrived.
+// One macro-step t (paac.py:140-205). Pipelined mode keeps the GPU ahead of the host's launch
+// calls: step 0 enqueues the chains of steps 1..T (each behind device-side waits on the host's
+// words: the ready word per env in pull mode, else wait_seq -> preprocess(t -> t+1)), from the
+// second rollout on as one replayed graph, so when the emulators finish, the host only stores the
+// words and the GPU runs the chain without a launch on the critical path. Stream order keeps every
+// buffer hand-off safe: the staging of step t is read by chain t+1 only after the word, and
+// rewritten by the emulators of step t+1 only after chain t+1's indices arrived.
 extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64_t *global_step,
                                mt_stream_t stream) {
   MT_CHECK_ARG(ro && params && global_step, "null argument");
