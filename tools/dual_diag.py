@@ -1,0 +1,29 @@
+"""Diagnostic (tools only): the conv1 weight gradient of an RGB NIPS net at B=5 (the
+test_loss_backward_parity[5-NIPS-3-4-11] case) with its fp64 oracle, saved to an npz, so two
+library variants can be compared elementwise:
+    python tools/dual_diag.py out.npz            (MANETTE_HIP_LIB selects the variant)
+Used for the two-accumulator GEMM-core experiment."""
+import os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.environ.get('GRAFT_REPO_ROOT', '/root/repo'))
+sys.path.insert(0, os.path.join(os.environ.get('GRAFT_REPO_ROOT', '/root/repo'), 'tests'))
+from manette_amd.network import DeviceNetwork
+from oracle import nets
+B, depth, A, R = 5, 3, 4, 11
+conf = dict(arch='NIPS', num_actions=A, nb_choices=R, rgb=True, softmax_temp=1.0, entropy_regularisation_strength=0.02,
+            clip_norm=3.0, clip_norm_type='global')
+net = DeviceNetwork(conf, device='cuda:0'); net.init_params(7 + B)
+rs = np.random.RandomState(100 + B)
+obs = rs.randint(0, 256, size=(B, 84, 84, 4 * depth)).astype(np.uint8)
+a_idx = rs.randint(0, A, size=B).astype(np.int32); r_idx = rs.randint(0, R, size=B).astype(np.int32)
+y = rs.randn(B).astype(np.float32); adv = rs.randn(B).astype(np.float32)
+d = lambda x: torch.from_numpy(x).cuda()
+v, pi, rep = net.forward(d(obs))
+net.loss_backward(d(obs), B, v, pi, rep, d(a_idx), d(r_idx), d(y), d(adv))
+torch.cuda.synchronize()
+got = net.get_variables('grad')['Network/conv1/conv1_weights']
+spec = nets.arch_spec('NIPS', depth, A, R)
+_, G, _ = nets.loss_and_grads(spec, net.get_variables(), obs, a_idx, r_idx, y, adv, 0.02)
+np.savez(sys.argv[1], got=got, ref=G['Network/conv1/conv1_weights'])
+print('saved', sys.argv[1])
