@@ -37,6 +37,8 @@ CONFIGS = {
     'mspacman-lstm-figar': dict(game='ms_pacman', arch='LSTM', ec=32, ew=8, max_repetition=10, nb_choices=11,
                                 rgb=False),
 }
+# BASELINE.json configs[0]: the reference's CPU-only case, timed only in the cpu_baseline leg
+CPU_CONFIG0 = dict(game='pong', arch='NIPS', ec=4, ew=2, max_repetition=0, nb_choices=1, rgb=False)
 MI355X_FP32_TFLOPS = 157.3   # dense fp32 (vector = MFMA), MI355X_MICROARCH.md
 MI355X_HBM_GBS = 8000.0      # HBM3E peak, MI355X_MICROARCH.md
 
@@ -114,6 +116,76 @@ def train_pass_flops(layers, N, frame_rows=None):
     per_frame = sum(l[1] for l in layers if l[0] in FRAME_LAYERS)
     per_win = sum(l[1] for l in layers if l[0] not in FRAME_LAYERS)
     return frame_rows * (2 * per_frame - layers[0][1]) + N * 2 * per_win
+
+
+def graph_time(fn, inner, reps=5):
+    """Device time per call of fn (which launches on torch's current stream): `inner` calls are
+    captured as ONE hipGraph on a side stream, replayed once to warm up and then `reps` times, each
+    replay between a HIP event pair on that stream. The kernels run back to back with no host
+    launch gap (an eager loop of small launches measures the host's launch rate on a loaded box:
+    BENCH_r02's 32 us vs 14 us). Returns the per-call microseconds of each replay."""
+    import ctypes as C
+    import torch
+    from manette_amd import _lib
+    lib = _lib.hip()
+    cur = torch.cuda.current_stream()
+    side = torch.cuda.Stream()
+    side.wait_stream(cur)
+    torch.cuda.synchronize()
+    out = []
+    with torch.cuda.stream(side):
+        sp = C.c_void_p(side.cuda_stream)
+        _lib.check(lib.mt_graph_begin(sp), 'mt_graph_begin')
+        g = C.c_void_p()
+        try:
+            for _ in range(inner):
+                fn()
+        finally:
+            rc = lib.mt_graph_end(sp, C.byref(g))
+        _lib.check(rc, 'mt_graph_end')
+        try:
+            _lib.check(lib.mt_graph_launch(g, sp), 'mt_graph_launch')
+            evs = []
+            for _ in range(reps):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(side)
+                _lib.check(lib.mt_graph_launch(g, sp), 'mt_graph_launch')
+                b.record(side)
+                evs.append((a, b))
+            side.synchronize()
+            out = [a.elapsed_time(b) * 1e3 / inner for a, b in evs]
+        finally:
+            lib.mt_graph_destroy(g)
+    cur.wait_stream(side)
+    return out
+
+
+def stats_us(xs):
+    xs = sorted(xs)
+    return {'min_us': round(xs[0], 2), 'median_us': round(xs[len(xs) // 2], 2), 'max_us': round(xs[-1], 2),
+            'n': len(xs)}
+
+
+def launch_breakdown(fn, inner=20, reps=3):
+    """Per-launch device time of a multi-launch call fn (the update's backward): the call is timed
+    (graph_time) with only its first k launches issued (mt_launch_window(0, k)), k = 1..L; launch
+    k's time = t(k) - t(k-1), each including its dependent kernel boundary."""
+    from manette_amd import _lib
+    lib = _lib.hip()
+    lib.mt_launch_window(0, -1)
+    try:
+        fn()
+    finally:
+        L = lib.mt_launch_window(-1, -1)
+    prev, out = 0.0, []
+    for k in range(1, L + 1):
+        try:
+            t = float(np.median(graph_time(lambda: (lib.mt_launch_window(0, k), fn()), inner, reps)))
+        finally:
+            lib.mt_launch_window(-1, -1)
+        out.append(t - prev)
+        prev = t
+    return out, prev
 
 
 def build_args(cfg, T, sampling, seed, debugging_folder=None):
@@ -279,8 +351,10 @@ def main():
         stats = (C.c_double * 7)()
         _lib.hip().mt_rollout_stats_ex(learner.native_step, stats, 7, 1)
     t0 = time.perf_counter()
+    marks = []  # host clock after each update: the value of sub-windows of the timed region
     for _ in range(a.steps):
         one_update()
+        marks.append(time.perf_counter())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -319,64 +393,8 @@ def main():
         _lib.check(lib.mt_rollout_trunk_timing(learner.native_step, 0, C.byref(tot), C.byref(cnt)))
         if cnt.value:
             inloop_us = tot.value / cnt.value
-    # (2) the update's train pass (backward of the last rollout) alone: 20 launches back to back
-    #     between one event pair (the timed region replays it inside the update's hipGraph)
-    learner.train_backward()
-    s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s_ev.record()
-    for _ in range(20):
-        learner.train_backward()
-    e_ev.record()
-    torch.cuda.synchronize()
-    prof['train_pass'] = [s_ev.elapsed_time(e_ev) / 20.0]
-    # (3) the trunk kernels back to back, HIP events on the stream they are launched on (torch's
-    #     current stream), 40 launches between one event pair: the stacking rollout chain's kernels
-    #     (NIPS: mt_forward_trunk_stacking = the in-kernel-pull conv kernel + the dense kernel, with
-    #     every env's ready word already set and its pushes resident in HBM, so nothing waits),
-    #     else mt_forward_trunk; and the whole rollout-batch forward (E rows, with the heads)
-    E = cfg['ec']
-    net = learner.network
-    stacking = getattr(learner, 'slot0_in_rollout', False)
-    if learner.lstm_bool:  # a step's new frames (trunk + cell x-product), + its E windows
-        roll_fwd = lambda: learner._lstm_forward(1, learner.v_boot)
-        roll_trunk = lambda: net.lstm_frames_forward(learner.fstore, 1 + 5 * E, E, E, T)
-    elif stacking:
-        depth_ = 3 if cfg['rgb'] else 1
-        gen = torch.Generator(device='cuda').manual_seed(11)
-        pushes = torch.randint(0, 256, (4 * E, 84, 84, depth_), dtype=torch.uint8, device='cuda', generator=gen)
-        counts = torch.ones(E, dtype=torch.int32) if cfg['max_repetition'] == 0 else \
-            torch.from_numpy(np.random.RandomState(5).randint(1, 5, E).astype(np.int32))
-        ready = torch.zeros(E, 32, dtype=torch.int32)  # MH_READY_STRIDE words per env
-        ready[:, 0] = (7 << 3) | counts
-        stack_pushes = int(counts.sum())
-        ready = ready.cuda()
-        stk_out = torch.empty_like(learner.states[0])
-        roll_fwd = lambda: net.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
-                                       ws_key='rollout', infer=True)
-        roll_trunk = lambda: net.forward_trunk_stacking(learner.states[0], pushes, ready, 7, stk_out, E,
-                                                        ws_key='rollout')
-    else:
-        roll_fwd = lambda: net.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
-                                       ws_key='rollout', infer=True)
-        roll_trunk = lambda: net.forward_trunk(learner.states[0], E, ws_key='rollout')
-    fw = []
-    for it in range(30):
-        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s_ev.record()
-        roll_fwd()
-        e_ev.record()
-        fw.append((s_ev, e_ev))
-    for _ in range(5):
-        roll_trunk()
-    s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s_ev.record()
-    for _ in range(40):
-        roll_trunk()
-    e_ev.record()
-    torch.cuda.synchronize()
-    prof['rollout_forward'] = [s_ev_.elapsed_time(e_ev_) for (s_ev_, e_ev_) in fw[5:]]
-    prof['rollout_trunk'] = [s_ev.elapsed_time(e_ev) / 40.0]
-    # (4) data parallel: the replicas must hold identical parameters after the run
+    # (2) data parallel: the replicas must hold identical parameters after the run (checked before
+    #     the kernel timings below, which run clip + RMSProp again)
     replicas = None
     if world > 1:
         pf = learner.network.params.double()
@@ -384,6 +402,64 @@ def main():
         allck = [torch.zeros_like(ck) for _ in range(world)]
         dist.all_gather(allck, ck)
         replicas = all(torch.equal(x, allck[0]) for x in allck)
+    # (3) kernels in isolation, each as a hipGraph of back-to-back calls replayed 5 times between
+    #     HIP event pairs on its stream (graph_time: no host launch gaps); min / median per call
+    E = cfg['ec']
+    net = learner.network
+    depth_ = 3 if cfg['rgb'] else 1
+    stacking = getattr(learner, 'slot0_in_rollout', False)
+    # the update's train pass (fused returns + loss + backward of the last rollout)
+    bwd = learner.train_backward if learner.lstm_bool else learner._update_backward
+    prof['train_pass'] = graph_time(bwd, 20)
+    # (the LSTM backward has launches outside the budgeted grouped launches: no breakdown)
+    prof['train_launches'] = None if learner.lstm_bool else launch_breakdown(bwd)[0]
+    # A11: clip + RMSProp alone (the norm partials the backward left; world > 1 adds mt_grad_sumsq)
+    prof['clip_rmsprop'] = graph_time(lambda: net.apply_gradients(partials_ready=True), 40)
+    gen = torch.Generator(device='cuda').manual_seed(11)
+    pushes = torch.randint(0, 256, (4 * E, 84, 84, depth_), dtype=torch.uint8, device='cuda', generator=gen)
+    counts = torch.ones(E, dtype=torch.int32) if cfg['max_repetition'] == 0 else \
+        torch.from_numpy(np.random.RandomState(5).randint(1, 5, E).astype(np.int32))
+    stack_pushes = int(counts.sum())
+    stk_out = torch.empty_like(learner.states[0])
+    # A2: the stacking op on its own (mt_preprocess_resized: prev shifted by p channels + p frames)
+    offs = torch.arange(0, 4 * E, 4, dtype=torch.int32, device='cuda')
+    cnt_d = counts.to('cuda')
+    from manette_amd import network as devnet_
+    prof['stack'] = graph_time(lambda: devnet_.preprocess(pushes, offs, cnt_d, E, depth_, None, None, learner.states[0],
+                                                          stk_out, resized=True), 40)
+    if learner.lstm_bool:  # a step's new frames (trunk + cell x-product), + its E windows
+        roll_fwd = lambda: learner._lstm_forward(1, learner.v_boot)
+        roll_trunk = lambda: net.lstm_frames_forward(learner.fstore, 1 + 5 * E, E, E, T)
+        plain_trunk = None
+    else:
+        roll_fwd = lambda: net.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
+                                       ws_key='rollout', infer=True)
+        plain_trunk = lambda: net.forward_trunk(learner.states[0], E, ws_key='rollout')
+        if stacking:
+            # the stacking rollout chain's kernels (the in-kernel-pull conv kernel + the dense
+            # kernel) with every env's ready word already set and its pushes in HBM: nothing waits
+            ready = torch.zeros(E, 32, dtype=torch.int32)  # MH_READY_STRIDE words per env
+            ready[:, 0] = (7 << 3) | counts
+            ready = ready.cuda()
+            roll_trunk = lambda: net.forward_trunk_stacking(learner.states[0], pushes, ready, 7, stk_out, E,
+                                                            ws_key='rollout')
+        else:
+            roll_trunk = plain_trunk
+    prof['rollout_forward'] = graph_time(roll_fwd, 20)
+    prof['rollout_trunk'] = graph_time(roll_trunk, 40)
+    if stacking:
+        prof['plain_trunk'] = graph_time(plain_trunk, 40)
+    # the eager form (40 Python calls back to back between one event pair, BENCH_r02's method):
+    # bounded by the host's launch rate when the box is loaded, kept to show the difference
+    for _ in range(3):
+        roll_trunk()
+    s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_ev.record()
+    for _ in range(40):
+        roll_trunk()
+    e_ev.record()
+    torch.cuda.synchronize()
+    prof['rollout_trunk_eager'] = s_ev.elapsed_time(e_ev) * 1e3 / 40.0
     # the same trunk launch at larger batches (supplementary: how far the kernel is from its
     # bounds once the grid fills the chip; the workload's own batch is E = ec above)
     sweep = []
@@ -392,15 +468,9 @@ def main():
         g = torch.Generator(device='cuda').manual_seed(7)
         for Eb in [int(x) for x in a.trunk_sweep.split(',')]:
             obs_b = torch.randint(0, 256, (Eb, 84, 84, 4 * depth_), dtype=torch.uint8, device='cuda', generator=g)
-            for _ in range(3):
-                net.forward_trunk(obs_b, Eb, ws_key=('sweep', Eb))
-            s_b, e_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s_b.record()
-            for _ in range(10):
-                net.forward_trunk(obs_b, Eb, ws_key=('sweep', Eb))
-            e_b.record()
-            torch.cuda.synchronize()
-            sweep.append((Eb, s_b.elapsed_time(e_b) / 10.0))
+            net.forward_trunk(obs_b, Eb, ws_key=('sweep', Eb))  # (workspace allocated outside the capture)
+            sweep.append((Eb, float(np.median(graph_time(lambda: net.forward_trunk(obs_b, Eb, ws_key=('sweep', Eb)), 10,
+                                                         3))) * 1e-3))
             del obs_b
             net._ws.pop(('sweep', Eb), None)
     ec = cfg['ec']
@@ -412,10 +482,11 @@ def main():
         layers = arch_flops(cfg['arch'], depth, A, cfg['nb_choices'])
         N = ec * T
         lstm = cfg['arch'] == 'LSTM'
-        tp_ms = float(np.mean(prof['train_pass']))
+        med = lambda xs: float(np.median(xs))
+        tp_ms = med(prof['train_pass']) * 1e-3
         tp_flops = train_pass_flops(layers, N, 1 + (T + 4) * ec if lstm else None)
-        rf_ms = float(np.mean(prof['rollout_forward']))
-        iso_ms = float(np.mean(prof['rollout_trunk']))
+        rf_ms = med(prof['rollout_forward']) * 1e-3
+        iso_ms = med(prof['rollout_trunk']) * 1e-3
         # one rollout step: E new frames (trunk) + E windows (LSTM) / E states
         fwd_flops = ec * sum(l[1] for l in layers)
         fwd_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in layers) + 4 * ec * sum(l[3] for l in layers)
@@ -427,16 +498,21 @@ def main():
         tk_bytes = ec * 84 * 84 * 4 * depth + 4 * sum(l[2] for l in trunk) + 4 * ec * out_floats
         tk_flops = ec * sum(l[1] for l in trunk)
         C_in = 4 * depth
+        frame = 84 * 84 * depth
+        # A2 stacking: the surviving channels of the previous state read, the p new frames read,
+        # the new state written (mt_preprocess_resized, and the same work inside the conv kernel)
+        stack_bytes = (4 * ec - stack_pushes) * frame + stack_pushes * frame + 4 * ec * frame
+        graph_note = ('hipGraph of back-to-back calls replayed 5 times between HIP event pairs on its stream '
+                      '(bench.graph_time); median per call, dispatch gaps included')
         if stacking:  # + the fused A2 stacking: the pushes read and the new state written
-            tk_bytes += int(stack_pushes) * 84 * 84 * depth + ec * 84 * 84 * 4 * depth
+            tk_bytes += stack_pushes * frame + 4 * ec * frame
             # the rollout chain's own kernels; in the loop each conv block also waits for its env's
             # emulator (in-kernel pull), so the roofline times them with every env published
             tk_ms = iso_ms
             kern = 'nips_conv_kernel<%d, true> (in-kernel pull) + nips_fc_kernel<%d>: the stacking rollout chain' % (
                 C_in, C_in)
-            timing = ('40 mt_forward_trunk_stacking calls back to back between one HIP event pair, every env '
-                      'published and its pushes in HBM (the kernels the timed loop runs; there the conv blocks '
-                      'also wait for their env: trunk_in_loop)')
+            timing = ('mt_forward_trunk_stacking (every env published, its pushes in HBM: the kernels the timed loop '
+                      'runs, with nothing to wait for), ' + graph_note)
             pmc_kernels = ['nips_conv_kernel<%d, true>' % C_in, 'nips_fc_kernel<%d>' % C_in]
         elif inloop_us is not None and not lstm:  # (LSTM: step 0's forward has 1 + 5E rows, the others E)
             tk_ms = inloop_us * 1e-3
@@ -447,12 +523,59 @@ def main():
         else:
             tk_ms = iso_ms
             kern = 'mt_forward_trunk (%s)' % ('LSTM frame trunk + cell x-product' if lstm else 'layered')
-            timing = 'isolated: 40 mt_forward_trunk calls back to back between one HIP event pair'
+            timing = 'isolated mt_forward_trunk, ' + graph_note
             pmc_kernels = None
         tk_gbs = tk_bytes / (tk_ms * 1e-3) / 1e9
         tk_tf = tk_flops / (tk_ms * 1e-3) / 1e12
         pmc = load_pmc(a.config, pmc_kernels)
         achieved = tp_flops / (tp_ms * 1e-3) / 1e12
+        # per-kernel rows of SURVEY §8(d): A2, A9/A10 (the loss kernel with the fused n-step scan),
+        # the backward's grouped launches, A11
+        A_, R_ = A, cfg['nb_choices']
+        O_ = 1 + A_ + R_
+        F_ = layers[-2][3]
+        P_ = net.nparams
+        def row(name, ref, kernel, us, nbytes=None, flops=None, note=None):
+            r = {'row': name, 'reference': ref, 'kernel': kernel, 'us': round(us, 2)}
+            if nbytes is not None:
+                gbs = nbytes / (us * 1e-6) / 1e9
+                r.update(bound='hbm', algorithmic_bytes=int(nbytes), achieved_gbs=round(gbs, 1),
+                         frac=round(gbs / MI355X_HBM_GBS, 4))
+            if flops is not None:
+                tf = flops / (us * 1e-6) / 1e12
+                r.update(bound='mfma', algorithmic_flop=float(flops), achieved_tflops=round(tf, 3),
+                         frac=round(tf / MI355X_FP32_TFLOPS, 4))
+            if note:
+                r['note'] = note
+            return r
+        kernels = [row('A2', 'atari_emulator.py:79-124, environment.py:58-80', 'preprocess_kernel (resized: stacking only)',
+                       med(prof['stack']), stack_bytes,
+                       note='standalone mt_preprocess_resized of the E envs (%d pushes); %s' % (stack_pushes, graph_note))]
+        if stacking:
+            share = (med(prof['rollout_trunk']) - med(prof['plain_trunk']))
+            kernels.append({'row': 'A2 (fused)', 'kernel': 'stacking share of nips_conv_kernel<%d, true>' % C_in,
+                            'us': round(share, 2), 'note': 'stacking trunk minus the same trunk on a resident state '
+                            '(mt_forward_trunk): the cost of the in-kernel stack in the benchmarked chain'})
+        tl = prof['train_launches']
+        if tl:
+            boot = 4 * 9 * ec * F_ if stacking else 0
+            loss_bytes = 4 * N * (2 * F_ + 2 * O_ + 4 + 6) + 4 * (F_ + 1) * O_ + boot
+            kernels.append(row('A9+A10', 'paac.py:219-231, policy_v_network.py:25-74', 'loss_bwd_kernel (n-step scan'
+                               + (' + V(s_T) from the bootstrap slabs' if stacking else '') + ' + loss + head dz / dH)',
+                               tl[0], loss_bytes, note='launch 1 of the update backward (bench.launch_breakdown)'))
+            names = ['dense dX + dense dW + head dW'] + ['conv%d dX + conv%d dW (+ the layer above\'s slab sum)' % (
+                i + 1, i + 1) if i > 0 else 'conv1 dW (+ conv2\'s slab sum)' for i in range(len(trunk) - 2, -1, -1)] + [
+                'conv1 slab sum + global-norm partials']
+            for k, us in enumerate(tl[1:]):
+                kernels.append(row('A10', 'actor_learner.py:49', 'group_kernel: ' + (names[k] if k < len(names) else
+                                                                                      'launch %d' % (k + 2)), us))
+        kernels.append(row('A11', 'actor_learner.py:55-74', 'clip_rmsprop_kernel', med(prof['clip_rmsprop']),
+                           28 * P_ + 4 * 512 + 4, note='%d params: w, ms, mom, g read (16 B) and w, ms, mom written '
+                           '(12 B) per parameter; ' % P_ + graph_note))
+        # the timed region in sub-windows (host clock after each update)
+        w = max(1, a.steps // 4)
+        edges = [t0] + marks
+        wins = [world * ec * T * w / (edges[i + w] - edges[i]) for i in range(0, a.steps - w + 1, w)]
         line = {
             'metric': 'env-steps/sec (ec x t_max frames per update)',
             'value': round(value, 1),
@@ -498,10 +621,23 @@ def main():
                            'flop_count': 'executed backward: dW of every layer + dX of every layer but conv1',
                            'achieved': round(achieved, 3), 'peak': MI355X_FP32_TFLOPS, 'unit': 'TFLOP/s',
                            'frac': round(achieved / MI355X_FP32_TFLOPS, 4),
-                           'ms_per_launch': round(tp_ms, 4), 'flop_per_launch': tp_flops},
+                           'ms_per_launch': round(tp_ms, 4), 'flop_per_launch': tp_flops,
+                           'timing': graph_note, **stats_us(prof['train_pass'])},
+            'kernels': kernels,
+            'trunk_isolated': {'graph': stats_us(prof['rollout_trunk']),
+                               'plain_trunk_graph': stats_us(prof['plain_trunk']) if 'plain_trunk' in prof else None,
+                               'eager_us': round(prof['rollout_trunk_eager'], 2),
+                               'note': 'graph = the roofline launch replayed as a hipGraph (5 replays of 40 calls); '
+                                       'plain = mt_forward_trunk on a resident state (no stacking, no ready words); '
+                                       'eager = 40 Python calls between one event pair (BENCH_r02\'s method: bounded '
+                                       'by the host launch rate on a loaded box)'},
             'rollout_forward': {'ms': round(rf_ms, 4), 'tflops': round(fwd_flops / (rf_ms * 1e-3) / 1e12, 3),
                                 'hbm_gbs': round(fwd_bytes / (rf_ms * 1e-3) / 1e9, 1),
                                 'hbm_frac': round(fwd_bytes / (rf_ms * 1e-3) / 1e9 / MI355X_HBM_GBS, 4)},
+            'value_windows': {'updates_per_window': w, 'values': [round(v, 1) for v in wins],
+                              'spread': round((max(wins) - min(wins)) / float(np.median(wins)), 4),
+                              'note': 'env-steps/s of consecutive sub-windows of the timed region (host clock after '
+                                      'each update; the rollout waits on the device every macro-step)'},
         }
         if replicas is not None:
             line['replicas_identical'] = replicas
@@ -522,6 +658,11 @@ def main():
             learner.cleanup()
             learner = None
             line['cpu_baseline'] = cpu_baseline(cfg, T, a.cpu_seconds, rank)
+            # BASELINE configs[0] (Pong NIPS ec=4 ew=2, the reference's CPU-only case), a shorter sample
+            c0 = cpu_baseline(CPU_CONFIG0, T, a.cpu_seconds / 2, rank)
+            c0.pop('_net_ms_per_update')
+            c0['config'] = 'BASELINE.json configs[0]: pong NIPS ec=4 ew=2 t_max=%d' % T
+            line['cpu_baseline_configs0'] = c0
             # learner-only: the network work of one update on each side (GPU: T + 1 rollout
             # forwards of E rows + the train pass; CPU port: its T + 1 forwards + train step)
             cpu_net = line['cpu_baseline'].pop('_net_ms_per_update')

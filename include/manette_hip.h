@@ -78,6 +78,14 @@ int mt_net_feature_dim(const mt_net *net, int *f); /* width of the trunk output 
 int mt_net_get_config(const mt_net *net, mt_net_config *cfg);
 /* Bytes of device workspace a forward/backward on `batch` rows needs. */
 int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes);
+/* Diagnostics / parity: where a workspace keeps pooled conv layer `layer`'s 2x2 max-pool argmax bytes
+ * ([rows][OH/2][OW/2][COUT] uint8, the window position 0..3 of the first maximum in (row, col)
+ * order that the backward routes the gradient to, TF MaxPoolGrad): byte offset and size.
+ * layout 0 = the workspace of mt_forward / mt_forward_rows on a = batch rows; layout 1 = the LSTM
+ * frame-store workspace of (E = a, T = b), rows = fstore rows; layout 2 = the LSTM mt_forward
+ * workspace of a windows, rows = window frames (window-major, 5 per window). */
+int mt_net_pool_argmax_region(const mt_net *net, int layout, int a, int b, int layer, size_t *offset,
+                              size_t *bytes);
 
 /* ---- forward (A5-A7) ----------------------------------------------------------------------
  * Replaces session.run([output_layer_v, output_layer_pi, output_layer_rep], {input_ph: s})
@@ -432,6 +440,17 @@ int mt_broadcast(mt_comm *comm, void *buf, size_t bytes, int root, mt_stream_t s
 /* ---- small helpers ----------------------------------------------------------------------- */
 /* out[i] = sum_z parts[z*n + i] (deterministic order); used for split reductions. */
 int mt_sum_slabs(const float *parts, int nslabs, size_t n, float *out, mt_stream_t stream);
+
+/* Launch window: after mt_launch_window(first, count), first >= 0, the library numbers its grouped
+ * launches and loss-kernel launches from 0 in issue order and issues only those with index in
+ * [first, first + count) (count < 0: no upper end); the others return MT_OK without launching.
+ * mt_launch_window(-1, -1), the default, turns it off. Used while CAPTURING: one
+ * mt_returns_loss_backward* call recorded as two graphs, [0, 2) = the loss + the dense / head
+ * gradient launch and [2, ...) = the conv backward, so a data-parallel learner all-reduces the
+ * dense / head bucket while the conv backward runs (paac.py); and by bench.py to time a backward
+ * launch by launch. Library-global: set it around calls of one thread only. Returns how many
+ * launches were numbered since the previous call. */
+int mt_launch_window(int first, int count);
 
 /* hipGraph capture of everything launched on `stream` between begin and end. */
 int mt_graph_begin(mt_stream_t stream);

@@ -41,14 +41,30 @@ def build_hip(force=False, verbose=False, out=None, defines=()):
                                                                   os.path.join(INCLUDE, 'manette_host.h'), HOST_LIB]
     if not force and not _stale(target, deps):
         return target
+    # one hipcc per translation unit, in parallel (net.hip alone takes most of a serial build), then
+    # one link; objects are written beside the target so variants do not clobber each other
+    import concurrent.futures as cf
+    flags = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wno-unused-result'] + ['-D' + d for d in defines]
+    objs = [target + '.' + os.path.basename(src) + '.o' for src in srcs]
+    jobs = int(os.environ.get('MT_BUILD_JOBS', '4'))
+
+    def compile_one(src, obj):
+        cmd = [_hipcc()] + flags + ['-c', src, '-o', obj]
+        if verbose:
+            print(' '.join(cmd))
+        subprocess.check_call(cmd, cwd=CSRC)
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for f in [ex.submit(compile_one, src, obj) for src, obj in zip(srcs, objs)]:
+            f.result()
     tmp = target + '.tmp'
-    cmd = [_hipcc(), '--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
-           '-Wno-unused-result'] + ['-D' + d for d in defines] + ['-o', tmp] + srcs + [
-               '-L' + HERE, '-lmanette_host', '-Wl,-rpath,$ORIGIN', '-L/opt/rocm/lib', '-lrccl',
-               '-Wl,-rpath,/opt/rocm/lib']
+    cmd = [_hipcc(), '--offload-arch=gfx950', '-shared', '-fPIC', '-o', tmp] + objs + [
+        '-L' + HERE, '-lmanette_host', '-Wl,-rpath,$ORIGIN', '-L/opt/rocm/lib', '-lrccl', '-Wl,-rpath,/opt/rocm/lib']
     if verbose:
         print(' '.join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)
+    for o in objs:
+        os.remove(o)
     os.replace(tmp, target)
     return target
 

@@ -36,6 +36,18 @@ void set_error(const char *fmt, ...);
 // Check the launch that was just issued.
 #define MT_LAUNCHED() MT_HIP(hipGetLastError())
 
+// Launch window (mt_launch_window): off by default. When on, the grouped launches (launch_group) and
+// the loss kernel are numbered from 0 in issue order and only those in [first, first + count) are
+// issued — the rest return MT_OK without launching — so one backward call can be captured as
+// several graphs (its data-parallel gradient buckets) or timed launch by launch (bench.py).
+extern bool g_win_on;
+extern int g_win_first, g_win_count, g_win_index;
+__host__ inline bool launch_allowed() {
+  if (!g_win_on) return true;
+  const int i = g_win_index++;
+  return i >= g_win_first && (g_win_count < 0 || i < g_win_first + g_win_count);
+}
+
 __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // Wave-wide (64 lanes) reductions, every lane receiving the result, in a fixed order: DPP within

@@ -26,6 +26,10 @@
 
 #include "common.h"
 
+#ifndef MT_GEMM_DUAL  // two accumulators for one-tile waves (gemm_body_t); 0 = one chain
+#define MT_GEMM_DUAL 1
+#endif
+
 namespace mt {
 
 template <int BM_, int BN_, int WM_, int WN_, int BK_ = 32>
@@ -168,12 +172,21 @@ struct Stage {
 // == 0) of column n that one lane's accumulator holds — a 2x2 max pool over pool-ordered rows
 // (LdIm2col<G, U8, true>) becomes a register reduction. M must be a multiple of 4.
 // Two-phase epilogues (EP::Pre): ep.pre(m, n) loads the operands of output (m, n) — called for
-// every output of the lane (clamped to the last valid row / column) before any ep(pre, ...) or
-// ep.quad(pre, ...) stores.
+// every output of the lane (clamped to the last valid row / column) when the block starts, right
+// behind its first chunk's loads, long before any ep(pre, ...) or ep.quad(pre, ...) stores.
 template <class E, class = void>
 struct HasPre : std::false_type {};
 template <class E>
 struct HasPre<E, std::void_t<typename E::Pre>> : std::true_type {};
+
+template <class E, bool = HasPre<E>::value>
+struct PreOf {
+  struct type {};
+};
+template <class E>
+struct PreOf<E, true> {
+  using type = typename E::Pre;
+};
 
 template <class E, class = void>
 struct IsQuadEp : std::false_type {};
@@ -219,7 +232,12 @@ __device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP
   const int wm = w / T::WN, wn = w % T::WN;
   const int r = lane & 15, g = lane >> 4;
 
+  // One-tile waves (TM = TN = 1) would chain every MFMA on one accumulator: the dependent latency
+  // of v_mfma_f32_16x16x4_f32 (40 cycles) exceeds its issue interval (32), so the k steps alternate
+  // between two accumulators (s even / odd), added once at the end.
+  constexpr bool DUAL = MT_GEMM_DUAL && T::TM * T::TN == 1;
   f32x4 acc[T::TM][T::TN];
+  f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < T::TM; ++i)
 #pragma unroll
@@ -232,6 +250,26 @@ __device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP
   if (kb < ke) {
     sa.load(la, m0, kb, ke, M);
     sb.load(lb, n0, kb, ke, N);
+  }
+  // Two-phase epilogue (EP::Pre): every operand load of the lane's outputs (a bias, the activation
+  // whose derivative masks a dX, a pool's argmax) depends only on the tile, so it is issued here,
+  // behind the first chunk's loads, and its latency hides under the K walk — a block of these
+  // latency-bound products otherwise waits one more memory round trip after its last MFMA. (Issued
+  // before any store: the stores may alias the loaded arrays as far as the compiler knows.)
+  constexpr int NQ = IsQuadEp<EP>::value ? 1 : 4;
+  typename PreOf<EP>::type pre[T::TM][T::TN][NQ];
+  if constexpr (HasPre<EP>::value) {
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j) {
+        const int n = min(n0 + (wn * T::TN + j) * 16 + r, N - 1);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int m = min(m0 + (wm * T::TM + i) * 16 + g * 4 + q, NQ == 1 ? M - 4 : M - 1);
+          pre[i][j][q] = ep.pre(m, n);
+        }
+      }
   }
   for (int k0 = kb; k0 < ke; k0 += T::BK) {
     sa.store(As);
@@ -252,34 +290,26 @@ __device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP
 #pragma unroll
       for (int j = 0; j < T::TN; ++j)
         b[j] = load_frag<LB::KMAJOR, T::BN, T::BK>(Bs, (wn * T::TN + j) * 16 + r, kc * 16 + g * 4);
+      if constexpr (DUAL) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][0], b[0][0], acc[0][0], 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][1], b[0][1], acc2, 0, 0, 0);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][2], b[0][2], acc[0][0], 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][3], b[0][3], acc2, 0, 0, 0);
+      } else {
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int i = 0; i < T::TM; ++i)
+          for (int i = 0; i < T::TM; ++i)
 #pragma unroll
-          for (int j = 0; j < T::TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < T::TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+      }
     }
     __syncthreads();
   }
+  if constexpr (DUAL) acc[0][0] += acc2;
 
   if constexpr (HasPre<EP>::value) {
-    // Two-phase epilogue: every operand load of the lane's outputs is issued before the first
-    // store (the stores may alias the loaded arrays as far as the compiler knows, so a fused
-    // load-compute-store per element waits one memory latency per element).
-    constexpr int NQ = IsQuadEp<EP>::value ? 1 : 4;
-    typename EP::Pre pre[T::TM][T::TN][NQ];
-#pragma unroll
-    for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < T::TN; ++j) {
-        const int n = min(n0 + (wn * T::TN + j) * 16 + r, N - 1);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const int m = min(m0 + (wm * T::TM + i) * 16 + g * 4 + q, NQ == 1 ? M - 4 : M - 1);
-          pre[i][j][q] = ep.pre(m, n);
-        }
-      }
 #pragma unroll
     for (int i = 0; i < T::TM; ++i)
 #pragma unroll
@@ -420,47 +450,46 @@ struct NoJob {
   __device__ __forceinline__ void run(int, float *) const {}
 };
 
-template <class J1, class J2, class J3>
-__global__ __launch_bounds__(256) void group_kernel(J1 j1, J2 j2, J3 j3) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  int id = blockIdx.x;
+template <class J1, class... Rest>
+__device__ __forceinline__ void run_group(int id, float *smem, const J1 &j1, const Rest &...rest) {
   if (id < j1.blocks()) {
     j1.run(id, smem);
     return;
   }
-  id -= j1.blocks();
-  if (id < j2.blocks()) {
-    j2.run(id, smem);
-    return;
-  }
-  j3.run(id - j2.blocks(), smem);
+  if constexpr (sizeof...(Rest) > 0) run_group(id - j1.blocks(), smem, rest...);
 }
 
-// One grid for up to three jobs (blocks in argument order: put the critical path first).
-template <class J1, class J2 = NoJob, class J3 = NoJob>
-inline int launch_group(hipStream_t s, const J1 &j1, const J2 &j2 = NoJob{}, const J3 &j3 = NoJob{}) {
+template <class... J>
+__global__ __launch_bounds__(256) void group_kernel(J... j) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  run_group(blockIdx.x, smem, j...);
+}
+
+// One grid for any number of jobs (blocks in argument order: put the critical path first).
+template <class... J>
+inline int launch_group(hipStream_t s, const J &...j) {
 #ifdef MT_SPLIT_GROUPS  // experiment builds: every job of a group in its own launch (per-job rocprof times)
-  if constexpr (!std::is_same_v<J2, NoJob> || !std::is_same_v<J3, NoJob>) {
-    int rc = launch_group(s, j1);
-    if (rc == MT_OK) rc = launch_group(s, j2);
-    if (rc == MT_OK) rc = launch_group(s, j3);
+  if constexpr (sizeof...(J) > 1) {
+    int rc = MT_OK;
+    ((rc = rc == MT_OK ? launch_group(s, j) : rc), ...);
     return rc;
   }
 #endif
-  const int nb = j1.blocks() + j2.blocks() + j3.blocks();
-  if (nb == 0) return MT_OK;
-  const size_t lds = std::max(j1.blocks() ? j1.lds() : 0, std::max(j2.blocks() ? j2.lds() : 0, j3.blocks() ? j3.lds() : 0));
+  const int nb = (0 + ... + j.blocks());
+  if (nb == 0 || !launch_allowed()) return MT_OK;
+  size_t lds = 0;
+  ((lds = std::max(lds, j.blocks() ? j.lds() : (size_t)0)), ...);
   if (lds > 160 * 1024) {
     set_error("grouped launch needs %zu bytes of LDS", lds);
     return MT_ERR_ARG;
   }
   static bool attr_set = false;  // per instantiation: allow up to 160 KB of dynamic LDS once
   if (!attr_set && lds > 64 * 1024) {
-    MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&group_kernel<J1, J2, J3>),
+    MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&group_kernel<J...>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  hipLaunchKernelGGL((group_kernel<J1, J2, J3>), dim3(nb), dim3(256), lds, s, j1, j2, j3);
+  hipLaunchKernelGGL((group_kernel<J...>), dim3(nb), dim3(256), lds, s, j...);
   MT_LAUNCHED();
   return MT_OK;
 }
@@ -535,15 +564,32 @@ struct LdColMajor {
   __device__ __forceinline__ void next(KS &s) const {
     s.p += (size_t)BK * ld;
   }
+  // The guarded (edge) fetch. A row quad wholly inside [0, nx) — every quad of the conv weight
+  // gradients' dY operand — is one load from a clamped k (k0 < ke is always in range) and a
+  // zero by select: no branch around the load and no partial register-quad fill (the round-2
+  // form, kept under MT_EXP_OLD_GUARD for tools/dual_diag.py, is compared in tools/gemm_repro.hip;
+  // DESIGN.md §8).
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
     const int row = row0 + rr, k = k0 + kk;
     const int nx = ones_row >= 0 ? ones_row : nrows;
+    const bool kok = k < ke;
+#ifdef MT_EXP_OLD_GUARD  // diagnosis builds only (tools/dual_diag.py): the round-2 form
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (k < ke) {
+    if (kok) {
       const float *p = X + (size_t)k * ld + row;
       if (row + 3 < nx && (ld & 3) == 0) {
         v = *reinterpret_cast<const f32x4 *>(p);
       } else {
+#else
+    if (row + 3 < nx && (ld & 3) == 0) {
+      const f32x4 v = *reinterpret_cast<const f32x4 *>(X + (size_t)(kok ? k : k0) * ld + row);
+      return kok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (kok) {
+      const float *p = X + (size_t)k * ld + row;
+      {
+#endif
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int rw = row + e;

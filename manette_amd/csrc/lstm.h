@@ -287,11 +287,8 @@ static int lstm_forward_impl(const mt_net *n, const float *P, const uint8_t *obs
                      ws + X.hprev, ws + X.h5, ws + X.out32, ws + X.slab6);
   MT_LAUNCHED();
   HeadParams hp = head_params(n, P);
-  hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + X.slab6, 1, B, W6 + (size_t)Ar::NH * Ar::F,
-                     n->cfg.activation, n->cfg.alpha_leaky, hp, n->cfg.softmax_temp, ws + L.H, v, pi, rep,
-                     smp ? *smp : SampleArgs{});
-  MT_LAUNCHED();
-  return MT_OK;
+  return launch_heads(B, s, ws + X.slab6, 1, B, W6 + (size_t)Ar::NH * Ar::F, n->cfg.activation, n->cfg.alpha_leaky,
+                      hp, n->cfg.softmax_temp, ws + L.H, v, pi, rep, smp ? *smp : SampleArgs{});
 }
 
 template <class Ar>
@@ -470,11 +467,9 @@ static int lstm_windows_fwd_impl(const mt_net *n, const float *P, int32_t *nz_t,
                      ws + X.slab6 + w0 * Ar::F);
   MT_LAUNCHED();
   HeadParams hp = head_params(n, P);
-  hipLaunchKernelGGL(heads_fwd_kernel, dim3(E), dim3(256), 0, s, ws + X.slab6 + w0 * Ar::F, 1, E,
-                     W6 + (size_t)Ar::NH * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp, n->cfg.softmax_temp,
-                     ws + X.L.H + w0 * Ar::F, v, pi, rep, smp ? *smp : SampleArgs{});
-  MT_LAUNCHED();
-  return MT_OK;
+  return launch_heads(E, s, ws + X.slab6 + w0 * Ar::F, 1, E, W6 + (size_t)Ar::NH * Ar::F, n->cfg.activation,
+                      n->cfg.alpha_leaky, hp, n->cfg.softmax_temp, ws + X.L.H + w0 * Ar::F, v, pi, rep,
+                      smp ? *smp : SampleArgs{});
 }
 
 // One macro-step forward of the frame-store LSTM inside the native rollout (rollout.hip): the

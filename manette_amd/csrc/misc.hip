@@ -283,6 +283,17 @@ extern "C" const char *mt_last_error(void) { return g_err; }
 
 extern "C" int mt_version(void) { return 1; }
 
+bool mt::g_win_on = false;
+int mt::g_win_first = 0, mt::g_win_count = -1, mt::g_win_index = 0;
+extern "C" int mt_launch_window(int first, int count) {
+  const int seen = g_win_index;
+  g_win_on = first >= 0;
+  g_win_first = first;
+  g_win_count = count;
+  g_win_index = 0;
+  return seen;
+}
+
 extern "C" int mt_returns(const float *rewards, const float *masks, const float *values,
                           const float *v_boot, double gamma, int T, int E, float *y, float *adv,
                           mt_stream_t stream) {

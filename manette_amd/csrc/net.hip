@@ -243,6 +243,9 @@ static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
 #ifndef MT_WGRAD_CHUNKS
 #define MT_WGRAD_CHUNKS 4
 #endif
+#ifndef MT_DENSE_DW_LATE  // the dense weight gradient in the first conv layer's launch (backward_impl)
+#define MT_DENSE_DW_LATE 1
+#endif
 constexpr int kWgradChunks = MT_WGRAD_CHUNKS;
 constexpr size_t kSlabFloats = (size_t)4 << 20;
 template <class G>
@@ -475,54 +478,87 @@ __device__ __forceinline__ int wave_draw(float p, int n, double u) {
 
 // One workgroup per row b (4 waves):
 //  1. h = act(sum_z slabs[z][b] + b_fc) — the split-K dense layer finished here
-//     (networks.py:57-70); every thread owns F/256 features, the slab loads of a feature are
-//     issued 8 at a time;
+//     (networks.py:57-70); every thread owns F/256 features;
 //  2. logits_o = [h, 1] . W_o for the 1+A+R head outputs (policy_v_network.py:22, :31, :47):
-//     wave w takes outputs o = w, w+4, ...; lanes split F and reduce with shuffles;
+//     wave w takes outputs o = w, w+4, ...; lanes split F and reduce with DPP;
 //  3. wave 0: v = logit_0, pi = softmax(logits_A / temp), rep = softmax(logits_R / temp);
 //  4. rollout path (smp.counters != null): wave 0 draws (a, r) for the row (A3, common.h).
+// Latency is everything here (32 blocks at E = 32, on the macro-step's critical chain), so every
+// global load is issued at the start, in the order it is needed — vmcnt retires loads in issue
+// order, so a wait for the first ones never waits for the later: the draw counter, then the slab
+// partials, then the dense bias, the head weights AND biases of the wave's outputs (a bias read
+// after the reduction cost one more memory round trip) — and the row's uniforms are hashed from
+// the counter while the slabs are in flight.
+// Column o of the head weights ([F][.] row-major, stride A / R for the actor / repetition heads) and
+// its bias, selected without branches (o is wave-uniform).
+__device__ __forceinline__ void head_col(const HeadParams &hp, int o, const float *&w, int &stride, const float *&bias) {
+  const bool c = o == 0, a = o <= hp.A;
+  w = c ? hp.Wc : (a ? hp.Wa + (o - 1) : hp.Wr + (o - 1 - hp.A));
+  stride = c ? 1 : (a ? hp.A : hp.R);
+  bias = c ? hp.bc : (a ? hp.ba + (o - 1) : hp.br + (o - 1 - hp.A));
+}
+
+__device__ uint64_t g_zero_u64 = 0;  // read in place of an absent draw counter / sequence base
+
+template <int FT, int SB>
 __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs, int S, int B,
                                           const float *__restrict__ fc_b, int act, float alpha, const HeadParams &hp,
                                           float temp, float *__restrict__ H, float *__restrict__ v,
                                           float *__restrict__ pi, float *__restrict__ rep, const SampleArgs &smp) {
-  __shared__ float hs[512];
+  __shared__ float hs[256 * FT];
   __shared__ float zs[64];
   const int F = hp.F, O = 1 + hp.A + hp.R;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // the head weights of this wave's first PRE outputs (o = w, w + 4, ...) and the row's draw counter
-  // do not depend on the slabs: requested before the slab loads so their latency overlaps
-  constexpr int PRE = 6, FMAX = 8;  // F <= 512; 4 * PRE = 24 >= 1 + A + R of every bench config
-  float wpre[PRE][FMAX];
+  constexpr int PRE = 6;  // 4 * PRE = 24 >= 1 + A + R of every config (more: read after the reduction)
+  constexpr int FMAX = 4 * FT;
+  // every load below is unconditional (clamped addresses, zeros by select): a guarded load would
+  // end its basic block with a wait for it
+  // (1) the draw counter and the sequence base (the uniforms need them first)
+  const uint64_t cnt = *(smp.counters ? smp.counters + b : &g_zero_u64);
+  const uint32_t seq_base = *(smp.seq_base ? smp.seq_base : reinterpret_cast<const uint32_t *>(&g_zero_u64));
+  // (2) the slab partials of the thread's features (S = 9 for the NIPS trunk: one batch)
+  const size_t zs_stride = (size_t)B * F;
+  float t[FT][SB];
 #pragma unroll
-  for (int k = 0; k < PRE; ++k)
+  for (int fi = 0; fi < FT; ++fi) {
+    const float *p = slabs + (size_t)b * F + min((int)threadIdx.x + 256 * fi, F - 1);
 #pragma unroll
-    for (int j = 0; j < FMAX; ++j) {
-      const int o = w + 4 * k, f = lane + 64 * j;
-      wpre[k][j] = (o < O && f < F) ? head_w(hp, f, o) : 0.f;
-    }
-  const uint64_t cnt = smp.counters ? smp.counters[b] : 0;
-  const uint32_t seq = smp.seq_base ? *smp.seq_base + smp.seq : smp.seq;  // (graph replay: device base)
+    for (int u = 0; u < SB; ++u) t[fi][u] = p[(size_t)min(u, S - 1) * zs_stride];
+  }
+  // (3) dense bias, head weights and biases of this wave's first PRE outputs (o = w, w + 4, ...)
+  float fb[FT];
+#pragma unroll
+  for (int fi = 0; fi < FT; ++fi) fb[fi] = fc_b[min((int)threadIdx.x + 256 * fi, F - 1)];
+  float wpre[PRE][FMAX], zb[PRE];
+#pragma unroll
+  for (int k = 0; k < PRE; ++k) {
+    const float *wp, *bp;
+    int st;
+    head_col(hp, min(w + 4 * k, O - 1), wp, st, bp);
+#pragma unroll
+    for (int j = 0; j < FMAX; ++j) wpre[k][j] = wp[(size_t)min(lane + 64 * j, F - 1) * st];
+    zb[k] = *bp;
+  }
   if (smp.advance && b == 0 && threadIdx.x == 0) {  // the replayed rollout's last reader has run
     smp.advance[0] += smp.advance_by;
     smp.advance[1] += smp.advance_by;
   }
-  for (int f = threadIdx.x; f < F; f += 256) {
-    const float *p = slabs + (size_t)b * F + f;
-    const size_t zs_stride = (size_t)B * F;
+  double ua = 0.0, ur = 0.0;
+  if (w == 0) row_uniforms(smp.seed, b + smp.row0, cnt, &ua, &ur);
+  // slab sum in slab order + bias + activation
+#pragma unroll
+  for (int fi = 0; fi < FT; ++fi) {
+    const int f = threadIdx.x + 256 * fi;
     float acc = 0.f;
-    // up to 16 predicated loads in flight (S = 9 for the NIPS trunk: one round trip), adds in
-    // slab order
-    for (int z = 0; z < S; z += 16) {
-      float t[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) t[u] = p[(size_t)min(z + u, S - 1) * zs_stride];  // clamped: no branches
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (z + u < S) acc += t[u];
+    for (int u = 0; u < SB; ++u)
+      if (u < S) acc += t[fi][u];
+    for (int z = SB; z < S; ++z) acc += slabs[(size_t)b * F + min(f, F - 1) + (size_t)z * zs_stride];  // (S > SB)
+    const float h = act_fwd(acc + fb[fi], act, alpha);
+    if (f < F) {
+      hs[f] = h;
+      H[(size_t)b * F + f] = h;
     }
-    const float h = act_fwd(acc + fc_b[f], act, alpha);
-    hs[f] = h;
-    H[(size_t)b * F + f] = h;
   }
   __syncthreads();
   MT_PROBE_AT(2, b, 1);
@@ -535,7 +571,7 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
       for (int j = 0; j < FMAX; ++j)
         if (lane + 64 * j < F) acc += hs[lane + 64 * j] * wpre[k][j];
       acc = wave_sum(acc);
-      if (lane == 0) zs[o] = acc + head_w(hp, F, o);
+      if (lane == 0) zs[o] = acc + zb[k];
     }
   }
   for (int o = w + 4 * PRE; o < O; o += 4) {
@@ -551,20 +587,15 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   if (lane == 0) v[b] = z;
   // actor logits sit in lanes 1..A, repetition logits in lanes 1+A..A+R: shift them to 0..
   const float za = __shfl(z, (lane + 1) & 63, 64) / temp;
-  const float pa = wave_softmax(za, lane, hp.A);
-  if (lane < hp.A) pi[(size_t)b * hp.A + lane] = pa;
   const float zr = __shfl(z, (lane + 1 + hp.A) & 63, 64) / temp;
+  const float pa = wave_softmax(za, lane, hp.A);
   const float pr = wave_softmax(zr, lane, hp.R);
+  if (lane < hp.A) pi[(size_t)b * hp.A + lane] = pa;
   if (lane < hp.R) rep[(size_t)b * hp.R + lane] = pr;
   if (smp.counters) {
-    const uint64_t c = cnt;
-    double ua, ur;
-    row_uniforms(smp.seed, b + smp.row0, c, &ua, &ur);
     const int a = wave_draw(pa, hp.A, ua), r = wave_draw(pr, hp.R, ur);
     if (lane == 0) {
-      smp.counters[b] = c + 1;
-      smp.a_idx[b] = a;
-      smp.r_idx[b] = r;
+      const uint32_t seq = seq_base + smp.seq;  // (graph replay: device base)
       if (smp.packed) {  // tagged pair, one 8-byte store, no fence (SampleArgs::packed)
         const uint64_t tag = (uint64_t)(seq & 0xffffu) << 16;
         const uint64_t word = ((tag | (uint32_t)r) << 32) | tag | (uint32_t)a;
@@ -573,6 +604,9 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
         smp.pair[b] = a;
         smp.pair[B + b] = r;
       }
+      smp.counters[b] = cnt + 1;
+      smp.a_idx[b] = a;
+      smp.r_idx[b] = r;
       if (smp.ready && !smp.packed) {  // release: the pair stores are visible to the host before the flag
         __threadfence_system();
         __hip_atomic_store(smp.ready + b, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -581,6 +615,7 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   }
 }
 
+template <int FT, int SB>
 __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict__ slabs, int S, int B,
                                                         const float *__restrict__ fc_b, int act,
                                                         float alpha, HeadParams hp, float temp,
@@ -588,8 +623,34 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict_
                                                         float *__restrict__ pi,
                                                         float *__restrict__ rep, SampleArgs smp) {
   MT_PROBE_AT(2, blockIdx.x, 0);
-  heads_row(blockIdx.x, slabs, S, B, fc_b, act, alpha, hp, temp, H, v, pi, rep, smp);
+  heads_row<FT, SB>(blockIdx.x, slabs, S, B, fc_b, act, alpha, hp, temp, H, v, pi, rep, smp);
   MT_PROBE_AT(2, blockIdx.x, 3);
+}
+
+// heads_fwd_kernel for F features (<= 512) and S slabs: the instantiation whose register arrays
+// hold exactly the row's features (FT = F / 256 rounded up) and slabs (SB >= S, else one batch of 16).
+static int launch_heads(int rows, hipStream_t s, const float *slabs, int S, int B, const float *fc_b, int act,
+                        float alpha, const HeadParams &hp, float temp, float *H, float *v, float *pi, float *rep,
+                        const SampleArgs &smp) {
+  if (hp.F > 512 || 1 + hp.A + hp.R > kMaxHeads) {
+    set_error("heads: F = %d > 512 or %d outputs > %d", hp.F, 1 + hp.A + hp.R, kMaxHeads);
+    return MT_ERR_ARG;
+  }
+#define MT_HEADS(FT_, SB_)                                                                                 \
+  hipLaunchKernelGGL((heads_fwd_kernel<FT_, SB_>), dim3(rows), dim3(256), 0, s, slabs, S, B, fc_b, act, alpha, hp, \
+                     temp, H, v, pi, rep, smp)
+  if (hp.F <= 256) {
+    if (S <= 1) MT_HEADS(1, 1);
+    else if (S <= 9) MT_HEADS(1, 9);
+    else MT_HEADS(1, 16);
+  } else {
+    if (S <= 1) MT_HEADS(2, 1);
+    else if (S <= 9) MT_HEADS(2, 9);
+    else MT_HEADS(2, 16);
+  }
+#undef MT_HEADS
+  MT_LAUNCHED();
+  return MT_OK;
 }
 
 #ifdef MT_PROBE
@@ -1059,10 +1120,10 @@ struct NormOut {
   size_t n = 0;               // gradient floats
 };
 
-template <class Ar, int I>
+template <class Ar, int I, class X = NoJob>
 static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
                           const WsLayout &L, float *grad, hipStream_t s, SlabJob pending = SlabJob{},
-                          const NormOut &no = NormOut{}) {
+                          const NormOut &no = NormOut{}, const X &extra = X{}) {
   using G = LayerG<Ar, I>;
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
@@ -1080,15 +1141,15 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
       MT_TRY(launch_group(s, conv_dgrad_unpool_job<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
                                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act,
                                                            al),
-                          wg.gemm, pending));
+                          wg.gemm, pending, extra));
     } else {
       MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
                                                act, al),
-                          wg.gemm, pending));
+                          wg.gemm, pending, extra));
     }
     return trunk_backward<Ar, J>(n, P, obs, B, ws, L, grad, s, wg.sum, no);
   } else {
-    MT_TRY(launch_group(s, wg.gemm, pending));
+    MT_TRY(launch_group(s, wg.gemm, pending, extra));
     SlabJob last = wg.sum;
     if (no.partials && last.blocks() <= MT_NORM_PARTIALS / 2) {
       // conv1's slab sum writes the norm partials of its region, the rest of the gradient (complete
@@ -1154,11 +1215,9 @@ static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int
                               EpSlab{ws + L.fcslab, B, Ar::F}, B, Ar::F, Ar::FLAT, L.fc_splits, s)));
   if (marks) MT_HIP(hipEventRecord(marks[1], s));
   HeadParams hp = head_params(n, P);
-  hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, L.fc_splits, B,
-                     Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp,
-                     n->cfg.softmax_temp, A.base + A.h_off, v, pi, rep, smp ? *smp : SampleArgs{});
-  MT_LAUNCHED();
-  return MT_OK;
+  return launch_heads(B, s, ws + L.fcslab, L.fc_splits, B, Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation,
+                      n->cfg.alpha_leaky, hp, n->cfg.softmax_temp, A.base + A.h_off, v, pi, rep,
+                      smp ? *smp : SampleArgs{});
 }
 
 // Inference forward (rollout steps, bootstrap): the NIPS trunk kernels where the arch has them
@@ -1182,11 +1241,9 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
     MT_LAUNCHED();
     if (marks) MT_HIP(hipEventRecord(marks[1], s));
     HeadParams hp = head_params(n, P);
-    hipLaunchKernelGGL(heads_fwd_kernel, dim3(B), dim3(256), 0, s, ws + L.fcslab, Fz::ROWS2, B,
-                       Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation, n->cfg.alpha_leaky, hp,
-                       n->cfg.softmax_temp, A.base + A.h_off, v, pi, rep, smp ? *smp : SampleArgs{});
-    MT_LAUNCHED();
-    return MT_OK;
+    return launch_heads(B, s, ws + L.fcslab, Fz::ROWS2, B, Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation,
+                        n->cfg.alpha_leaky, hp, n->cfg.softmax_temp, A.base + A.h_off, v, pi, rep,
+                        smp ? *smp : SampleArgs{});
   } else {
     if (st) {
       set_error("stacking forward is built for the NIPS arch only");
@@ -1234,6 +1291,7 @@ static int loss_bwd_launch(const mt_net *n, const float *P, int B, float *ws, co
   // loss scaling 5.0 and the batch mean (policy_v_network.py:70-74): scale = 5/B.
   const float scale = 5.0f / (float)B;
   HeadParams hp = head_params(n, P);
+  if (!launch_allowed()) return MT_OK;
   hipLaunchKernelGGL(loss_bwd_kernel, dim3(B), dim3(256), 0, s, hp, ws + L.H, pi, rep, v, a_idx, r_idx, y, adv,
                      beta, scale, n->cfg.softmax_temp, n->cfg.activation, n->cfg.alpha_leaky, ws + L.dz, ws + L.dH,
                      loss_terms, rs);
@@ -1287,11 +1345,17 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
   const HeadWgradJob hw = head_wgrad_job<Ar>(n, B, ws, L, grad);
   // dense dX: dH . W^T, masked by the last conv's activation (every trunk ends in an unpooled conv)
   static_assert(!pooled<Ar, K>(), "the trunk ends in an unpooled conv (networks.py:178-278)");
-  MT_TRY(launch_group(s, gemm_job<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
-                                              EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT,
-                                              Ar::F, 1),
-                      dw, hw));
+  const auto dx = gemm_job<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+                                       EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1);
+#if MT_DENSE_DW_LATE
+  // the dense dX is the only job of this launch on the critical path (the next conv layer's dX
+  // needs it); the dense weight gradient, as long, runs beside the conv layer's dX in the next one
+  MT_TRY(launch_group(s, dx, hw));
+  return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s, SlabJob{}, no, dw);
+#else
+  MT_TRY(launch_group(s, dx, dw, hw));
   return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s, SlabJob{}, no);
+#endif
 }
 
 }  // namespace mt
@@ -1393,6 +1457,64 @@ extern "C" int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *byte
   MT_CHECK_ARG(net && bytes, "null argument");
   MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
   MT_ARCH_SWITCH(net, { *bytes = ws_layout<Ar>(net, batch).total * sizeof(float); });
+  return MT_OK;
+}
+
+// Byte range of conv layer `layer`'s max-pool argmax bytes in a workspace (diagnostics / parity).
+template <class Ar, int I = 0>
+static int pool_arg_region(const WsLayout &L, int layer, size_t rows, size_t *offset, size_t *bytes) {
+  if constexpr (I < Ar::NCONV) {
+    if (layer != I) return pool_arg_region<Ar, I + 1>(L, layer, rows, offset, bytes);
+    if constexpr (!pooled<Ar, I>()) {
+      set_error("conv layer %d is not pooled", layer);
+      return MT_ERR_ARG;
+    } else {
+      using G = LayerG<Ar, I>;
+      *offset = L.parg[I] * sizeof(float);
+      *bytes = rows * (G::OH / 2) * (G::OW / 2) * G::COUT;
+      return MT_OK;
+    }
+  }
+  set_error("no conv layer %d", layer);
+  return MT_ERR_ARG;
+}
+
+template <class Ar>
+static int pool_arg_region_windows(const mt_net *net, int a, int layer, size_t *offset, size_t *bytes) {
+  return pool_arg_region<Ar>(lstm_ws_layout<Ar>(net, a, nullptr), layer, (size_t)a * Ar::STEPS, offset, bytes);
+}
+
+extern "C" int mt_net_pool_argmax_region(const mt_net *net, int layout, int a, int b, int layer, size_t *offset,
+                                         size_t *bytes) {
+  MT_CHECK_ARG(net && offset && bytes, "null argument");
+  MT_CHECK_ARG(a >= 1 && (layout == 0 || b >= 1), "bad sizes");
+  MT_ARCH_SWITCH(net, {
+    if (layout == 0) {
+      if constexpr (Ar::LSTM) {
+        set_error("layout 0 is the non-LSTM workspace");
+        return MT_ERR_ARG;
+      } else {
+        return pool_arg_region<Ar>(ws_layout<Ar>(net, a), layer, (size_t)a, offset, bytes);
+      }
+    } else if (layout == 1) {
+      if constexpr (!Ar::LSTM) {
+        set_error("layout 1 is the LSTM frame-store workspace");
+        return MT_ERR_ARG;
+      } else {
+        const LstmFrameWs X = lstm_frame_layout<Ar>(net, a, b);
+        return pool_arg_region<Ar>(X.L, layer, (size_t)X.R_max, offset, bytes);
+      }
+    } else if (layout == 2) {
+      if constexpr (!Ar::LSTM) {
+        set_error("layout 2 is the LSTM window workspace");
+        return MT_ERR_ARG;
+      } else {
+        return pool_arg_region_windows<Ar>(net, a, layer, offset, bytes);
+      }
+    }
+    set_error("layout %d", layout);
+    return MT_ERR_ARG;
+  });
   return MT_OK;
 }
 

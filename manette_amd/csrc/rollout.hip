@@ -70,6 +70,11 @@ struct mt_rollout {
   bool capturing = false;  // enqueue_forward / arm_step record offsets + bases
   bool graph_live = false; // this rollout runs from the replayed graph
   bool graph_off = false;  // MT_ROLLOUT_GRAPH=0
+  // the one stream every macro-step runs on (the first call's): the chains' in-kernel waits spin on
+  // host words, and two streams of waiting kernels that land on one hardware queue serialise into a
+  // timeout (env groups), so a second stream is refused
+  hipStream_t stream0 = nullptr;
+  bool stream_set = false;
   // update launched at the end of the rollout (mt_rollout_set_update)
   hipGraphExec_t update_graph = nullptr;
   float *lr_host = nullptr;
@@ -566,6 +571,13 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   MT_CHECK_ARG(t >= 0 && t < ro->T, "t=%d out of [0,%d)", t, ro->T);
   const mt_rollout_buffers &b = ro->b;
   hipStream_t s = (hipStream_t)stream;
+  if (!ro->stream_set) {
+    ro->stream0 = s;
+    ro->stream_set = true;
+  }
+  MT_CHECK_ARG(s == ro->stream0, "every macro-step of a rollout handle runs on one stream (its in-kernel waits "
+               "must not share a hardware queue with another stream's): got %p after %p", (void *)s,
+               (void *)ro->stream0);
   const int E = ro->E, T = ro->T;
   const double t0 = now_us();
   int32_t *a_h = b.idx_host + (size_t)t * E, *r_h = b.idx_host + (size_t)T * E + (size_t)t * E;

@@ -137,6 +137,27 @@ class DeviceNetwork(object):
             self._out[k] = o
         return o
 
+    def pool_argmax(self, ws, layout, a, b=0):
+        """Diagnostics / parity: the 2x2 max-pool argmax bytes every pooled conv layer left in
+        workspace `ws` (mt_net_pool_argmax_region; layout 0 = a forward of `a` rows, 1 = the LSTM
+        frame store of E = a, T = b, rows = its 1 + (T + 5) E frames, 2 = an LSTM forward of `a`
+        windows, rows = their 5 a frames): {'convK': uint8
+        [rows, OH/2, OW/2, C]} (window position 0..3 = 2 * row + col of the routed maximum)."""
+        rows = {0: int(a), 1: 1 + (int(b) + 5) * int(a), 2: 5 * int(a)}[int(layout)]
+        raw = ws.cpu().numpy()
+        convs = [v for v in self.vars if v[0].startswith('Network/conv') and v[0].endswith('_weights')]
+        out = {}
+        for i, (name, shape, _, _) in enumerate(convs):
+            off, n = C.c_size_t(), C.c_size_t()
+            if _lib.hip().mt_net_pool_argmax_region(self._h, int(layout), int(a), int(b), i, C.byref(off),
+                                                    C.byref(n)) != 0:
+                continue  # not a pooled layer
+            cout = int(shape[3])
+            side = int(round((n.value // (rows * cout)) ** 0.5))
+            assert rows * side * side * cout == n.value, (name, n.value, rows, cout)
+            out[name.split('/')[1]] = raw[off.value:off.value + n.value].reshape(rows, side, side, cout).copy()
+        return out
+
     # ---- compute -----------------------------------------------------------------------------
     def forward(self, obs, batch=None, out=None, ws_key=None, infer=False):
         """obs: uint8 cuda tensor [B,84,84,4*depth]. Returns (v, pi, rep) device tensors.

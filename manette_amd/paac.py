@@ -38,6 +38,13 @@ from .runners import NativeRunners, Runners
 from .emulator_runner import EmulatorRunner
 
 
+def merge_episode_records(parts):
+    """Episode records (global_step, reward, length) of every rank, in the order one process owning
+    every env would have finished them: by global step (each env's step is unique in a macro-step:
+    global_step + env id + 1, paac.py:184), the rank order breaking no tie."""
+    return sorted((int(g), float(r), int(n)) for part in parts for (g, r, n) in part)
+
+
 class PAACLearner(ActorLearner):
     def __init__(self, network_creator, environment_creator, explo_policy, args):
         self.seed = int(getattr(args, 'seed', 0))
@@ -134,6 +141,7 @@ class PAACLearner(ActorLearner):
         self._update_in_rollout = False  # mt_rollout_set_update registered (_register_update)
         self._boot_ws = None  # the rollout's workspace whose bootstrap dense slabs the loss kernel finishes
         self._eager_updates = 0
+        self._buckets = None  # data parallel: flat offset splitting the two all-reduce buckets
         self.summaries = None  # TensorBoard event files of the chief (manette_amd/summary.py)
         self._logged_episodes = 0
 
@@ -369,6 +377,10 @@ class PAACLearner(ActorLearner):
         self.book.drain()
         lr = self.get_lr()
         if self._update_in_rollout:  # the rollout's last step stored lr and launched the update graph
+            # the native step restates get_lr (actor_learner.py:132-136) in C++; the two must agree
+            if np.float32(self._lr_word[0]) != np.float32(lr):
+                raise RuntimeError('native LR schedule %r != get_lr() %r at global step %d'
+                                   % (float(self._lr_word[0]), lr, self.global_step))
             return lr
         self.network.set_lr(lr)
         if self._graph_ok():
@@ -376,11 +388,14 @@ class PAACLearner(ActorLearner):
                 self._capture_update()
             if self._graphs is not None:
                 s = devnet._stream()
-                self._launch_graph(self._graphs[0], s)
-                if len(self._graphs) > 1:  # the all-reduce could not be captured
+                if self._buckets is not None:  # data parallel, bucketed (see _capture_update)
+                    self._bucketed_update(s)
+                elif len(self._graphs) > 1:  # backward | eager all-reduce | apply
+                    self._launch_graph(self._graphs[0], s)
                     self.comm.allreduce(self.network.grad)
                     self._launch_graph(self._graphs[1], s)
                 else:
+                    self._launch_graph(self._graphs[0], s)
                     self._register_update()
                 return lr
         self._eager_updates += 1
@@ -389,6 +404,31 @@ class PAACLearner(ActorLearner):
             self.comm.allreduce(self.network.grad)
         self._update_apply()
         return lr
+
+    def _bucketed_update(self, s):
+        """Data-parallel update with the gradient all-reduced in two buckets on a side stream: the
+        dense + head variables (the tail of the flat gradient, ~98 % of its bytes) as soon as the
+        backward's second launch has written them, while the conv backward runs on the learner's
+        stream, then the conv variables; clip + RMSProp wait for both. Every rollout kernel (the
+        in-kernel waits) stays on the learner's stream; the side stream only ever runs the
+        all-reduces, between the update's first launch and its apply."""
+        cur = torch.cuda.current_stream()
+        side, (e1, e2, e3) = self._ar_stream, self._ar_events
+        g1, g2, g3 = self._graphs
+        grad = self.network.grad
+        self._launch_graph(g1, s)             # loss + dense dX / dW + head dW
+        e1.record(cur)
+        with torch.cuda.stream(side):
+            side.wait_event(e1)
+            self.comm.allreduce(grad[self._buckets:])
+        self._launch_graph(g2, s)             # conv backward (+ its slab sums)
+        e2.record(cur)
+        with torch.cuda.stream(side):
+            side.wait_event(e2)
+            self.comm.allreduce(grad[:self._buckets])
+            e3.record(side)
+        cur.wait_event(e3)
+        self._launch_graph(g3, s)             # global-norm partials + clip + RMSProp
 
     def _graph_ok(self):
         return (self.use_update_graph and self.profile is None
@@ -466,8 +506,6 @@ class PAACLearner(ActorLearner):
         torch.cuda.synchronize()
         def whole():
             self._update_backward()
-            if self.world > 1:
-                self.comm.allreduce(self.network.grad)
             self._update_apply()
 
         def capture(parts):
@@ -488,18 +526,37 @@ class PAACLearner(ActorLearner):
                     graphs.append(g)
             return graphs
 
-        graphs = None
-        if self.world == 1 or self.comm.capturable:
-            try:  # one graph, the RCCL all-reduce inside it
-                graphs = capture([whole])
-            except _lib.MTError:
-                if self.world == 1:
-                    raise
-                graphs = None
-        if graphs is None:  # split around the all-reduce, which then runs eagerly
+        def window(first, count, fn):
+            def run():
+                lib.mt_launch_window(first, count)
+                try:
+                    fn()
+                finally:
+                    lib.mt_launch_window(-1, -1)
+            return run
+
+        self._buckets = None
+        if self.world == 1:  # one graph; the rollout's last step launches it (_register_update)
+            graphs = capture([whole])
+        elif not self.lstm_bool and os.environ.get('MT_DP_BUCKETS', '1') != '0':
+            # data parallel: the backward captured as its first two launches (loss + the dense / head
+            # gradients) and the rest (conv backward), the all-reduces of the two gradient buckets
+            # run eagerly on a side stream between them (_bucketed_update)
+            graphs = capture([window(0, 2, self._update_backward), window(2, -1, self._update_backward),
+                              self._update_apply])
+            self._buckets = self._dense_offset()
+            self._ar_stream = torch.cuda.Stream()
+            self._ar_events = tuple(torch.cuda.Event() for _ in range(3))
+        else:  # backward | eager all-reduce of the whole gradient | apply
             graphs = capture([self._update_backward, self._update_apply])
         self._graphs = graphs
         self._graph_stream = side  # keep the capture stream alive with the graphs
+
+    def _dense_offset(self):
+        """Flat-gradient offset of the first non-conv variable (the dense layer): variables are in
+        TF creation order, the convs first (networks.py:178-278), so [0, off) is the conv bucket and
+        [off, n) the dense + head bucket."""
+        return min(off for name, _, off, _ in self.network.vars if '/conv' not in name)
 
     @staticmethod
     def _launch_graph(g, s):
@@ -510,13 +567,17 @@ class PAACLearner(ActorLearner):
         """From the next rollout on, its last macro-step stores the LR and launches the (single)
         update graph itself, right behind the bootstrap chain (mt_rollout_set_update): no host
         round trip between the last emulator step and the update. MT_UPDATE_IN_ROLLOUT=0: off."""
-        if os.environ.get('MT_UPDATE_IN_ROLLOUT', '1') == '0' or self.native_step is None or self.lstm_bool:
-            return  # (LSTM: its update also moves the frame-store slots the next rollout starts from)
+        if os.environ.get('MT_UPDATE_IN_ROLLOUT', '1') == '0' or self.native_step is None or self.lstm_bool \
+                or self.world > 1:
+            # (LSTM: its update also moves the frame-store slots the next rollout starts from; data
+            # parallel: the learner launches the update, its all-reduces eagerly between graphs)
+            return
         from . import _lib
         _lib.check(_lib.hip().mt_rollout_set_update(self.native_step, self._graphs[0],
                                                     self.network._lr_host.data_ptr(),
                                                     float(self.initial_lr), float(self.lr_annealing_steps)),
                    'mt_rollout_set_update')
+        self._lr_word = self.network._lr_host.numpy()  # (the pinned word the rollout writes)
         self._update_in_rollout = True
 
     def _destroy_graphs(self):
@@ -557,7 +618,14 @@ class PAACLearner(ActorLearner):
     def write_summaries(self):
         """The reference's TensorBoard scalars of the last rollout + update (chief only):
         rl/reward and rl/episode_length per finished episode (paac.py:191-199), then
-        rewards_per_episode/* and steps_per_episode/* (paac.py:65-77, :265-266)."""
+        rewards_per_episode/* and steps_per_episode/* (paac.py:65-77, :265-266).
+        Data parallel: the episodes of every rank (the union's, as one process owning every env
+        would log them) are gathered to the chief over the control channel at the reference's
+        logging interval (2048 / ec updates, paac.py:277-285) — a per-update gather would cost more
+        than the update — and the episode statistics are written when the gathered span crossed a
+        multiple of 500 global steps (the reference tests global_step % 500 == 0 per update)."""
+        if self.world > 1:
+            return self._write_summaries_dp()
         if self.summaries is None:
             if not self.is_chief:
                 return
@@ -569,6 +637,33 @@ class PAACLearner(ActorLearner):
         self._logged_episodes = len(eps)
         self.summaries.log_values(self.book.total_rewards, 'rewards_per_episode', self.global_step)
         self.summaries.log_values(self.book.total_steps, 'steps_per_episode', self.global_step)
+        self.summaries.flush()
+
+    def _write_summaries_dp(self, interval=None):
+        self._summary_calls = getattr(self, '_summary_calls', 0) + 1
+        interval = interval or max(1, 2048 // self.emulator_counts)
+        if self._summary_calls % interval != 0:
+            return
+        self.book.drain()
+        mine = [tuple(e) for e in self.book.episodes[self._logged_episodes:]]
+        self._logged_episodes = len(self.book.episodes)
+        parts = [None] * self.world
+        torch.distributed.all_gather_object(parts, mine)
+        if not self.is_chief:
+            return
+        if self.summaries is None:
+            from .summary import LearnerSummaries
+            self.summaries = LearnerSummaries(self.debugging_folder)
+            self._union_rewards, self._union_steps, self._summary_step = [], [], self.global_step_start
+        merged = merge_episode_records(parts)
+        self.summaries.episodes(merged)
+        self._union_rewards.extend(r for _, r, _ in merged)
+        self._union_steps.extend(int(n) for _, _, n in merged)
+        crossed = self.global_step // 500 > self._summary_step // 500
+        self._summary_step = self.global_step
+        if crossed:
+            self.summaries.log_values(self._union_rewards, 'rewards_per_episode', self.global_step, timestep=1)
+            self.summaries.log_values(self._union_steps, 'steps_per_episode', self.global_step, timestep=1)
         self.summaries.flush()
 
     def train(self):

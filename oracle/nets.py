@@ -117,11 +117,19 @@ def maxpool2(x):
     return y
 
 
-def maxpool2_bwd(x, y, dy):
-    # TF MaxPoolGrad routes the gradient to the first max in the window (row-major scan).
+def maxpool2_bwd(x, y, dy, route=None):
+    """TF MaxPoolGrad routes the gradient to the first max in the window (row-major scan).
+    route (optional, [B, OH, OW, C] in 0..3 = 2 * row + col): the window position to route to
+    instead — a device's own choice at near-ties, where fp32 rounding may order the top two
+    values differently (tests/parity_util.py device_routes)."""
     B, H, W, C = x.shape
     OH, OW = H // 2, W // 2
     dx = np.zeros_like(x)
+    if route is not None:
+        for dy_ in range(2):
+            for dx_ in range(2):
+                dx[:, dy_:OH * 2:2, dx_:OW * 2:2, :] = np.where(route == 2 * dy_ + dx_, dy, 0)
+        return dx
     taken = np.zeros((B, OH, OW, C), dtype=bool)
     for dy_ in range(2):
         for dx_ in range(2):
@@ -130,6 +138,18 @@ def maxpool2_bwd(x, y, dy):
             dx[:, dy_:OH * 2:2, dx_:OW * 2:2, :] += np.where(hit, dy, 0)
             taken |= hit
     return dx
+
+
+def pool_route(x):
+    """2x2/2 VALID max-pool windows of x [B,H,W,C]: the position of the first maximum (0..3,
+    2 * row + col, MaxPoolGrad's choice) and the relative gap between the top two values."""
+    B, H, W, C = x.shape
+    OH, OW = H // 2, W // 2
+    win = x[:, :OH * 2, :OW * 2, :].reshape(B, OH, 2, OW, 2, C).transpose(0, 1, 3, 5, 2, 4).reshape(B, OH, OW, C, 4)
+    arg = np.argmax(win, axis=-1).astype(np.uint8)  # first maximum
+    srt = np.sort(win, axis=-1)
+    gap = (srt[..., 3] - srt[..., 2]) / np.maximum(np.abs(srt[..., 3]), 1e-30)
+    return arg, gap
 
 
 def softmax(z):
@@ -225,15 +245,16 @@ def trunk_forward(spec, P, obs, act='relu', alpha=0.1, dtype=np.float64):
     return x.reshape(x.shape[0], -1), layers
 
 
-def trunk_backward(spec, P, layers, dflat, G, act='relu', alpha=0.1, dtype=np.float64):
+def trunk_backward(spec, P, layers, dflat, G, act='relu', alpha=0.1, dtype=np.float64, routes=None):
     """Gradient of trunk_forward for dflat [B, flat]: conv weight / bias gradients ADDED into G
-    (so chunks of frames accumulate), TF's Conv2DBackprop* / ReluGrad / MaxPoolGrad."""
+    (so chunks of frames accumulate), TF's Conv2DBackprop* / ReluGrad / MaxPoolGrad. routes
+    (optional): {conv name: [B, OH/2, OW/2, C] pool positions} replacing MaxPoolGrad's own choice."""
     last = layers[-1]
     dx = dflat.reshape(last['yp'].shape if last['pool'] else last['y'].shape)
     for li in range(len(layers) - 1, -1, -1):
         L = layers[li]
         if L['pool']:
-            dx = maxpool2_bwd(L['y'], L['yp'], dx)
+            dx = maxpool2_bwd(L['y'], L['yp'], dx, None if routes is None else routes.get(L['name']))
         dy = dx * act_bwd(L['y'], act, alpha)
         cols, _ = im2col(L['x'], L['k'], L['s'], L['pad'])
         dy2 = dy.reshape(-1, L['cout'])
@@ -337,17 +358,17 @@ def heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act
 
 
 def loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1, temp=1.0,
-                   dtype=np.float64):
+                   dtype=np.float64, routes=None):
     """Loss of policy_v_network.py:25-74 and its gradient for every variable (dict)."""
     v, pi, rep, c = forward(spec, P, obs, act, alpha, temp, dtype)
     loss, G, dflat, aux = heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act, alpha,
                                                temp, dtype)
-    trunk_backward(spec, P, c['layers'], dflat, G, act, alpha, dtype)
+    trunk_backward(spec, P, c['layers'], dflat, G, act, alpha, dtype, routes)
     return loss, G, aux
 
 
 def window_frames_loss_and_grads(spec, P, frames, win, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1,
-                                 temp=1.0, dtype=np.float64, chunk=32):
+                                 temp=1.0, dtype=np.float64, chunk=32, routes=None):
     """loss_and_grads of LSTM windows given as indices into distinct frames: window b's position k
     is frames[win[b, k]] (the reference builds each window as an explicit [5][84][84][C] slice of
     whole_memory, paac.py:79-83, :233-234; zeroed positions after an episode end are a zero frame).
@@ -365,7 +386,8 @@ def window_frames_loss_and_grads(spec, P, frames, win, a_idx, r_idx, y, adv, bet
     np.add.at(dflat, np.asarray(win).reshape(-1), dflat_w)
     for c0 in range(0, F, chunk):
         _, layers = trunk_forward(spec, P, frames[c0:c0 + chunk], act, alpha, dtype)
-        trunk_backward(spec, P, layers, dflat[c0:c0 + chunk], G, act, alpha, dtype)
+        rt = None if routes is None else {k: r[c0:c0 + chunk] for k, r in routes.items()}
+        trunk_backward(spec, P, layers, dflat[c0:c0 + chunk], G, act, alpha, dtype, rt)
     return loss, G, aux
 
 

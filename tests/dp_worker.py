@@ -67,6 +67,8 @@ def gpu_rank(out_dir, rank, world):
             rec['gs'].append(L.global_step)
         L.book.drain()
         assert L._graphs is not None  # the graph path ran
+        if world > 1:  # the data-parallel update: two gradient buckets all-reduced on a side stream
+            assert L._buckets is not None and len(L._graphs) == 3 and not L._update_in_rollout
         np.savez(os.path.join(out_dir, 'w%d_r%d.npz' % (world, rank)), params0=params0, params=np.stack(rec['params']),
                  states=np.stack(rec['states']), gs=np.array(rec['gs']),
                  episodes=np.array(L.book.episodes, dtype=np.float64).reshape(-1, 3))

@@ -1,4 +1,5 @@
-"""End-to-end oracle parity of the BENCHMARKED path at every 1-GPU config size.
+"""End-to-end oracle parity of the BENCHMARKED path at every 1-GPU config size, the
+PWYX + RGB + FiGAR10 config included.
 
 The learner is bench.make_learner(config) — the exact object bench.py times: native emulator
 threads, device sampling fused into the heads kernel, resized staging, the pipelined native
@@ -13,7 +14,9 @@ checked against the oracle on everything it consumed and produced:
   forward     v / pi / rep of every rollout row and V(s_T) == oracle forward      2e-5 relative
   returns     y / adv == oracle.returns.nstep_returns (paac.py:219-231)          bit-exact
   gradient    every variable == oracle.nets.loss_and_grads of the T*E rows        2e-4 rel. L2
-              (LSTM: of the T*E windows over the distinct frames)
+              (LSTM: of the T*E windows over the distinct frames), per variable and per
+              output channel; max-pool windows routed where the device did, whose argmax
+              equals the oracle's away from fp64 near-ties                       bit-exact
   loss terms  per row == oracle                                                   1e-4 relative
   optimizer   lr == get_lr(global_step); norm == ||grad|| (1e-5); params / ms / mom after the
               update == oracle.optim clip + TF1 RMSProp on the device gradient    bit-exact
@@ -75,7 +78,14 @@ def _window_rows(nz, t, E):
     return w
 
 
-@pytest.mark.parametrize('config', ['pong-nips', 'breakout-nature-figar', 'seaquest-nature', 'mspacman-lstm-figar'])
+def _chunked_feats(spec, P, frames, chunk=32):
+    """Trunk features of frames [F,84,84,C] in chunks (the fp64 im2col of 192 RGB PWYX frames at
+    once would be 3 GB)."""
+    return np.concatenate([nets.trunk_forward(spec, P, frames[c0:c0 + chunk])[0] for c0 in range(0, len(frames), chunk)])
+
+
+@pytest.mark.parametrize('config', ['pong-nips', 'breakout-nature-figar', 'seaquest-nature', 'mspacman-lstm-figar',
+                                    'breakout-pwyx-figar-rgb'])
 def test_benchmarked_path_matches_oracle(config, tmp_path):
     import parity_util
     L, args, cfg = _run(config, tmp_path)
@@ -112,6 +122,9 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
             fstore, nz = c(L.fstore), c(L.nz_d)  # (nz derived on the device by the native step)
         L.update()
         torch.cuda.synchronize()
+        # the max-pool windows' routed positions the rollout's forwards left (PWYX / LSTM trunks)
+        dev_routes = L.network.pool_argmax(L.network.lstm_workspace(E, T), 1, E, T) if lstm else \
+            L.network.pool_argmax(L.train_ws, 0, N)
         assert L._update_in_rollout == (not lstm)  # the benchmarked path: the rollout launched this update
         # V(s_T): the rollout's last chain (pipelined native step) or the update's first forward (LSTM)
         v_boot, pi_all, rep_all = c(L.v_boot), c(L.pi_all), c(L.rep_all)
@@ -136,8 +149,7 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
     # ---- forward of every rollout row + V(s_T) ----------------------------------------------
     spec = nets.arch_spec(cfg['arch'], 3 if cfg['rgb'] else 1, A, R)
     if lstm:
-        Fr = 1 + (T + 5) * E
-        feats = np.concatenate([nets.trunk_forward(spec, P, fstore[c0:c0 + 32])[0] for c0 in range(0, Fr, 32)])
+        feats = _chunked_feats(spec, P, fstore[:1 + (T + 5) * E])
         for t in range(T + 1):
             rows = _window_rows(nz[t], t, E)
             v0, pi0, rep0, _ = nets.heads_forward(spec, P, feats[rows.reshape(-1)])
@@ -147,7 +159,7 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
             np.testing.assert_allclose(rep_all[t], rep0, rtol=2e-5, atol=1e-6, err_msg='rep step %d' % t)
     else:
         obs = states[:T + 1].reshape((T + 1) * E, 84, 84, -1)
-        v0, pi0, rep0, _ = nets.forward(spec, P, obs)
+        v0, pi0, rep0, _ = nets.heads_forward(spec, P, _chunked_feats(spec, P, obs))
         np.testing.assert_allclose(values.reshape(-1), v0[:N], rtol=2e-5, atol=2e-5)
         np.testing.assert_allclose(v_boot, v0[N:], rtol=2e-5, atol=2e-5)
         np.testing.assert_allclose(pi_all[:T].reshape(N, A), pi0[:N], rtol=2e-5, atol=1e-6)
@@ -165,14 +177,17 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
     if lstm:
         win = np.concatenate([_window_rows(nz[t], t, E) for t in range(T)])
         Fb = 1 + (T + 4) * E
+        routes, _ = parity_util.device_routes(spec, P, fstore[:Fb], {k: v[:Fb] for k, v in dev_routes.items()})
         _, G, aux = nets.window_frames_loss_and_grads(spec, P, fstore[:Fb], win, a_idx, r_idx, y.reshape(N),
-                                                      adv.reshape(N), beta)
-        loose = parity_util.near_tie_layers_frames(spec, P, fstore[:Fb])
-    else:
+                                                      adv.reshape(N), beta, routes=routes)
+    else:  # (row n = frame n: the chunked form of nets.loss_and_grads, pinned to it by a CPU test)
         obs_n = states[:T].reshape(N, 84, 84, -1)
-        _, G, aux = nets.loss_and_grads(spec, P, obs_n, a_idx, r_idx, y.reshape(N), adv.reshape(N), beta)
-        loose = set()
-    parity_util.check_grads(spec, grad, G, loose)
+        routes, _ = parity_util.device_routes(spec, P, obs_n, dev_routes)
+        _, G, aux = nets.window_frames_loss_and_grads(spec, P, obs_n, np.arange(N)[:, None], a_idx, r_idx,
+                                                      y.reshape(N), adv.reshape(N), beta, routes=routes)
+    # every max-pool window routed as the device did (argmax bit-exact away from fp64 near-ties):
+    # the pooled convs' gradients at the tight bound too (round 2 allowed 5e-3 on a near-tie batch)
+    parity_util.check_grads(spec, grad, G, set())
     np.testing.assert_allclose(terms, aux['terms'], rtol=1e-4, atol=1e-5)
 
     # ---- global-norm clip + TF1 RMSProp (bit-exact given the device gradient and norm) --------

@@ -337,3 +337,16 @@ def test_native_runner_resized_staging_is_pool_and_resize(rgb):
     finally:
         full.stop()
         rsz.stop()
+
+
+def test_emulator_count_scope():
+    """-ec per rank (the reference's per-agent count) or for the whole job (--ec_scope global):
+    BASELINE's "ec=256 sharded 8x32" is -ec 256 --ec_scope global on 8 ranks."""
+    import train
+    assert train.shard_emulators(32, 'rank', 8, 3) == (32, 96)
+    assert train.shard_emulators(256, 'global', 8, 3) == (32, 96)
+    assert train.shard_emulators(256, 'global', 1, 0) == (256, 0)
+    with pytest.raises(ValueError):
+        train.shard_emulators(30, 'global', 8, 0)
+    a = train.get_arg_parser().parse_args(['--ec_scope', 'global', '-ec', '256'])
+    assert a.ec_scope == 'global' and a.emulator_counts == 256 and a.sampling == 'host'

@@ -222,3 +222,27 @@ def test_dp_resume_from_rank0_checkpoint(tmp_path):
     assert int(r0['end']) == int(r1['end']) == int(r0['saved']) + 2 * 5 * 16
     np.testing.assert_array_equal(r0['p_start'], r1['p_start'])
     np.testing.assert_array_equal(r0['params'], r1['params'])
+
+
+def test_rollout_refuses_a_second_stream(tmp_path):
+    """The native rollout's chains spin in-kernel on host words; they must all run on one stream (two
+    streams of waiting kernels sharing one of the GPU_MAX_HW_QUEUES hardware queues serialised into a
+    timeout in round 2's env-group experiment), so a rollout handle refuses any stream but its first —
+    before it launches anything — and then carries on on its own stream."""
+    from manette_amd import _lib
+    L = _learner(tmp_path, 'native', 'device', staging='resized', pipeline=True)
+    try:
+        L.book.new_update()
+        L.rollout()
+        L.update()
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            with pytest.raises(_lib.MTError, match='one stream'):
+                L.rollout()
+        L.book.new_update()
+        L.rollout()  # the handle is still usable on its own stream
+        L.update()
+        torch.cuda.synchronize()
+        assert np.isfinite(L.network.params.cpu().numpy()).all()
+    finally:
+        L.cleanup()

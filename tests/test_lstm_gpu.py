@@ -40,11 +40,6 @@ def _rel(a, b):
     return float(np.linalg.norm(np.asarray(a, np.float64) - b) / max(np.linalg.norm(b), 1e-12))
 
 
-def _near_tie_layers(spec, P, obs, act):
-    import parity_util
-    return parity_util.near_tie_layers(spec, P, obs, act)
-
-
 def _windows(rs, B, depth, zero_frac=0.3):
     obs = rs.randint(0, 256, size=(B, 5, 84, 84, 4 * depth)).astype(np.uint8)
     # zeroed leading frames, as after an episode end (paac.py:202-203)
@@ -89,13 +84,13 @@ def test_lstm_loss_backward_parity(depth, A, R, act, B):
     net.loss_backward(obs_d, B, v, pi, rep, d(a_idx), d(r_idx), d(y), d(adv), loss_terms=terms)
     torch.cuda.synchronize()
     spec = nets.arch_spec('LSTM', depth, A, R)
-    loss, G, aux = nets.loss_and_grads(spec, net.get_variables(), obs, a_idx, r_idx, y, adv, 0.02, act=act,
-                                       alpha=0.1)
+    import parity_util  # max-pool windows routed as the device did (argmax checked away from near-ties)
+    P = net.get_variables()
+    frames = obs.reshape((-1,) + obs.shape[2:])
+    routes, _ = parity_util.device_routes(spec, P, frames, net.pool_argmax(net.workspace(B), 2, B), act)
+    loss, G, aux = nets.loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, 0.02, act=act, alpha=0.1, routes=routes)
     got = net.get_variables('grad')
-    loose = _near_tie_layers(spec, net.get_variables(), obs, act)
-    errs = {name: _rel(got[name], G[name]) for name, _, _ in spec['vars']}
-    bad = {n: e for n, e in errs.items() if e >= (5e-3 if n in loose else 2e-4)}
-    assert not bad, (bad, sorted(loose))
+    parity_util.check_grads(spec, got, G, set())
     np.testing.assert_allclose(terms.cpu().numpy(), aux['terms'], rtol=1e-4, atol=1e-5)
     flat = net.grad.cpu().numpy()
     mask = np.ones(net.nparams, bool)
@@ -128,6 +123,16 @@ def test_memory_push_bit_exact(E, depth):
         whole = _np_memory_push(mem, fresh, masks)
         np.testing.assert_array_equal(whole_d.cpu().numpy(), whole)
         np.testing.assert_array_equal(mem_d.cpu().numpy(), mem)
+
+
+def _window_rows_store(nz, t, E):
+    """Frame-store rows [E][5] of the windows of step t: 0 (the zero frame) for the nz leading
+    positions, else 1 + (t + k) * E + e (slot t + k of env e)."""
+    w = np.zeros((E, 5), np.int64)
+    for e in range(E):
+        for k in range(5):
+            w[e, k] = 0 if k < nz[e] else 1 + (t + k) * E + e
+    return w
 
 
 def _windows_from_store(slots, nz, t):
@@ -182,12 +187,14 @@ def test_lstm_frame_store_parity(E, T, depth):
                              loss_terms=terms)
     torch.cuda.synchronize()
     wt = win[:N]
-    _, G, aux = nets.loss_and_grads(spec, P, wt, a_idx, r_idx, y, adv, 0.02, act=act, alpha=0.1)
+    import parity_util  # routes of the distinct frames, gathered per window position
+    dev = net.pool_argmax(net.lstm_workspace(E, T), 1, E, T)
+    routes, _ = parity_util.device_routes(spec, P, fstore, dev, act)
+    rows = np.concatenate([_window_rows_store(nz[t], t, E) for t in range(T)]).reshape(-1)
+    _, G, aux = nets.loss_and_grads(spec, P, wt, a_idx, r_idx, y, adv, 0.02, act=act, alpha=0.1,
+                                    routes={k: v[rows] for k, v in routes.items()})
     got = net.get_variables('grad')
-    loose = _near_tie_layers(spec, P, wt, act)
-    errs = {name: _rel(got[name], G[name]) for name, _, _ in spec['vars']}
-    bad = {n: e for n, e in errs.items() if e >= (5e-3 if n in loose else 2e-4)}
-    assert not bad, (bad, sorted(loose))
+    parity_util.check_grads(spec, got, G, set())
     np.testing.assert_allclose(terms.cpu().numpy(), aux['terms'], rtol=1e-4, atol=1e-5)
 
 

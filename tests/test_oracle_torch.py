@@ -126,3 +126,24 @@ def test_window_frames_oracle_equals_explicit_windows():
     np.testing.assert_allclose(aux1['terms'], aux0['terms'], rtol=1e-12)
     for k in G0:
         np.testing.assert_allclose(G1[k], G0[k], rtol=1e-9, atol=1e-14, err_msg=k)
+
+
+@pytest.mark.parametrize('arch,depth', [('NIPS', 1), ('PWYX', 3)])
+def test_chunked_frames_oracle_equals_loss_and_grads(arch, depth):
+    """Non-recurrent archs: nets.window_frames_loss_and_grads with one frame per row (win = [[n]],
+    the trunk in chunks — how tests/test_e2e_gpu.py bounds the oracle's memory at N = 160 RGB PWYX
+    rows) == nets.loss_and_grads on the whole batch."""
+    spec = nets.arch_spec(arch, depth, 4, 11)
+    P = nets.init_params(spec, 5)
+    rs = np.random.RandomState(6)
+    B = 5
+    obs = rs.randint(0, 256, size=(B, 84, 84, 4 * depth)).astype(np.uint8)
+    a, r = rs.randint(0, 4, B), rs.randint(0, 11, B)
+    y, adv = rs.randn(B), rs.randn(B)
+    l0, G0, aux0 = nets.loss_and_grads(spec, P, obs, a, r, y, adv, 0.05)
+    l1, G1, aux1 = nets.window_frames_loss_and_grads(spec, P, obs, np.arange(B)[:, None], a, r, y, adv, 0.05,
+                                                     chunk=2)
+    assert abs(l0 - l1) <= 1e-12 * abs(l0)
+    np.testing.assert_allclose(aux1['terms'], aux0['terms'], rtol=1e-12)
+    for k in G0:
+        np.testing.assert_allclose(G1[k], G0[k], rtol=1e-9, atol=1e-14, err_msg=k)

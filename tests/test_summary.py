@@ -59,3 +59,15 @@ def test_learner_summaries_follow_reference(tmp_path):
     assert v['rewards_per_episode/max'] == np.float32(last.max())
     assert v['rewards_per_episode/std'] == np.float32(last.std())
     assert v['rewards_per_episode/std_over_mean'] == np.float32(min(2, abs(last.std() / last.mean())))
+
+
+def test_dp_episode_records_merge_in_global_step_order():
+    """Data parallel summaries: the chief logs the union of the ranks' episodes in the order
+    one process owning every env would have finished them (by their global step, paac.py:184-199)."""
+    from manette_amd.paac import merge_episode_records
+    r0 = [(17, 1.0, 40), (33, -1.0, 12)]
+    r1 = [(21, 0.0, 7), (29, 2.0, 9), (41, 1.0, 3)]
+    got = merge_episode_records([r0, r1])
+    assert [g for g, _, _ in got] == [17, 21, 29, 33, 41]
+    assert got[1] == (21, 0.0, 7) and got[3] == (33, -1.0, 12)
+    assert merge_episode_records([[], []]) == []

@@ -25,5 +25,8 @@ torch.cuda.synchronize()
 got = net.get_variables('grad')['Network/conv1/conv1_weights']
 spec = nets.arch_spec('NIPS', depth, A, R)
 _, G, _ = nets.loss_and_grads(spec, net.get_variables(), obs, a_idx, r_idx, y, adv, 0.02)
-np.savez(sys.argv[1], got=got, ref=G['Network/conv1/conv1_weights'])
+ref = G['Network/conv1/conv1_weights']
+np.savez(sys.argv[1], got=got, ref=ref)
+d = np.linalg.norm((got - ref).reshape(-1, 16), axis=0) / np.linalg.norm(ref.reshape(-1, 16), axis=0)
+print(os.environ.get('MANETTE_HIP_LIB', 'product library'), 'per-channel rel L2:', ' '.join('%.1e' % x for x in d))
 print('saved', sys.argv[1])

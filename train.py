@@ -4,8 +4,13 @@
 Extra flags (this build only): --runner {native,python}, --sampling {host,device},
 --staging {resized,in_place,zero_copy,copy,pooled}, --no_pipeline, --seed.
 Multi-GPU: launch one process per GPU with torch.distributed.run; each rank trains
--ec emulators of its own (global env ids offset by rank) and gradients are all-reduced by RCCL
-behind the C ABI (--comm rccl; torch.distributed runs on gloo as the control channel only).
+-ec emulators of its own (--ec_scope rank, the default) or -ec / WORLD_SIZE of them (--ec_scope
+global: -ec 256 on 8 GPUs = 32 per GPU, BASELINE's "ec=256 sharded 8x32"); global env ids are
+offset by rank, args.json records both counts, and gradients are all-reduced by RCCL behind the
+C ABI (--comm rccl; torch.distributed runs on gloo as the control channel only).
+Sampling: --sampling host (the default) draws with the reference's numpy multinomial stream
+(exploration_policy.py:108-116, bit-exact parity with the reference); the benchmarked native
+macro-step (bench.py) is --sampling device.
 """
 import argparse
 import copy
@@ -24,6 +29,10 @@ logging.basicConfig(stream=sys.stdout, level=logging.DEBUG)
 def main(args):
     logging.debug('Configuration: {}'.format(args))
     _setup_distributed(args)
+    logger_utils.save_args(args, args.debugging_folder)  # (per rank: rank r > 0 writes under rank<r>/)
+    if args.sampling == 'host':
+        logging.info('--sampling host: the reference\'s numpy sampling stream (parity mode); '
+                     '--sampling device runs the benchmarked native macro-step')
     explo_policy = ExplorationPolicy(args)
     print('Repetition table : ' + str(explo_policy.tab_rep))
     network_creator, env_creator = get_network_and_environment_creator(args, explo_policy)
@@ -45,9 +54,25 @@ def _setup_distributed(args):
         # control channel only (RCCL unique id, resume step); the gradient goes over mt_allreduce
         torch.distributed.init_process_group('gloo')
     rank = torch.distributed.get_rank() if world > 1 else 0
-    args.env_id_offset = rank * args.emulator_counts
+    per_rank, offset = shard_emulators(args.emulator_counts, getattr(args, 'ec_scope', 'rank'), world, rank)
+    args.emulator_counts = per_rank
+    args.emulator_counts_per_rank = per_rank
+    args.emulator_counts_global = per_rank * world
+    args.world_size = world
+    args.env_id_offset = offset
     if rank != 0:
         args.debugging_folder = os.path.join(args.debugging_folder, 'rank%d' % rank)
+
+
+def shard_emulators(ec, scope, world, rank):
+    """(emulators of this rank, global id of its first env): -ec per rank (scope 'rank') or for the
+    whole job (scope 'global', split evenly); rank r owns the contiguous global ids
+    [r * per_rank, (r + 1) * per_rank) — the np.split of runners.py:17-18 applied over ranks."""
+    if scope == 'global':
+        if ec % world:
+            raise ValueError('-ec %d is not divisible by WORLD_SIZE %d' % (ec, world))
+        ec //= world
+    return ec, rank * ec
 
 
 def setup_kill_signal_handler(learner):
@@ -140,7 +165,8 @@ def get_arg_parser():
     parser.add_argument('--no_pipeline', action='store_false', help='native device-sampling step: do not enqueue '
                         'step t+1\'s preprocess + forward behind a device wait on a host step word '
                         '(MT_ROLLOUT_PIPELINED, on by default)', dest='pipeline')
-    parser.add_argument('--sampling', default='host', choices=['host', 'device'], help='host: numpy multinomial (reference stream); device: mt_sample', dest='sampling')
+    parser.add_argument('--sampling', default='host', choices=['host', 'device'], help='host (default): numpy multinomial, the reference\'s stream (parity mode); device: mt_sample fused into the heads kernel, the benchmarked native macro-step', dest='sampling')
+    parser.add_argument('--ec_scope', default='rank', choices=['rank', 'global'], help='data parallel: -ec emulators per rank (rank, the reference\'s meaning for one process) or for the whole job, split evenly over WORLD_SIZE ranks (global)', dest='ec_scope')
     parser.add_argument('--seed', default=0, type=int, help='parameter init / device sampling seed', dest='seed')
     parser.add_argument('--comm', default='rccl', choices=['rccl', 'torch'], help='data-parallel gradient all-reduce: '
                         'rccl = RCCL behind the C ABI (mt_allreduce, one GPU per rank); torch = torch.distributed on '
@@ -150,6 +176,5 @@ def get_arg_parser():
 
 if __name__ == '__main__':
     args = get_arg_parser().parse_args()
-    logger_utils.save_args(args, args.debugging_folder)
     logging.debug(args)
     main(args)
