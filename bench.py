@@ -563,8 +563,16 @@ def main():
             kernels.append(row('A9+A10', 'paac.py:219-231, policy_v_network.py:25-74', 'loss_bwd_kernel (n-step scan'
                                + (' + V(s_T) from the bootstrap slabs' if stacking else '') + ' + loss + head dz / dH)',
                                tl[0], loss_bytes, note='launch 1 of the update backward (bench.launch_breakdown)'))
-            names = ['dense dX + dense dW + head dW'] + ['conv%d dX + conv%d dW (+ the layer above\'s slab sum)' % (
-                i + 1, i + 1) if i > 0 else 'conv1 dW (+ conv2\'s slab sum)' for i in range(len(trunk) - 2, -1, -1)] + [
+            import ctypes as C
+            from manette_amd import _lib
+            nb = C.c_int()
+            _lib.check(_lib.hip().mt_net_backward_bucket_launches(net._h, C.byref(nb)))
+            late = nb.value == 3  # the dense weight gradient runs beside the first conv layer's dX
+            nconv = len(trunk) - 1
+            names = ['dense dX + head dW' + ('' if late else ' + dense dW')] + [
+                ('conv%d dX + conv%d dW' % (i + 1, i + 1) if i > 0 else 'conv1 dW') +
+                (' + dense dW' if late and i == nconv - 1 else '') +
+                (' + conv%d slab sum' % (i + 2) if i < nconv - 1 else '') for i in range(nconv - 1, -1, -1)] + [
                 'conv1 slab sum + global-norm partials']
             for k, us in enumerate(tl[1:]):
                 kernels.append(row('A10', 'actor_learner.py:49', 'group_kernel: ' + (names[k] if k < len(names) else

@@ -78,14 +78,17 @@ int mt_net_feature_dim(const mt_net *net, int *f); /* width of the trunk output 
 int mt_net_get_config(const mt_net *net, mt_net_config *cfg);
 /* Bytes of device workspace a forward/backward on `batch` rows needs. */
 int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes);
-/* Diagnostics / parity: where a workspace keeps pooled conv layer `layer`'s 2x2 max-pool argmax bytes
- * ([rows][OH/2][OW/2][COUT] uint8, the window position 0..3 of the first maximum in (row, col)
- * order that the backward routes the gradient to, TF MaxPoolGrad): byte offset and size.
- * layout 0 = the workspace of mt_forward / mt_forward_rows on a = batch rows; layout 1 = the LSTM
- * frame-store workspace of (E = a, T = b), rows = fstore rows; layout 2 = the LSTM mt_forward
- * workspace of a windows, rows = window frames (window-major, 5 per window). */
-int mt_net_pool_argmax_region(const mt_net *net, int layout, int a, int b, int layer, size_t *offset,
-                              size_t *bytes);
+/* Diagnostics / parity: where a workspace keeps a forward value the backward branches on — kind 0:
+ * conv layer `layer`'s stored output, post-activation ([rows][OH][OW][COUT] fp32; a pooled layer's
+ * pooled map [rows][OH/2][OW/2][COUT]), whose sign is the ReLU branch; kind 1: a pooled layer's 2x2
+ * max-pool argmax bytes ([rows][OH/2][OW/2][COUT] uint8, the window position 0..3 of the first
+ * maximum in (row, col) order that the backward routes the gradient to, TF MaxPoolGrad); kind 2:
+ * the dense layer's output H ([rows][F] fp32). Byte offset and size. layout 0 = the workspace of
+ * mt_forward / mt_forward_rows on a = batch rows; layout 1 = the LSTM frame-store workspace of
+ * (E = a, T = b), conv rows = fstore rows, H rows = the (T+1)E windows; layout 2 = the LSTM
+ * mt_forward workspace of a windows, conv rows = window frames (window-major, 5 per window). */
+int mt_net_workspace_region(const mt_net *net, int layout, int a, int b, int kind, int layer, size_t *offset,
+                            size_t *bytes);
 
 /* ---- forward (A5-A7) ----------------------------------------------------------------------
  * Replaces session.run([output_layer_v, output_layer_pi, output_layer_rep], {input_ph: s})
@@ -451,6 +454,11 @@ int mt_sum_slabs(const float *parts, int nslabs, size_t n, float *out, mt_stream
  * launch by launch. Library-global: set it around calls of one thread only. Returns how many
  * launches were numbered since the previous call. */
 int mt_launch_window(int first, int count);
+/* How many leading launches of mt_returns_loss_backward* (non-LSTM) complete the gradient of every
+ * variable from the dense layer on (the tail of the flat gradient, ~98 % of its bytes): a
+ * data-parallel learner captures launches [0, n) and [n, ...) as two graphs and all-reduces the
+ * tail between them while the rest of the conv backward runs. */
+int mt_net_backward_bucket_launches(const mt_net *net, int *launches);
 
 /* hipGraph capture of everything launched on `stream` between begin and end. */
 int mt_graph_begin(mt_stream_t stream);

@@ -58,6 +58,7 @@ _HIP_SIGS = {
     'mt_last_error': (C.c_char_p, []),
     'mt_version': (_I, []),
     'mt_launch_window': (_I, [_I, _I]),
+    'mt_net_backward_bucket_launches': (_I, [_P, C.POINTER(_I)]),
     'mt_net_create': (_I, [C.POINTER(mt_net_config), C.POINTER(_P)]),
     'mt_net_destroy': (None, [_P]),
     'mt_net_num_params': (_I, [_P, C.POINTER(_SZ)]),
@@ -66,7 +67,7 @@ _HIP_SIGS = {
                              C.POINTER(_SZ), C.POINTER(_F)]),
     'mt_net_feature_dim': (_I, [_P, C.POINTER(_I)]),
     'mt_net_workspace_bytes': (_I, [_P, _I, C.POINTER(_SZ)]),
-    'mt_net_pool_argmax_region': (_I, [_P, _I, _I, _I, _I, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    'mt_net_workspace_region': (_I, [_P, _I, _I, _I, _I, _I, C.POINTER(_SZ), C.POINTER(_SZ)]),
     'mt_forward': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _P, _P, _P]),
     'mt_lstm_frames_workspace_bytes': (_I, [_P, _I, _I, C.POINTER(_SZ)]),
     'mt_lstm_frames_forward': (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),

@@ -26,8 +26,11 @@
 
 #include "common.h"
 
-#ifndef MT_GEMM_DUAL  // two accumulators for one-tile waves (gemm_body_t); 0 = one chain
-#define MT_GEMM_DUAL 1
+#ifndef MT_GEMM_PF2  // two register buffers: global loads two K chunks ahead (gemm_body_t)
+#define MT_GEMM_PF2 0
+#endif
+#ifndef MT_GEMM_DUAL  // two accumulators for one-tile waves (gemm_body_t): experiment builds only —
+#define MT_GEMM_DUAL 0  // the RGB conv1 weight gradient's channel 10 comes out wrong
 #endif
 
 namespace mt {
@@ -103,11 +106,11 @@ struct HasKs<L, std::void_t<typename L::KS>> : std::true_type {
 // (tap, channel) decomposition, computed once per tile in init) and the per-k remainder
 // (fetch_ctx, or the k state above): the integer divisions of an implicit im2col run once, not
 // once per chunk.
-template <class LD, int ROWS, int BK>
+template <class LD, int ROWS, int BK, int NB = 1>
 struct Stage {
   using S = LdsShape<LD::KMAJOR, ROWS, BK>;
   static constexpr bool KST = HasKs<LD>::value;
-  f32x4 r[S::ITEMS];
+  f32x4 r[NB][S::ITEMS];  // NB register buffers: chunk c lands in r[c % NB] (slots are compile-time)
   typename LD::Ctx cx[S::ITEMS];
   typename HasKs<LD>::KS ks[KST ? S::ITEMS : 1];
   __device__ __forceinline__ void init(const LD &ld, int row0, int kb) {
@@ -125,6 +128,7 @@ struct Stage {
   // Interior tiles (uniform per workgroup) take the branch-free fetch: every load of the chunk
   // is issued back to back and waited for once (a per-element guarded load would make hipcc
   // wait vmcnt(0) per element — cdna_hip_programming.md §5 trap (c)).
+  template <int SLOT = 0>
   __device__ __forceinline__ void load(const LD &ld, int row0, int k0, int ke, int nrows) {
     if (ld.interior(row0, ROWS, k0, BK, ke, nrows)) {
 #pragma unroll
@@ -134,9 +138,9 @@ struct Stage {
           int rr, kk;
           item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
           if constexpr (KST)
-            r[i] = ld.fetch_ks(cx[i], ks[i]);
+            r[SLOT][i] = ld.fetch_ks(cx[i], ks[i]);
           else
-            r[i] = ld.fetch_ctx(cx[i], k0 + kk);
+            r[SLOT][i] = ld.fetch_ctx(cx[i], k0 + kk);
         }
       }
     } else {
@@ -146,7 +150,7 @@ struct Stage {
         if (S::QUADS % 256 == 0 || it < S::QUADS) {
           int rr, kk;
           item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
-          r[i] = ld.fetch(row0, rr, k0, kk, ke, nrows);
+          r[SLOT][i] = ld.fetch(row0, rr, k0, kk, ke, nrows);
         }
       }
     }
@@ -155,6 +159,7 @@ struct Stage {
       for (int i = 0; i < S::ITEMS; ++i) ld.template next<BK>(ks[i]);
     }
   }
+  template <int SLOT = 0>
   __device__ __forceinline__ void store(float *L) const {
 #pragma unroll
     for (int i = 0; i < S::ITEMS; ++i) {
@@ -162,7 +167,7 @@ struct Stage {
       if (S::QUADS % 256 == 0 || it < S::QUADS) {
         int rr, kk;
         item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
-        lds_put<LD::KMAJOR, ROWS, BK>(L, rr, kk, r[i]);
+        lds_put<LD::KMAJOR, ROWS, BK>(L, rr, kk, r[SLOT][i]);
       }
     }
   }
@@ -243,13 +248,24 @@ __device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP
 #pragma unroll
     for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Stage<LA, T::BM, T::BK> sa;
-  Stage<LB, T::BN, T::BK> sb;
+  // Register prefetch: chunk c's global loads are issued while chunk c - 1 (PF = 1) or, with two
+  // register buffers (MT_GEMM_PF2), chunks c - 2 and c - 1 are multiplied — a gathered operand's
+  // latency then has two chunks of MFMAs to hide under instead of one.
+  constexpr int NB = (MT_GEMM_PF2 && LdsShape<LA::KMAJOR, T::BM, T::BK>::ITEMS + LdsShape<LB::KMAJOR, T::BN, T::BK>::ITEMS <= 8)
+                         ? 2 : 1;  // (a second buffer of more than 32 VGPRs would cost occupancy)
+  Stage<LA, T::BM, T::BK, NB> sa;
+  Stage<LB, T::BN, T::BK, NB> sb;
   sa.init(la, m0, kb);
   sb.init(lb, n0, kb);
   if (kb < ke) {
-    sa.load(la, m0, kb, ke, M);
-    sb.load(lb, n0, kb, ke, N);
+    sa.template load<0>(la, m0, kb, ke, M);
+    sb.template load<0>(lb, n0, kb, ke, N);
+  }
+  if constexpr (NB == 2) {
+    if (kb + T::BK < ke) {
+      sa.template load<1>(la, m0, kb + T::BK, ke, M);
+      sb.template load<1>(lb, n0, kb + T::BK, ke, N);
+    }
   }
   // Two-phase epilogue (EP::Pre): every operand load of the lane's outputs (a bias, the activation
   // whose derivative masks a dX, a pool's argmax) depends only on the tile, so it is issued here,
@@ -271,14 +287,8 @@ __device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP
         }
       }
   }
-  for (int k0 = kb; k0 < ke; k0 += T::BK) {
-    sa.store(As);
-    sb.store(Bs);
-    __syncthreads();
-    if (k0 + T::BK < ke) {  // prefetch the next chunk while this one is multiplied
-      sa.load(la, m0, k0 + T::BK, ke, M);
-      sb.load(lb, n0, k0 + T::BK, ke, N);
-    }
+  // the MFMAs of one staged chunk starting at k0
+  auto compute = [&](int k0) {
     const int kcn = min(T::BK, ke - k0);  // valid k in this chunk (rest is zero-filled)
 #pragma unroll
     for (int kc = 0; kc < T::BK / 16; ++kc) {
@@ -305,7 +315,41 @@ __device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
       }
     }
-    __syncthreads();
+  };
+  if constexpr (NB == 1) {
+    for (int k0 = kb; k0 < ke; k0 += T::BK) {
+      sa.store(As);
+      sb.store(Bs);
+      __syncthreads();
+      if (k0 + T::BK < ke) {  // prefetch the next chunk while this one is multiplied
+        sa.load(la, m0, k0 + T::BK, ke, M);
+        sb.load(lb, n0, k0 + T::BK, ke, N);
+      }
+      compute(k0);
+      __syncthreads();
+    }
+  } else {
+    for (int k0 = kb; k0 < ke; k0 += 2 * T::BK) {  // two chunks per trip: the buffer slots stay static
+      sa.template store<0>(As);
+      sb.template store<0>(Bs);
+      __syncthreads();
+      if (k0 + 2 * T::BK < ke) {
+        sa.template load<0>(la, m0, k0 + 2 * T::BK, ke, M);
+        sb.template load<0>(lb, n0, k0 + 2 * T::BK, ke, N);
+      }
+      compute(k0);
+      __syncthreads();
+      if (k0 + T::BK >= ke) break;
+      sa.template store<1>(As);
+      sb.template store<1>(Bs);
+      __syncthreads();
+      if (k0 + 3 * T::BK < ke) {
+        sa.template load<1>(la, m0, k0 + 3 * T::BK, ke, M);
+        sb.template load<1>(lb, n0, k0 + 3 * T::BK, ke, N);
+      }
+      compute(k0 + T::BK);
+      __syncthreads();
+    }
   }
   if constexpr (DUAL) acc[0][0] += acc2;
 

@@ -11,6 +11,7 @@
 #include <tuple>
 
 #include "gemm.h"
+#include "jobs.h"
 #include "trunk_fused.h"
 
 namespace mt {
@@ -203,9 +204,16 @@ struct TileFor<32, BK> {
 
 // K-chunk of a forward conv: the whole K when it fits 256, else the largest of 256/192/128
 // dividing it (one fill per chunk, all loads of a chunk in flight together).
+#ifndef MT_CONV_BK_CAP  // experiment builds: a smaller forward K chunk (with MT_GEMM_PF2: deeper prefetch)
+#define MT_CONV_BK_CAP 256
+#endif
+template <int K>
+constexpr int conv_bk_full() {
+  return K <= 256 ? ((K + 15) / 16) * 16 : (K % 256 == 0 ? 256 : (K % 192 == 0 ? 192 : 128));
+}
 template <int K>
 constexpr int conv_bk() {
-  return K <= 256 ? ((K + 15) / 16) * 16 : (K % 256 == 0 ? 256 : (K % 192 == 0 ? 192 : 128));
+  return conv_bk_full<K>() <= MT_CONV_BK_CAP ? conv_bk_full<K>() : MT_CONV_BK_CAP;
 }
 
 template <class G>
@@ -243,8 +251,8 @@ static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
 #ifndef MT_WGRAD_CHUNKS
 #define MT_WGRAD_CHUNKS 4
 #endif
-#ifndef MT_DENSE_DW_LATE  // the dense weight gradient in the first conv layer's launch (backward_impl)
-#define MT_DENSE_DW_LATE 1
+#ifndef MT_DENSE_DW_LATE  // experiment: the dense weight gradient in the first conv layer's launch
+#define MT_DENSE_DW_LATE 0  // (backward_impl; measured: Pong backward 53 vs 51 us, off)
 #endif
 constexpr int kWgradChunks = MT_WGRAD_CHUNKS;
 constexpr size_t kSlabFloats = (size_t)4 << 20;
@@ -320,105 +328,6 @@ static WsLayout ws_layout(const mt_net *n, int B) {
 // ---------------------------------------------------------------------------------------------
 // Kernels: slab sum, heads forward, loss + heads backward, heads weight gradient.
 // ---------------------------------------------------------------------------------------------
-// out[i] = sum_z P[z*n + i], fixed order. A block owns kSlabCols float4 columns; its 256 threads
-// are 16 slab subsets x kSlabCols columns, each thread adding slabs z = sub, sub+16, ... with 16
-// loads in flight (a few hundred slabs: one round trip), then the 16 subset sums of a column are
-// added in subset order. smem: 4 KB.
-constexpr int kSlabCols = 16;
-__device__ __forceinline__ void sum_slabs_body(const float *__restrict__ P, int S, size_t n, float *__restrict__ out,
-                                               int bid, float *smem, float *__restrict__ sq_out = nullptr) {
-  f32x4 *part = reinterpret_cast<f32x4 *>(smem);  // [16][kSlabCols]
-  const int col = threadIdx.x % kSlabCols, sub = threadIdx.x / kSlabCols;
-  const size_t n4 = n / 4;
-  const size_t c = (size_t)bid * kSlabCols + col;  // float4 column
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (c < n4) {
-    const f32x4 *p = reinterpret_cast<const f32x4 *>(P) + c;
-    // batches of up to 16 predicated loads, all issued before the first add (a plain remainder
-    // loop would wait out one load latency per slab); the adds stay in slab order
-    for (int z = sub; z < S; z += 256) {
-      f32x4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = p[(size_t)min(z + 16 * u, S - 1) * n4];  // clamped: no branches
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (z + 16 * u < S) acc += v[u];
-    }
-  }
-  part[sub * kSlabCols + col] = acc;
-  __syncthreads();
-  double sq = 0.0;  // sq_out: sum of the squares of this block's outputs (global-norm partial)
-  if (sub == 0 && c < n4) {
-    f32x4 t = part[col];
-#pragma unroll
-    for (int u = 1; u < 16; ++u) t += part[u * kSlabCols + col];
-    reinterpret_cast<f32x4 *>(out)[c] = t;
-    sq = (double)(t[0] * t[0]) + (double)(t[1] * t[1]) + (double)(t[2] * t[2]) + (double)(t[3] * t[3]);
-  }
-  // scalar tail (n not a multiple of 4)
-  if (bid == 0) {
-    for (size_t i = n4 * 4 + threadIdx.x; i < n; i += 256) {
-      float t = 0.f;
-      for (int z = 0; z < S; ++z) t += P[(size_t)z * n + i];
-      out[i] = t;
-      sq += (double)(t * t);
-    }
-  }
-  if (sq_out) {
-    double *red = reinterpret_cast<double *>(smem);
-    sq = wave_sum_d(sq);
-    __syncthreads();  // part[] is no longer read
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
-    __syncthreads();
-    if (threadIdx.x == 0) *sq_out = (float)(red[0] + red[1] + red[2] + red[3]);
-  }
-}
-
-// Global-norm partials of g outside [skip_b, skip_e) (float offsets, multiples of 4), as a job of a
-// grouped launch: block b writes partials[b] = sum of the squares of its grid-stride share
-// (sumsq_kernel's arithmetic; the grid of this job is fixed, so the partials are deterministic).
-struct SumsqJob {
-  const float *g = nullptr;
-  size_t n = 0, skip_b = 0, skip_e = 0;
-  float *partials = nullptr;
-  int nb = 0;
-  __host__ __device__ int blocks() const { return nb; }
-  size_t lds() const { return 64; }
-  __device__ __forceinline__ void run(int bid, float *smem) const {
-    double acc = 0.0;
-    const size_t n4 = n / 4, sb = skip_b / 4, se = skip_e / 4;
-    const size_t stride = (size_t)nb * 256;
-    for (size_t i = (size_t)bid * 256 + threadIdx.x; i < n4; i += stride) {
-      if (i >= sb && i < se) continue;
-      const f32x4 v = reinterpret_cast<const f32x4 *>(g)[i];
-      acc += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
-    }
-    for (size_t i = n4 * 4 + (size_t)bid * 256 + threadIdx.x; i < n; i += stride) acc += (double)(g[i] * g[i]);
-    double *red = reinterpret_cast<double *>(smem);
-    acc = wave_sum_d(acc);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) partials[bid] = (float)(red[0] + red[1] + red[2] + red[3]);
-  }
-};
-
-// Slab sum as a job of a grouped launch (gemm.h); n = 0: no job.
-struct SlabJob {
-  const float *P = nullptr;
-  int S = 0;
-  size_t n = 0;
-  float *out = nullptr;
-  float *sq = nullptr;  // optional: per-block global-norm partials sq[block]
-  __host__ __device__ int blocks() const {
-    const size_t b = (n / 4 + kSlabCols - 1) / kSlabCols;
-    return n ? (int)(b ? b : 1) : 0;
-  }
-  size_t lds() const { return 4096; }
-  __device__ __forceinline__ void run(int id, float *smem) const {
-    sum_slabs_body(P, S, n, out, id, smem, sq ? sq + id : nullptr);
-  }
-};
-
 static int sum_slabs(const float *P, int S, size_t n, float *out, hipStream_t s) {
   return launch_group(s, SlabJob{P, S, n, out});
 }
@@ -966,61 +875,6 @@ static int conv_forward_pool(const void *X, const float *Wt, const float *bias, 
   return launch_gemm<T>(la, lb, ep, M, G::COUT, G::KK, 1, s);
 }
 
-// Bias gradient rows of a split conv weight gradient: block z sums dY over split z's GEMM-K range
-// [z*kchunk, min(K, (z+1)*kchunk)) (pixels) for every channel and writes the sum to row KK of slab
-// z (the slab sum then adds the splits in z order, as for the weight rows). 256 threads = 16 row
-// subsets x 16 channel lanes; subsets summed in fixed order through LDS.
-template <int COUT>
-struct BiasRowJob {
-  const float *dY = nullptr;  // [K][COUT]
-  float *out = nullptr;       // slab row KK of split z at out + z * zstride
-  size_t zstride = 0;
-  int K = 0, kchunk = 0, nz = 0;
-  __host__ __device__ int blocks() const { return nz; }
-  size_t lds() const { return sizeof(float) * 256; }
-  __device__ __forceinline__ void run(int z, float *smem) const {
-    static_assert(COUT % 16 == 0 || COUT < 16, "channel lanes");
-    const int k0 = z * kchunk, k1 = min(K, k0 + kchunk);
-    const int sub = threadIdx.x >> 4, c = threadIdx.x & 15;
-    for (int n0 = 0; n0 < COUT; n0 += 16) {
-      float acc = 0.f;
-      if (n0 + c < COUT)
-        for (int k = k0 + sub; k < k1; k += 16 * 8) {  // 8 loads in flight, added in row order
-          float v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = dY[(size_t)min(k + 16 * u, k1 - 1) * COUT + n0 + c];
-#pragma unroll
-          for (int u = 0; u < 8; ++u)
-            if (k + 16 * u < k1) acc += v[u];
-        }
-      smem[threadIdx.x] = acc;
-      __syncthreads();
-      if (sub == 0 && n0 + c < COUT) {
-        float t = smem[c];
-#pragma unroll
-        for (int u = 1; u < 16; ++u) t += smem[u * 16 + c];
-        out[(size_t)z * zstride + n0 + c] = t;
-      }
-      __syncthreads();
-    }
-  }
-};
-
-// Two jobs as one (blocks of the first, then the second): the dW GEMM and its bias-row sums.
-template <class J1, class J2>
-struct PairJob {
-  J1 a;
-  J2 b;
-  __host__ __device__ int blocks() const { return a.blocks() + b.blocks(); }
-  size_t lds() const { return std::max(a.blocks() ? a.lds() : 0, b.blocks() ? b.lds() : 0); }
-  __device__ __forceinline__ void run(int id, float *smem) const {
-    if (id < a.blocks())
-      a.run(id, smem);
-    else
-      b.run(id - a.blocks(), smem);
-  }
-};
-
 // dW (+db) of a conv -> grad[(KK+1) x COUT] (weights then biases): dW = im2col(X)^T . dY as a GEMM
 // job into K-split slabs [S][KK+1][COUT] (one split: straight into gwb) and the slab-sum job that
 // finishes it (no job when unsplit). db: when KK fills whole M-tiles (NIPS / NATURE, PWYX conv3),
@@ -1460,56 +1314,82 @@ extern "C" int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *byte
   return MT_OK;
 }
 
-// Byte range of conv layer `layer`'s max-pool argmax bytes in a workspace (diagnostics / parity).
-template <class Ar, int I = 0>
-static int pool_arg_region(const WsLayout &L, int layer, size_t rows, size_t *offset, size_t *bytes) {
-  if constexpr (I < Ar::NCONV) {
-    if (layer != I) return pool_arg_region<Ar, I + 1>(L, layer, rows, offset, bytes);
-    if constexpr (!pooled<Ar, I>()) {
-      set_error("conv layer %d is not pooled", layer);
-      return MT_ERR_ARG;
+extern "C" int mt_net_backward_bucket_launches(const mt_net *net, int *launches) {
+  MT_CHECK_ARG(net && launches, "null argument");
+  MT_ARCH_SWITCH(net, {
+    if constexpr (Ar::LSTM) {
+      set_error("the LSTM backward is not bucketed");
+      return MT_ERR_UNSUPPORTED;
     } else {
-      using G = LayerG<Ar, I>;
-      *offset = L.parg[I] * sizeof(float);
-      *bytes = rows * (G::OH / 2) * (G::OW / 2) * G::COUT;
+      *launches = MT_DENSE_DW_LATE ? 3 : 2;  // backward_impl: loss | dense dX + head dW | first conv (+ dense dW)
+    }
+  });
+  return MT_OK;
+}
+
+// Byte range of a stored forward value in a workspace (diagnostics / parity; mt_net_workspace_region):
+// kind 0 = conv layer `layer`'s stored output (post-activation; the pooled map of a pooled layer),
+// kind 1 = a pooled layer's argmax bytes, kind 2 = the dense layer's post-activation output H.
+template <class Ar, int I = 0>
+static int ws_region(const WsLayout &L, int kind, int layer, size_t rows, size_t *offset, size_t *bytes) {
+  if (kind == 2) {
+    *offset = L.H * sizeof(float);
+    *bytes = rows * Ar::F * sizeof(float);
+    return MT_OK;
+  }
+  if constexpr (I < Ar::NCONV) {
+    if (layer != I) return ws_region<Ar, I + 1>(L, kind, layer, rows, offset, bytes);
+    using G = LayerG<Ar, I>;
+    constexpr bool P = pooled<Ar, I>();
+    const size_t px = P ? (size_t)(G::OH / 2) * (G::OW / 2) : (size_t)G::OH * G::OW;
+    if (kind == 0) {
+      *offset = (P ? L.pool[I] : L.act[I]) * sizeof(float);
+      *bytes = rows * px * G::COUT * sizeof(float);
       return MT_OK;
     }
+    if (kind == 1 && P) {
+      *offset = L.parg[I] * sizeof(float);
+      *bytes = rows * px * G::COUT;
+      return MT_OK;
+    }
+    set_error("conv layer %d has no region of kind %d", layer, kind);
+    return MT_ERR_ARG;
   }
   set_error("no conv layer %d", layer);
   return MT_ERR_ARG;
 }
 
 template <class Ar>
-static int pool_arg_region_windows(const mt_net *net, int a, int layer, size_t *offset, size_t *bytes) {
-  return pool_arg_region<Ar>(lstm_ws_layout<Ar>(net, a, nullptr), layer, (size_t)a * Ar::STEPS, offset, bytes);
+static int ws_region_windows(const mt_net *net, int a, int kind, int layer, size_t *offset, size_t *bytes) {
+  const WsLayout L = lstm_ws_layout<Ar>(net, a, nullptr);
+  return ws_region<Ar>(L, kind, layer, kind == 2 ? (size_t)a : (size_t)a * Ar::STEPS, offset, bytes);
 }
 
-extern "C" int mt_net_pool_argmax_region(const mt_net *net, int layout, int a, int b, int layer, size_t *offset,
-                                         size_t *bytes) {
+template <class Ar>
+static int ws_region_frames(const mt_net *net, int E, int T, int kind, int layer, size_t *offset, size_t *bytes) {
+  const LstmFrameWs X = lstm_frame_layout<Ar>(net, E, T);
+  return ws_region<Ar>(X.L, kind, layer, kind == 2 ? (size_t)X.W : (size_t)X.R_max, offset, bytes);
+}
+
+extern "C" int mt_net_workspace_region(const mt_net *net, int layout, int a, int b, int kind, int layer,
+                                       size_t *offset, size_t *bytes) {
   MT_CHECK_ARG(net && offset && bytes, "null argument");
-  MT_CHECK_ARG(a >= 1 && (layout == 0 || b >= 1), "bad sizes");
+  MT_CHECK_ARG(a >= 1 && (layout != 1 || b >= 1) && kind >= 0 && kind <= 2, "bad sizes or kind");
   MT_ARCH_SWITCH(net, {
     if (layout == 0) {
       if constexpr (Ar::LSTM) {
         set_error("layout 0 is the non-LSTM workspace");
         return MT_ERR_ARG;
       } else {
-        return pool_arg_region<Ar>(ws_layout<Ar>(net, a), layer, (size_t)a, offset, bytes);
+        return ws_region<Ar>(ws_layout<Ar>(net, a), kind, layer, (size_t)a, offset, bytes);
       }
-    } else if (layout == 1) {
+    } else if (layout == 1 || layout == 2) {
       if constexpr (!Ar::LSTM) {
-        set_error("layout 1 is the LSTM frame-store workspace");
+        set_error("layouts 1 and 2 are LSTM workspaces");
         return MT_ERR_ARG;
       } else {
-        const LstmFrameWs X = lstm_frame_layout<Ar>(net, a, b);
-        return pool_arg_region<Ar>(X.L, layer, (size_t)X.R_max, offset, bytes);
-      }
-    } else if (layout == 2) {
-      if constexpr (!Ar::LSTM) {
-        set_error("layout 2 is the LSTM window workspace");
-        return MT_ERR_ARG;
-      } else {
-        return pool_arg_region_windows<Ar>(net, a, layer, offset, bytes);
+        return layout == 1 ? ws_region_frames<Ar>(net, a, b, kind, layer, offset, bytes)
+                           : ws_region_windows<Ar>(net, a, kind, layer, offset, bytes);
       }
     }
     set_error("layout %d", layout);

@@ -137,25 +137,38 @@ class DeviceNetwork(object):
             self._out[k] = o
         return o
 
-    def pool_argmax(self, ws, layout, a, b=0):
-        """Diagnostics / parity: the 2x2 max-pool argmax bytes every pooled conv layer left in
-        workspace `ws` (mt_net_pool_argmax_region; layout 0 = a forward of `a` rows, 1 = the LSTM
-        frame store of E = a, T = b, rows = its 1 + (T + 5) E frames, 2 = an LSTM forward of `a`
-        windows, rows = their 5 a frames): {'convK': uint8
-        [rows, OH/2, OW/2, C]} (window position 0..3 = 2 * row + col of the routed maximum)."""
-        rows = {0: int(a), 1: 1 + (int(b) + 5) * int(a), 2: 5 * int(a)}[int(layout)]
+    def forward_branches(self, ws, layout, a, b=0):
+        """Diagnostics / parity: the forward values a workspace keeps that the backward branches on
+        (mt_net_workspace_region): {'convK': (output, argmax)} — the conv layer's post-activation
+        output [rows, H', W', C] fp32 (a pooled layer's pooled map; its sign is the ReLU branch) and,
+        for a pooled layer, the max-pool argmax [rows, H', W', C] uint8 (window position 0..3 =
+        2 * row + col) else None — and 'H': the dense output [rows', F]. layout 0 = a forward of `a`
+        rows; 1 = the LSTM frame store of E = a, T = b (conv rows = its 1 + (T + 5) E frames, H rows =
+        its (T + 1) E windows); 2 = an LSTM forward of `a` windows (conv rows = 5 a frames)."""
+        lib = _lib.hip()
         raw = ws.cpu().numpy()
+        rows = {0: int(a), 1: 1 + (int(b) + 5) * int(a), 2: 5 * int(a)}[int(layout)]
+        hrows = {0: int(a), 1: (int(b) + 1) * int(a), 2: int(a)}[int(layout)]
         convs = [v for v in self.vars if v[0].startswith('Network/conv') and v[0].endswith('_weights')]
+
+        def region(kind, layer):
+            off, n = C.c_size_t(), C.c_size_t()
+            rc = lib.mt_net_workspace_region(self._h, int(layout), int(a), int(b), int(kind), int(layer),
+                                             C.byref(off), C.byref(n))
+            return (off.value, n.value) if rc == 0 else None
+
         out = {}
         for i, (name, shape, _, _) in enumerate(convs):
-            off, n = C.c_size_t(), C.c_size_t()
-            if _lib.hip().mt_net_pool_argmax_region(self._h, int(layout), int(a), int(b), i, C.byref(off),
-                                                    C.byref(n)) != 0:
-                continue  # not a pooled layer
             cout = int(shape[3])
-            side = int(round((n.value // (rows * cout)) ** 0.5))
-            assert rows * side * side * cout == n.value, (name, n.value, rows, cout)
-            out[name.split('/')[1]] = raw[off.value:off.value + n.value].reshape(rows, side, side, cout).copy()
+            off, n = region(0, i)
+            side = int(round((n // 4 // (rows * cout)) ** 0.5))
+            assert rows * side * side * cout * 4 == n, (name, n, rows, cout)
+            y = raw[off:off + n].view(np.float32).reshape(rows, side, side, cout).copy()
+            r = region(1, i)
+            arg = raw[r[0]:r[0] + r[1]].reshape(rows, side, side, cout).copy() if r else None
+            out[name.split('/')[1]] = (y, arg)
+        off, n = region(2, 0)
+        out['H'] = raw[off:off + n].view(np.float32).reshape(hrows, -1).copy()
         return out
 
     # ---- compute -----------------------------------------------------------------------------

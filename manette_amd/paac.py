@@ -416,12 +416,12 @@ class PAACLearner(ActorLearner):
         side, (e1, e2, e3) = self._ar_stream, self._ar_events
         g1, g2, g3 = self._graphs
         grad = self.network.grad
-        self._launch_graph(g1, s)             # loss + dense dX / dW + head dW
+        self._launch_graph(g1, s)             # loss + dense dX / dW + head dW (+ the first conv layer's)
         e1.record(cur)
         with torch.cuda.stream(side):
             side.wait_event(e1)
             self.comm.allreduce(grad[self._buckets:])
-        self._launch_graph(g2, s)             # conv backward (+ its slab sums)
+        self._launch_graph(g2, s)             # the rest of the conv backward (+ its slab sums)
         e2.record(cur)
         with torch.cuda.stream(side):
             side.wait_event(e2)
@@ -539,10 +539,15 @@ class PAACLearner(ActorLearner):
         if self.world == 1:  # one graph; the rollout's last step launches it (_register_update)
             graphs = capture([whole])
         elif not self.lstm_bool and os.environ.get('MT_DP_BUCKETS', '1') != '0':
-            # data parallel: the backward captured as its first two launches (loss + the dense / head
-            # gradients) and the rest (conv backward), the all-reduces of the two gradient buckets
-            # run eagerly on a side stream between them (_bucketed_update)
-            graphs = capture([window(0, 2, self._update_backward), window(2, -1, self._update_backward),
+            # data parallel: the backward captured as its first launches, up to the one that completes
+            # the dense / head gradients (mt_net_backward_bucket_launches), and the rest (the conv
+            # backward); the all-reduces of the two gradient buckets run eagerly on a side stream
+            # between them (_bucketed_update)
+            n_tail = C.c_int()
+            _lib.check(lib.mt_net_backward_bucket_launches(self.network._h, C.byref(n_tail)),
+                       'mt_net_backward_bucket_launches')
+            k = n_tail.value
+            graphs = capture([window(0, k, self._update_backward), window(k, -1, self._update_backward),
                               self._update_apply])
             self._buckets = self._dense_offset()
             self._ar_stream = torch.cuda.Stream()

@@ -234,8 +234,9 @@ def trunk_forward(spec, P, obs, act='relu', alpha=0.1, dtype=np.float64):
         W = P['Network/%s/%s_weights' % (name, name)].astype(dtype)
         b = P['Network/%s/%s_biases' % (name, name)].astype(dtype)
         cols, (OH, OW, _, _) = im2col(x, k, s, pad)
-        y = act_fwd(cols @ W.reshape(-1, cout) + b, act, alpha).reshape(x.shape[0], OH, OW, cout)
-        entry = dict(x=x, y=y, k=k, s=s, pad=pad, pool=pool, cout=cout, name=name)
+        z = (cols @ W.reshape(-1, cout) + b).reshape(x.shape[0], OH, OW, cout)  # pre-activation
+        y = act_fwd(z, act, alpha)
+        entry = dict(x=x, y=y, z=z, k=k, s=s, pad=pad, pool=pool, cout=cout, name=name)
         if pool:
             y2 = maxpool2(y)
             entry['yp'] = y2
@@ -245,17 +246,31 @@ def trunk_forward(spec, P, obs, act='relu', alpha=0.1, dtype=np.float64):
     return x.reshape(x.shape[0], -1), layers
 
 
-def trunk_backward(spec, P, layers, dflat, G, act='relu', alpha=0.1, dtype=np.float64, routes=None):
+def branch_factor(branch, act, alpha, dtype=np.float64):
+    """act'(.) from the branch taken (True = the positive side: ReLU's x > 0, leaky's x >= 0)."""
+    return np.where(branch, 1.0, 0.0 if act == 'relu' else alpha).astype(dtype)
+
+
+def trunk_backward(spec, P, layers, dflat, G, act='relu', alpha=0.1, dtype=np.float64, routes=None,
+                   branches=None):
     """Gradient of trunk_forward for dflat [B, flat]: conv weight / bias gradients ADDED into G
-    (so chunks of frames accumulate), TF's Conv2DBackprop* / ReluGrad / MaxPoolGrad. routes
-    (optional): {conv name: [B, OH/2, OW/2, C] pool positions} replacing MaxPoolGrad's own choice."""
+    (so chunks of frames accumulate), TF's Conv2DBackprop* / ReluGrad / MaxPoolGrad.
+    routes (optional): {conv name: [B, OH/2, OW/2, C] pool positions} replacing MaxPoolGrad's own
+    choice; branches (optional): {conv name: bool, the activation branch of every stored output
+    (the pooled map of a pooled layer)} replacing ReluGrad's own — a device's decisions at the
+    gradient's discontinuities (tests/parity_util.py device_branches)."""
     last = layers[-1]
     dx = dflat.reshape(last['yp'].shape if last['pool'] else last['y'].shape)
     for li in range(len(layers) - 1, -1, -1):
         L = layers[li]
+        br = None if branches is None else branches.get(L['name'])
         if L['pool']:
+            if br is not None:  # act' of the routed (max) position = act' of the pooled value
+                dx = dx * branch_factor(br, act, alpha, dtype)
             dx = maxpool2_bwd(L['y'], L['yp'], dx, None if routes is None else routes.get(L['name']))
-        dy = dx * act_bwd(L['y'], act, alpha)
+            dy = dx if br is not None else dx * act_bwd(L['y'], act, alpha)
+        else:
+            dy = dx * (branch_factor(br, act, alpha, dtype) if br is not None else act_bwd(L['y'], act, alpha))
         cols, _ = im2col(L['x'], L['k'], L['s'], L['pad'])
         dy2 = dy.reshape(-1, L['cout'])
         name = L['name']
@@ -278,8 +293,9 @@ def heads_forward(spec, P, flat, act='relu', alpha=0.1, temp=1.0, dtype=np.float
     fc = spec['fc'][0]
     Wf = P['Network/%s/%s_weights' % (fc, fc)].astype(dtype)
     bf = P['Network/%s/%s_biases' % (fc, fc)].astype(dtype)
-    h = act_fwd(fc_in @ Wf + bf, act, alpha)
-    cache.update(fc_in=fc_in, h=h)
+    hz = fc_in @ Wf + bf
+    h = act_fwd(hz, act, alpha)
+    cache.update(fc_in=fc_in, h=h, hz=hz)
     Wc = P['Training/Critic/critic_output/critic_output_weights'].astype(dtype)
     bc = P['Training/Critic/critic_output/critic_output_biases'].astype(dtype)
     Wa = P['Training/Actor/actor_output/actor_output_weights'].astype(dtype)
@@ -304,7 +320,7 @@ def forward(spec, P, obs, act='relu', alpha=0.1, temp=1.0, dtype=np.float64):
 
 
 def heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1, temp=1.0,
-                         dtype=np.float64):
+                         dtype=np.float64, hbranch=None):
     """Loss of policy_v_network.py:25-74 from heads_forward's outputs; gradients of the head,
     dense [and LSTM] variables into a new dict G. Returns (loss, G, dflat, aux)."""
     B = len(v)
@@ -345,7 +361,8 @@ def heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act
     Wc = P['Training/Critic/critic_output/critic_output_weights'].astype(dtype)
     Wa = P['Training/Actor/actor_output/actor_output_weights'].astype(dtype)
     Wr = P['Training/Repetition/repetition_output/repetition_output_weights'].astype(dtype)
-    dh = (dv[:, None] @ Wc.T + dza @ Wa.T + dzr @ Wr.T) * act_bwd(h, act, alpha)
+    dh = (dv[:, None] @ Wc.T + dza @ Wa.T + dzr @ Wr.T) * (
+        act_bwd(h, act, alpha) if hbranch is None else branch_factor(hbranch, act, alpha, dtype))
     fc = spec['fc'][0]
     Wf = P['Network/%s/%s_weights' % (fc, fc)].astype(dtype)
     G['Network/%s/%s_weights' % (fc, fc)] = c['fc_in'].T @ dh
@@ -358,17 +375,17 @@ def heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act
 
 
 def loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1, temp=1.0,
-                   dtype=np.float64, routes=None):
+                   dtype=np.float64, routes=None, branches=None, hbranch=None):
     """Loss of policy_v_network.py:25-74 and its gradient for every variable (dict)."""
     v, pi, rep, c = forward(spec, P, obs, act, alpha, temp, dtype)
     loss, G, dflat, aux = heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act, alpha,
-                                               temp, dtype)
-    trunk_backward(spec, P, c['layers'], dflat, G, act, alpha, dtype, routes)
+                                               temp, dtype, hbranch)
+    trunk_backward(spec, P, c['layers'], dflat, G, act, alpha, dtype, routes, branches)
     return loss, G, aux
 
 
 def window_frames_loss_and_grads(spec, P, frames, win, a_idx, r_idx, y, adv, beta, act='relu', alpha=0.1,
-                                 temp=1.0, dtype=np.float64, chunk=32, routes=None):
+                                 temp=1.0, dtype=np.float64, chunk=32, routes=None, branches=None, hbranch=None):
     """loss_and_grads of LSTM windows given as indices into distinct frames: window b's position k
     is frames[win[b, k]] (the reference builds each window as an explicit [5][84][84][C] slice of
     whole_memory, paac.py:79-83, :233-234; zeroed positions after an episode end are a zero frame).
@@ -381,13 +398,14 @@ def window_frames_loss_and_grads(spec, P, frames, win, a_idx, r_idx, y, adv, bet
                            for c0 in range(0, F, chunk)])
     v, pi, rep, c = heads_forward(spec, P, flat[np.asarray(win).reshape(-1)], act, alpha, temp, dtype)
     loss, G, dflat_w, aux = heads_loss_and_grads(spec, P, v, pi, rep, c, a_idx, r_idx, y, adv, beta, act, alpha,
-                                                 temp, dtype)
+                                                 temp, dtype, hbranch)
     dflat = np.zeros_like(flat)
     np.add.at(dflat, np.asarray(win).reshape(-1), dflat_w)
     for c0 in range(0, F, chunk):
         _, layers = trunk_forward(spec, P, frames[c0:c0 + chunk], act, alpha, dtype)
         rt = None if routes is None else {k: r[c0:c0 + chunk] for k, r in routes.items()}
-        trunk_backward(spec, P, layers, dflat[c0:c0 + chunk], G, act, alpha, dtype, rt)
+        bt = None if branches is None else {k: r[c0:c0 + chunk] for k, r in branches.items()}
+        trunk_backward(spec, P, layers, dflat[c0:c0 + chunk], G, act, alpha, dtype, rt, bt)
     return loss, G, aux
 
 

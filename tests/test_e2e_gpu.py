@@ -15,8 +15,8 @@ checked against the oracle on everything it consumed and produced:
   returns     y / adv == oracle.returns.nstep_returns (paac.py:219-231)          bit-exact
   gradient    every variable == oracle.nets.loss_and_grads of the T*E rows        2e-4 rel. L2
               (LSTM: of the T*E windows over the distinct frames), per variable and per
-              output channel; max-pool windows routed where the device did, whose argmax
-              equals the oracle's away from fp64 near-ties                       bit-exact
+              output channel; max-pool windows and ReLU branches taken where the device
+              took them, each decision equal to the oracle's away from fp64 near-ties  bit-exact
   loss terms  per row == oracle                                                   1e-4 relative
   optimizer   lr == get_lr(global_step); norm == ||grad|| (1e-5); params / ms / mom after the
               update == oracle.optim clip + TF1 RMSProp on the device gradient    bit-exact
@@ -122,9 +122,10 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
             fstore, nz = c(L.fstore), c(L.nz_d)  # (nz derived on the device by the native step)
         L.update()
         torch.cuda.synchronize()
-        # the max-pool windows' routed positions the rollout's forwards left (PWYX / LSTM trunks)
-        dev_routes = L.network.pool_argmax(L.network.lstm_workspace(E, T), 1, E, T) if lstm else \
-            L.network.pool_argmax(L.train_ws, 0, N)
+        # the forward values the rollout left that the backward branches on (ReLU outputs, max-pool
+        # argmax, the dense output)
+        dev = L.network.forward_branches(L.network.lstm_workspace(E, T), 1, E, T) if lstm else \
+            L.network.forward_branches(L.train_ws, 0, N)
         assert L._update_in_rollout == (not lstm)  # the benchmarked path: the rollout launched this update
         # V(s_T): the rollout's last chain (pipelined native step) or the update's first forward (LSTM)
         v_boot, pi_all, rep_all = c(L.v_boot), c(L.pi_all), c(L.rep_all)
@@ -177,16 +178,19 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
     if lstm:
         win = np.concatenate([_window_rows(nz[t], t, E) for t in range(T)])
         Fb = 1 + (T + 4) * E
-        routes, _ = parity_util.device_routes(spec, P, fstore[:Fb], {k: v[:Fb] for k, v in dev_routes.items()})
+        br = parity_util.device_branches(spec, P, fstore[:Fb], dev, win=win, rows=slice(0, Fb))
         _, G, aux = nets.window_frames_loss_and_grads(spec, P, fstore[:Fb], win, a_idx, r_idx, y.reshape(N),
-                                                      adv.reshape(N), beta, routes=routes)
+                                                      adv.reshape(N), beta, routes=br['routes'],
+                                                      branches=br['branches'], hbranch=br['hbranch'])
     else:  # (row n = frame n: the chunked form of nets.loss_and_grads, pinned to it by a CPU test)
         obs_n = states[:T].reshape(N, 84, 84, -1)
-        routes, _ = parity_util.device_routes(spec, P, obs_n, dev_routes)
+        br = parity_util.device_branches(spec, P, obs_n, dev)
         _, G, aux = nets.window_frames_loss_and_grads(spec, P, obs_n, np.arange(N)[:, None], a_idx, r_idx,
-                                                      y.reshape(N), adv.reshape(N), beta, routes=routes)
-    # every max-pool window routed as the device did (argmax bit-exact away from fp64 near-ties):
-    # the pooled convs' gradients at the tight bound too (round 2 allowed 5e-3 on a near-tie batch)
+                                                      y.reshape(N), adv.reshape(N), beta, routes=br['routes'],
+                                                      branches=br['branches'], hbranch=br['hbranch'])
+    # every max-pool window and ReLU branch as the device took it (each decision bit-exact vs the
+    # oracle away from fp64 near-ties): every gradient at the tight bound (round 2 allowed 5e-3 for
+    # the pooled convs of a batch with a max-pool near-tie)
     parity_util.check_grads(spec, grad, G, set())
     np.testing.assert_allclose(terms, aux['terms'], rtol=1e-4, atol=1e-5)
 

@@ -156,9 +156,10 @@ def test_forward_rows_then_backward_only(arch, depth, A, R, E, T):
     np.testing.assert_allclose(v.cpu().numpy().reshape(-1), v0, rtol=2e-5, atol=2e-5)
     np.testing.assert_allclose(pi.cpu().numpy().reshape(N, A), pi0, rtol=2e-5, atol=1e-6)
     _, G, _ = nets.loss_and_grads(spec, P, obs_n, a_idx, r_idx, y, adv, 0.02)
-    import parity_util  # max-pool windows routed as the device did (argmax checked away from near-ties)
-    routes, _ = parity_util.device_routes(spec, P, obs_n, net.pool_argmax(tws, 0, N))
-    _, G, _ = nets.loss_and_grads(spec, P, obs_n, a_idx, r_idx, y, adv, 0.02, routes=routes)
+    import parity_util  # the device's branches at the discontinuities (checked away from near-ties)
+    br = parity_util.device_branches(spec, P, obs_n, net.forward_branches(tws, 0, N))
+    _, G, _ = nets.loss_and_grads(spec, P, obs_n, a_idx, r_idx, y, adv, 0.02, routes=br['routes'],
+                                  branches=br['branches'], hbranch=br['hbranch'])
     parity_util.check_grads(spec, net.get_variables('grad'), G, set())
 
 

@@ -84,11 +84,12 @@ def test_lstm_loss_backward_parity(depth, A, R, act, B):
     net.loss_backward(obs_d, B, v, pi, rep, d(a_idx), d(r_idx), d(y), d(adv), loss_terms=terms)
     torch.cuda.synchronize()
     spec = nets.arch_spec('LSTM', depth, A, R)
-    import parity_util  # max-pool windows routed as the device did (argmax checked away from near-ties)
+    import parity_util  # the device's branches at the discontinuities (checked away from near-ties)
     P = net.get_variables()
     frames = obs.reshape((-1,) + obs.shape[2:])
-    routes, _ = parity_util.device_routes(spec, P, frames, net.pool_argmax(net.workspace(B), 2, B), act)
-    loss, G, aux = nets.loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, 0.02, act=act, alpha=0.1, routes=routes)
+    br = parity_util.device_branches(spec, P, frames, net.forward_branches(net.workspace(B), 2, B), act)
+    loss, G, aux = nets.loss_and_grads(spec, P, obs, a_idx, r_idx, y, adv, 0.02, act=act, alpha=0.1,
+                                       routes=br['routes'], branches=br['branches'], hbranch=br['hbranch'])
     got = net.get_variables('grad')
     parity_util.check_grads(spec, got, G, set())
     np.testing.assert_allclose(terms.cpu().numpy(), aux['terms'], rtol=1e-4, atol=1e-5)
@@ -187,12 +188,14 @@ def test_lstm_frame_store_parity(E, T, depth):
                              loss_terms=terms)
     torch.cuda.synchronize()
     wt = win[:N]
-    import parity_util  # routes of the distinct frames, gathered per window position
-    dev = net.pool_argmax(net.lstm_workspace(E, T), 1, E, T)
-    routes, _ = parity_util.device_routes(spec, P, fstore, dev, act)
-    rows = np.concatenate([_window_rows_store(nz[t], t, E) for t in range(T)]).reshape(-1)
+    import parity_util  # the distinct frames' branches, gathered per window position
+    rows = np.concatenate([_window_rows_store(nz[t], t, E) for t in range(T)])
+    br = parity_util.device_branches(spec, P, fstore, net.forward_branches(net.lstm_workspace(E, T), 1, E, T), act,
+                                     win=rows)
     _, G, aux = nets.loss_and_grads(spec, P, wt, a_idx, r_idx, y, adv, 0.02, act=act, alpha=0.1,
-                                    routes={k: v[rows] for k, v in routes.items()})
+                                    routes={k: v[rows.reshape(-1)] for k, v in br['routes'].items()},
+                                    branches={k: v[rows.reshape(-1)] for k, v in br['branches'].items()},
+                                    hbranch=br['hbranch'])
     got = net.get_variables('grad')
     parity_util.check_grads(spec, got, G, set())
     np.testing.assert_allclose(terms.cpu().numpy(), aux['terms'], rtol=1e-4, atol=1e-5)

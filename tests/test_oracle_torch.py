@@ -147,3 +147,42 @@ def test_chunked_frames_oracle_equals_loss_and_grads(arch, depth):
     np.testing.assert_allclose(aux1['terms'], aux0['terms'], rtol=1e-12)
     for k in G0:
         np.testing.assert_allclose(G1[k], G0[k], rtol=1e-9, atol=1e-14, err_msg=k)
+
+
+@pytest.mark.parametrize('arch', ['PWYX', 'NIPS'])
+def test_oracle_follows_supplied_branches(arch):
+    """nets.loss_and_grads with routes / branches / hbranch equal to the oracle's own decisions (a
+    'device' whose stored outputs are the oracle's, through tests/parity_util.device_branches) gives
+    the default gradient exactly; flipping one ReLU branch of the last conv changes it."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import parity_util
+    spec = nets.arch_spec(arch, 1, 4, 3)
+    P = nets.init_params(spec, 2)
+    rs = np.random.RandomState(3)
+    B = 3
+    obs = rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)
+    a, r = rs.randint(0, 4, B), rs.randint(0, 3, B)
+    y, adv = rs.randn(B), rs.randn(B)
+    flat, layers = nets.trunk_forward(spec, P, obs)
+    dev = {}
+    for L in layers:
+        if L['pool']:
+            dev[L['name']] = (L['yp'].astype(np.float32), nets.pool_route(L['y'])[0])
+        else:
+            dev[L['name']] = (L['y'].astype(np.float32), None)
+    _, _, _, cache = nets.heads_forward(spec, P, flat)
+    dev['H'] = cache['h'].astype(np.float32)
+    br = parity_util.device_branches(spec, P, obs, dev)
+    _, G0, _ = nets.loss_and_grads(spec, P, obs, a, r, y, adv, 0.02)
+    _, G1, _ = nets.loss_and_grads(spec, P, obs, a, r, y, adv, 0.02, routes=br['routes'], branches=br['branches'],
+                                   hbranch=br['hbranch'])
+    for k in G0:
+        np.testing.assert_array_equal(G1[k], G0[k], err_msg=k)
+    last = layers[-1]['name']
+    flip = {k: v.copy() for k, v in br['branches'].items()}
+    idx = np.argwhere(flip[last])[0]
+    flip[last][tuple(idx)] = False
+    _, G2, _ = nets.loss_and_grads(spec, P, obs, a, r, y, adv, 0.02, routes=br['routes'], branches=flip,
+                                   hbranch=br['hbranch'])
+    assert not np.array_equal(G2['Network/%s/%s_weights' % (last, last)], G0['Network/%s/%s_weights' % (last, last)])

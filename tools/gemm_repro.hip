@@ -1,24 +1,24 @@
 // Standalone reproducer for the GEMM core's conv weight-gradient product: the RGB
 // NIPS conv1 dW of tests/test_kernels_gpu.py::test_loss_backward_parity[5-NIPS-3-4-11] —
 // A = the transposed im2col of uint8 frames [5][84][84][12] (LdIm2colT), B = dY [2000][16]
-// (column-major loader), M = 768 weight rows, N = 16 channels, K = 2000 pixels in 8 splits of 256
-// (the last split 208 = 3 full BK chunks + one 16-deep partial chunk) — run with two B loaders:
-//   old: the round-2 guarded fetch (a k < ke branch around the f32x4 load, zeros merged into the
-//        register quad when it is not taken)
-//   new: gemm.h's LdColMajor (clamped k, one load, zero by select)
-// and compared per output channel against a double-precision host product. Build once per
-// accumulator mode and run both:
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMT_GEMM_DUAL=1 tools/gemm_repro.hip -o /tmp/repro1
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMT_GEMM_DUAL=0 tools/gemm_repro.hip -o /tmp/repro0
-// Prints the max relative error of every (loader, channel) and exits 1 if any exceeds 1e-5.
+// (column-major loader), M = 768 weight rows, N = 16 channels, K = 2000 pixels — launched six ways
+// (launch_variant: plain kernel with 8 or 32 K splits, grouped launches with the product's
+// companion jobs, the round-2 B loader) and compared per output channel against a double-precision
+// host product. Build once per accumulator mode and run both:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMT_GEMM_DUAL=1 tools/gemm_repro.hip -o tools/bin/gemm_repro1
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMT_GEMM_DUAL=0 tools/gemm_repro.hip -o tools/bin/gemm_repro0
+// Prints every channel whose relative L2 error exceeds 1e-5 and exits 1 if any does.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 
 #include "../manette_amd/csrc/gemm.h"
+#include "../manette_amd/csrc/jobs.h"
 
 namespace mt {
+bool g_win_on = false;
+int g_win_first = 0, g_win_count = -1, g_win_index = 0;
 void set_error(const char *fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -55,7 +55,8 @@ struct LdColMajorOld : LdColMajor {
 
 using G = ConvGeom<12, 16, 8, 4, 84, 84, false>;
 using T = Tile<64, 16, 4, 1, 64>;
-constexpr int B = 5, M = G::KK, N = G::COUT, K = B * G::OH * G::OW, SPLITS = 8;
+constexpr int B = 5, M = G::KK, N = G::COUT, K = B * G::OH * G::OW;
+constexpr int SMAX = 32;
 
 #define CK(x)                                                             \
   do {                                                                    \
@@ -66,19 +67,27 @@ constexpr int B = 5, M = G::KK, N = G::COUT, K = B * G::OH * G::OW, SPLITS = 8;
     }                                                                     \
   } while (0)
 
+// variant v: 0 = gemm_f32_kernel, 8 splits (a 256-pixel split = 4 chunks); 1 = gemm_f32_kernel,
+// 32 splits (one 64-pixel chunk per split, the last one partial: the product's split rule at
+// B = 5); 2 = the same as a grouped launch of the GemmJob alone; 3 = with the bias-row job
+// (PairJob, net.hip's conv_wgrad_jobs); 4 = PairJob + the slab-sum job of a pending layer in one
+// grid (the product's conv1 launch); 5 = as 4 with the round-2 B loader.
 template <class LB>
-static std::vector<float> run(const uint8_t *dX, const float *dY, float *dP) {
-  CK(hipMemset(dP, 0, sizeof(float) * SPLITS * M * N));
+static int launch_variant(int v, const uint8_t *dX, const float *dY, float *dP, float *dBias, float *gsum) {
   LdIm2colT<G, true> la{dX};
   LB lb;
   lb.X = dY;
   lb.ld = N;
   lb.ones_row = -1;
-  if (launch_gemm<T>(la, lb, EpSlab{dP, M, N}, M, N, K, SPLITS, nullptr) != MT_OK) exit(3);
-  CK(hipDeviceSynchronize());
-  std::vector<float> P((size_t)SPLITS * M * N);
-  CK(hipMemcpy(P.data(), dP, sizeof(float) * P.size(), hipMemcpyDeviceToHost));
-  return P;
+  const int splits = v == 0 ? 8 : SMAX;
+  if (v <= 1) return launch_gemm<T>(la, lb, EpSlab{dP, M + 1, N}, M, N, K, splits, nullptr);
+  const auto g = gemm_job<T>(la, lb, EpSlab{dP, M + 1, N}, M, N, K, splits);
+  if (v == 2) return launch_group(nullptr, g);
+  const BiasRowJob<G::COUT> bias{dY, dP + (size_t)M * N, (size_t)(M + 1) * N, K, g.kchunk, g.gz};
+  if (v == 3) return launch_group(nullptr, PairJob<decltype(g), BiasRowJob<G::COUT>>{g, bias});
+  (void)dBias;
+  return launch_group(nullptr, PairJob<decltype(g), BiasRowJob<G::COUT>>{g, bias},
+                      SlabJob{dP, 4, (size_t)(M + 1) * N, gsum});  // (sums 4 of the slabs: traffic only)
 }
 
 int main() {
@@ -92,49 +101,59 @@ int main() {
   };
   for (auto &x : X) x = (uint8_t)rnd();
   for (auto &y : dY) y = ((int)(rnd() % 2001) - 1000) * 1e-3f;
-  // reference: slab z, row kr = (ky, kx, ci), channel n = sum over pixels m of split z
-  const int kchunk = cdiv(cdiv(K, T::BK), SPLITS) * T::BK;
-  std::vector<double> ref((size_t)SPLITS * M * N, 0.0);
-  for (int m = 0; m < K; ++m) {
-    const int z = m / kchunk, b = m / (G::OH * G::OW), rem = m % (G::OH * G::OW);
-    const int oy = rem / G::OW, ox = rem % G::OW;
-    for (int kr = 0; kr < M; ++kr) {
-      const int ky = kr / (G::KW * G::CIN), kx = (kr / G::CIN) % G::KW, ci = kr % G::CIN;
-      const double a = X[(((size_t)b * G::H + oy * G::S + ky) * G::W + ox * G::S + kx) * G::CIN + ci] / 255.0;
-      for (int n = 0; n < N; ++n) ref[((size_t)z * M + kr) * N + n] += a * dY[(size_t)m * N + n];
-    }
-  }
   uint8_t *dX;
-  float *ddY, *dP;
+  float *ddY, *dP, *dB, *dG;
+  const size_t slab = (size_t)(M + 1) * N;
   CK(hipMalloc(&dX, X.size()));
   CK(hipMalloc(&ddY, sizeof(float) * dY.size()));
-  CK(hipMalloc(&dP, sizeof(float) * SPLITS * M * N));
+  CK(hipMalloc(&dP, sizeof(float) * SMAX * slab));
+  CK(hipMalloc(&dB, sizeof(float) * N));
+  CK(hipMalloc(&dG, sizeof(float) * slab));
   CK(hipMemcpy(dX, X.data(), X.size(), hipMemcpyHostToDevice));
   CK(hipMemcpy(ddY, dY.data(), sizeof(float) * dY.size(), hipMemcpyHostToDevice));
   int bad = 0;
-  const char *names[2] = {"old", "new"};
-  for (int v = 0; v < 2; ++v) {
-    const std::vector<float> P = v == 0 ? run<LdColMajorOld>(dX, ddY, dP) : run<LdColMajor>(dX, ddY, dP);
-    printf("MT_GEMM_DUAL=%d loader=%s:", MT_GEMM_DUAL, names[v]);
+  for (int v = 0; v <= 5; ++v) {
+    const int splits = v == 0 ? 8 : SMAX;
+    const int kchunk = cdiv(cdiv(K, T::BK), splits) * T::BK;
+    const int S = cdiv(K, kchunk);
+    // reference: slab z, row kr = (ky, kx, ci), channel n = sum over the pixels m of split z
+    std::vector<double> ref((size_t)S * slab, 0.0);
+    for (int m = 0; m < K; ++m) {
+      const int z = m / kchunk, b = m / (G::OH * G::OW), rem = m % (G::OH * G::OW);
+      const int oy = rem / G::OW, ox = rem % G::OW;
+      for (int kr = 0; kr < M; ++kr) {
+        const int ky = kr / (G::KW * G::CIN), kx = (kr / G::CIN) % G::KW, ci = kr % G::CIN;
+        const double a = X[(((size_t)b * G::H + oy * G::S + ky) * G::W + ox * G::S + kx) * G::CIN + ci] / 255.0;
+        for (int n = 0; n < N; ++n) ref[((size_t)z * (M + 1) + kr) * N + n] += a * dY[(size_t)m * N + n];
+      }
+    }
+    CK(hipMemset(dP, 0, sizeof(float) * SMAX * slab));
+    if ((v == 5 ? launch_variant<LdColMajorOld>(v, dX, ddY, dP, dB, dG) : launch_variant<LdColMajor>(v, dX, ddY, dP, dB, dG)) != MT_OK)
+      return 3;
+    CK(hipDeviceSynchronize());
+    std::vector<float> P((size_t)S * slab);
+    CK(hipMemcpy(P.data(), dP, sizeof(float) * P.size(), hipMemcpyDeviceToHost));
+    printf("MT_GEMM_DUAL=%d variant %d (%d splits):", MT_GEMM_DUAL, v, S);
+    int vbad = 0;
     for (int n = 0; n < N; ++n) {
-      double num = 0, den = 0, last = 0;  // whole channel; and the last split alone
-      for (int z = 0; z < SPLITS; ++z)
+      double num = 0, den = 0, last = 0;
+      for (int z = 0; z < S; ++z)
         for (int kr = 0; kr < M; ++kr) {
-          const size_t i = ((size_t)z * M + kr) * N + n;
+          const size_t i = ((size_t)z * (M + 1) + kr) * N + n;
           const double d = P[i] - ref[i];
           num += d * d;
           den += ref[i] * ref[i];
-          if (z == SPLITS - 1) last = std::fmax(last, std::fabs(d));
+          if (z == S - 1) last = std::fmax(last, std::fabs(d));
         }
       const double rel = std::sqrt(num / den);
-      printf(" c%d=%.1e", n, rel);
       if (rel > 1e-5) {
-        ++bad;
-        printf("(!last-split max abs %.2e)", last);
+        ++vbad;
+        printf(" c%d=%.1e(last split max abs %.1e)", n, rel, last);
       }
     }
-    printf("\n");
+    printf(vbad ? "\n" : " all 16 channels within 1e-5\n");
+    bad += vbad;
   }
-  printf("%s\n", bad ? "MISMATCH" : "all channels within 1e-5");
+  printf("%s\n", bad ? "MISMATCH" : "all variants match");
   return bad ? 1 : 0;
 }
