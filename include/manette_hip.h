@@ -83,7 +83,8 @@ int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes);
  * pooled map [rows][OH/2][OW/2][COUT]), whose sign is the ReLU branch; kind 1: a pooled layer's 2x2
  * max-pool argmax bytes ([rows][OH/2][OW/2][COUT] uint8, the window position 0..3 of the first
  * maximum in (row, col) order that the backward routes the gradient to, TF MaxPoolGrad); kind 2:
- * the dense layer's output H ([rows][F] fp32). Byte offset and size. layout 0 = the workspace of
+ * the dense layer's output H ([rows][F] fp32); kind 3: the gradient of conv layer `layer`'s output
+ * after a backward ([rows][OH][OW][COUT] fp32, full resolution). Byte offset and size. layout 0 = the workspace of
  * mt_forward / mt_forward_rows on a = batch rows; layout 1 = the LSTM frame-store workspace of
  * (E = a, T = b), conv rows = fstore rows, H rows = the (T+1)E windows; layout 2 = the LSTM
  * mt_forward workspace of a windows, conv rows = window frames (window-major, 5 per window). */

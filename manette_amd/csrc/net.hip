@@ -1329,7 +1329,8 @@ extern "C" int mt_net_backward_bucket_launches(const mt_net *net, int *launches)
 
 // Byte range of a stored forward value in a workspace (diagnostics / parity; mt_net_workspace_region):
 // kind 0 = conv layer `layer`'s stored output (post-activation; the pooled map of a pooled layer),
-// kind 1 = a pooled layer's argmax bytes, kind 2 = the dense layer's post-activation output H.
+// kind 1 = a pooled layer's argmax bytes, kind 2 = the dense layer's post-activation output H,
+// kind 3 = the conv output's gradient (the backward's dY of the layer's weight gradient).
 template <class Ar, int I = 0>
 static int ws_region(const WsLayout &L, int kind, int layer, size_t rows, size_t *offset, size_t *bytes) {
   if (kind == 2) {
@@ -1350,6 +1351,11 @@ static int ws_region(const WsLayout &L, int kind, int layer, size_t rows, size_t
     if (kind == 1 && P) {
       *offset = L.parg[I] * sizeof(float);
       *bytes = rows * px * G::COUT;
+      return MT_OK;
+    }
+    if (kind == 3) {  // the gradient of the conv output (full resolution; written by the backward)
+      *offset = L.dact[I] * sizeof(float);
+      *bytes = rows * G::OH * G::OW * G::COUT * sizeof(float);
       return MT_OK;
     }
     set_error("conv layer %d has no region of kind %d", layer, kind);
@@ -1374,7 +1380,7 @@ static int ws_region_frames(const mt_net *net, int E, int T, int kind, int layer
 extern "C" int mt_net_workspace_region(const mt_net *net, int layout, int a, int b, int kind, int layer,
                                        size_t *offset, size_t *bytes) {
   MT_CHECK_ARG(net && offset && bytes, "null argument");
-  MT_CHECK_ARG(a >= 1 && (layout != 1 || b >= 1) && kind >= 0 && kind <= 2, "bad sizes or kind");
+  MT_CHECK_ARG(a >= 1 && (layout != 1 || b >= 1) && kind >= 0 && kind <= 3, "bad sizes or kind");
   MT_ARCH_SWITCH(net, {
     if (layout == 0) {
       if constexpr (Ar::LSTM) {

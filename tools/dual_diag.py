@@ -26,6 +26,21 @@ got = net.get_variables('grad')['Network/conv1/conv1_weights']
 spec = nets.arch_spec('NIPS', depth, A, R)
 _, G, _ = nets.loss_and_grads(spec, net.get_variables(), obs, a_idx, r_idx, y, adv, 0.02)
 ref = G['Network/conv1/conv1_weights']
+# the product's inputs to the conv1 weight gradient, for tools/gemm_repro.hip (argv: <X.u8> <dY.f32>):
+# obs [5][84][84][12] uint8 and the device's dY = conv1's output gradient [5][20][20][16] fp32
+import ctypes as C
+from manette_amd import _lib
+off, n = C.c_size_t(), C.c_size_t()
+ws = net.workspace(B)
+_lib.check(_lib.hip().mt_net_workspace_region(net._h, 0, B, 0, 3, 0, C.byref(off), C.byref(n)))
+dY = ws.cpu().numpy()[off.value:off.value + n.value].view(np.float32)
+obs.tofile(sys.argv[1] + '.X.u8')
+dY.tofile(sys.argv[1] + '.dY.f32')
+print('dY: %d values, %d exact zeros, %d subnormal, channel 10: %d zeros %d subnormal, |max| %.3e' % (
+    dY.size, (dY == 0).sum(), ((dY != 0) & (np.abs(dY) < np.finfo(np.float32).tiny)).sum(),
+    (dY.reshape(-1, 16)[:, 10] == 0).sum(), ((dY.reshape(-1, 16)[:, 10] != 0) &
+                                              (np.abs(dY.reshape(-1, 16)[:, 10]) < np.finfo(np.float32).tiny)).sum(),
+    np.abs(dY).max()))
 np.savez(sys.argv[1], got=got, ref=ref)
 d = np.linalg.norm((got - ref).reshape(-1, 16), axis=0) / np.linalg.norm(ref.reshape(-1, 16), axis=0)
 print(os.environ.get('MANETTE_HIP_LIB', 'product library'), 'per-channel rel L2:', ' '.join('%.1e' % x for x in d))

@@ -4,13 +4,15 @@
 // (column-major loader), M = 768 weight rows, N = 16 channels, K = 2000 pixels — launched six ways
 // (launch_variant: plain kernel with 8 or 32 K splits, grouped launches with the product's
 // companion jobs, the round-2 B loader) and compared per output channel against a double-precision
-// host product. Build once per accumulator mode and run both:
+// host product, on seeded random inputs or (argv[1] = a prefix written by tools/dual_diag.py) the
+// product's own frames and conv1 output gradient. Build once per accumulator mode and run both:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMT_GEMM_DUAL=1 tools/gemm_repro.hip -o tools/bin/gemm_repro1
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMT_GEMM_DUAL=0 tools/gemm_repro.hip -o tools/bin/gemm_repro0
 // Prints every channel whose relative L2 error exceeds 1e-5 and exits 1 if any does.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../manette_amd/csrc/gemm.h"
@@ -85,12 +87,15 @@ static int launch_variant(int v, const uint8_t *dX, const float *dY, float *dP, 
   if (v == 2) return launch_group(nullptr, g);
   const BiasRowJob<G::COUT> bias{dY, dP + (size_t)M * N, (size_t)(M + 1) * N, K, g.kchunk, g.gz};
   if (v == 3) return launch_group(nullptr, PairJob<decltype(g), BiasRowJob<G::COUT>>{g, bias});
-  (void)dBias;
+  if (v <= 5)
+    return launch_group(nullptr, PairJob<decltype(g), BiasRowJob<G::COUT>>{g, bias},
+                        SlabJob{dP, 4, (size_t)(M + 1) * N, gsum});  // (sums 4 of the slabs: traffic only)
+  // 6: the product's exact launch: pending = the slab sum of another region, and the unused extra job
   return launch_group(nullptr, PairJob<decltype(g), BiasRowJob<G::COUT>>{g, bias},
-                      SlabJob{dP, 4, (size_t)(M + 1) * N, gsum});  // (sums 4 of the slabs: traffic only)
+                      SlabJob{dBias, 1, (size_t)N, gsum}, NoJob{});
 }
 
-int main() {
+int main(int argc, char **argv) {
   static_assert(K == 2000, "the failing test's shape");
   std::vector<uint8_t> X((size_t)B * G::H * G::W * G::CIN);
   std::vector<float> dY((size_t)K * N);
@@ -101,6 +106,18 @@ int main() {
   };
   for (auto &x : X) x = (uint8_t)rnd();
   for (auto &y : dY) y = ((int)(rnd() % 2001) - 1000) * 1e-3f;
+  if (argc > 1) {  // the product's own inputs, dumped by tools/dual_diag.py <prefix>
+    std::string p = argv[1];
+    FILE *fx = fopen((p + ".X.u8").c_str(), "rb"), *fy = fopen((p + ".dY.f32").c_str(), "rb");
+    if (!fx || !fy || fread(X.data(), 1, X.size(), fx) != X.size() ||
+        fread(dY.data(), sizeof(float), dY.size(), fy) != dY.size()) {
+      fprintf(stderr, "cannot read %s.X.u8 / .dY.f32\n", argv[1]);
+      return 4;
+    }
+    fclose(fx);
+    fclose(fy);
+    printf("inputs: %s\n", argv[1]);
+  }
   uint8_t *dX;
   float *ddY, *dP, *dB, *dG;
   const size_t slab = (size_t)(M + 1) * N;
@@ -112,7 +129,7 @@ int main() {
   CK(hipMemcpy(dX, X.data(), X.size(), hipMemcpyHostToDevice));
   CK(hipMemcpy(ddY, dY.data(), sizeof(float) * dY.size(), hipMemcpyHostToDevice));
   int bad = 0;
-  for (int v = 0; v <= 5; ++v) {
+  for (int v = 0; v <= 6; ++v) {
     const int splits = v == 0 ? 8 : SMAX;
     const int kchunk = cdiv(cdiv(K, T::BK), splits) * T::BK;
     const int S = cdiv(K, kchunk);

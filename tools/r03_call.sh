@@ -18,7 +18,9 @@ for step in ${STEPS:-tests bench}; do
   case $step in
     repro) run repro1 60 tools/bin/gemm_repro1; run repro0 60 tools/bin/gemm_repro0 ;;
     diag) MANETTE_HIP_LIB=$PWD/manette_amd/libmanette_hip_dual.so run diag_dual 180 python tools/dual_diag.py "$OUT/diag_dual.npz"
-          run diag_product 180 python tools/dual_diag.py "$OUT/diag_product.npz" ;;
+          run diag_product 180 python tools/dual_diag.py "$OUT/diag_product.npz"
+          run repro1_real 60 tools/bin/gemm_repro1 "$OUT/diag_dual.npz"
+          run repro0_real 60 tools/bin/gemm_repro0 "$OUT/diag_dual.npz" ;;
     ab) for v in ${VARIANTS:-base dual}; do  # bench of libmanette_hip_<v>.so beside the product, alternating
           MANETTE_HIP_LIB=$PWD/manette_amd/libmanette_hip_$v.so run "ab_$v" 300 python bench.py --no_cpu_baseline --trunk_sweep '' --steps 20 --warmup 5 --config ${AB_CONFIG:-pong-nips}
           run "ab_product_$v" 300 python bench.py --no_cpu_baseline --trunk_sweep '' --steps 20 --warmup 5 --config ${AB_CONFIG:-pong-nips}
