@@ -118,7 +118,13 @@ def train_pass_flops(layers, N, frame_rows=None):
     return frame_rows * (2 * per_frame - layers[0][1]) + N * 2 * per_win
 
 
-def graph_time(fn, inner, reps=5):
+# CLOCK_BOOTTIME windows (ns) of each labelled graph_time measurement's timed replays: the clock of
+# rocprofv3's dispatch timestamps, so tools/rocpd_summary.py can restrict a profile of this same
+# command to the dispatches a bench number was computed from ("profile_windows" in the JSON line)
+PROFILE_WINDOWS = {}
+
+
+def graph_time(fn, inner, reps=5, label=None):
     """Device time per call of fn (which launches on torch's current stream): `inner` calls are
     captured as ONE hipGraph on a side stream, replayed once to warm up and then `reps` times, each
     replay between a HIP event pair on that stream. The kernels run back to back with no host
@@ -145,6 +151,8 @@ def graph_time(fn, inner, reps=5):
         _lib.check(rc, 'mt_graph_end')
         try:
             _lib.check(lib.mt_graph_launch(g, sp), 'mt_graph_launch')
+            side.synchronize()  # (the warm-up replay stays outside the labelled window)
+            t0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
             evs = []
             for _ in range(reps):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -153,6 +161,8 @@ def graph_time(fn, inner, reps=5):
                 b.record(side)
                 evs.append((a, b))
             side.synchronize()
+            if label:
+                PROFILE_WINDOWS[label] = [t0, time.clock_gettime_ns(time.CLOCK_BOOTTIME), inner * reps]
             out = [a.elapsed_time(b) * 1e3 / inner for a, b in evs]
         finally:
             lib.mt_graph_destroy(g)
@@ -180,7 +190,7 @@ def launch_breakdown(fn, inner=20, reps=3):
     prev, out = 0.0, []
     for k in range(1, L + 1):
         try:
-            t = float(np.median(graph_time(lambda: (lib.mt_launch_window(0, k), fn()), inner, reps)))
+            t = float(np.median(graph_time(lambda: (lib.mt_launch_window(0, k), fn()), inner, reps, label=f'train_launches_{k}')))
         finally:
             lib.mt_launch_window(-1, -1)
         out.append(t - prev)
@@ -410,11 +420,11 @@ def main():
     stacking = getattr(learner, 'slot0_in_rollout', False)
     # the update's train pass (fused returns + loss + backward of the last rollout)
     bwd = learner.train_backward if learner.lstm_bool else learner._update_backward
-    prof['train_pass'] = graph_time(bwd, 20)
+    prof['train_pass'] = graph_time(bwd, 20, label='train_pass')
     # (the LSTM backward has launches outside the budgeted grouped launches: no breakdown)
     prof['train_launches'] = None if learner.lstm_bool else launch_breakdown(bwd)[0]
     # A11: clip + RMSProp alone (the norm partials the backward left; world > 1 adds mt_grad_sumsq)
-    prof['clip_rmsprop'] = graph_time(lambda: net.apply_gradients(partials_ready=True), 40)
+    prof['clip_rmsprop'] = graph_time(lambda: net.apply_gradients(partials_ready=True), 40, label='clip_rmsprop')
     gen = torch.Generator(device='cuda').manual_seed(11)
     pushes = torch.randint(0, 256, (4 * E, 84, 84, depth_), dtype=torch.uint8, device='cuda', generator=gen)
     counts = torch.ones(E, dtype=torch.int32) if cfg['max_repetition'] == 0 else \
@@ -426,7 +436,7 @@ def main():
     cnt_d = counts.to('cuda')
     from manette_amd import network as devnet_
     prof['stack'] = graph_time(lambda: devnet_.preprocess(pushes, offs, cnt_d, E, depth_, None, None, learner.states[0],
-                                                          stk_out, resized=True), 40)
+                                                          stk_out, resized=True), 40, label='stack')
     if learner.lstm_bool:  # a step's new frames (trunk + cell x-product), + its E windows
         roll_fwd = lambda: learner._lstm_forward(1, learner.v_boot)
         roll_trunk = lambda: net.lstm_frames_forward(learner.fstore, 1 + 5 * E, E, E, T)
@@ -445,10 +455,10 @@ def main():
                                                             ws_key='rollout')
         else:
             roll_trunk = plain_trunk
-    prof['rollout_forward'] = graph_time(roll_fwd, 20)
-    prof['rollout_trunk'] = graph_time(roll_trunk, 40)
+    prof['rollout_forward'] = graph_time(roll_fwd, 20, label='rollout_forward')
+    prof['rollout_trunk'] = graph_time(roll_trunk, 40, label='roofline')
     if stacking:
-        prof['plain_trunk'] = graph_time(plain_trunk, 40)
+        prof['plain_trunk'] = graph_time(plain_trunk, 40, label='plain_trunk')
     # the eager form (40 Python calls back to back between one event pair, BENCH_r02's method):
     # bounded by the host's launch rate when the box is loaded, kept to show the difference
     for _ in range(3):
@@ -680,6 +690,8 @@ def main():
                                     'note': 'network work only (no emulators, no host loop): GPU = (T+1) isolated '
                                             'rollout forwards + the train pass; CPU = the port\'s torch-CPU forwards '
                                             '+ train step inside the cpu_baseline sample'}
+        if PROFILE_WINDOWS:  # [boottime start ns, end ns, calls] of each labelled graph measurement
+            line['profile_windows'] = dict(PROFILE_WINDOWS)
         print(json.dumps(line), flush=True)
     if learner is not None:
         learner.cleanup()

@@ -12,6 +12,7 @@
 
 #include "gemm.h"
 #include "jobs.h"
+#include "nips_bwd.h"
 #include "trunk_fused.h"
 
 namespace mt {
@@ -58,6 +59,17 @@ struct PwyxArch {  // networks.py:206-225: SAME convs, 2x2 pools after conv1-3
 
 template <class Ar, int I>
 using LayerG = std::tuple_element_t<I, typename Ar::Layers>;
+
+// The NIPS gray trunk's conv backward as one launch of per-image workgroups (nips_bwd.h) instead of
+// the layered trunk_backward (experiment builds: MT_NIPS_FUSED_BWD=0 for the layered path).
+#ifndef MT_NIPS_FUSED_BWD
+#define MT_NIPS_FUSED_BWD 1
+#endif
+template <class Ar>
+constexpr bool nips_fused_bwd() {
+  if constexpr (Ar::LSTM || Ar::NCONV != 2 || Ar::FUSED_SLABS == 0) return false;
+  else return MT_NIPS_FUSED_BWD && LayerG<Ar, 0>::CIN == 4;
+}
 template <class Ar, int I>
 constexpr bool pooled() {
   return (Ar::POOL >> I) & 1u;
@@ -314,6 +326,7 @@ static WsLayout ws_layout(const mt_net *n, int B) {
   };
   size_t wslab = 0;
   ws_layers<Ar>(L, off, B, wslab);
+  if constexpr (nips_fused_bwd<Ar>()) wslab = std::max(wslab, (size_t)B * NipsConvBwdJob::SLAB2);  // per-image slabs
   L.fc_splits = fc_splits<Ar>(B, Ar::F);
   L.fcslab = take((size_t)std::max(L.fc_splits, Ar::FUSED_SLABS) * B * Ar::F);
   L.H = take((size_t)B * Ar::F);
@@ -1021,6 +1034,31 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
   }
 }
 
+// NIPS gray conv backward (nips_bwd.h): the per-image job, then the image-order slab sums of both
+// layers (conv1's in region wslab, conv2's in wslab2) with the global-norm partials of the whole
+// gradient when asked (the rest of the gradient, complete since the dense launch, beside them).
+template <class Ar>
+static int nips_conv_backward(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
+                              const WsLayout &L, float *grad, hipStream_t s, const NormOut &no) {
+  using J = NipsConvBwdJob;
+  static_assert(LayerG<Ar, 0>::KK + 1 == 257 && LayerG<Ar, 1>::KK + 1 == 257, "slab rows");
+  float *slab1 = ws + L.wslab, *slab2 = ws + L.wslab2;
+  MT_TRY(launch_group(s, J{obs, ws + L.act[0], ws + L.dact[1], P + n->off_conv[1], ws + L.dact[0], slab1, slab2, B,
+                           n->cfg.activation, n->cfg.alpha_leaky}));
+  SlabJob s1{slab1, B, (size_t)J::SLAB1, grad + n->off_conv[0]};
+  SlabJob s2{slab2, B, (size_t)J::SLAB2, grad + n->off_conv[1]};
+  if (!no.partials) return launch_group(s, s1, s2);
+  s1.sq = no.partials;
+  s2.sq = no.partials + s1.blocks();
+  const int used = s1.blocks() + s2.blocks();
+  static_assert(MT_NORM_PARTIALS >= 2 * ((257 * 16 / 4 + kSlabCols - 1) / kSlabCols + (257 * 32 / 4 + kSlabCols - 1) / kSlabCols),
+                "norm partials");
+  // (the alignment padding between the two regions is zero in both the gradient and the skip)
+  return launch_group(s, s1, s2,
+                      SumsqJob{grad, no.n, n->off_conv[0], n->off_conv[1] + s2.n, no.partials + used,
+                               MT_NORM_PARTIALS - used});
+}
+
 // Per-row conv buffers of a layout moved to start at row `row0` (the dense/head buffers stay).
 template <class Ar, int I = 0>
 static void shift_rows(WsLayout &L, size_t row0) {
@@ -1208,6 +1246,7 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
   return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s, SlabJob{}, no, dw);
 #else
   MT_TRY(launch_group(s, dx, dw, hw));
+  if constexpr (nips_fused_bwd<Ar>()) return nips_conv_backward<Ar>(n, P, obs, B, ws, L, grad, s, no);
   return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s, SlabJob{}, no);
 #endif
 }

@@ -60,6 +60,29 @@ using T = Tile<64, 16, 4, 1, 64>;
 constexpr int B = 5, M = G::KK, N = G::COUT, K = B * G::OH * G::OW;
 constexpr int SMAX = 32;
 
+// State-dependence probes: fill every CU's LDS (dirty_lds) or a wave's VGPRs (dirty_vgpr) with v just
+// before the product launch, so a read of unwritten LDS or an uninitialised register shows up as a
+// channel error that scales with v (the product's conv1 launch follows the conv2 launch, which
+// leaves its own tiles in LDS and registers).
+__global__ __launch_bounds__(256) void dirty_lds(float v, float *sink) {
+  extern __shared__ float sm[];
+  for (int i = threadIdx.x; i < 160 * 1024 / 4; i += 256) sm[i] = v + 1e-3f * (i & 63);
+  __syncthreads();
+  if (sm[(threadIdx.x * 97) & 4095] == 1234.5f) sink[blockIdx.x] = 1.f;  // (keeps the stores)
+}
+__global__ __launch_bounds__(256) void dirty_vgpr(float v, float *sink) {
+  float r[192];
+#pragma unroll
+  for (int i = 0; i < 192; ++i) {
+    r[i] = v + 1e-3f * i;
+    asm volatile("" : "+v"(r[i]));
+  }
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < 192; ++i) t += r[i];
+  if (t == 1234.5f) sink[blockIdx.x] = t;
+}
+
 #define CK(x)                                                             \
   do {                                                                    \
     hipError_t e = (x);                                                   \
@@ -90,7 +113,7 @@ static int launch_variant(int v, const uint8_t *dX, const float *dY, float *dP, 
   if (v <= 5)
     return launch_group(nullptr, PairJob<decltype(g), BiasRowJob<G::COUT>>{g, bias},
                         SlabJob{dP, 4, (size_t)(M + 1) * N, gsum});  // (sums 4 of the slabs: traffic only)
-  // 6: the product's exact launch: pending = the slab sum of another region, and the unused extra job
+  // 6-8: the product's exact launch: pending = the slab sum of another region, and the unused extra job
   return launch_group(nullptr, PairJob<decltype(g), BiasRowJob<G::COUT>>{g, bias},
                       SlabJob{dBias, 1, (size_t)N, gsum}, NoJob{});
 }
@@ -129,7 +152,9 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(dX, X.data(), X.size(), hipMemcpyHostToDevice));
   CK(hipMemcpy(ddY, dY.data(), sizeof(float) * dY.size(), hipMemcpyHostToDevice));
   int bad = 0;
-  for (int v = 0; v <= 6; ++v) {
+  CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&dirty_lds), hipFuncAttributeMaxDynamicSharedMemorySize,
+                         160 * 1024));
+  for (int v = 0; v <= 8; ++v) {
     const int splits = v == 0 ? 8 : SMAX;
     const int kchunk = cdiv(cdiv(K, T::BK), splits) * T::BK;
     const int S = cdiv(K, kchunk);
@@ -145,6 +170,9 @@ int main(int argc, char **argv) {
       }
     }
     CK(hipMemset(dP, 0, sizeof(float) * SMAX * slab));
+    // 7: variant 6 after dirtying the LDS of every CU; 8: after dirtying the VGPRs
+    if (v == 7) hipLaunchKernelGGL(dirty_lds, dim3(4096), dim3(256), 160 * 1024, nullptr, 7.0f, dG);
+    if (v == 8) hipLaunchKernelGGL(dirty_vgpr, dim3(4096), dim3(256), 0, nullptr, 7.0f, dG);
     if ((v == 5 ? launch_variant<LdColMajorOld>(v, dX, ddY, dP, dB, dG) : launch_variant<LdColMajor>(v, dX, ddY, dP, dB, dG)) != MT_OK)
       return 3;
     CK(hipDeviceSynchronize());

@@ -28,6 +28,9 @@ for step in ${STEPS:-tests bench}; do
     bar) run bar 60 tools/bin/bar_probe ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run tests 1200 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread ${TEST_ARGS:-} ;;
+    vtests) for v in ${VARIANTS:-fb}; do  # GPU tests against libmanette_hip_<v>.so (VTK: a -k filter)
+              MANETTE_HIP_LIB=$PWD/manette_amd/libmanette_hip_$v.so run "vtests_$v" 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -k "${VTK:-NIPS or pong}"
+            done ;;
     bench) run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_ARGS:-} ;;
     benchcfg) for c in ${CONFIGS:-}; do run "bench_$c" 600 python bench.py --config "$c" --steps 20 --warmup 5 --no_cpu_baseline; done ;;
     prof) (export TMPDIR=/tmp; run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5) ;;
