@@ -303,6 +303,43 @@ def cpu_baseline(cfg, T, seconds, rank):
                        'processes, torch-CPU fp32 network on %d threads, %.1f s' % (timed, ec, T, cfg['arch'], ew, cores, elapsed))
 
 
+def time_allreduce(learner, world, dist):
+    """Per-rank device time of the RCCL all-reduce of each gradient bucket (paac._bucketed_update) and
+    of the whole gradient, on a scratch copy: barrier, then HIP events around mt_allreduce on the
+    rank's stream, 20 calls each; medians gathered to every rank. Never fails the bench line (a
+    failure is reported in the object)."""
+    import torch
+    try:
+        scratch = learner.network.grad.clone()
+        k = getattr(learner, '_buckets', None)
+        parts = {'whole': scratch}
+        if k:
+            parts['dense+heads (bucket 1)'] = scratch[k:]
+            parts['conv (bucket 2)'] = scratch[:k]
+        mine = {}
+        for name, t in parts.items():
+            for _ in range(3):
+                learner.comm.allreduce(t)
+            xs = []
+            for _ in range(20):
+                dist.barrier()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                learner.comm.allreduce(t)
+                e1.record()
+                e1.synchronize()
+                xs.append(e0.elapsed_time(e1) * 1e3)
+            mine[name] = {'bytes': 4 * t.numel(), 'median_us': round(float(np.median(xs)), 2),
+                          'min_us': round(float(np.min(xs)), 2)}
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        return {'per_rank': every, 'note': 'RCCL in-place sum of the bucket alone (barrier, then HIP events around '
+                                           'mt_allreduce on the rank\'s stream; 20 calls); in the update the buckets '
+                                           'run on a side stream beside the conv backward'}
+    except Exception as e:  # (reported, not raised: the timed value above is already measured)
+        return {'error': repr(e)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -412,6 +449,12 @@ def main():
         allck = [torch.zeros_like(ck) for _ in range(world)]
         dist.all_gather(allck, ck)
         replicas = all(torch.equal(x, allck[0]) for x in allck)
+    # (2b) data parallel: the RCCL all-reduce of each gradient bucket (and of the whole gradient) on
+    #      its own, every rank timing it with HIP events on its stream (in the update the buckets run
+    #      on a side stream beside the conv backward: paac._bucketed_update); per-rank medians
+    allreduce = None
+    if world > 1 and getattr(learner.comm, 'kind', None) == 'rccl':
+        allreduce = time_allreduce(learner, world, dist)
     # (3) kernels in isolation, each as a hipGraph of back-to-back calls replayed 5 times between
     #     HIP event pairs on its stream (graph_time: no host launch gaps); min / median per call
     E = cfg['ec']
@@ -659,6 +702,8 @@ def main():
         }
         if replicas is not None:
             line['replicas_identical'] = replicas
+        if allreduce is not None:
+            line['allreduce'] = allreduce
         if sweep:
             per_env_bytes = 84 * 84 * 4 * depth + 4 * out_floats
             w_bytes = 4 * sum(l[2] for l in trunk)

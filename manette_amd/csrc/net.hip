@@ -12,8 +12,8 @@
 
 #include "gemm.h"
 #include "jobs.h"
-#include "nips_bwd.h"
 #include "trunk_fused.h"
+#include "nips_bwd.h"
 
 namespace mt {
 
@@ -1043,8 +1043,8 @@ static int nips_conv_backward(const mt_net *n, const float *P, const uint8_t *ob
   using J = NipsConvBwdJob;
   static_assert(LayerG<Ar, 0>::KK + 1 == 257 && LayerG<Ar, 1>::KK + 1 == 257, "slab rows");
   float *slab1 = ws + L.wslab, *slab2 = ws + L.wslab2;
-  MT_TRY(launch_group(s, J{obs, ws + L.act[0], ws + L.dact[1], P + n->off_conv[1], ws + L.dact[0], slab1, slab2, B,
-                           n->cfg.activation, n->cfg.alpha_leaky}));
+  MT_TRY(launch_nips_conv_bwd(s, J{obs, ws + L.act[0], ws + L.dact[1], P + n->off_conv[1], ws + L.dact[0], slab1,
+                                   slab2, B, n->cfg.activation, n->cfg.alpha_leaky}));
   SlabJob s1{slab1, B, (size_t)J::SLAB1, grad + n->off_conv[0]};
   SlabJob s2{slab2, B, (size_t)J::SLAB2, grad + n->off_conv[1]};
   if (!no.partials) return launch_group(s, s1, s2);

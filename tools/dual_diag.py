@@ -36,6 +36,13 @@ _lib.check(_lib.hip().mt_net_workspace_region(net._h, 0, B, 0, 3, 0, C.byref(off
 dY = ws.cpu().numpy()[off.value:off.value + n.value].view(np.float32)
 obs.tofile(sys.argv[1] + '.X.u8')
 dY.tofile(sys.argv[1] + '.dY.f32')
+# and the conv2 backward-data product's (tools/dgrad_repro.hip): dY2 = conv2's output gradient
+# [5][9][9][32], W2 [4][4][16][32], act1 = conv1's output [5][20][20][16]
+wsn = ws.cpu().numpy()
+for kind, layer, name in ((3, 1, 'dY2'), (0, 0, 'act1')):
+    _lib.check(_lib.hip().mt_net_workspace_region(net._h, 0, B, 0, kind, layer, C.byref(off), C.byref(n)))
+    wsn[off.value:off.value + n.value].view(np.float32).tofile(sys.argv[1] + '.%s.f32' % name)
+net.get_variables()['Network/conv2/conv2_weights'].astype(np.float32).tofile(sys.argv[1] + '.W2.f32')
 print('dY: %d values, %d exact zeros, %d subnormal, channel 10: %d zeros %d subnormal, |max| %.3e' % (
     dY.size, (dY == 0).sum(), ((dY != 0) & (np.abs(dY) < np.finfo(np.float32).tiny)).sum(),
     (dY.reshape(-1, 16)[:, 10] == 0).sum(), ((dY.reshape(-1, 16)[:, 10] != 0) &

@@ -20,7 +20,10 @@ for step in ${STEPS:-tests bench}; do
     diag) MANETTE_HIP_LIB=$PWD/manette_amd/libmanette_hip_dual.so run diag_dual 180 python tools/dual_diag.py "$OUT/diag_dual.npz"
           run diag_product 180 python tools/dual_diag.py "$OUT/diag_product.npz"
           run repro1_real 60 tools/bin/gemm_repro1 "$OUT/diag_dual.npz"
-          run repro0_real 60 tools/bin/gemm_repro0 "$OUT/diag_dual.npz" ;;
+          run repro0_real 60 tools/bin/gemm_repro0 "$OUT/diag_dual.npz"
+          run dgrad1_real 60 tools/bin/dgrad_repro1 "$OUT/diag_dual.npz"
+          run dgrad0_real 60 tools/bin/dgrad_repro0 "$OUT/diag_dual.npz"
+          run dgrad1 60 tools/bin/dgrad_repro1 ;;
     ab) for v in ${VARIANTS:-base dual}; do  # bench of libmanette_hip_<v>.so beside the product, alternating
           MANETTE_HIP_LIB=$PWD/manette_amd/libmanette_hip_$v.so run "ab_$v" 300 python bench.py --no_cpu_baseline --trunk_sweep '' --steps 20 --warmup 5 --config ${AB_CONFIG:-pong-nips}
           run "ab_product_$v" 300 python bench.py --no_cpu_baseline --trunk_sweep '' --steps 20 --warmup 5 --config ${AB_CONFIG:-pong-nips}
@@ -34,10 +37,15 @@ for step in ${STEPS:-tests bench}; do
     bench) run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_ARGS:-} ;;
     benchcfg) for c in ${CONFIGS:-}; do run "bench_$c" 600 python bench.py --config "$c" --steps 20 --warmup 5 --no_cpu_baseline; done ;;
     prof) (export TMPDIR=/tmp; run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5) ;;
+    proflib) for v in ${VARIANTS:-product}; do for c in ${CONFIGS:-mspacman-lstm-figar}; do  # rocprof of a variant's bench
+               L=$PWD/manette_amd/libmanette_hip_$v.so; [ "$v" = product ] && L=$PWD/manette_amd/libmanette_hip.so
+               (export TMPDIR=/tmp MANETTE_HIP_LIB=$L; run "proflib_${v}_$c" 400 rocprofv3 --kernel-trace --stats -d "$OUT/proflib_${v}_$c" -o run -- python3 bench.py --config "$c" --steps 10 --warmup 3 --no_cpu_baseline --trunk_sweep '')
+             done; done ;;
     pmc) for c in ${PMC_CONFIGS:-breakout-pwyx-figar-rgb}; do
            NAME=pmc_fwd_$c PASSES="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
              run "pmc_fwd_$c" 400 bash tools/pmc_any.sh tools/sweep_only.py --config "$c" --envs 32 --reps 10
          done ;;
+    pbwd) MANETTE_HIP_LIB=$PWD/manette_amd/libmanette_hip_probe.so run probe_bwd 180 python tools/probe_bwd.py ;;
     probe) MANETTE_HIP_LIB=$PWD/manette_amd/libmanette_hip_probe.so run probe 300 python tools/probe.py ${PROBE_ARGS:-} ;;
     sweep) for c in ${SWEEP_CONFIGS:-breakout-pwyx-figar-rgb mspacman-lstm-figar}; do
              (export TMPDIR=/tmp; run "sweep_$c" 300 rocprofv3 --kernel-trace --stats -d "$OUT/sweep_$c" -o run -- python3 tools/sweep_only.py --config "$c" --envs 32 --reps 20)
