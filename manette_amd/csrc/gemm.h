@@ -29,8 +29,8 @@
 #ifndef MT_GEMM_PF2  // two register buffers: global loads two K chunks ahead (gemm_body_t)
 #define MT_GEMM_PF2 0
 #endif
-#ifndef MT_GEMM_DUAL  // two accumulators for one-tile waves (gemm_body_t): experiment builds only —
-#define MT_GEMM_DUAL 0  // the RGB conv1 weight gradient's channel 10 comes out wrong
+#ifndef MT_GEMM_DUAL  // two accumulators for one-tile waves (gemm_body_t); its different summation
+#define MT_GEMM_DUAL 0  // order flips near-zero ReLU decisions, which the oracle follows
 #endif
 
 namespace mt {

@@ -326,7 +326,8 @@ static WsLayout ws_layout(const mt_net *n, int B) {
   };
   size_t wslab = 0;
   ws_layers<Ar>(L, off, B, wslab);
-  if constexpr (nips_fused_bwd<Ar>()) wslab = std::max(wslab, (size_t)B * NipsConvBwdJob::SLAB2);  // per-image slabs
+  if constexpr (nips_fused_bwd<Ar>())  // per-image conv1 slabs (wslab), per-pair conv2 slabs (wslab2)
+    wslab = std::max(wslab, std::max((size_t)B * NipsConvBwdJob::SLAB1, (size_t)((B + 1) / 2) * NipsConvBwdJob::SLAB2));
   L.fc_splits = fc_splits<Ar>(B, Ar::F);
   L.fcslab = take((size_t)std::max(L.fc_splits, Ar::FUSED_SLABS) * B * Ar::F);
   L.H = take((size_t)B * Ar::F);
@@ -1046,7 +1047,7 @@ static int nips_conv_backward(const mt_net *n, const float *P, const uint8_t *ob
   MT_TRY(launch_nips_conv_bwd(s, J{obs, ws + L.act[0], ws + L.dact[1], P + n->off_conv[1], ws + L.dact[0], slab1,
                                    slab2, B, n->cfg.activation, n->cfg.alpha_leaky}));
   SlabJob s1{slab1, B, (size_t)J::SLAB1, grad + n->off_conv[0]};
-  SlabJob s2{slab2, B, (size_t)J::SLAB2, grad + n->off_conv[1]};
+  SlabJob s2{slab2, (B + 1) / 2, (size_t)J::SLAB2, grad + n->off_conv[1]};  // (per image pair)
   if (!no.partials) return launch_group(s, s1, s2);
   s1.sq = no.partials;
   s2.sq = no.partials + s1.blocks();

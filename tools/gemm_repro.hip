@@ -1,11 +1,14 @@
 // Standalone reproducer for the GEMM core's conv weight-gradient product: the RGB
 // NIPS conv1 dW of tests/test_kernels_gpu.py::test_loss_backward_parity[5-NIPS-3-4-11] —
 // A = the transposed im2col of uint8 frames [5][84][84][12] (LdIm2colT), B = dY [2000][16]
-// (column-major loader), M = 768 weight rows, N = 16 channels, K = 2000 pixels — launched six ways
+// (column-major loader), M = 768 weight rows, N = 16 channels, K = 2000 pixels — launched nine ways
 // (launch_variant: plain kernel with 8 or 32 K splits, grouped launches with the product's
 // companion jobs, the round-2 B loader) and compared per output channel against a double-precision
 // host product, on seeded random inputs or (argv[1] = a prefix written by tools/dual_diag.py) the
-// product's own frames and conv1 output gradient. Build once per accumulator mode and run both:
+// product's own frames and conv1 output gradient; variants 7 / 8 run variant 6 after a kernel that
+// leaves garbage in every CU's LDS / a wave's VGPRs. Result: exact in every
+// form — the dual build's conv1 dW difference came from its operand (one ReLU decision of conv1's
+// forward), not from this product. Build once per accumulator mode and run both:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMT_GEMM_DUAL=1 tools/gemm_repro.hip -o tools/bin/gemm_repro1
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMT_GEMM_DUAL=0 tools/gemm_repro.hip -o tools/bin/gemm_repro0
 // Prints every channel whose relative L2 error exceeds 1e-5 and exits 1 if any does.

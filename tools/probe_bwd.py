@@ -17,8 +17,6 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PHASES = ['stage (loads -> LDS)', 'conv2 dX + mask', 'bias rows', 'conv1 dW', 'conv2 dW']
-
 
 def main():
     ap = argparse.ArgumentParser()
@@ -50,16 +48,22 @@ def main():
         net.loss_backward(obs, B, v, pi, rep, a_idx, r_idx, y, adv)
         torch.cuda.synchronize()
     _lib.check(lib.mt_probe_read(C.c_void_p(buf.ctypes.data), buf.size), 'mt_probe_read')
-    P = buf.reshape(4, 512, 8)[3, :B, :6].astype(np.int64)
+    pairs = (B + 1) // 2
+    P = buf.reshape(4, 512, 8)[3, :B + pairs, :5].astype(np.int64)
     us = lambda x: x * 0.01  # 100 MHz
     t0 = P[:, 0].min()
-    print('blocks %d: start spread %.2f us (median start %+.2f), last block end %+.2f us' % (
-        B, us(P[:, 0].max() - t0), us(np.median(P[:, 0] - t0)), us(P[:, 5].max() - t0)))
-    for i, name in enumerate(PHASES):
-        dt = us(P[:, i + 1] - P[:, i])
+    img, par = P[:B], P[B:]
+    print('image blocks %d: start spread %.2f us, end %+.2f .. %+.2f us' % (
+        B, us(img[:, 0].max() - t0), us(img[:, 4].min() - t0), us(img[:, 4].max() - t0)))
+    for name, i0, i1 in (('stage (loads -> LDS)', 0, 1), ('conv2 dX + mask', 1, 2), ('conv1 dW + db', 2, 4),
+                         ('block total', 0, 4)):
+        dt = us(img[:, i1] - img[:, i0])
         print('  %-22s median %6.2f us  max %6.2f us' % (name, np.median(dt), dt.max()))
-    tot = us(P[:, 5] - P[:, 0])
-    print('  %-22s median %6.2f us  max %6.2f us' % ('block total', np.median(tot), tot.max()))
+    print('pair blocks %d: start %+.2f .. %+.2f us, end %+.2f .. %+.2f us' % (
+        pairs, us(par[:, 0].min() - t0), us(par[:, 0].max() - t0), us(par[:, 4].min() - t0), us(par[:, 4].max() - t0)))
+    for name, i0, i1 in (('stage (2 images)', 0, 1), ('conv2 dW + db', 1, 4), ('block total', 0, 4)):
+        dt = us(par[:, i1] - par[:, i0])
+        print('  %-22s median %6.2f us  max %6.2f us' % (name, np.median(dt), dt.max()))
 
 
 if __name__ == '__main__':
