@@ -14,6 +14,7 @@
 #include "jobs.h"
 #include "trunk_fused.h"
 #include "nips_bwd.h"
+#include "dconv.h"
 
 namespace mt {
 
@@ -955,6 +956,10 @@ static auto conv_dgrad_unpool_job(const float *dY, const float *Wt, const float 
     if (rc_ != MT_OK) return rc_; \
   } while (0)
 
+#ifndef MT_DCONV  // direct conv for the stride-1 SAME layers (0: the generic implicit-im2col GEMM)
+#define MT_DCONV 1
+#endif
+
 template <class Ar, int I>
 static const float *layer_out(float *ws, const WsLayout &L) {
   return ws + (pooled<Ar, I>() ? L.pool[I] : L.act[I]);
@@ -966,6 +971,13 @@ static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, 
   if constexpr (I < Ar::NCONV) {
     using G = LayerG<Ar, I>;
     const float *W = P + n->off_conv[I];
+#if MT_DCONV
+    if constexpr (G::S == 1 && G::SAME)  // PWYX / LSTM frame trunk: direct conv, patch in LDS (dconv.h)
+      MT_TRY((conv_forward_direct<G, I == 0, pooled<Ar, I>()>(
+          x, W, W + G::KK * G::COUT, ws + (pooled<Ar, I>() ? L.pool[I] : L.act[I]),
+          pooled<Ar, I>() ? (uint8_t *)(ws + L.parg[I]) : nullptr, B, n->cfg.activation, n->cfg.alpha_leaky, s)));
+    else
+#endif
     if constexpr (pooled<Ar, I>())
       MT_TRY((conv_forward_pool<G, I == 0>(x, W, W + G::KK * G::COUT, ws + L.pool[I], (uint8_t *)(ws + L.parg[I]), B,
                                            n->cfg.activation, n->cfg.alpha_leaky, s)));
