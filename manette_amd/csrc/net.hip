@@ -282,7 +282,10 @@ static int conv_wgrad_splits(int B) {
 template <class G>
 static size_t conv_wgrad_slab(int B) {
   const int s = conv_wgrad_splits<G>(B);
-  return s > 1 ? (size_t)s * (G::KK + 1) * G::COUT : 0;
+  const size_t generic = s > 1 ? (size_t)s * (G::KK + 1) * G::COUT : 0;
+  if constexpr (dconv_wgrad<G>())  // direct weight gradient (dconv.h)
+    return std::max(generic, dwgrad_slab_floats<G, false>(B));
+  return generic;
 }
 
 template <class Ar>
@@ -918,6 +921,25 @@ static WgradJobs<G, U8> conv_wgrad_jobs(const void *X, const float *dY, float *s
   return j;
 }
 
+// The weight-gradient jobs of conv layer G: the direct kernel for the stride-1 SAME layers
+// (DWgradJob, dconv.h), the generic GEMM otherwise; same slab layout and SlabJob either way.
+template <class G, bool U8>
+struct DWgradJobs {
+  DWJobFor<G, U8> gemm;
+  SlabJob sum;
+};
+template <class G, bool U8>
+static auto conv_wgrad_jobs_sel(const void *X, const float *dY, float *slab, float *gwb, int B) {
+  if constexpr (dconv_wgrad<G>()) {
+    using J = DWJobFor<G, U8>;
+    const int S = dwgrad_splits<G, U8>(B);
+    return DWgradJobs<G, U8>{J{reinterpret_cast<const typename J::InT *>(X), dY, slab, B, S},
+                             SlabJob{slab, B > 0 ? S : 0, J::D::SLAB, gwb}};
+  } else {
+    return conv_wgrad_jobs<G, U8>(X, dY, slab, gwb, B);
+  }
+}
+
 // dX of a conv (transposed-conv gather), masked by the activation derivative of X, as a GEMM job.
 template <class G>
 static auto conv_dgrad_job(const float *dY, const float *Wt, const float *Xact, float *dX, int B, int act,
@@ -1012,12 +1034,21 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
     set_error("batch %d too large for the conv %d weight gradient", B, I);
     return MT_ERR_ARG;
   }
-  const auto wg = conv_wgrad_jobs<G, I == 0>(x, ws + L.dact[I], ws + (I % 2 ? L.wslab2 : L.wslab),
+  const auto wg = conv_wgrad_jobs_sel<G, I == 0>(x, ws + L.dact[I], ws + (I % 2 ? L.wslab2 : L.wslab),
                                              grad + n->off_conv[I], B);
   if constexpr (I > 0) {
     constexpr int J = I - 1;
     using GJ = LayerG<Ar, J>;
-    if constexpr (pooled<Ar, J>()) {
+    if constexpr (pooled<Ar, J>() && G::S == 1 && G::SAME && dconv_bwd_solo<G>()) {  // direct dX launch, then dW
+      MT_TRY((conv_dgrad_unpool_solo<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
+                                           (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act, al, s)));
+      MT_TRY(launch_group(s, wg.gemm, pending, extra));
+    } else if constexpr (pooled<Ar, J>() && MT_DCONV_BWD == 1 && G::S == 1 && G::SAME) {  // direct conv (dconv.h)
+      MT_TRY(launch_group(s, conv_dgrad_unpool_direct<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
+                                                              (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B,
+                                                              act, al),
+                          wg.gemm, pending, extra));
+    } else if constexpr (pooled<Ar, J>()) {
       MT_TRY(launch_group(s, conv_dgrad_unpool_job<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
                                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act,
                                                            al),
