@@ -219,7 +219,7 @@ def build_args(cfg, T, sampling, seed, debugging_folder=None):
 
 
 def make_learner(config, T=5, sampling='device', seed=0, staging='resized', pipeline=True, update_graph=True,
-                 rank=0, debugging_folder=None, episode_len=None):
+                 rank=0, debugging_folder=None, episode_len=None, comm='rccl'):
     """The benchmarked learner of `config` (BASELINE.json configs[1..4]; tests/test_e2e_gpu.py
     checks exactly this path against the oracle). episode_len: a shorter synthetic episode (tests
     exercise resets); None = the synthetic default."""
@@ -232,6 +232,7 @@ def make_learner(config, T=5, sampling='device', seed=0, staging='resized', pipe
     args.staging = staging
     args.pipeline = pipeline
     args.update_graph = update_graph
+    args.comm = comm
     np.random.seed(1234 + rank)
     explo = ExplorationPolicy(args)
     net_creator, env_creator = train_cli.get_network_and_environment_creator(args, explo)
@@ -360,6 +361,9 @@ def main():
                     help='launch the update eagerly instead of replaying it as a hipGraph')
     ap.add_argument('--measure_updates', type=int, default=20,
                     help='updates after the timed region during which the rollout times its trunk kernels in place')
+    ap.add_argument('--comm', default='rccl', choices=['rccl', 'torch'],
+                    help='data-parallel gradient all-reduce (torch: torch.distributed on gloo — a rehearsal of the '
+                         'N > 1 path on one GPU with MT_BENCH_SHARED_GPU=1, every rank on cuda:0)')
     ap.add_argument('--trunk_sweep', default='256,1024,4096',
                     help='extra batch sizes the trunk kernel is timed at after the run ("" = none)')
     a = ap.parse_args()
@@ -369,12 +373,13 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(0 if os.environ.get('MT_BENCH_SHARED_GPU') == '1' else local)
     if world > 1:  # control channel (barriers, max-over-ranks time, RCCL unique id); data: mt_allreduce
         dist.init_process_group('gloo')
     cfg = CONFIGS[a.config]
     T = a.t_max
-    learner, args = make_learner(a.config, T, a.sampling, a.seed, a.staging, a.pipeline, a.update_graph, rank)
+    learner, args = make_learner(a.config, T, a.sampling, a.seed, a.staging, a.pipeline, a.update_graph, rank,
+                                 comm=a.comm)
     learner.start()
     if a.step_impl == 'python' and learner.native_step is not None:
         from manette_amd import _lib
@@ -622,11 +627,20 @@ def main():
             _lib.check(_lib.hip().mt_net_backward_bucket_launches(net._h, C.byref(nb)))
             late = nb.value == 3  # the dense weight gradient runs beside the first conv layer's dX
             nconv = len(trunk) - 1
-            names = ['dense dX + head dW' + ('' if late else ' + dense dW')] + [
-                ('conv%d dX + conv%d dW' % (i + 1, i + 1) if i > 0 else 'conv1 dW') +
-                (' + dense dW' if late and i == nconv - 1 else '') +
-                (' + conv%d slab sum' % (i + 2) if i < nconv - 1 else '') for i in range(nconv - 1, -1, -1)] + [
-                'conv1 slab sum + global-norm partials']
+            if cfg['arch'] == 'NIPS' and not cfg['rgb']:  # the fused NIPS conv backward (nips_bwd.h)
+                names = ['dense dX + head dW + dense dW',
+                         'nips_conv_bwd_kernel (conv2 dX, conv1 dW + db per image; conv2 dW + db per image pair)',
+                         'conv1 + conv2 slab sums + global-norm partials']
+            else:
+                names = ['dense dX + head dW' + ('' if late else ' + dense dW')]
+                for i in range(nconv - 1, -1, -1):
+                    sfx = (' + dense dW' if late and i == nconv - 1 else '') + \
+                          (' + conv%d slab sum' % (i + 2) if i < nconv - 1 else '')
+                    if i > 0 and cfg['arch'] == 'PWYX' and i == 1:  # its own direct dX launch (dconv.h dconv_bwd_solo)
+                        names += ['conv2 dX (direct conv)', 'conv2 dW' + sfx]
+                    else:
+                        names.append(('conv%d dX + conv%d dW' % (i + 1, i + 1) if i > 0 else 'conv1 dW') + sfx)
+                names.append('conv1 slab sum + global-norm partials')
             for k, us in enumerate(tl[1:]):
                 kernels.append(row('A10', 'actor_learner.py:49', 'group_kernel: ' + (names[k] if k < len(names) else
                                                                                       'launch %d' % (k + 2)), us))

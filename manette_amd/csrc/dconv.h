@@ -155,6 +155,10 @@ struct DBwdUnpool {
   }
 };
 
+#ifndef MT_DCONV_PERSIST  // one-chunk problems (conv1): persistent blocks, weights staged once —
+#define MT_DCONV_PERSIST 0  // measured no faster (PWYX-RGB conv1 51.7 vs 51.6 us, LSTM 84.2 vs 86.4 us
+#endif                      // at 160 frames, profiles/r03g) and it doubles conv1's VGPRs: off
+
 // ---- tiling ------------------------------------------------------------------------------------
 template <class Pr, int WM_, int WN_, int TMW_, int CK_>
 struct DConvCfg {
@@ -198,18 +202,14 @@ struct DConvCfg {
   static constexpr int AIT = (AQ + NT - 1) / NT;
 };
 
-// One block (bid of nblk) of problem p; smem = D::LDS bytes of dynamic LDS.
+// Tiles [t0, t1) of problem p, one after the other (a tile = UPB units of one image); smem =
+// D::LDS bytes of dynamic LDS. With the whole K in one chunk (NCH = 1) the weights are staged once
+// for all of them (the persistent launch, dconv_kernel); otherwise t1 = t0 + 1.
 template <class Pr, int WM, int WN, int TMW, int CK>
-__device__ __forceinline__ void dconv_body(const Pr &p, int bid, int nblk, float *smem) {
+__device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *smem) {
   using D = DConvCfg<Pr, WM, WN, TMW, CK>;
   float *As = smem;
   float *Bs = smem + D::ASZ;
-  // XCD-aware: an XCD takes a contiguous run of blocks, so the overlapping patches of one image's
-  // blocks are fetched into one L2
-  bid = xcd_tile(bid, nblk);
-  const int b = bid / D::BPI;
-  const int u0 = (bid - b * D::BPI) * D::UPB;
-  const int oy0 = Pr::POOL ? 2 * (u0 / D::PW) : (4 * u0) / D::W;  // output row of patch row 0
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w % WN;
   const int r = lane & 15, g = lane >> 4;
@@ -237,7 +237,24 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int bid, int nblk, float
       }
     }
   };
+  // A offsets of the k-chunks (one chunk: K not tap-aligned, small CI): tap and channel quad of
+  // quad index 4 kc + g (past the last tap: any tap, its weights are zero)
+  int aoffs[D::TAPALIGNED ? 1 : D::KC];
+  if constexpr (!D::TAPALIGNED) {
+#pragma unroll
+    for (int kc = 0; kc < D::KC; ++kc) {
+      const int q4 = 4 * kc + g, t0q = q4 / D::QT, cq = q4 - t0q * D::QT;
+      const int t = min(t0q, D::TAPS - 1), ky = t / D::KW, kx = t - ky * D::KW;
+      aoffs[kc] = (ky * D::WP + kx) * D::CS + 4 * cq;
+    }
+  }
   wload(0);
+  if constexpr (D::NCH > 1) t1 = t0 + 1;  // (chunked weights: one tile per block, no loop)
+  for (int bid = t0; bid < t1; ++bid) {
+  const int b = bid / D::BPI;
+  const int u0 = (bid - b * D::BPI) * D::UPB;
+  const int oy0 = Pr::POOL ? 2 * (u0 / D::PW) : (4 * u0) / D::W;  // output row of patch row 0
+  if (bid > t0) __syncthreads();  // the previous tile's LDS reads are done
   // epilogue operands (bias; or the pooled values + argmax of the unpool) issued up front
   typename Pr::Pre pre[TMW][D::TNW];
 #pragma unroll
@@ -292,18 +309,6 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int bid, int nblk, float
     }
     abase[i] = ((oy - oy0) * D::WP + ox) * D::CS;
   }
-  // A offsets of the k-chunks (one chunk: K not tap-aligned, small CI): tap and channel quad of
-  // quad index 4 kc + g (past the last tap: any tap, its weights are zero)
-  int aoffs[D::TAPALIGNED ? 1 : D::KC];
-  if constexpr (!D::TAPALIGNED) {
-#pragma unroll
-    for (int kc = 0; kc < D::KC; ++kc) {
-      const int q4 = 4 * kc + g, t0 = q4 / D::QT, cq = q4 - t0 * D::QT;
-      const int t = min(t0, D::TAPS - 1), ky = t / D::KW, kx = t - ky * D::KW;
-      aoffs[kc] = (ky * D::WP + kx) * D::CS + 4 * cq;
-    }
-  }
-
   f32x4 acc[TMW][D::TNW];
 #pragma unroll
   for (int i = 0; i < TMW; ++i)
@@ -336,7 +341,7 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int bid, int nblk, float
     }
   };
 
-  wstore(Bs);
+  if (D::NCH > 1 || bid == t0) wstore(Bs);
   __syncthreads();
   if constexpr (D::NCH == 1) {
     compute(Bs, 0);
@@ -360,12 +365,24 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int bid, int nblk, float
 #pragma unroll
     for (int j = 0; j < D::TNW; ++j) p.store(pre[i][j], b, u, (wn * D::TNW + j) * 16 + r, acc[i][j]);
   }
+  }
 }
 
+// ntiles > gridDim.x (persistent, NCH = 1): block k runs the contiguous tiles [k T / G, (k+1) T / G)
+// — an image's neighbouring tiles share their patch rows in the CU's caches. Otherwise one tile
+// per block, XCD-aware (an XCD takes a contiguous run of blocks, so the overlapping patches of
+// one image's blocks are fetched into one L2).
 template <class Pr, int WM, int WN, int TMW, int CK>
-__global__ __launch_bounds__(64 * WM * WN) void dconv_kernel(Pr p) {
+__global__ __launch_bounds__(64 * WM * WN) void dconv_kernel(Pr p, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  dconv_body<Pr, WM, WN, TMW, CK>(p, blockIdx.x, gridDim.x, smem);
+  const int G = gridDim.x;
+  if (ntiles > G) {
+    const int t0 = (int)((long)blockIdx.x * ntiles / G), t1 = (int)((long)(blockIdx.x + 1) * ntiles / G);
+    dconv_body<Pr, WM, WN, TMW, CK>(p, t0, t1, smem);
+  } else {
+    const int t = xcd_tile(blockIdx.x, G);
+    dconv_body<Pr, WM, WN, TMW, CK>(p, t, t + 1, smem);
+  }
 }
 
 template <class Pr, int WM, int WN, int TMW, int CK>
@@ -380,7 +397,13 @@ static int launch_dconv(const Pr &p, int B, hipStream_t s) {
                                (int)D::LDS));
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)B * D::BPI), dim3(D::NT), D::LDS, s, p);
+  const int ntiles = B * D::BPI;
+  int grid = ntiles;
+  if constexpr (D::NCH == 1 && MT_DCONV_PERSIST) {  // weights staged once per block: as many blocks as fit
+    const int per_cu = std::max(1, std::min((int)(160 * 1024 / D::LDS), 16 / D::NW));
+    grid = std::min(ntiles, per_cu * 256);
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(D::NT), D::LDS, s, p, ntiles);
   MT_LAUNCHED();
   return MT_OK;
 }
@@ -394,7 +417,10 @@ struct DConvJob {
   int nblk;
   __host__ __device__ int blocks() const { return nblk; }
   size_t lds() const { return D::LDS; }
-  __device__ __forceinline__ void run(int id, float *smem) const { dconv_body<Pr, WM, WN, TMW, CK>(p, id, nblk, smem); }
+  __device__ __forceinline__ void run(int id, float *smem) const {
+    const int t = xcd_tile(id, nblk);
+    dconv_body<Pr, WM, WN, TMW, CK>(p, t, t + 1, smem);
+  }
 };
 
 // ---- tile choice per PWYX layer shape (E = 32 frames: conv1 1,792 blocks, conv2 448, conv3

@@ -24,7 +24,9 @@ def main():
     net.init_params(0)
     depth = 3 if cfg['rgb'] else 1
     g = torch.Generator(device='cuda').manual_seed(7)
-    obs = torch.randint(0, 256, (a.envs, 84, 84, 4 * depth), dtype=torch.uint8, device='cuda', generator=g)
+    # (mt_forward_trunk reads a window of 5 frames per row for the LSTM arch: [B][5][84][84][C])
+    shape = (a.envs, 5, 84, 84, 4 * depth) if cfg['arch'] == 'LSTM' else (a.envs, 84, 84, 4 * depth)
+    obs = torch.randint(0, 256, shape, dtype=torch.uint8, device='cuda', generator=g)
     for _ in range(a.reps):
         net.forward_trunk(obs, a.envs, ws_key='sweep')
     torch.cuda.synchronize()
