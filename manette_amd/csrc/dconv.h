@@ -160,6 +160,29 @@ struct DBwdUnpool {
 #endif                      // at 160 frames, profiles/r03g) and it doubles conv1's VGPRs: off
 
 // ---- tiling ------------------------------------------------------------------------------------
+// Patch pixel stride CS (floats) and extra row padding of the layers whose A-fragment reads
+// (ds_read_b128, lane groups of 16) conflicted: searched with a model of the LDS banks over every
+// tile of the image (tools/lds_banks.py; conflict-free = 4 LDS cycles per read): PWYX conv3
+// forward 8.9 -> 4.4, conv4 10.0 -> 5.0, the 5x5 dX 9.3 -> 4.1, within each one's LDS budget (the
+// conv2 forward's better strides need a patch that halves its occupancy: kept at CI + 4).
+#ifndef MT_DCONV_CS_TABLE  // measured no faster (conv3 / conv4 forward within 1 %), and the 5x5 dX
+#define MT_DCONV_CS_TABLE 0  // slower (168 vs 149 us: its 80 KB patch + weights fit one block per CU): off
+#endif
+constexpr int dconv_cs(int ci, int w, bool pool, int upb) {
+  return !MT_DCONV_CS_TABLE ? (ci % 16 == 0 ? ci + 4 : ci)
+       : (ci == 32 && w == 21 && pool && upb == 16) ? 40
+       : (ci == 64 && w == 10 && !pool && upb == 8) ? 72
+       : (ci == 32 && w == 42 && !pool && upb == 32) ? 40
+       : (ci % 16 == 0 ? ci + 4 : ci);
+}
+constexpr int dconv_row_pad(int ci, int w, bool pool, int upb) {
+  return !MT_DCONV_CS_TABLE ? 0
+       : (ci == 32 && w == 21 && pool && upb == 16) ? 4
+       : (ci == 64 && w == 10 && !pool && upb == 8) ? 6
+       : (ci == 32 && w == 42 && !pool && upb == 32) ? 4
+       : 0;
+}
+
 template <class Pr, int WM_, int WN_, int TMW_, int CK_>
 struct DConvCfg {
   static constexpr int WM = WM_, WN = WN_, TMW = TMW_, NW = WM * WN, NT = 64 * NW;
@@ -182,9 +205,10 @@ struct DConvCfg {
   static constexpr int RSPAN0 = Pr::POOL ? 2 * ((UPB - 1) / PW + 2) : (4 * UPB - 1) / W + 2;
   static constexpr int RSPAN = RSPAN0 < H ? RSPAN0 : H;
   static constexpr int RIN = RSPAN + KH - 1;
-  static constexpr int WP = W + KW - 1;
-  static constexpr int CS = CI % 16 == 0 ? CI + 4 : CI;  // floats per patch pixel (bank spread)
-  static constexpr int ASZ = (RIN * WP * CS + 3) / 4 * 4;
+  static constexpr int WP = W + KW - 1;                               // patch columns staged
+  static constexpr int CS = dconv_cs(CI, W, Pr::POOL, UPB);           // floats per patch pixel
+  static constexpr int WPX = WP + dconv_row_pad(CI, W, Pr::POOL, UPB);  // patch row stride (pixels)
+  static constexpr int ASZ = (RIN * WPX * CS + 3) / 4 * 4;
   static constexpr int CK = CK_ > 0 ? CK_ : KP;  // k per weight chunk
   static_assert(CK % 16 == 0, "chunk of whole 16-k steps");
   static constexpr bool TAPALIGNED = QT % 4 == 0 && CK % CI == 0;
@@ -245,7 +269,7 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
     for (int kc = 0; kc < D::KC; ++kc) {
       const int q4 = 4 * kc + g, t0q = q4 / D::QT, cq = q4 - t0q * D::QT;
       const int t = min(t0q, D::TAPS - 1), ky = t / D::KW, kx = t - ky * D::KW;
-      aoffs[kc] = (ky * D::WP + kx) * D::CS + 4 * cq;
+      aoffs[kc] = (ky * D::WPX + kx) * D::CS + 4 * cq;
     }
   }
   wload(0);
@@ -283,7 +307,7 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
         const f32x4 x = InElem<std::is_same<typename Pr::InT, uint8_t>::value>::load4(
             img + (size_t)(ok ? iy * D::W + ix : 0) * D::CI + 4 * cq);
         v[t] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
-        dst[t] = (D::AQ % D::NT == 0 || tid + it * D::NT < D::AQ) ? (pr * D::WP + pc) * D::CS + 4 * cq : -1;
+        dst[t] = (D::AQ % D::NT == 0 || tid + it * D::NT < D::AQ) ? (pr * D::WPX + pc) * D::CS + 4 * cq : -1;
       }
     }
 #pragma unroll
@@ -307,7 +331,7 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
       oy = px / D::W;
       ox = px - oy * D::W;
     }
-    abase[i] = ((oy - oy0) * D::WP + ox) * D::CS;
+    abase[i] = ((oy - oy0) * D::WPX + ox) * D::CS;
   }
   f32x4 acc[TMW][D::TNW];
 #pragma unroll
@@ -321,7 +345,7 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
       int ao;
       if constexpr (D::TAPALIGNED) {  // tap t (wave-uniform) and channel quad (4 kcl) % QT + g
         const int t = c * D::TPC + (4 * kcl) / D::QT;
-        ao = ((t / D::KW) * D::WP + t % D::KW) * D::CS + 4 * ((4 * kcl) % D::QT) + 4 * g;
+        ao = ((t / D::KW) * D::WPX + t % D::KW) * D::CS + 4 * ((4 * kcl) % D::QT) + 4 * g;
       } else {
         ao = aoffs[kcl];
       }
@@ -431,6 +455,12 @@ struct DConvJob {
 #ifndef MT_DCONV_TMW1  // conv1 (CIN 4 / 12): M-tiles per wave
 #define MT_DCONV_TMW1 2
 #endif
+#ifndef MT_DCONV_C2CK  // conv2 (32 -> 32): k per weight chunk (0: one tap = CIN)
+#define MT_DCONV_C2CK 0
+#endif
+#ifndef MT_DCONV_C2W8  // conv2 (32 -> 32): 8-wave blocks (two N halves), two blocks per CU
+#define MT_DCONV_C2W8 0
+#endif
 #ifndef MT_DCONV_W8  // 8-wave blocks for the small-grid layers (conv3, conv4)
 #define MT_DCONV_W8 1
 #endif
@@ -438,10 +468,10 @@ template <class G, bool POOL>
 struct DConvFor {
   static constexpr bool SMALLC = G::CIN % 16 != 0;  // conv1: the whole K in one chunk
   static constexpr bool C64 = G::COUT >= 64;
-  static constexpr int WN = C64 ? (MT_DCONV_W8 ? (POOL ? 2 : 4) : (POOL ? 1 : 2)) : 1;
+  static constexpr int WN = C64 ? (MT_DCONV_W8 ? (POOL ? 2 : 4) : (POOL ? 1 : 2)) : (!SMALLC && MT_DCONV_C2W8 ? 2 : 1);
   static constexpr int WM = C64 ? (MT_DCONV_W8 ? (POOL ? 4 : 2) : (POOL ? 4 : 2)) : 4;
   static constexpr int TMW = SMALLC ? MT_DCONV_TMW1 : (C64 ? 1 : MT_DCONV_TMW2);
-  static constexpr int CK = SMALLC ? 0 : G::CIN;
+  static constexpr int CK = SMALLC ? 0 : (!C64 && MT_DCONV_C2CK ? MT_DCONV_C2CK : G::CIN);
 };
 
 template <class G, bool U8, bool POOL>
