@@ -458,8 +458,11 @@ struct DConvJob {
 #ifndef MT_DCONV_C2CK  // conv2 (32 -> 32): k per weight chunk (0: one tap = CIN)
 #define MT_DCONV_C2CK 0
 #endif
-#ifndef MT_DCONV_C2W8  // conv2 (32 -> 32): 8-wave blocks (two N halves), two blocks per CU
-#define MT_DCONV_C2W8 0
+#ifndef MT_DCONV_C2W8  // conv2 (32 -> 32): 8-wave blocks (two N halves), two blocks per CU: four
+#define MT_DCONV_C2W8 1  // waves per SIMD hide the per-chunk barrier (PWYX-RGB E=32 33.4 vs 36.7 us,
+#endif                   // LSTM 161 frames 143.6 vs 157.5 us, profiles/r03i)
+#ifndef MT_DCONV_C1W8  // conv1 (CIN 4 / 12): 8-wave blocks
+#define MT_DCONV_C1W8 0
 #endif
 #ifndef MT_DCONV_W8  // 8-wave blocks for the small-grid layers (conv3, conv4)
 #define MT_DCONV_W8 1
@@ -468,7 +471,8 @@ template <class G, bool POOL>
 struct DConvFor {
   static constexpr bool SMALLC = G::CIN % 16 != 0;  // conv1: the whole K in one chunk
   static constexpr bool C64 = G::COUT >= 64;
-  static constexpr int WN = C64 ? (MT_DCONV_W8 ? (POOL ? 2 : 4) : (POOL ? 1 : 2)) : (!SMALLC && MT_DCONV_C2W8 ? 2 : 1);
+  static constexpr int WN = C64 ? (MT_DCONV_W8 ? (POOL ? 2 : 4) : (POOL ? 1 : 2))
+                                : (SMALLC ? (MT_DCONV_C1W8 ? 2 : 1) : (MT_DCONV_C2W8 ? 2 : 1));
   static constexpr int WM = C64 ? (MT_DCONV_W8 ? (POOL ? 4 : 2) : (POOL ? 4 : 2)) : 4;
   static constexpr int TMW = SMALLC ? MT_DCONV_TMW1 : (C64 ? 1 : MT_DCONV_TMW2);
   static constexpr int CK = SMALLC ? 0 : (!C64 && MT_DCONV_C2CK ? MT_DCONV_C2CK : G::CIN);
