@@ -34,8 +34,8 @@ namespace mt {
 // activation [B][OH][OW][COUT].
 template <class G, bool U8, bool POOL_>
 struct DFwd {
-  static constexpr int CI = G::CIN, CO = G::COUT, KH = G::KH, KW = G::KW, PT = G::PT, PL = G::PL;
-  static constexpr int H = G::OH, W = G::OW, KK = G::KK;
+  static constexpr int CI = G::CIN, CO = G::COUT, KH = G::KH, KW = G::KW, PT = G::PT, PL = G::PL, S = G::S;
+  static constexpr int H = G::H, W = G::W, OH = G::OH, OW = G::OW, KK = G::KK;
   static constexpr bool POOL = POOL_;
   using InT = typename InElem<U8>::T;
   const InT *X;
@@ -77,7 +77,7 @@ struct DFwd {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int px = 4 * u + q;
-        if (px < H * W) Y[((size_t)b * H * W + px) * CO + n] = act_fwd(v[q] + p.b, act, alpha);
+        if (px < OH * OW) Y[((size_t)b * OH * OW + px) * CO + n] = act_fwd(v[q] + p.b, act, alpha);
       }
     }
   }
@@ -92,7 +92,7 @@ struct DBwdUnpool {
   static_assert(G::S == 1 && G::SAME && G::H == G::OH && GJ::COUT == G::CIN, "pooled input of a stride-1 conv");
   static constexpr int CI = G::COUT, CO = G::CIN, KH = G::KH, KW = G::KW;
   static constexpr int PT = G::KH - 1 - G::PT, PL = G::KW - 1 - G::PL;
-  static constexpr int H = G::H, W = G::W, KK = G::KH * G::KW * G::COUT;
+  static constexpr int H = G::H, W = G::W, OH = G::H, OW = G::W, S = 1, KK = G::KH * G::KW * G::COUT;
   static constexpr bool POOL = false;
   using InT = float;
   const float *X;     // dY
@@ -187,7 +187,8 @@ template <class Pr, int WM_, int WN_, int TMW_, int CK_>
 struct DConvCfg {
   static constexpr int WM = WM_, WN = WN_, TMW = TMW_, NW = WM * WN, NT = 64 * NW;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  static constexpr int CI = Pr::CI, CO = Pr::CO, KH = Pr::KH, KW = Pr::KW, H = Pr::H, W = Pr::W;
+  static constexpr int CI = Pr::CI, CO = Pr::CO, KH = Pr::KH, KW = Pr::KW, H = Pr::H, W = Pr::W, S = Pr::S;
+  static constexpr int OH = Pr::OH, OW = Pr::OW;  // (input H x W, output OH x OW, stride S)
   static constexpr int QT = CI / 4;  // channel quads per tap
   static_assert(CI % 4 == 0, "channel quads");
   static constexpr int TAPS = KH * KW;
@@ -197,15 +198,15 @@ struct DConvCfg {
   static_assert(CO % 16 == 0 && TN % WN == 0, "N tiles");
   static constexpr int TNW = TN / WN;
   static constexpr int UPB = WM * TMW * 4;  // units per block
-  static constexpr int PW = W / 2;
-  static constexpr int NPIX = H * W;
-  static constexpr int U = Pr::POOL ? (H / 2) * PW : (NPIX + 3) / 4;  // units per image
-  static constexpr int BPI = (U + UPB - 1) / UPB;                      // blocks per image
+  static constexpr int PW = OW / 2;
+  static constexpr int NPIX = OH * OW;
+  static constexpr int U = Pr::POOL ? (OH / 2) * PW : (NPIX + 3) / 4;  // units per image
+  static constexpr int BPI = (U + UPB - 1) / UPB;                       // blocks per image
   // output rows a block's units can touch, and the input rows / columns of its patch
-  static constexpr int RSPAN0 = Pr::POOL ? 2 * ((UPB - 1) / PW + 2) : (4 * UPB - 1) / W + 2;
-  static constexpr int RSPAN = RSPAN0 < H ? RSPAN0 : H;
-  static constexpr int RIN = RSPAN + KH - 1;
-  static constexpr int WP = W + KW - 1;                               // patch columns staged
+  static constexpr int RSPAN0 = Pr::POOL ? 2 * ((UPB - 1) / PW + 2) : (4 * UPB - 1) / OW + 2;
+  static constexpr int RSPAN = RSPAN0 < OH ? RSPAN0 : OH;
+  static constexpr int RIN = (RSPAN - 1) * S + KH;
+  static constexpr int WP = (OW - 1) * S + KW;                          // patch columns staged
   static constexpr int CS = dconv_cs(CI, W, Pr::POOL, UPB);           // floats per patch pixel
   static constexpr int WPX = WP + dconv_row_pad(CI, W, Pr::POOL, UPB);  // patch row stride (pixels)
   static constexpr int ASZ = (RIN * WPX * CS + 3) / 4 * 4;
@@ -277,7 +278,7 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
   for (int bid = t0; bid < t1; ++bid) {
   const int b = bid / D::BPI;
   const int u0 = (bid - b * D::BPI) * D::UPB;
-  const int oy0 = Pr::POOL ? 2 * (u0 / D::PW) : (4 * u0) / D::W;  // output row of patch row 0
+  const int oy0 = Pr::POOL ? 2 * (u0 / D::PW) : (4 * u0) / D::OW;  // output row of patch row 0
   if (bid > t0) __syncthreads();  // the previous tile's LDS reads are done
   // epilogue operands (bias; or the pooled values + argmax of the unpool) issued up front
   typename Pr::Pre pre[TMW][D::TNW];
@@ -302,7 +303,7 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
         const int item = min(tid + it * D::NT, D::AQ - 1);
         const int pix = item / D::QT, cq = item - pix * D::QT;
         const int pr = pix / D::WP, pc = pix - pr * D::WP;
-        const int iy = oy0 - Pr::PT + pr, ix = pc - Pr::PL;
+        const int iy = oy0 * D::S - Pr::PT + pr, ix = pc - Pr::PL;
         const bool ok = (unsigned)iy < (unsigned)D::H && (unsigned)ix < (unsigned)D::W;
         const f32x4 x = InElem<std::is_same<typename Pr::InT, uint8_t>::value>::load4(
             img + (size_t)(ok ? iy * D::W + ix : 0) * D::CI + 4 * cq);
@@ -328,10 +329,10 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
       ox = 2 * (u - py * D::PW) + (q & 1);
     } else {
       const int px = min(4 * u + q, D::NPIX - 1);
-      oy = px / D::W;
-      ox = px - oy * D::W;
+      oy = px / D::OW;
+      ox = px - oy * D::OW;
     }
-    abase[i] = ((oy - oy0) * D::WPX + ox) * D::CS;
+    abase[i] = ((oy - oy0) * D::S * D::WPX + ox * D::S) * D::CS;
   }
   f32x4 acc[TMW][D::TNW];
 #pragma unroll
@@ -455,6 +456,9 @@ struct DConvJob {
 #ifndef MT_DCONV_TMW1  // conv1 (CIN 4 / 12): M-tiles per wave
 #define MT_DCONV_TMW1 2
 #endif
+#ifndef MT_DCONV_STRIDED  // the NATURE trunk's strided VALID convs on the direct forward too
+#define MT_DCONV_STRIDED 1
+#endif
 #ifndef MT_DCONV_C2CK  // conv2 (32 -> 32): k per weight chunk (0: one tap = CIN)
 #define MT_DCONV_C2CK 0
 #endif
@@ -474,7 +478,7 @@ struct DConvFor {
   static constexpr int WN = C64 ? (MT_DCONV_W8 ? (POOL ? 2 : 4) : (POOL ? 1 : 2))
                                 : (SMALLC ? (MT_DCONV_C1W8 ? 2 : 1) : (MT_DCONV_C2W8 ? 2 : 1));
   static constexpr int WM = C64 ? (MT_DCONV_W8 ? (POOL ? 4 : 2) : (POOL ? 4 : 2)) : 4;
-  static constexpr int TMW = SMALLC ? MT_DCONV_TMW1 : (C64 ? 1 : MT_DCONV_TMW2);
+  static constexpr int TMW = SMALLC ? (G::S > 1 ? 1 : MT_DCONV_TMW1) : (C64 ? 1 : MT_DCONV_TMW2);
   static constexpr int CK = SMALLC ? 0 : (!C64 && MT_DCONV_C2CK ? MT_DCONV_C2CK : G::CIN);
 };
 

@@ -994,7 +994,9 @@ static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, 
     using G = LayerG<Ar, I>;
     const float *W = P + n->off_conv[I];
 #if MT_DCONV
-    if constexpr (G::S == 1 && G::SAME)  // PWYX / LSTM frame trunk: direct conv, patch in LDS (dconv.h)
+    // PWYX / LSTM frame trunk (stride-1 SAME) and NATURE (strided VALID): direct conv, patch in LDS (dconv.h)
+    // (the RGB NATURE conv1's 768-deep K with its 24-row patch exceeds the LDS: generic)
+    if constexpr ((G::S == 1 && G::SAME) || (MT_DCONV_STRIDED && Ar::NCONV == 3 && !G::SAME && G::CIN != 12))
       MT_TRY((conv_forward_direct<G, I == 0, pooled<Ar, I>()>(
           x, W, W + G::KK * G::COUT, ws + (pooled<Ar, I>() ? L.pool[I] : L.act[I]),
           pooled<Ar, I>() ? (uint8_t *)(ws + L.parg[I]) : nullptr, B, n->cfg.activation, n->cfg.alpha_leaky, s)));
