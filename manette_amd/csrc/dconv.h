@@ -552,8 +552,9 @@ constexpr int dw_pad(int c, int wd) {  // channel stride whose row stride wd * c
 
 template <class G, bool U8, int TMW_>
 struct DWCfg {
-  static_assert(G::S == 1 && G::SAME && G::H == G::OH && G::W == G::OW, "stride-1 SAME conv");
-  static constexpr int CIN = G::CIN, COUT = G::COUT, KH = G::KH, KW = G::KW, H = G::H, W = G::W;
+  static_assert((G::S == 1 && G::SAME) || !G::SAME, "stride-1 SAME or VALID conv");
+  static constexpr int CIN = G::CIN, COUT = G::COUT, KH = G::KH, KW = G::KW, H = G::H, W = G::W, S = G::S;
+  static constexpr int OH = G::OH, OW = G::OW;  // (input H x W, output OH x OW)
   static constexpr int KK = G::KK, TMW = TMW_;
   static constexpr int TN = COUT / 16;
   static_assert(COUT % 16 == 0 && 4 % TN == 0, "N tiles per 4 waves");
@@ -562,12 +563,12 @@ struct DWCfg {
   static constexpr int MT = (KK + 15) / 16;
   static constexpr int TG = (MT + MPB - 1) / MPB;  // tap groups
   static constexpr int R = 4;                      // output rows per chunk (= lane groups g)
-  static constexpr int RG = (H + R - 1) / R;       // chunks per image
-  static constexpr int WPAD = (W + 3) / 4 * 4;
+  static constexpr int RG = (OH + R - 1) / R;      // chunks per image
+  static constexpr int WPAD = (OW + 3) / 4 * 4;    // output columns, padded
   static constexpr int KQ = WPAD / 4;              // 16-k steps per chunk
-  static constexpr int WP = WPAD + KW - 1;
-  static constexpr int RIN = R + KH - 1;
-  static constexpr int CS = dw_pad(CIN, WP), COS = dw_pad(COUT, WPAD);
+  static constexpr int WP = (WPAD - 1) * S + KW;   // patch columns
+  static constexpr int RIN = (R - 1) * S + KH;     // patch rows
+  static constexpr int CS = dw_pad(CIN, S * WP), COS = dw_pad(COUT, WPAD);
   static constexpr int XSZ = (RIN * WP * CS + 3) / 4 * 4, YSZ = R * WPAD * COS;
   static constexpr size_t LDS = (size_t)(XSZ + YSZ) * 4;
   static constexpr int XQ = RIN * WP * (CIN / 4), YQ = R * WPAD * (COUT / 4);  // quads per chunk
@@ -602,7 +603,7 @@ struct DWgradJob {
     for (int i = 0; i < TMW; ++i) {
       const int row = min(16 * (tg * D::MPB + wm + D::WROWS * i) + r, D::KK - 1);  // (rows >= KK: not stored)
       const int t = row / D::CIN, ci = row - t * D::CIN, ky = t / D::KW, kx = t - ky * D::KW;
-      abase[i] = ((g + ky) * D::WP + kx) * D::CS + ci;
+      abase[i] = ((g * D::S + ky) * D::WP + kx) * D::CS + ci;
     }
     const int bbase = g * D::WPAD * D::COS + 16 * j + r;
 
@@ -610,13 +611,13 @@ struct DWgradJob {
     auto load = [&](int c) {
       const int b = c / D::RG, y0 = (c - b * D::RG) * D::R;
       const InT *xi = X + (size_t)b * D::H * D::W * D::CIN;
-      const float *yi = dY + (size_t)b * D::H * D::W * D::COUT;
+      const float *yi = dY + (size_t)b * D::OH * D::OW * D::COUT;
 #pragma unroll
       for (int it = 0; it < D::XIT; ++it) {
         const int item = min(tid + 256 * it, D::XQ - 1);
         const int pix = item / (D::CIN / 4), cq = item - pix * (D::CIN / 4);
         const int pr = pix / D::WP, pc = pix - pr * D::WP;
-        const int iy = y0 - G::PT + pr, ix = pc - G::PL;
+        const int iy = y0 * D::S - G::PT + pr, ix = pc - G::PL;
         const bool ok = (unsigned)iy < (unsigned)D::H && (unsigned)ix < (unsigned)D::W;
         const f32x4 v = InElem<U8>::load4(xi + (size_t)(ok ? iy * D::W + ix : 0) * D::CIN + 4 * cq);
         xr[it] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -627,8 +628,8 @@ struct DWgradJob {
         const int pix = item / (D::COUT / 4), cq = item - pix * (D::COUT / 4);
         const int pr = pix / D::WPAD, pc = pix - pr * D::WPAD;
         const int oy = y0 + pr;
-        const bool ok = oy < D::H && pc < D::W;
-        const f32x4 v = *reinterpret_cast<const f32x4 *>(yi + (size_t)(ok ? oy * D::W + pc : 0) * D::COUT + 4 * cq);
+        const bool ok = oy < D::OH && pc < D::OW;
+        const f32x4 v = *reinterpret_cast<const f32x4 *>(yi + (size_t)(ok ? oy * D::OW + pc : 0) * D::COUT + 4 * cq);
         yr[it] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     };
@@ -674,7 +675,7 @@ struct DWgradJob {
 #pragma unroll
         for (int i = 0; i < TMW; ++i)
 #pragma unroll
-          for (int s = 0; s < 4; ++s) av[i][s] = Xs[abase[i] + (4 * kq + s) * D::CS];
+          for (int s = 0; s < 4; ++s) av[i][s] = Xs[abase[i] + (4 * kq + s) * D::S * D::CS];
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -709,9 +710,13 @@ struct DWgradJob {
 #ifndef MT_DCONV_WGRAD
 #define MT_DCONV_WGRAD 1
 #endif
+#ifndef MT_DCONV_WGRAD_STRIDED  // the strided VALID layers (NATURE, NIPS RGB conv2) direct too:
+#define MT_DCONV_WGRAD_STRIDED 0  // parity-green but slower (NATURE E=64 conv2 dX + dW group 94 vs 60 us,
+#endif                            // conv3 53 vs 46, conv1 dW 36 vs 33; profiles/r03k): off
 template <class G>
 constexpr bool dconv_wgrad() {
-  return G::S == 1 && G::SAME && (MT_DCONV_WGRAD == 2 || (MT_DCONV_WGRAD == 1 && G::KH == 5));
+  return (G::S == 1 && G::SAME && (MT_DCONV_WGRAD == 2 || (MT_DCONV_WGRAD == 1 && G::KH == 5))) ||
+         (MT_DCONV_WGRAD_STRIDED && !G::SAME && G::CIN != 12 && G::COUT >= 32);
 }
 template <class G, bool U8>
 using DWJobFor = DWgradJob<G, U8, (G::COUT >= 64 ? 4 : 5)>;
