@@ -718,8 +718,19 @@ constexpr bool dconv_wgrad() {
   return (G::S == 1 && G::SAME && (MT_DCONV_WGRAD == 2 || (MT_DCONV_WGRAD == 1 && G::KH == 5))) ||
          (MT_DCONV_WGRAD_STRIDED && !G::SAME && G::CIN != 12 && G::COUT >= 32);
 }
+// M-tiles per wave: 5 (4 for 64 output channels), or for a short K (the gray conv1: 7 M-tiles of
+// (tap, ci) rows) just enough for one tap group — 5 would leave 3 of its 10 tile slots empty
+template <class G>
+constexpr int dw_tmw() {
+  constexpr int mt = (G::KK + 15) / 16, wrows = 4 / (G::COUT / 16);
+  if (G::COUT >= 64) return 4;
+  if (mt <= 5 * wrows) return (mt + wrows - 1) / wrows;
+  constexpr int w5 = (mt + 5 * wrows - 1) / (5 * wrows) * 5 * wrows - mt;  // empty tile slots at 5
+  constexpr int w4 = (mt + 4 * wrows - 1) / (4 * wrows) * 4 * wrows - mt;  // and at 4
+  return w4 < w5 ? 4 : 5;
+}
 template <class G, bool U8>
-using DWJobFor = DWgradJob<G, U8, (G::COUT >= 64 ? 4 : 5)>;
+using DWJobFor = DWgradJob<G, U8, dw_tmw<G>()>;
 
 // splits: ~512 blocks (two per CU), at most one chunk each, slabs within kDwSlabCap
 template <class G, bool U8>
