@@ -1,7 +1,10 @@
 // Direct convolution for the stride-1 SAME convs of the PWYX trunk (networks.py:206-225; the LSTM
-// arch runs it per window frame, networks.py:227-258): the forward (conv + bias + activation, + the
-// 2x2/2 max pool and its argmax bytes) and the backward-data product (dX of a conv whose input is a
-// pooled layer: MaxPoolGrad routing and the activation mask in the epilogue).
+// arch runs it per window frame, networks.py:227-258) and the strided VALID convs of the NATURE
+// trunk (networks.py:261-278): the forward (conv + bias + activation, + the 2x2/2 max pool and its
+// argmax bytes), the backward-data product of the 5x5 layer (dX of a conv whose input is a pooled
+// layer: MaxPoolGrad routing and the activation mask in the epilogue) and the weight gradients of
+// the 5x5 layers (DWgradJob, at the end of the file). Which layers take which product is set by the
+// build knobs below; each non-default one was measured and is documented where it is defined.
 //
 // Why not the generic implicit-im2col GEMM (gemm.h, LdIm2col / LdConvBwdA): there every A element
 // of every K chunk is re-derived from (row, k) — tap / channel divisions, SAME-padding clamps and
@@ -713,6 +716,9 @@ struct DWgradJob {
 #ifndef MT_DCONV_WGRAD_STRIDED  // the strided VALID layers (NATURE, NIPS RGB conv2) direct too:
 #define MT_DCONV_WGRAD_STRIDED 0  // parity-green but slower (NATURE E=64 conv2 dX + dW group 94 vs 60 us,
 #endif                            // conv3 53 vs 46, conv1 dW 36 vs 33; profiles/r03k): off
+#ifndef MT_DCONV_WGRAD_SPLIT  // (with MT_DCONV_WGRAD_STRIDED) the strided layers' dX and dW in two launches
+#define MT_DCONV_WGRAD_SPLIT 0
+#endif
 template <class G>
 constexpr bool dconv_wgrad() {
   return (G::S == 1 && G::SAME && (MT_DCONV_WGRAD == 2 || (MT_DCONV_WGRAD == 1 && G::KH == 5))) ||
