@@ -715,10 +715,8 @@ struct DWgradJob {
 #endif
 #ifndef MT_DCONV_WGRAD_STRIDED  // the strided VALID layers (NATURE, NIPS RGB conv2) direct too:
 #define MT_DCONV_WGRAD_STRIDED 0  // parity-green but slower (NATURE E=64 conv2 dX + dW group 94 vs 60 us,
-#endif                            // conv3 53 vs 46, conv1 dW 36 vs 33; profiles/r03k): off
-#ifndef MT_DCONV_WGRAD_SPLIT  // (with MT_DCONV_WGRAD_STRIDED) the strided layers' dX and dW in two launches
-#define MT_DCONV_WGRAD_SPLIT 0
-#endif
+#endif                            // conv3 53 vs 46, conv1 dW 36 vs 33; profiles/r03k; in launches of
+                                  // their own after the generic dX: 49 + 42 vs 60, profiles/r03n): off
 template <class G>
 constexpr bool dconv_wgrad() {
   return (G::S == 1 && G::SAME && (MT_DCONV_WGRAD == 2 || (MT_DCONV_WGRAD == 1 && G::KH == 5))) ||

@@ -1055,12 +1055,6 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
                                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act,
                                                            al),
                           wg.gemm, pending, extra));
-    } else if constexpr (dconv_wgrad<G>() && MT_DCONV_WGRAD_SPLIT) {
-      // experiment: the direct weight gradient in a launch of its own after the generic dX (its
-      // LDS would otherwise set the occupancy of the dX blocks of a shared grid)
-      MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
-                                               act, al)));
-      MT_TRY(launch_group(s, wg.gemm, pending, extra));
     } else {
       MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
                                                act, al),
