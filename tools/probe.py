@@ -49,7 +49,7 @@ def main():
     lib = _lib.hip()
     lib.mt_probe_read.restype = C.c_int
     lib.mt_probe_read.argtypes = [C.c_void_p, C.c_size_t]
-    buf = np.zeros(4 * 512 * 8, dtype=np.uint64)
+    buf = np.zeros(4 * 1024 * 8, dtype=np.uint64)
     for _ in range(a.updates):
         L.book.new_update()
         for t in range(L.max_local_steps):
@@ -74,14 +74,14 @@ def main():
         torch.cuda.synchronize()
     buf[:] = 0
     _lib.check(lib.mt_probe_read(C.c_void_p(buf.ctypes.data), buf.size), 'mt_probe_read')
-    P = buf.reshape(4, 512, 8).astype(np.int64)
+    P = buf.reshape(4, 1024, 8).astype(np.int64)
     E = cfg['ec']
     ro = np.zeros(512 * 4, dtype=np.uint64)
     lib.mt_probe_read_rollout.restype = C.c_int
     lib.mt_probe_read_rollout.argtypes = [C.c_void_p, C.c_size_t]
     _lib.check(lib.mt_probe_read_rollout(C.c_void_p(ro.ctypes.data), ro.size), 'mt_probe_read_rollout')
     R = ro.reshape(512, 4)[:E].astype(np.int64)
-    nblocks = {0: 9 * E, 1: 16 * 9 * ((E + 31) // 32), 2: E}
+    nblocks = {0: int((P[0, :, 0] != 0).sum()), 1: 16 * 9 * ((E + 31) // 32), 2: E}  # (conv: 9 or 18 per env)
     t0 = P[0, :nblocks[0], 0].min()
     us = lambda x: x * 0.01  # 100 MHz ticks
     if R[:, 0].any():  # a pull kernel ran (non-stacking chains)
