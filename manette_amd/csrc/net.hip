@@ -248,6 +248,14 @@ using TileFc = Tile<32, 64, 2, 2, 64>;       // dense forward, M = batch (small)
 // 12.1 -> 10.6 us; LSTM dense dW 17.1 -> 13.1 us)
 using TileDenseW = Tile<32, 64, 2, 2, 80>;
 using TileDenseX = Tile<32, 32, 2, 2, 128>;
+// the trunk archs' dense backward (backward_impl). MT_DENSE_BWD_BK (experiment): one K chunk per
+// block at ec = 32 (dW: GEMM-K = 160 rows, dX: GEMM-K = F = 256) — one operand round trip instead
+// of two, at 66 KB of LDS per block
+#ifndef MT_DENSE_BWD_BK
+#define MT_DENSE_BWD_BK 0
+#endif
+using TileDenseWB = std::conditional_t<MT_DENSE_BWD_BK != 0, Tile<32, 64, 2, 2, 160>, TileDenseW>;
+using TileDenseXB = std::conditional_t<MT_DENSE_BWD_BK != 0, Tile<32, 32, 2, 2, 256>, TileDenseX>;
 
 static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
   int s = target / (grid_mn > 0 ? grid_mn : 1);
@@ -628,9 +636,10 @@ struct ReturnsSrc {
 // V(s_T)[e] of the bootstrap (ReturnsSrc::boot_slabs): the dense layer's split-K slabs summed in
 // slab order + bias + act (heads_row's phase 1), then the critic's dot product as heads_row forms
 // it (lanes over features in 64-strides, DPP wave sum, + bias). Called by the whole block; the
-// result is in *vt (LDS) after the call.
+// result is in *vt (LDS) after the call. wcb: wave 0's critic weights Wc[lane + 64 j], loaded by
+// the caller at kernel start (off the slab -> dot chain).
 __device__ __forceinline__ void boot_value(const ReturnsSrc &rs, const HeadParams &hp, int e, int act, float alpha,
-                                           float *hsb, float *vt) {
+                                           const float (&wcb)[8], float *hsb, float *vt) {
   const int F = hp.F;
   for (int f = threadIdx.x; f < F; f += 256) {
     const float *p = rs.boot_slabs + (size_t)e * F + f;
@@ -652,7 +661,7 @@ __device__ __forceinline__ void boot_value(const ReturnsSrc &rs, const HeadParam
     float acc = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (lane + 64 * j < F) acc += hsb[lane + 64 * j] * hp.Wc[lane + 64 * j];
+      if (lane + 64 * j < F) acc += hsb[lane + 64 * j] * wcb[j];
     acc = wave_sum(acc);
     if (lane == 0) *vt = acc + hp.bc[0];
   }
@@ -700,6 +709,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
   __shared__ float ya[2];
   __shared__ float buf[2 * kMaxScan];
   const int b = blockIdx.x;
+  MT_PROBE_AT(4, b, 0);
   const int A = hp.A, R = hp.R, O = 1 + A + R, F = hp.F;
   // Every load that does not depend on the return is issued first, so its latency overlaps the
   // scan's (the rewards / masks are read over PCIe from pinned memory): the row's head inputs
@@ -730,14 +740,24 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
     for (int k = 0; k < KW; ++k)
       wk[fi][k] = !pre ? 0.f : (k < A ? hp.Wa[(size_t)f * A + k] : (k < A + R ? hp.Wr[(size_t)f * R + (k - A)] : 0.f));
   }
+  float wcb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rs.boot_slabs && threadIdx.x < 64) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wcb[j] = hp.Wc[min(lane + 64 * j, F - 1)];
+  }
   if (rs.r) {
     // this row's rewards / masks (pinned host memory, a PCIe round trip) requested first
     float rk = 0.f, mk = 0.f;
     {
       const int t = b / rs.E, e = b - t * rs.E;
       if ((int)threadIdx.x < rs.T - t) {
+#ifdef MT_EXP_RM_LOCAL  // timing experiment only (wrong values): the reward / mask loads from HBM
+        rk = rs.boot_slabs[(size_t)(t + threadIdx.x) * rs.E + e];
+        mk = rs.boot_slabs[(size_t)(rs.T + t + threadIdx.x) * rs.E + e];
+#else
         rk = rs.r[(size_t)(t + threadIdx.x) * rs.E + e];
         mk = rs.mask[(size_t)(t + threadIdx.x) * rs.E + e];
+#endif
       }
     }
     float vt;
@@ -745,14 +765,16 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
       __shared__ float hsb[512];
       __shared__ float vts;
       const int e = b % rs.E;
-      boot_value(rs, hp, e, act, alpha, hsb, &vts);
+      boot_value(rs, hp, e, act, alpha, wcb, hsb, &vts);
       vt = vts;
       if (rs.vt_out && b < rs.E && threadIdx.x == 0) rs.vt_out[e] = vt;
     } else {
       vt = rs.VT[b % rs.E];
     }
+    MT_PROBE_AT(4, b, 1);
     row_return(rs, v, b, vt, rk, mk, ya, buf);
   }
+  MT_PROBE_AT(4, b, 2);
   if (threadIdx.x < 64) {
     const float ad = rs.r ? ya[1] : adv_in;
     const float yb = rs.r ? ya[0] : y_in;
@@ -773,6 +795,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
     }
   }
   __syncthreads();
+  MT_PROBE_AT(4, b, 3);
   for (int o = threadIdx.x; o < O; o += 256) dz[(size_t)b * O + o] = dzs[o];
 #pragma unroll
   for (int fi = 0; fi < FT; ++fi) {
@@ -800,6 +823,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
     for (int k = 0; k < R; ++k) acc += dzs[1 + A + k] * wr[k];
     dH[(size_t)b * F + f] = acc * act_bwd(H[(size_t)b * F + f], act, alpha);
   }
+  MT_PROBE_AT(4, b, 4);
 }
 
 // Head weight/bias gradient: G[f][o] = sum_b [H,1][b][f] * dz[b][o], scattered into the three
@@ -1278,12 +1302,12 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
   const float *flat = layer_out<Ar, K>(ws, L);
   const float *Wfc = P + n->off_fc;
   // dense dW, db: [flat, 1]^T . dH -> grad[(FLAT+1) x F]
-  const auto dw = gemm_job<TileDenseW>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
+  const auto dw = gemm_job<TileDenseWB>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
                                        EpStore{grad + n->off_fc, Ar::F}, Ar::FLAT + 1, Ar::F, B, 1);
   const HeadWgradJob hw = head_wgrad_job<Ar>(n, B, ws, L, grad);
   // dense dX: dH . W^T, masked by the last conv's activation (every trunk ends in an unpooled conv)
   static_assert(!pooled<Ar, K>(), "the trunk ends in an unpooled conv (networks.py:178-278)");
-  const auto dx = gemm_job<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+  const auto dx = gemm_job<TileDenseXB>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
                                        EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1);
 #if MT_DENSE_DW_LATE
   // the dense dX is the only job of this launch on the critical path (the next conv layer's dX

@@ -39,7 +39,7 @@
 // s_memrealtime (100 MHz, one clock for the whole device) of lane 0 at phase boundaries of every
 // block of the rollout-forward kernels, read back with mt_probe_read (tools/probe.py).
 #ifdef MT_PROBE
-static __device__ unsigned long long mt_probe_buf[4 * 1024 * 8];
+static __device__ unsigned long long mt_probe_buf[5 * 1024 * 8];  // kernels 0-2 rollout, 3 conv bwd, 4 loss
 #define MT_PROBE_AT(k, b, p)                                                                     \
   do {                                                                                           \
     if (threadIdx.x == 0 && (b) < 1024) mt_probe_buf[((k) * 1024 + (b)) * 8 + (p)] = __builtin_amdgcn_s_memrealtime(); \

@@ -49,7 +49,7 @@ def main():
     lib = _lib.hip()
     lib.mt_probe_read.restype = C.c_int
     lib.mt_probe_read.argtypes = [C.c_void_p, C.c_size_t]
-    buf = np.zeros(4 * 1024 * 8, dtype=np.uint64)
+    buf = np.zeros(5 * 1024 * 8, dtype=np.uint64)
     for _ in range(a.updates):
         L.book.new_update()
         for t in range(L.max_local_steps):
@@ -74,7 +74,7 @@ def main():
         torch.cuda.synchronize()
     buf[:] = 0
     _lib.check(lib.mt_probe_read(C.c_void_p(buf.ctypes.data), buf.size), 'mt_probe_read')
-    P = buf.reshape(4, 1024, 8).astype(np.int64)
+    P = buf.reshape(5, 1024, 8).astype(np.int64)
     E = cfg['ec']
     ro = np.zeros(512 * 4, dtype=np.uint64)
     lib.mt_probe_read_rollout.restype = C.c_int
@@ -121,6 +121,21 @@ def main():
             print('    %-20s med %6.2f  p90 %6.2f  max %6.2f us' % (nm, us(np.median(d)), us(np.percentile(d, 90)),
                                                                      us(d.max())))
         prev_end = end.max()
+    lb = P[4, :E * L.max_local_steps, :5]
+    if lb[:, 0].any():  # the last update's loss kernel (slot 4) and the conv backward after it (slot 3)
+        t4 = lb[:, 0].min()
+        print('loss   blocks %4d  start %+7.2f..%+7.2f us  end %+7.2f..%+7.2f us  block dur med %.2f max %.2f' % (
+            len(lb), 0.0, us(lb[:, 0].max() - t4), us(lb[:, 4].min() - t4), us(lb[:, 4].max() - t4),
+            us(np.median(lb[:, 4] - lb[:, 0])), us((lb[:, 4] - lb[:, 0]).max())))
+        for j, nm in enumerate(['loads + V(s_T)', 'n-step return', 'head grads', 'dz + dH stores']):
+            d = lb[:, j + 1] - lb[:, j]
+            print('    %-20s med %6.2f  p90 %6.2f  max %6.2f us' % (nm, us(np.median(d)), us(np.percentile(d, 90)),
+                                                                     us(d.max())))
+        cb = P[3, :, 0]
+        cb = cb[cb > t4]
+        if cb.size:
+            print('conv bwd first block start %+7.2f us after the loss kernel start (loss end -> conv bwd start '
+                  '%.2f us: the dense group and two boundaries)' % (us(cb.min() - t4), us(cb.min() - lb[:, 4].max())))
     L.cleanup()
 
 

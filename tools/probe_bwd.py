@@ -43,13 +43,13 @@ def main():
     lib = _lib.hip()
     lib.mt_probe_read.restype = C.c_int
     lib.mt_probe_read.argtypes = [C.c_void_p, C.c_size_t]
-    buf = np.zeros(4 * 1024 * 8, dtype=np.uint64)
+    buf = np.zeros(5 * 1024 * 8, dtype=np.uint64)
     for _ in range(a.reps):
         net.loss_backward(obs, B, v, pi, rep, a_idx, r_idx, y, adv)
         torch.cuda.synchronize()
     _lib.check(lib.mt_probe_read(C.c_void_p(buf.ctypes.data), buf.size), 'mt_probe_read')
     pairs = (B + 1) // 2
-    P = buf.reshape(4, 1024, 8)[3, :B + pairs, :5].astype(np.int64)
+    P = buf.reshape(5, 1024, 8)[3, :B + pairs, :5].astype(np.int64)
     us = lambda x: x * 0.01  # 100 MHz
     t0 = P[:, 0].min()
     img, par = P[:B], P[B:]
