@@ -620,6 +620,9 @@ __device__ __forceinline__ float head_softmax_grad(float p, int lane, int n, int
 
 // One workgroup per row b: head gradients dz[b][0..O) and dH[b][f] = act'(H) * sum_o dz_o W[f][o].
 // Optional n-step scan inside the loss kernel (mt_returns_loss_backward): row b = t*E + e.
+#ifndef MT_LOSS_RM_EARLY
+#define MT_LOSS_RM_EARLY 0
+#endif
 struct ReturnsSrc {
   const float *r = nullptr, *mask = nullptr, *VT = nullptr;  // r / mask [T][E] (host-mapped ok)
   double gamma = 0.0;
@@ -670,9 +673,9 @@ __device__ __forceinline__ void boot_value(const ReturnsSrc &rs, const HeadParam
 
 // returns_kernel's arithmetic for row b = (t, e): R from T-1 down to t, bit-identical to
 // mt_returns. Thread k < 256 brings step t + k's reward / mask in (rk, mk: requested by the caller
-// before its other work, one round trip), the rest load here; thread 0 scans. Called by the whole
-// block.
-__device__ __forceinline__ void row_return(const ReturnsSrc &rs, const float *__restrict__ V, int b, float vt,
+// before its other work, one round trip), the rest load here; thread 0 scans (vb = V[b], which it
+// loaded with the head inputs). Called by the whole block.
+__device__ __forceinline__ void row_return(const ReturnsSrc &rs, float vb, int b, float vt,
                                            float rk, float mk, float *ya, float *buf) {
 #pragma clang fp contract(off)
   const int T = rs.T, E = rs.E;
@@ -692,7 +695,7 @@ __device__ __forceinline__ void row_return(const ReturnsSrc &rs, const float *__
     const double gd = rs.gamma;
     for (int k = n - 2; k >= 0; --k) R = (double)buf[2 * k] + (gd * R) * (double)buf[2 * k + 1];
     ya[0] = (float)R;
-    ya[1] = (float)(R - (double)V[b]);
+    ya[1] = (float)(R - (double)vb);
     rs.y_out[b] = ya[0];
     rs.adv_out[b] = ya[1];
   }
@@ -743,7 +746,8 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
   float wcb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (rs.boot_slabs && threadIdx.x < 64) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) wcb[j] = hp.Wc[min(lane + 64 * j, F - 1)];
+    for (int j = 0; j < 8; ++j)  // (relaxed atomic: an invariant load would be sunk to its use, past two barriers)
+      wcb[j] = __hip_atomic_load(hp.Wc + min(lane + 64 * j, F - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (rs.r) {
     // this row's rewards / masks (pinned host memory, a PCIe round trip) requested first
@@ -755,8 +759,14 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
         rk = rs.boot_slabs[(size_t)(t + threadIdx.x) * rs.E + e];
         mk = rs.boot_slabs[(size_t)(rs.T + t + threadIdx.x) * rs.E + e];
 #else
+#if MT_LOSS_RM_EARLY  // experiment: relaxed agent-scope atomics, so the loads are not sunk to their use
+        rk = __hip_atomic_load(rs.r + (size_t)(t + threadIdx.x) * rs.E + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mk = __hip_atomic_load(rs.mask + (size_t)(t + threadIdx.x) * rs.E + e, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+#else
         rk = rs.r[(size_t)(t + threadIdx.x) * rs.E + e];
         mk = rs.mask[(size_t)(t + threadIdx.x) * rs.E + e];
+#endif
 #endif
       }
     }
@@ -772,7 +782,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
       vt = rs.VT[b % rs.E];
     }
     MT_PROBE_AT(4, b, 1);
-    row_return(rs, v, b, vt, rk, mk, ya, buf);
+    row_return(rs, vb, b, vt, rk, mk, ya, buf);
   }
   MT_PROBE_AT(4, b, 2);
   if (threadIdx.x < 64) {
