@@ -111,8 +111,16 @@ __global__ __launch_bounds__(256) void clip_rmsprop_kernel(
   // reduction instead of following the barrier
   const float lr = *lr_dev;
   if (threadIdx.x < 64) {
+    // every partial of the lane requested before the first add (a rolled loop waited out one load
+    // latency per partial: 8 round trips); the adds stay in index order
+    static_assert(MT_NORM_PARTIALS % 64 == 0, "partials per lane");
+    constexpr int PL = MT_NORM_PARTIALS / 64;
+    float pv[PL];
+#pragma unroll
+    for (int u = 0; u < PL; ++u) pv[u] = partials[threadIdx.x + 64 * u];
     double acc = 0.0;
-    for (int i = threadIdx.x; i < MT_NORM_PARTIALS; i += 64) acc += (double)partials[i];
+#pragma unroll
+    for (int u = 0; u < PL; ++u) acc += (double)pv[u];
     acc = wave_sum_d(acc);
     if (threadIdx.x == 0) {
       const float norm = sqrtf((float)acc);

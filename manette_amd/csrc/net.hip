@@ -855,6 +855,15 @@ __device__ __forceinline__ void head_wgrad_body(const float *__restrict__ H, con
   if (f <= F) {
     int b = b0;
     if (f < F) {
+      // 16 rows' loads in flight per trip (a 4-row trip waited out one load latency per 4 rows);
+      // accumulator u still takes rows b0 + u, b0 + 4 + u, ... in order
+      for (; b + 15 < b1; b += 16) {
+        float h[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) h[u] = H[(size_t)(b + u) * F + f];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) a[u & 3] += h[u] * dzs[b + u];
+      }
       for (; b + 3 < b1; b += 4) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) a[u] += H[(size_t)(b + u) * F + f] * dzs[b + u];
