@@ -158,6 +158,22 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
     zx[t] = 0.f;
     xoff[t] = (size_t)map.row(b, t, z) * G4 + g;
   }
+  // the projection column (threads < NH) and fc6 columns of the epilogue, requested now with the
+  // slab partials (relaxed atomics: plain read-only loads are sunk to their use, behind the STEPS
+  // recurrence barriers, one load latency per 8 products there); same products, same order below
+  constexpr int NN = 1;  // fc6 columns per thread: F <= NN * G4 (the launch sites assert it)
+  float wpc[NH], w6c[NN][NH];
+  const int gp = min(g, NH - 1);
+#pragma unroll
+  for (int m = 0; m < NH; ++m)
+    wpc[m] = __hip_atomic_load(Wp + m * NH + gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    const int nn = min(g + G4 * j, F - 1);
+#pragma unroll
+    for (int k = 0; k < NH; ++k)
+      w6c[j][k] = __hip_atomic_load(W6 + (size_t)k * F + nn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   for (int s0 = 0; s0 < S; s0 += 8) {
     float v[STEPS][8];
 #pragma unroll
@@ -195,18 +211,22 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
   if (g < NH) {
     h5[(size_t)b * NH + g] = hs[g];
     float o = 0.f;
-#pragma unroll 8
-    for (int m = 0; m < NH; ++m) o += hs[m] * Wp[m * NH + g];
+#pragma unroll
+    for (int m = 0; m < NH; ++m) o += hs[m] * wpc[m];
     o += bp[g];
     os[g] = o;
     out32[(size_t)b * NH + g] = o;
   }
   __syncthreads();
-  for (int nn = g; nn < F; nn += G4) {
-    float z6 = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < NH; ++k) z6 += os[k] * W6[(size_t)k * F + nn];
-    slab6[(size_t)b * F + nn] = z6;
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    const int nn = g + G4 * j;
+    if (nn < F) {
+      float z6 = 0.f;
+#pragma unroll
+      for (int k = 0; k < NH; ++k) z6 += os[k] * w6c[j][k];
+      slab6[(size_t)b * F + nn] = z6;
+    }
   }
 }
 
@@ -222,27 +242,51 @@ __global__ __launch_bounds__(128) void lstm_bwd_kernel(const float *__restrict__
   __shared__ float dos[NH], dzs[G4];
   const int b = blockIdx.x, g = threadIdx.x;
   for (int i = g; i < NH * G4; i += G4) khs[i] = Kh[i];
-  if (g < NH) {  // d out = dH W6^T  (fc6 input gradient)
+  // every operand of the window requested up front (relaxed atomics: plain read-only loads are
+  // sunk to their use — one load latency per step and per 8 products otherwise): the projection
+  // row, every step's gates and cell states; same products, same order below
+  const int gc = min(g, NH - 1);
+  float wpr[NH], gt[STEPS][4], cs[STEPS];
+#pragma unroll
+  for (int k = 0; k < NH; ++k) wpr[k] = __hip_atomic_load(Wp + gc * NH + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int t = 0; t < STEPS; ++t) {
+    const float *ga = gates + (size_t)(b * STEPS + t) * G4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gt[t][q] = __hip_atomic_load(ga + q * NH + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cs[t] = __hip_atomic_load(cst + (size_t)(b * STEPS + t) * NH + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (g < NH) {  // d out = dH W6^T  (fc6 input gradient): 32 products' loads per trip, added in order
     float a = 0.f;
     const float *w = W6 + (size_t)g * F;
     const float *d = dH + (size_t)b * F;
-    for (int nn = 0; nn < F; ++nn) a += d[nn] * w[nn];
+    for (int n0 = 0; n0 < F; n0 += 32) {
+      float dv[32], wv[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        dv[u] = d[min(n0 + u, F - 1)];
+        wv[u] = w[min(n0 + u, F - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        if (n0 + u < F) a += dv[u] * wv[u];
+    }
     dos[g] = a;
     dout32[(size_t)b * NH + g] = a;
   }
   __syncthreads();
   float dh = 0.f, dc = 0.f;
   if (g < NH) {  // d h_5 = d out w^T
-#pragma unroll 8
-    for (int k = 0; k < NH; ++k) dh += dos[k] * Wp[g * NH + k];
+#pragma unroll
+    for (int k = 0; k < NH; ++k) dh += dos[k] * wpr[k];
   }
+#pragma unroll
   for (int t = STEPS - 1; t >= 0; --t) {
     const int row = b * STEPS + t;
     if (g < NH) {
-      const float *ga = gates + (size_t)row * G4;
-      const float si = ga[g], tj = ga[NH + g], sf = ga[2 * NH + g], so = ga[3 * NH + g];
-      const float c = cst[(size_t)row * NH + g];
-      const float cp = t > 0 ? cst[(size_t)(row - 1) * NH + g] : 0.f;
+      const float si = gt[t][0], tj = gt[t][1], sf = gt[t][2], so = gt[t][3];
+      const float c = cs[t];
+      const float cp = t > 0 ? cs[t > 0 ? t - 1 : 0] : 0.f;
       const float tc = tanhf(c);
       const float dzo = dh * tc * (so * (1.f - so));
       dc = dc + dh * so * (1.f - tc * tc);
@@ -282,6 +326,7 @@ static int lstm_forward_impl(const mt_net *n, const float *P, const uint8_t *obs
                               EpSlab{ws + X.xg, rows, Ar::G4}, rows, Ar::G4, Ar::FLAT, X.xg_splits, s)));
   const float *Wp = P + n->off_proj;
   const float *W6 = P + n->off_fc;
+  static_assert(Ar::F <= Ar::G4, "lstm_fwd_kernel: one fc6 column per thread");
   hipLaunchKernelGGL((lstm_fwd_kernel<Ar::NH, Ar::STEPS>), dim3(B), dim3(Ar::G4), 0, s, ws + X.xg, X.xg_splits,
                      rows, XgRows{nullptr, 0, 0}, Kh, kb, Wp, Wp + Ar::NH * Ar::NH, W6, Ar::F, 1.0f, ws + X.gates, ws + X.cst,
                      ws + X.hprev, ws + X.h5, ws + X.out32, ws + X.slab6);
@@ -405,9 +450,14 @@ __global__ __launch_bounds__(128) void lstm_zero_partials_kernel(const float *__
   const int g = threadIdx.x, c = blockIdx.x;
   const int per = cdiv(W, gridDim.x);
   float acc = 0.f;
-  for (int w = c * per; w < min(W, (c + 1) * per); ++w) {
+  for (int w = c * per; w < min(W, (c + 1) * per); ++w) {  // (a window's loads in one round trip)
     const int z = nz[w];
-    for (int k = 0; k < z; ++k) acc += dgates[((size_t)w * 5 + k) * 128 + g];
+    float v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[k] = dgates[((size_t)w * 5 + k) * 128 + g];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (k < z) acc += v[k];
   }
   part[(size_t)c * 128 + g] = acc;
 }
@@ -424,10 +474,20 @@ __global__ __launch_bounds__(128) void lstm_gather_dxg_kernel(const float *__res
     for (int c = 0; c < nparts; ++c) acc += zpart[(size_t)c * 128 + g];
   } else {
     const int j = (r - 1) / E, e = (r - 1) % E;
+    // every load first, from clamped addresses (a guarded load ends its block with a wait for it);
+    // the terms that do not apply are skipped as before
+    int zk[5];
+    float v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int tc = min(max(j - k, 0), T - 1);
+      zk[k] = nz[tc * E + e];
+      v[k] = dgates[(((size_t)tc * E + e) * 5 + k) * 128 + g];
+    }
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const int t = j - k;
-      if (t >= 0 && t < T && k >= nz[t * E + e]) acc += dgates[(((size_t)t * E + e) * 5 + k) * 128 + g];
+      if (t >= 0 && t < T && k >= zk[k]) acc += v[k];
     }
   }
   dxg[(size_t)r * 128 + g] = acc;
@@ -460,6 +520,7 @@ static int lstm_windows_fwd_impl(const mt_net *n, const float *P, int32_t *nz_t,
   const float *Kh = P + n->off_lstm + (size_t)Ar::FLAT * Ar::G4;
   const float *Wp = P + n->off_proj;
   const float *W6 = P + n->off_fc;
+  static_assert(Ar::F <= Ar::G4, "lstm_fwd_kernel: one fc6 column per thread");
   hipLaunchKernelGGL((lstm_fwd_kernel<Ar::NH, Ar::STEPS>), dim3(E), dim3(Ar::G4), 0, s, ws + X.xg, X.S, X.R_max,
                      XgRows{nz_t, t, E, nz_prev, over}, Kh, Kh + Ar::NH * Ar::G4, Wp, Wp + Ar::NH * Ar::NH, W6, Ar::F, 1.0f,
                      ws + X.gates + w0 * Ar::STEPS * Ar::G4, ws + X.cst + w0 * Ar::STEPS * Ar::NH,
