@@ -219,10 +219,11 @@ def build_args(cfg, T, sampling, seed, debugging_folder=None):
 
 
 def make_learner(config, T=5, sampling='device', seed=0, staging='resized', pipeline=True, update_graph=True,
-                 rank=0, debugging_folder=None, episode_len=None, comm='rccl'):
+                 rank=0, debugging_folder=None, episode_len=None, comm='rccl', dp_force=False):
     """The benchmarked learner of `config` (BASELINE.json configs[1..4]; tests/test_e2e_gpu.py
     checks exactly this path against the oracle). episode_len: a shorter synthetic episode (tests
-    exercise resets); None = the synthetic default."""
+    exercise resets); None = the synthetic default. dp_force: the data-parallel update (bucketed
+    side-stream all-reduce between three update graphs) even at world 1 (paac.PAACLearner.dp)."""
     from manette_amd.exploration_policy import ExplorationPolicy
     from manette_amd.paac import PAACLearner
     import train as train_cli
@@ -233,6 +234,7 @@ def make_learner(config, T=5, sampling='device', seed=0, staging='resized', pipe
     args.pipeline = pipeline
     args.update_graph = update_graph
     args.comm = comm
+    args.dp_force = dp_force
     np.random.seed(1234 + rank)
     explo = ExplorationPolicy(args)
     net_creator, env_creator = train_cli.get_network_and_environment_creator(args, explo)

@@ -3,8 +3,8 @@
 // trunk (networks.py:261-278): the forward (conv + bias + activation, + the 2x2/2 max pool and its
 // argmax bytes), the backward-data product of the 5x5 layer (dX of a conv whose input is a pooled
 // layer: MaxPoolGrad routing and the activation mask in the epilogue) and the weight gradients of
-// the 5x5 layers (DWgradJob, at the end of the file). Which layers take which product is set by the
-// build knobs below; each non-default one was measured and is documented where it is defined.
+// the 5x5 layers (DWgradJob, at the end of the file). Which layers take which product, and the
+// alternatives that were measured and not adopted, are documented where each choice is made.
 //
 // Why not the generic implicit-im2col GEMM (gemm.h, LdIm2col / LdConvBwdA): there every A element
 // of every K chunk is re-derived from (row, k) — tap / channel divisions, SAME-padding clamps and
@@ -158,33 +158,13 @@ struct DBwdUnpool {
   }
 };
 
-#ifndef MT_DCONV_PERSIST  // one-chunk problems (conv1): persistent blocks, weights staged once —
-#define MT_DCONV_PERSIST 0  // measured no faster (PWYX-RGB conv1 51.7 vs 51.6 us, LSTM 84.2 vs 86.4 us
-#endif                      // at 160 frames, profiles/r03g) and it doubles conv1's VGPRs: off
-
 // ---- tiling ------------------------------------------------------------------------------------
-// Patch pixel stride CS (floats) and extra row padding of the layers whose A-fragment reads
-// (ds_read_b128, lane groups of 16) conflicted: searched with a model of the LDS banks over every
-// tile of the image (tools/lds_banks.py; conflict-free = 4 LDS cycles per read): PWYX conv3
-// forward 8.9 -> 4.4, conv4 10.0 -> 5.0, the 5x5 dX 9.3 -> 4.1, within each one's LDS budget (the
-// conv2 forward's better strides need a patch that halves its occupancy: kept at CI + 4).
-#ifndef MT_DCONV_CS_TABLE  // measured no faster (conv3 / conv4 forward within 1 %), and the 5x5 dX
-#define MT_DCONV_CS_TABLE 0  // slower (168 vs 149 us: its 80 KB patch + weights fit one block per CU): off
-#endif
-constexpr int dconv_cs(int ci, int w, bool pool, int upb) {
-  return !MT_DCONV_CS_TABLE ? (ci % 16 == 0 ? ci + 4 : ci)
-       : (ci == 32 && w == 21 && pool && upb == 16) ? 40
-       : (ci == 64 && w == 10 && !pool && upb == 8) ? 72
-       : (ci == 32 && w == 42 && !pool && upb == 32) ? 40
-       : (ci % 16 == 0 ? ci + 4 : ci);
-}
-constexpr int dconv_row_pad(int ci, int w, bool pool, int upb) {
-  return !MT_DCONV_CS_TABLE ? 0
-       : (ci == 32 && w == 21 && pool && upb == 16) ? 4
-       : (ci == 64 && w == 10 && !pool && upb == 8) ? 6
-       : (ci == 32 && w == 42 && !pool && upb == 32) ? 4
-       : 0;
-}
+// Patch pixel stride CS (floats): CI + 4 for 16-channel multiples (the A-fragment reads of a lane
+// group then spread over the banks). Per-layer strides / row pads from a model of the LDS banks
+// (tools/lds_banks.py: conflict cycles 8 -> 4-5 per read) measured no faster — the reads are
+// latency, not LDS throughput — and cost the 5x5 dX an occupancy level (round 3). Persistent
+// conv1 blocks staging the weights once also measured no faster (round 3, profiles/r03g).
+constexpr int dconv_cs(int ci) { return ci % 16 == 0 ? ci + 4 : ci; }
 
 template <class Pr, int WM_, int WN_, int TMW_, int CK_>
 struct DConvCfg {
@@ -210,8 +190,8 @@ struct DConvCfg {
   static constexpr int RSPAN = RSPAN0 < OH ? RSPAN0 : OH;
   static constexpr int RIN = (RSPAN - 1) * S + KH;
   static constexpr int WP = (OW - 1) * S + KW;                          // patch columns staged
-  static constexpr int CS = dconv_cs(CI, W, Pr::POOL, UPB);           // floats per patch pixel
-  static constexpr int WPX = WP + dconv_row_pad(CI, W, Pr::POOL, UPB);  // patch row stride (pixels)
+  static constexpr int CS = dconv_cs(CI);                             // floats per patch pixel
+  static constexpr int WPX = WP;                                        // patch row stride (pixels)
   static constexpr int ASZ = (RIN * WPX * CS + 3) / 4 * 4;
   static constexpr int CK = CK_ > 0 ? CK_ : KP;  // k per weight chunk
   static_assert(CK % 16 == 0, "chunk of whole 16-k steps");
@@ -426,63 +406,28 @@ static int launch_dconv(const Pr &p, int B, hipStream_t s) {
     attr_set = true;
   }
   const int ntiles = B * D::BPI;
-  int grid = ntiles;
-  if constexpr (D::NCH == 1 && MT_DCONV_PERSIST) {  // weights staged once per block: as many blocks as fit
-    const int per_cu = std::max(1, std::min((int)(160 * 1024 / D::LDS), 16 / D::NW));
-    grid = std::min(ntiles, per_cu * 256);
-  }
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(D::NT), D::LDS, s, p, ntiles);
+  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(D::NT), D::LDS, s, p, ntiles);
   MT_LAUNCHED();
   return MT_OK;
 }
 
-// A 4-wave direct conv as a job of a grouped launch (gemm.h launch_group).
-template <class Pr, int WM, int WN, int TMW, int CK>
-struct DConvJob {
-  using D = DConvCfg<Pr, WM, WN, TMW, CK>;
-  static_assert(D::NW == 4, "group_kernel runs 256-thread blocks");
-  Pr p;
-  int nblk;
-  __host__ __device__ int blocks() const { return nblk; }
-  size_t lds() const { return D::LDS; }
-  __device__ __forceinline__ void run(int id, float *smem) const {
-    const int t = xcd_tile(id, nblk);
-    dconv_body<Pr, WM, WN, TMW, CK>(p, t, t + 1, smem);
-  }
-};
-
-// ---- tile choice per PWYX layer shape (E = 32 frames: conv1 1,792 blocks, conv2 448, conv3
-// 224, conv4 128) ------------------------------------------------------------------------------
-#ifndef MT_DCONV_TMW2  // conv2 (CIN = COUT = 32): 2 M-tiles per wave (32 units per block) or 1
-#define MT_DCONV_TMW2 2
-#endif
-#ifndef MT_DCONV_TMW1  // conv1 (CIN 4 / 12): M-tiles per wave
-#define MT_DCONV_TMW1 2
-#endif
-#ifndef MT_DCONV_STRIDED  // the NATURE trunk's strided VALID convs on the direct forward too
-#define MT_DCONV_STRIDED 1
-#endif
-#ifndef MT_DCONV_C2CK  // conv2 (32 -> 32): k per weight chunk (0: one tap = CIN)
-#define MT_DCONV_C2CK 0
-#endif
-#ifndef MT_DCONV_C2W8  // conv2 (32 -> 32): 8-wave blocks (two N halves), two blocks per CU: four
-#define MT_DCONV_C2W8 1  // waves per SIMD hide the per-chunk barrier (PWYX-RGB E=32 33.4 vs 36.7 us,
-#endif                   // LSTM 161 frames 143.6 vs 157.5 us, profiles/r03i)
-#ifndef MT_DCONV_C1W8  // conv1 (CIN 4 / 12): 8-wave blocks
-#define MT_DCONV_C1W8 0
-#endif
-#ifndef MT_DCONV_W8  // 8-wave blocks for the small-grid layers (conv3, conv4)
-#define MT_DCONV_W8 1
-#endif
+// ---- tile choice per layer shape (PWYX E = 32 frames: conv1 1,792 blocks, conv2 448, conv3 224,
+// conv4 128) ----------------------------------------------------------------------------------
+//  conv1 (CIN 4 / 12, the whole K in one chunk): 4 waves, 2 M-tiles per wave (8-wave blocks measured
+//    no faster); the strided NATURE conv1 1 M-tile;
+//  conv2 (32 -> 32): 8-wave blocks (two N halves), two blocks per CU: four waves per SIMD hide the
+//    per-chunk barrier (PWYX-RGB E=32 33.4 vs 36.7 us, LSTM 161 frames 143.6 vs 157.5 us,
+//    profiles/r03i); 2 M-tiles per wave; one tap (CIN k) per weight chunk (5-tap chunks: no faster);
+//  64 output channels (conv3, conv4, NATURE conv2 / conv3): 8-wave blocks for the small grids
+//    (18.2 -> 15.3 us and 11.0 -> 10.1 us), 1 M-tile per wave.
 template <class G, bool POOL>
 struct DConvFor {
   static constexpr bool SMALLC = G::CIN % 16 != 0;  // conv1: the whole K in one chunk
   static constexpr bool C64 = G::COUT >= 64;
-  static constexpr int WN = C64 ? (MT_DCONV_W8 ? (POOL ? 2 : 4) : (POOL ? 1 : 2))
-                                : (SMALLC ? (MT_DCONV_C1W8 ? 2 : 1) : (MT_DCONV_C2W8 ? 2 : 1));
-  static constexpr int WM = C64 ? (MT_DCONV_W8 ? (POOL ? 4 : 2) : (POOL ? 4 : 2)) : 4;
-  static constexpr int TMW = SMALLC ? (G::S > 1 ? 1 : MT_DCONV_TMW1) : (C64 ? 1 : MT_DCONV_TMW2);
-  static constexpr int CK = SMALLC ? 0 : (!C64 && MT_DCONV_C2CK ? MT_DCONV_C2CK : G::CIN);
+  static constexpr int WN = C64 ? (POOL ? 2 : 4) : (SMALLC ? 1 : 2);
+  static constexpr int WM = C64 ? (POOL ? 4 : 2) : 4;
+  static constexpr int TMW = SMALLC ? (G::S > 1 ? 1 : 2) : (C64 ? 1 : 2);
+  static constexpr int CK = SMALLC ? 0 : G::CIN;
 };
 
 template <class G, bool U8, bool POOL>
@@ -494,31 +439,15 @@ static int conv_forward_direct(const void *X, const float *W, const float *bias,
   return launch_dconv<Pr, F::WM, F::WN, F::TMW, F::CK>(p, B, s);
 }
 
-// dX of stride-1 conv G unpooled into GJ's conv-output gradient.
-//  MT_DCONV_BWD = 1: as a job of the layer's grouped backward launch (4 waves): slower than the
-//    generic GEMM dX there (PWYX-RGB conv2 group 417 vs 370 us, LSTM 751 vs 679 us,
-//    profiles/r03d/c4_*): its 54-88 KB patch sets the LDS of every block of the group, so the
-//    weight-gradient GEMM blocks beside it lose occupancy;
-//  2: its own 8-wave launch ahead of the (weight-gradient) group, every pooled-input layer;
-//  3 (default): that, for the 5x5 32 -> 32 layer only (conv2: PWYX-RGB dX 147 + dW group 193 us
-//    vs 370 grouped, LSTM 257 + 367 vs 679, profiles/r03d/c5_*; conv3's dX alone was slower: 83
-//    + 62 vs 123 us);
-//  0: the generic GEMM dX for every layer.
-#ifndef MT_DCONV_BWD
-#define MT_DCONV_BWD 3
-#endif
+// dX of stride-1 conv G unpooled into GJ's conv-output gradient: its own 8-wave launch ahead of the
+// (weight-gradient) group, for the 5x5 32 -> 32 layer only (conv2: PWYX-RGB dX 147 + dW group 193 us
+// vs 370 for the generic GEMM dX in the group, LSTM 257 + 367 vs 679, profiles/r03d/c5_*). Measured
+// and not adopted: the direct dX as a 4-wave job of the grouped launch (its 54-88 KB patch sets the
+// LDS of every block of the group, so the weight-gradient blocks beside it lose occupancy: 417 vs
+// 370 us), and conv3's dX in its own launch (83 + 62 vs 123 us).
 template <class G>
 constexpr bool dconv_bwd_solo() {
-  return MT_DCONV_BWD == 2 || (MT_DCONV_BWD == 3 && G::KH == 5 && G::CIN == 32 && G::COUT == 32);
-}
-template <class G, class GJ>
-using DBwdJob = DConvJob<DBwdUnpool<G, GJ>, 4, 1, (G::CIN >= 64 ? 1 : 2), G::COUT>;
-
-template <class G, class GJ>
-static DBwdJob<G, GJ> conv_dgrad_unpool_direct(const float *dY, const float *Wt, const float *Pj, const uint8_t *argj,
-                                               float *dactj, int B, int act, float alpha) {
-  using J = DBwdJob<G, GJ>;
-  return J{DBwdUnpool<G, GJ>{dY, Wt, Pj, argj, dactj, act, alpha}, B > 0 ? B * J::D::BPI : 0};
+  return G::KH == 5 && G::CIN == 32 && G::COUT == 32;
 }
 
 template <class G, class GJ>
@@ -705,22 +634,14 @@ struct DWgradJob {
   }
 };
 
-// Which stride-1 SAME layers take the direct weight gradient. MT_DCONV_WGRAD = 1 (default): the
-// 5x5 layers (PWYX / LSTM conv1, conv2: PWYX-RGB conv1 272 vs 345 us, conv2 161 vs 196 us; LSTM
-// conv2 281 vs 373, conv1 186 vs 267; profiles/r03e_*); the 4x4 / 3x3 layers (conv3, conv4) were
-// slower direct (PWYX conv3 group 151 vs 125 us, LSTM 262 vs 210, conv4 79 vs 60) and stay on the
-// generic GEMM. 2: every stride-1 SAME layer. 0: none.
-#ifndef MT_DCONV_WGRAD
-#define MT_DCONV_WGRAD 1
-#endif
-#ifndef MT_DCONV_WGRAD_STRIDED  // the strided VALID layers (NATURE, NIPS RGB conv2) direct too:
-#define MT_DCONV_WGRAD_STRIDED 0  // parity-green but slower (NATURE E=64 conv2 dX + dW group 94 vs 60 us,
-#endif                            // conv3 53 vs 46, conv1 dW 36 vs 33; profiles/r03k; in launches of
-                                  // their own after the generic dX: 49 + 42 vs 60, profiles/r03n): off
+// Which layers take the direct weight gradient: the 5x5 stride-1 SAME layers (PWYX / LSTM conv1,
+// conv2: PWYX-RGB conv1 272 vs 345 us, conv2 161 vs 196 us; LSTM conv2 281 vs 373, conv1 186 vs 267;
+// profiles/r03e_*). Measured slower direct and left on the generic GEMM: the 4x4 / 3x3 layers (PWYX
+// conv3 group 151 vs 125 us, LSTM 262 vs 210, conv4 79 vs 60) and the strided VALID layers (NATURE
+// E=64 conv2 dX + dW group 94 vs 60 us, conv3 53 vs 46; profiles/r03k, r03n).
 template <class G>
 constexpr bool dconv_wgrad() {
-  return (G::S == 1 && G::SAME && (MT_DCONV_WGRAD == 2 || (MT_DCONV_WGRAD == 1 && G::KH == 5))) ||
-         (MT_DCONV_WGRAD_STRIDED && !G::SAME && G::CIN != 12 && G::COUT >= 32);
+  return G::S == 1 && G::SAME && G::KH == 5;
 }
 // M-tiles per wave: 5 (4 for 64 output channels), or for a short K (the gray conv1: 7 M-tiles of
 // (tap, ci) rows) just enough for one tap group — 5 would leave 3 of its 10 tile slots empty

@@ -26,13 +26,6 @@
 
 #include "common.h"
 
-#ifndef MT_GEMM_PF2  // two register buffers: global loads two K chunks ahead (gemm_body_t)
-#define MT_GEMM_PF2 0
-#endif
-#ifndef MT_GEMM_DUAL  // two accumulators for one-tile waves (gemm_body_t); its different summation
-#define MT_GEMM_DUAL 0  // order flips near-zero ReLU decisions, which the oracle follows
-#endif
-
 namespace mt {
 
 template <int BM_, int BN_, int WM_, int WN_, int BK_ = 32>
@@ -106,11 +99,11 @@ struct HasKs<L, std::void_t<typename L::KS>> : std::true_type {
 // (tap, channel) decomposition, computed once per tile in init) and the per-k remainder
 // (fetch_ctx, or the k state above): the integer divisions of an implicit im2col run once, not
 // once per chunk.
-template <class LD, int ROWS, int BK, int NB = 1>
+template <class LD, int ROWS, int BK>
 struct Stage {
   using S = LdsShape<LD::KMAJOR, ROWS, BK>;
   static constexpr bool KST = HasKs<LD>::value;
-  f32x4 r[NB][S::ITEMS];  // NB register buffers: chunk c lands in r[c % NB] (slots are compile-time)
+  f32x4 r[S::ITEMS];
   typename LD::Ctx cx[S::ITEMS];
   typename HasKs<LD>::KS ks[KST ? S::ITEMS : 1];
   __device__ __forceinline__ void init(const LD &ld, int row0, int kb) {
@@ -128,7 +121,6 @@ struct Stage {
   // Interior tiles (uniform per workgroup) take the branch-free fetch: every load of the chunk
   // is issued back to back and waited for once (a per-element guarded load would make hipcc
   // wait vmcnt(0) per element — cdna_hip_programming.md §5 trap (c)).
-  template <int SLOT = 0>
   __device__ __forceinline__ void load(const LD &ld, int row0, int k0, int ke, int nrows) {
     if (ld.interior(row0, ROWS, k0, BK, ke, nrows)) {
 #pragma unroll
@@ -138,9 +130,9 @@ struct Stage {
           int rr, kk;
           item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
           if constexpr (KST)
-            r[SLOT][i] = ld.fetch_ks(cx[i], ks[i]);
+            r[i] = ld.fetch_ks(cx[i], ks[i]);
           else
-            r[SLOT][i] = ld.fetch_ctx(cx[i], k0 + kk);
+            r[i] = ld.fetch_ctx(cx[i], k0 + kk);
         }
       }
     } else {
@@ -150,7 +142,7 @@ struct Stage {
         if (S::QUADS % 256 == 0 || it < S::QUADS) {
           int rr, kk;
           item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
-          r[SLOT][i] = ld.fetch(row0, rr, k0, kk, ke, nrows);
+          r[i] = ld.fetch(row0, rr, k0, kk, ke, nrows);
         }
       }
     }
@@ -159,7 +151,6 @@ struct Stage {
       for (int i = 0; i < S::ITEMS; ++i) ld.template next<BK>(ks[i]);
     }
   }
-  template <int SLOT = 0>
   __device__ __forceinline__ void store(float *L) const {
 #pragma unroll
     for (int i = 0; i < S::ITEMS; ++i) {
@@ -167,7 +158,7 @@ struct Stage {
       if (S::QUADS % 256 == 0 || it < S::QUADS) {
         int rr, kk;
         item_pos<LD::KMAJOR, ROWS, BK>(it, rr, kk);
-        lds_put<LD::KMAJOR, ROWS, BK>(L, rr, kk, r[SLOT][i]);
+        lds_put<LD::KMAJOR, ROWS, BK>(L, rr, kk, r[i]);
       }
     }
   }
@@ -237,35 +228,21 @@ __device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP
   const int wm = w / T::WN, wn = w % T::WN;
   const int r = lane & 15, g = lane >> 4;
 
-  // One-tile waves (TM = TN = 1) would chain every MFMA on one accumulator: the dependent latency
-  // of v_mfma_f32_16x16x4_f32 (40 cycles) exceeds its issue interval (32), so the k steps alternate
-  // between two accumulators (s even / odd), added once at the end.
-  constexpr bool DUAL = MT_GEMM_DUAL && T::TM * T::TN == 1;
   f32x4 acc[T::TM][T::TN];
-  f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < T::TM; ++i)
 #pragma unroll
     for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Register prefetch: chunk c's global loads are issued while chunk c - 1 (PF = 1) or, with two
-  // register buffers (MT_GEMM_PF2), chunks c - 2 and c - 1 are multiplied — a gathered operand's
-  // latency then has two chunks of MFMAs to hide under instead of one.
-  constexpr int NB = (MT_GEMM_PF2 && LdsShape<LA::KMAJOR, T::BM, T::BK>::ITEMS + LdsShape<LB::KMAJOR, T::BN, T::BK>::ITEMS <= 8)
-                         ? 2 : 1;  // (a second buffer of more than 32 VGPRs would cost occupancy)
-  Stage<LA, T::BM, T::BK, NB> sa;
-  Stage<LB, T::BN, T::BK, NB> sb;
+  // Register prefetch: chunk c's global loads are issued while chunk c - 1 is multiplied (a second
+  // register buffer two chunks ahead measured no faster).
+  Stage<LA, T::BM, T::BK> sa;
+  Stage<LB, T::BN, T::BK> sb;
   sa.init(la, m0, kb);
   sb.init(lb, n0, kb);
   if (kb < ke) {
-    sa.template load<0>(la, m0, kb, ke, M);
-    sb.template load<0>(lb, n0, kb, ke, N);
-  }
-  if constexpr (NB == 2) {
-    if (kb + T::BK < ke) {
-      sa.template load<1>(la, m0, kb + T::BK, ke, M);
-      sb.template load<1>(lb, n0, kb + T::BK, ke, N);
-    }
+    sa.load(la, m0, kb, ke, M);
+    sb.load(lb, n0, kb, ke, N);
   }
   // Two-phase epilogue (EP::Pre): every operand load of the lane's outputs (a bias, the activation
   // whose derivative masks a dX, a pool's argmax) depends only on the tile, so it is issued here,
@@ -300,58 +277,26 @@ __device__ __forceinline__ void gemm_body_t(const LA &la, const LB &lb, const EP
 #pragma unroll
       for (int j = 0; j < T::TN; ++j)
         b[j] = load_frag<LB::KMAJOR, T::BN, T::BK>(Bs, (wn * T::TN + j) * 16 + r, kc * 16 + g * 4);
-      if constexpr (DUAL) {
-        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][0], b[0][0], acc[0][0], 0, 0, 0);
-        acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][1], b[0][1], acc2, 0, 0, 0);
-        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][2], b[0][2], acc[0][0], 0, 0, 0);
-        acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][3], b[0][3], acc2, 0, 0, 0);
-      } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int i = 0; i < T::TM; ++i)
+        for (int i = 0; i < T::TM; ++i)
 #pragma unroll
-            for (int j = 0; j < T::TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
-      }
+          for (int j = 0; j < T::TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
     }
   };
-  if constexpr (NB == 1) {
-    for (int k0 = kb; k0 < ke; k0 += T::BK) {
-      sa.store(As);
-      sb.store(Bs);
-      __syncthreads();
-      if (k0 + T::BK < ke) {  // prefetch the next chunk while this one is multiplied
-        sa.load(la, m0, k0 + T::BK, ke, M);
-        sb.load(lb, n0, k0 + T::BK, ke, N);
-      }
-      compute(k0);
-      __syncthreads();
+  for (int k0 = kb; k0 < ke; k0 += T::BK) {
+    sa.store(As);
+    sb.store(Bs);
+    __syncthreads();
+    if (k0 + T::BK < ke) {  // prefetch the next chunk while this one is multiplied
+      sa.load(la, m0, k0 + T::BK, ke, M);
+      sb.load(lb, n0, k0 + T::BK, ke, N);
     }
-  } else {
-    for (int k0 = kb; k0 < ke; k0 += 2 * T::BK) {  // two chunks per trip: the buffer slots stay static
-      sa.template store<0>(As);
-      sb.template store<0>(Bs);
-      __syncthreads();
-      if (k0 + 2 * T::BK < ke) {
-        sa.template load<0>(la, m0, k0 + 2 * T::BK, ke, M);
-        sb.template load<0>(lb, n0, k0 + 2 * T::BK, ke, N);
-      }
-      compute(k0);
-      __syncthreads();
-      if (k0 + T::BK >= ke) break;
-      sa.template store<1>(As);
-      sb.template store<1>(Bs);
-      __syncthreads();
-      if (k0 + 3 * T::BK < ke) {
-        sa.template load<1>(la, m0, k0 + 3 * T::BK, ke, M);
-        sb.template load<1>(lb, n0, k0 + 3 * T::BK, ke, N);
-      }
-      compute(k0 + T::BK);
-      __syncthreads();
-    }
+    compute(k0);
+    __syncthreads();
   }
-  if constexpr (DUAL) acc[0][0] += acc2;
 
   if constexpr (HasPre<EP>::value) {
 #pragma unroll
@@ -405,13 +350,9 @@ template <class T, class LA, class LB, class EP>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(LA la, LB lb, EP ep, int M, int N, int K,
                                                        int kchunk) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-#ifdef MT_NO_XCD_TILES
-  gemm_body<T>(la, lb, ep, M, N, K, kchunk, blockIdx.x, blockIdx.y, blockIdx.z, smem);
-#else
   const int gx = gridDim.x, gy = gridDim.y;
   const int t = xcd_tile(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
   gemm_body<T>(la, lb, ep, M, N, K, kchunk, t % gx, (t / gx) % gy, t / (gx * gy), smem);
-#endif
 }
 
 template <class T, class LA, class LB>
@@ -468,9 +409,7 @@ struct GemmJob {
   __host__ __device__ int blocks() const { return gx * gy * gz; }
   size_t lds() const { return gemm_lds_bytes<T, LA, LB>(); }
   __device__ __forceinline__ void run(int id, float *smem) const {
-#ifndef MT_NO_XCD_TILES
     id = xcd_tile(id, blocks());  // (a job's offset in its group only renames the residue classes)
-#endif
     const int bx = id % gx, t = id / gx;
     gemm_body<T>(la, lb, ep, M, N, K, kchunk, bx, t % gy, t / gy, smem);
   }
@@ -512,13 +451,6 @@ __global__ __launch_bounds__(256) void group_kernel(J... j) {
 // One grid for any number of jobs (blocks in argument order: put the critical path first).
 template <class... J>
 inline int launch_group(hipStream_t s, const J &...j) {
-#ifdef MT_SPLIT_GROUPS  // experiment builds: every job of a group in its own launch (per-job rocprof times)
-  if constexpr (sizeof...(J) > 1) {
-    int rc = MT_OK;
-    ((rc = rc == MT_OK ? launch_group(s, j) : rc), ...);
-    return rc;
-  }
-#endif
   const int nb = (0 + ... + j.blocks());
   if (nb == 0 || !launch_allowed()) return MT_OK;
   size_t lds = 0;
@@ -610,21 +542,11 @@ struct LdColMajor {
   }
   // The guarded (edge) fetch. A row quad wholly inside [0, nx) — every quad of the conv weight
   // gradients' dY operand — is one load from a clamped k (k0 < ke is always in range) and a
-  // zero by select: no branch around the load and no partial register-quad fill (the round-2
-  // form, kept under MT_EXP_OLD_GUARD for tools/dual_diag.py, is compared in tools/gemm_repro.hip;
-  // DESIGN.md §8).
+  // zero by select: no branch around the load and no partial register-quad fill.
   __device__ __forceinline__ f32x4 fetch(int row0, int rr, int k0, int kk, int ke, int nrows) const {
     const int row = row0 + rr, k = k0 + kk;
     const int nx = ones_row >= 0 ? ones_row : nrows;
     const bool kok = k < ke;
-#ifdef MT_EXP_OLD_GUARD  // diagnosis builds only (tools/dual_diag.py): the round-2 form
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (kok) {
-      const float *p = X + (size_t)k * ld + row;
-      if (row + 3 < nx && (ld & 3) == 0) {
-        v = *reinterpret_cast<const f32x4 *>(p);
-      } else {
-#else
     if (row + 3 < nx && (ld & 3) == 0) {
       const f32x4 v = *reinterpret_cast<const f32x4 *>(X + (size_t)(kok ? k : k0) * ld + row);
       return kok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -632,14 +554,11 @@ struct LdColMajor {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (kok) {
       const float *p = X + (size_t)k * ld + row;
-      {
-#endif
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int rw = row + e;
-          if (rw < nx) v[e] = p[e];
-          else if (rw == ones_row) v[e] = 1.f;
-        }
+      for (int e = 0; e < 4; ++e) {
+        const int rw = row + e;
+        if (rw < nx) v[e] = p[e];
+        else if (rw == ones_row) v[e] = 1.f;
       }
     }
     return v;

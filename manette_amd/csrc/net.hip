@@ -62,14 +62,11 @@ template <class Ar, int I>
 using LayerG = std::tuple_element_t<I, typename Ar::Layers>;
 
 // The NIPS gray trunk's conv backward as one launch of per-image workgroups (nips_bwd.h) instead of
-// the layered trunk_backward (experiment builds: MT_NIPS_FUSED_BWD=0 for the layered path).
-#ifndef MT_NIPS_FUSED_BWD
-#define MT_NIPS_FUSED_BWD 1
-#endif
+// the layered trunk_backward.
 template <class Ar>
 constexpr bool nips_fused_bwd() {
   if constexpr (Ar::LSTM || Ar::NCONV != 2 || Ar::FUSED_SLABS == 0) return false;
-  else return MT_NIPS_FUSED_BWD && LayerG<Ar, 0>::CIN == 4;
+  else return LayerG<Ar, 0>::CIN == 4;
 }
 template <class Ar, int I>
 constexpr bool pooled() {
@@ -200,47 +197,33 @@ template <int N, int BK>
 struct TileFor {
   using T = Tile<64, 64, 2, 2, BK>;
 };
-// Thin-N conv tiles (COUT or CIN of 16 / 32): the 4 waves split M, each wave TM = MT_THIN_BM/64
-// 16-row fragments, so one B fragment feeds TM MFMAs. BK is capped so the A stage stays <= 64 KB.
-#ifndef MT_THIN_BM
-#define MT_THIN_BM 64
-#endif
-constexpr int thin_bk(int bk) { return MT_THIN_BM * (bk + 4) * 4 > 98304 && bk % 32 == 0 ? thin_bk(bk / 2) : bk; }
+// Thin-N conv tiles (COUT or CIN of 16 / 32): the 4 waves split M, one 16-row fragment each
+// (128 / 256-row thin tiles measured slower). BK is capped so the A stage stays <= 96 KB.
+constexpr int kThinBM = 64;
+constexpr int thin_bk(int bk) { return kThinBM * (bk + 4) * 4 > 98304 && bk % 32 == 0 ? thin_bk(bk / 2) : bk; }
 template <int BK>
 struct TileFor<16, BK> {
-  using T = Tile<MT_THIN_BM, 16, 4, 1, thin_bk(BK)>;
+  using T = Tile<kThinBM, 16, 4, 1, thin_bk(BK)>;
 };
 template <int BK>
 struct TileFor<32, BK> {
-  using T = Tile<MT_THIN_BM, 32, 4, 1, thin_bk(BK)>;
+  using T = Tile<kThinBM, 32, 4, 1, thin_bk(BK)>;
 };
 
 // K-chunk of a forward conv: the whole K when it fits 256, else the largest of 256/192/128
 // dividing it (one fill per chunk, all loads of a chunk in flight together).
-#ifndef MT_CONV_BK_CAP  // experiment builds: a smaller forward K chunk (with MT_GEMM_PF2: deeper prefetch)
-#define MT_CONV_BK_CAP 256
-#endif
-template <int K>
-constexpr int conv_bk_full() {
-  return K <= 256 ? ((K + 15) / 16) * 16 : (K % 256 == 0 ? 256 : (K % 192 == 0 ? 192 : 128));
-}
 template <int K>
 constexpr int conv_bk() {
-  return conv_bk_full<K>() <= MT_CONV_BK_CAP ? conv_bk_full<K>() : MT_CONV_BK_CAP;
+  return K <= 256 ? ((K + 15) / 16) * 16 : (K % 256 == 0 ? 256 : (K % 192 == 0 ? 192 : 128));
 }
 
 template <class G>
 using TileConvFwd = typename TileFor<G::COUT, conv_bk<G::KK>()>::T;
-#ifndef MT_WGRAD_BK
-#define MT_WGRAD_BK 64
-#endif
 template <class G>
-using TileConvWgrad = typename TileFor<G::COUT, MT_WGRAD_BK>::T;
-#ifndef MT_DGRAD_BK  // 64: half the LDS of 128, twice the resident workgroups (LSTM conv2 dX -5 %, Pong conv2 dX -7 %)
-#define MT_DGRAD_BK 64
-#endif
+using TileConvWgrad = typename TileFor<G::COUT, 64>::T;
+// dX: BK 64 = half the LDS of 128, twice the resident workgroups (LSTM conv2 dX -5 %, Pong conv2 dX -7 %)
 template <class G>
-using TileConvDgrad = typename TileFor<G::CIN, MT_DGRAD_BK>::T;
+using TileConvDgrad = typename TileFor<G::CIN, 64>::T;
 
 using TileFc = Tile<32, 64, 2, 2, 64>;       // dense forward, M = batch (small), split-K
 // dense dW (GEMM-K = batch: 160 = 2 chunks at ec=32) and dX (GEMM-K = F, M = batch): latency-bound
@@ -248,14 +231,6 @@ using TileFc = Tile<32, 64, 2, 2, 64>;       // dense forward, M = batch (small)
 // 12.1 -> 10.6 us; LSTM dense dW 17.1 -> 13.1 us)
 using TileDenseW = Tile<32, 64, 2, 2, 80>;
 using TileDenseX = Tile<32, 32, 2, 2, 128>;
-// the trunk archs' dense backward (backward_impl). MT_DENSE_BWD_BK (experiment): one K chunk per
-// block at ec = 32 (dW: GEMM-K = 160 rows, dX: GEMM-K = F = 256) — one operand round trip instead
-// of two, at 66 KB of LDS per block
-#ifndef MT_DENSE_BWD_BK
-#define MT_DENSE_BWD_BK 0
-#endif
-using TileDenseWB = std::conditional_t<MT_DENSE_BWD_BK != 0, Tile<32, 64, 2, 2, 160>, TileDenseW>;
-using TileDenseXB = std::conditional_t<MT_DENSE_BWD_BK != 0, Tile<32, 32, 2, 2, 256>, TileDenseX>;
 
 static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
   int s = target / (grid_mn > 0 ? grid_mn : 1);
@@ -269,13 +244,8 @@ static int pick_splits(int grid_mn, int K, int bk, int target = 512) {
 // at most kWgradChunks BK-chunks (each chunk is one load latency: with only M x N / 1024 MFMA
 // tiles per wave the chunk chain, not the MFMA, sets a block's time), capped so the partial slabs
 // stay <= kSlabFloats.
-#ifndef MT_WGRAD_CHUNKS
-#define MT_WGRAD_CHUNKS 4
-#endif
-#ifndef MT_DENSE_DW_LATE  // experiment: the dense weight gradient in the first conv layer's launch
-#define MT_DENSE_DW_LATE 0  // (backward_impl; measured: Pong backward 53 vs 51 us, off)
-#endif
-constexpr int kWgradChunks = MT_WGRAD_CHUNKS;
+// (4 K-chunks of 64 per block: re-checked against 1, 2, 8, 16 — DESIGN §8)
+constexpr int kWgradChunks = 4;
 constexpr size_t kSlabFloats = (size_t)4 << 20;
 template <class G>
 static int conv_wgrad_splits(int B) {
@@ -620,9 +590,6 @@ __device__ __forceinline__ float head_softmax_grad(float p, int lane, int n, int
 
 // One workgroup per row b: head gradients dz[b][0..O) and dH[b][f] = act'(H) * sum_o dz_o W[f][o].
 // Optional n-step scan inside the loss kernel (mt_returns_loss_backward): row b = t*E + e.
-#ifndef MT_LOSS_RM_EARLY
-#define MT_LOSS_RM_EARLY 0
-#endif
 struct ReturnsSrc {
   const float *r = nullptr, *mask = nullptr, *VT = nullptr;  // r / mask [T][E] (host-mapped ok)
   double gamma = 0.0;
@@ -755,19 +722,8 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
     {
       const int t = b / rs.E, e = b - t * rs.E;
       if ((int)threadIdx.x < rs.T - t) {
-#ifdef MT_EXP_RM_LOCAL  // timing experiment only (wrong values): the reward / mask loads from HBM
-        rk = rs.boot_slabs[(size_t)(t + threadIdx.x) * rs.E + e];
-        mk = rs.boot_slabs[(size_t)(rs.T + t + threadIdx.x) * rs.E + e];
-#else
-#if MT_LOSS_RM_EARLY  // experiment: relaxed agent-scope atomics, so the loads are not sunk to their use
-        rk = __hip_atomic_load(rs.r + (size_t)(t + threadIdx.x) * rs.E + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mk = __hip_atomic_load(rs.mask + (size_t)(t + threadIdx.x) * rs.E + e, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-#else
         rk = rs.r[(size_t)(t + threadIdx.x) * rs.E + e];
         mk = rs.mask[(size_t)(t + threadIdx.x) * rs.E + e];
-#endif
-#endif
       }
     }
     float vt;
@@ -1006,13 +962,8 @@ static auto conv_dgrad_unpool_job(const float *dY, const float *Wt, const float 
                                   float *dactj, int B, int act, float alpha) {
   using T = TileConvDgrad<G>;
   static_assert(!PhaseGeom<G>::OK, "pooled inputs feed stride-1 convs (networks.py:206-225)");
-#ifdef MT_EXP_DX_POOLED_EP  // timing experiment only (wrong gradient): the pooled-resolution epilogue
-  return gemm_job<T>(LdConvBwdA<G>{dY}, LdConvBwdB<G>{Wt}, EpMasked{dactj, Pj, G::CIN, act, alpha},
-                     B * G::H * G::W, G::CIN, G::KH * G::KW * G::COUT, 1);
-#else
   return gemm_job<T>(LdConvBwdA<G>{dY}, LdConvBwdB<G>{Wt}, EpMaskedUnpool<GJ>{dactj, Pj, argj, act, alpha},
                      B * G::H * G::W, G::CIN, G::KH * G::KW * G::COUT, 1);
-#endif
 }
 
 #define MT_TRY(x)              \
@@ -1020,10 +971,6 @@ static auto conv_dgrad_unpool_job(const float *dY, const float *Wt, const float 
     int rc_ = (x);             \
     if (rc_ != MT_OK) return rc_; \
   } while (0)
-
-#ifndef MT_DCONV  // direct conv for the stride-1 SAME layers (0: the generic implicit-im2col GEMM)
-#define MT_DCONV 1
-#endif
 
 template <class Ar, int I>
 static const float *layer_out(float *ws, const WsLayout &L) {
@@ -1036,16 +983,13 @@ static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, 
   if constexpr (I < Ar::NCONV) {
     using G = LayerG<Ar, I>;
     const float *W = P + n->off_conv[I];
-#if MT_DCONV
     // PWYX / LSTM frame trunk (stride-1 SAME) and NATURE (strided VALID): direct conv, patch in LDS (dconv.h)
     // (the RGB NATURE conv1's 768-deep K with its 24-row patch exceeds the LDS: generic)
-    if constexpr ((G::S == 1 && G::SAME) || (MT_DCONV_STRIDED && Ar::NCONV == 3 && !G::SAME && G::CIN != 12))
+    if constexpr ((G::S == 1 && G::SAME) || (Ar::NCONV == 3 && !G::SAME && G::CIN != 12))
       MT_TRY((conv_forward_direct<G, I == 0, pooled<Ar, I>()>(
           x, W, W + G::KK * G::COUT, ws + (pooled<Ar, I>() ? L.pool[I] : L.act[I]),
           pooled<Ar, I>() ? (uint8_t *)(ws + L.parg[I]) : nullptr, B, n->cfg.activation, n->cfg.alpha_leaky, s)));
-    else
-#endif
-    if constexpr (pooled<Ar, I>())
+    else if constexpr (pooled<Ar, I>())
       MT_TRY((conv_forward_pool<G, I == 0>(x, W, W + G::KK * G::COUT, ws + L.pool[I], (uint8_t *)(ws + L.parg[I]), B,
                                            n->cfg.activation, n->cfg.alpha_leaky, s)));
     else
@@ -1088,11 +1032,6 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
       MT_TRY((conv_dgrad_unpool_solo<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act, al, s)));
       MT_TRY(launch_group(s, wg.gemm, pending, extra));
-    } else if constexpr (pooled<Ar, J>() && MT_DCONV_BWD == 1 && G::S == 1 && G::SAME) {  // direct conv (dconv.h)
-      MT_TRY(launch_group(s, conv_dgrad_unpool_direct<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
-                                                              (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B,
-                                                              act, al),
-                          wg.gemm, pending, extra));
     } else if constexpr (pooled<Ar, J>()) {
       MT_TRY(launch_group(s, conv_dgrad_unpool_job<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
                                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act,
@@ -1299,6 +1238,11 @@ static int heads_backward(const mt_net *n, const float *P, int B, float *ws, con
   return launch_group(s, head_wgrad_job<Ar>(n, B, ws, L, grad));
 }
 
+// Launches of backward_impl up to the one that completes every dense / head gradient: the loss
+// kernel, then [dense dX + dense dW + head dW] — the data-parallel split of the update
+// (mt_net_backward_bucket_launches; checked at run time by backward_impl under a launch window).
+constexpr int kDenseBucketLaunches = 2;
+
 // Backward of the non-LSTM archs as grouped launches (gemm.h, launch_group): each launch runs
 // every product whose inputs the previous one completed — loss | dense dX + dense dW + head dW |
 // per conv layer I (top down): conv dX + conv dW + the slab sum of layer I+1's dW | conv1's slab
@@ -1321,23 +1265,23 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
   const float *flat = layer_out<Ar, K>(ws, L);
   const float *Wfc = P + n->off_fc;
   // dense dW, db: [flat, 1]^T . dH -> grad[(FLAT+1) x F]
-  const auto dw = gemm_job<TileDenseWB>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
+  const auto dw = gemm_job<TileDenseW>(LdColMajor{flat, Ar::FLAT, Ar::FLAT}, LdColMajor{ws + L.dH, Ar::F, -1},
                                        EpStore{grad + n->off_fc, Ar::F}, Ar::FLAT + 1, Ar::F, B, 1);
   const HeadWgradJob hw = head_wgrad_job<Ar>(n, B, ws, L, grad);
   // dense dX: dH . W^T, masked by the last conv's activation (every trunk ends in an unpooled conv)
   static_assert(!pooled<Ar, K>(), "the trunk ends in an unpooled conv (networks.py:178-278)");
-  const auto dx = gemm_job<TileDenseXB>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
+  const auto dx = gemm_job<TileDenseX>(LdRowMajor{ws + L.dH, Ar::F}, LdRowMajor{Wfc, Ar::F},
                                        EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, B, Ar::FLAT, Ar::F, 1);
-#if MT_DENSE_DW_LATE
-  // the dense dX is the only job of this launch on the critical path (the next conv layer's dX
-  // needs it); the dense weight gradient, as long, runs beside the conv layer's dX in the next one
-  MT_TRY(launch_group(s, dx, hw));
-  return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s, SlabJob{}, no, dw);
-#else
   MT_TRY(launch_group(s, dx, dw, hw));
+  // the data-parallel split point: every dense / head gradient is complete after this launch
+  // (mt_net_backward_bucket_launches; paac._bucketed_update all-reduces that bucket next)
+  if (g_win_on && g_win_index != kDenseBucketLaunches) {
+    set_error("backward: the dense / head gradients completed after launch %d, not %d", g_win_index,
+              kDenseBucketLaunches);
+    return MT_ERR_UNSUPPORTED;
+  }
   if constexpr (nips_fused_bwd<Ar>()) return nips_conv_backward<Ar>(n, P, obs, B, ws, L, grad, s, no);
   return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s, SlabJob{}, no);
-#endif
 }
 
 }  // namespace mt
@@ -1449,7 +1393,7 @@ extern "C" int mt_net_backward_bucket_launches(const mt_net *net, int *launches)
       set_error("the LSTM backward is not bucketed");
       return MT_ERR_UNSUPPORTED;
     } else {
-      *launches = MT_DENSE_DW_LATE ? 3 : 2;  // backward_impl: loss | dense dX + head dW | first conv (+ dense dW)
+      *launches = kDenseBucketLaunches;  // backward_impl: loss | dense dX + dense dW + head dW | convs
     }
   });
   return MT_OK;

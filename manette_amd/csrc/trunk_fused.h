@@ -64,34 +64,20 @@ struct FusedNips {
   static constexpr int FEAT = OW2 * CO2;  // 288 features per conv2 row
   static constexpr int FLAT = ROWS2 * FEAT;
   static constexpr int F = 256;
-  // Half-row blocks (gray frames): block (e, i, h) computes conv2 pixels 5h .. 5h+4 of row i
-  // (h = 1: 5..8) from the 12 conv1 columns c0 .. c0+11 they read (c0 = 0 / 8), so an env's
-  // conv1 -> conv2 chain is spread over 18 blocks instead of 9 — half the conv1 MFMAs per block
-  // on the critical tail after the env's publication (the last env's blocks run on 18 CUs).
-  // Measured (round 3, profiles/r03p/): conv1 phase 2.60 vs 2.84 us per block, but the tail after
-  // the last publish unchanged (5.7 vs 5.6 us: the frame read over PCIe and conv2 do not shrink)
-  // and the isolated trunk slower (14.3 vs 13.6 us: 576 blocks share CUs) — off.
-#ifndef MT_NIPS_HALF
-#define MT_NIPS_HALF 0
-#endif
-  static constexpr bool HALF = C == 4 && MT_NIPS_HALF;
-  static constexpr int BPR = HALF ? 2 : 1;              // blocks per conv2 row
-  static constexpr int BPE = ROWS2 * BPR;               // blocks per env
-  static constexpr int CW1 = HALF ? 12 : OW1;           // conv1 columns a block computes
-  static constexpr int M1 = ROWS1 * CW1;  // conv1 pixels of a block (80; half rows 48)
-  static constexpr int MT1 = (M1 + 15) / 16;  // m-tiles (5; half rows 3)
+  // (Half-row blocks — an env's chain over 18 blocks, half the conv1 MFMAs each — measured in
+  // round 3: conv1 phase 2.60 vs 2.84 us, but the tail after the last publish unchanged and the
+  // isolated trunk slower, 14.3 vs 13.6 us; profiles/r03p/.)
+  static constexpr int BPE = ROWS2;       // blocks per env
+  static constexpr int M1 = ROWS1 * OW1;  // conv1 pixels of a block (80)
+  static constexpr int MT1 = (M1 + 15) / 16;  // m-tiles (5)
   static constexpr int KC1 = KK1 / 16, KC2 = KK2 / 16;
   // conv kernel waves. Gray frames: conv1's M-tiles x 2 K-halves ("units": each output is the
-  // sum of 2 partials; 10 waves for 5 tiles, 8 for the half rows' 3, 2 of them idle in conv1),
-  // conv2 = 2 N-tiles x 4 K-quarters on 8 of them, 4 partials; the former 8-wave K-split (every
-  // wave all 5 tiles over 1/8 of K) spent ~1.1 us per block writing and reducing 8 partials per
-  // output. RGB: 4 waves splitting K (its 3x input rows would not fit 64 KB of LDS beside more
-  // waves' partials).
-#ifndef MT_NIPS_NW_GRAY
-#define MT_NIPS_NW_GRAY 10
-#endif
-  static constexpr int NW = C == 4 ? (HALF ? 8 : MT_NIPS_NW_GRAY) : 4, NT = 64 * NW;
-  static constexpr bool UNITS = C == 4 && NW == (HALF ? 8 : 10);
+  // sum of 2 partials; 10 waves for 5 tiles), conv2 = 2 N-tiles x 4 K-quarters on 8 of them, 4
+  // partials; the former 8-wave K-split (every wave all 5 tiles over 1/8 of K) spent ~1.1 us per
+  // block writing and reducing 8 partials per output. RGB: 4 waves splitting K (its 3x input rows
+  // would not fit 64 KB of LDS beside more waves' partials).
+  static constexpr int NW = C == 4 ? 10 : 4, NT = 64 * NW;
+  static constexpr bool UNITS = C == 4;
   static constexpr int U1 = UNITS ? 2 * MT1 : 0;  // conv1 units (waves 0 .. U1-1)
   static_assert(UNITS ? (C == 4 && KC1 == 16 && KC2 == 16 && U1 <= NW && NW >= 8)
                       : (KC1 % NW == 0 && KC2 % NW == 0), "K chunks split over the waves");
@@ -116,7 +102,7 @@ struct FusedNips {
 // the new frames, writing the block's own rows of the new state.
 template <int C, bool STACK>
 __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs, const StackSrc &st, int e, int i,
-                                                int h, uint8_t *xin, uint8_t *fr) {
+                                                uint8_t *xin, uint8_t *fr) {
   using Fz = FusedNips<C>;
   const size_t row0 = ((size_t)e * 84 + 8 * i) * 84 * C;  // byte offset of row 8i of env e
   if constexpr (!STACK) {
@@ -174,15 +160,13 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
     // rows and byte w in each frame's rows (C = 4D). Same op as preprocess_kernel<D, kSrcFinal>.
     uint32_t *xw = reinterpret_cast<uint32_t *>(xin);
     uint32_t *ow = reinterpret_cast<uint32_t *>(st.out + row0);
-    // the row's own words (rows 8i .. 8i+7; the last row 64..83), split in halves between the
-    // row's BPR blocks
-    const int own = (i == Fz::ROWS2 - 1 ? Fz::RIN : 8) * 84 * Fz::D / Fz::BPR;
-    const int own_lo = h * own;
+    // the block's own words (rows 8i .. 8i+7; the last block 64..83)
+    const int own = (i == Fz::ROWS2 - 1 ? Fz::RIN : 8) * 84 * Fz::D;
     for (int w = threadIdx.x; w < Fz::RIN * 84 * Fz::D; w += Fz::NT) {
       uint32_t v = p < 4 ? xw[w] >> (8 * p) : 0u;
       for (int j = 0; j < p; ++j) v |= (uint32_t)fr[j * Fz::FR_BYTES + w] << (8 * (4 - p + j));
       xw[w] = v;
-      if (w >= own_lo && w < own_lo + own) ow[w] = v;
+      if (w < own) ow[w] = v;
     }
   }
 }
@@ -209,10 +193,7 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   MT_PROBE_AT(0, bid, 0);
   const int L = (nb % 8 == 0) ? (bid % 8) * (nb / 8) + bid / 8 : bid;
   // env-major: an env's blocks share an XCD
-  const int e = L / Fz::BPE, ih = L - e * Fz::BPE, i = ih / Fz::BPR, h = ih - i * Fz::BPR;
-  const int c0 = h ? Fz::OW1 - Fz::CW1 : 0;             // first conv1 column of the block
-  const int ox0 = h ? 5 : 0;                            // first conv2 pixel of the block
-  const int nox = Fz::HALF ? (h ? Fz::OW2 - 5 : 5) : Fz::OW2;  // its conv2 pixels
+  const int e = L / Fz::BPE, i = L - e * Fz::BPE;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
 
@@ -245,11 +226,11 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
       for (int s = 0; s < 4; ++s) b1f[j][s] = W1[(size_t)(k0 + s) * Fz::CO1 + r];
     }
   }
-  nips_stage_rows<C, STACK>(obs, st, e, i, h, xin, fr);
+  nips_stage_rows<C, STACK>(obs, st, e, i, xin, fr);
   __syncthreads();
   MT_PROBE_AT(0, bid, 1);
 
-  // ---- conv1 (VALID 8x8 stride 4): M = 4 rows x CW1 columns from c0, N = 16, K = 64*C ----
+  // ---- conv1 (VALID 8x8 stride 4): M = 4 rows x 20 columns, N = 16, K = 64*C ----
   if constexpr (Fz::UNITS) {
     // unit w < U1: M-tile t = w / 2, K-half kh = w % 2 (K chunks 8kh .. 8kh+7)
     if (w < Fz::U1) {
@@ -257,7 +238,7 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
     f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;  // even / odd chunks: independent MFMA chains
     const float sc = 1.0f / 255.0f;
     const int m = min(t * 16 + r, Fz::M1 - 1);
-    const int orow = m / Fz::CW1, ox = c0 + m - orow * Fz::CW1;
+    const int orow = m / Fz::OW1, ox = m - orow * Fz::OW1;
     const uint8_t *xb = xin + ((4 * orow) * 84 + 4 * ox) * C;
     // every LDS operand read of the unit first (8 words + 8 weight fragments in flight), then the
     // converts and the 32 MFMAs: the reads' latency is paid once, not once per chunk
@@ -350,25 +331,24 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
       }
       const float y = act_fwd(s + b1[n], act, alpha);
       a1[m * Fz::A1S + n] = y;
-      // conv1 rows 2i, 2i+1 (+ 18, 19), each column by one block (half rows: h = 0 columns 0..9)
-      const int orow = m / Fz::CW1, cx = c0 + m - orow * Fz::CW1;
-      if (act1 && (orow < 2 || i == Fz::ROWS2 - 1) && (!Fz::HALF || (cx < 10) == (h == 0)))
+      // conv1 rows 2i, 2i+1 (+ 18, 19), each by one block
+      const int orow = m / Fz::OW1, cx = m - orow * Fz::OW1;
+      if (act1 && (orow < 2 || i == Fz::ROWS2 - 1))
         act1[(((size_t)e * Fz::OW1 + 2 * i + orow) * Fz::OW1 + cx) * Fz::CO1 + n] = y;
     }
   }
   __syncthreads();
   MT_PROBE_AT(0, bid, 2);
 
-  // ---- conv2 row i (VALID 4x4 stride 2): M = the block's nox pixels from ox0 (padded to 16),
-  //      N = 32, K = 256 ----
+  // ---- conv2 row i (VALID 4x4 stride 2): M = its 9 pixels (padded to 16), N = 32, K = 256 ----
   if constexpr (Fz::UNITS) {
     if (w < 8) {  // unit w: N-tile w & 1, K-quarter kq = w >> 1 (chunks 4kq .. 4kq+3: ky = kq, kx = j)
       const int kq = w >> 1;
       f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-      const int ox = ox0 + min(r, nox - 1);
+      const int ox = min(r, Fz::OW2 - 1);
 #pragma unroll
       for (int j = 0; j < J2; ++j) {
-        const f32x4 a = *reinterpret_cast<const f32x4 *>(a1 + (kq * Fz::CW1 + 2 * ox - c0 + j) * Fz::A1S + 4 * g);
+        const f32x4 a = *reinterpret_cast<const f32x4 *>(a1 + (kq * Fz::OW1 + 2 * ox + j) * Fz::A1S + 4 * g);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           if (j & 1)
@@ -404,7 +384,7 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   {
     const float *b2 = W2 + (size_t)Fz::KK2 * Fz::CO2;
     constexpr int P = 16 * Fz::CO2;
-    for (int idx = threadIdx.x; idx < nox * Fz::CO2; idx += Fz::NT) {
+    for (int idx = threadIdx.x; idx < Fz::OW2 * Fz::CO2; idx += Fz::NT) {
       const int n = idx & (Fz::CO2 - 1);
       float s;
       if constexpr (Fz::UNITS) {  // K-quarters 0..3 (in order) of N-tile n / 16: units 2 kq + n / 16
@@ -417,7 +397,7 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
 #pragma unroll
         for (int v = 1; v < NW; ++v) s += red[v * P + idx];  // wave order
       }
-      act2[((size_t)e * Fz::ROWS2 + i) * Fz::FEAT + ox0 * Fz::CO2 + idx] = act_fwd(s + b2[n], act, alpha);
+      act2[((size_t)e * Fz::ROWS2 + i) * Fz::FEAT + idx] = act_fwd(s + b2[n], act, alpha);
     }
   }
   MT_PROBE_AT(0, bid, 4);

@@ -75,6 +75,12 @@ class PAACLearner(ActorLearner):
         self.env_offset = int(getattr(args, 'env_id_offset', self.rank * self.emulator_counts))
         self.comm_kind = getattr(args, 'comm', 'rccl')
         self.comm = None
+        # the data-parallel update (bucketed all-reduce on a side stream between three update graphs,
+        # norm partials after the all-reduce, the learner launching the update): world > 1, or forced
+        # at world 1 (args.dp_force / MT_DP_FORCE=1), where the RCCL sum is the identity, so the
+        # code the N-GPU run depends on runs, and is oracle-checked, on one GPU (tests/test_e2e_gpu.py)
+        self.dp = self.world > 1 or bool(getattr(args, 'dp_force', False)) or os.environ.get('MT_DP_FORCE') == '1'
+        self.grad_scale = 1.0 / self.world  # folded into clip + RMSProp: the all-reduced sum -> the mean
         if self.sampling == 'device' and getattr(args, 'egreedy', False):
             # the device draw is the multinomial of exploration_policy.py:108-116 only
             raise ValueError('--egreedy needs --sampling host (the device sampler draws multinomially)')
@@ -400,7 +406,7 @@ class PAACLearner(ActorLearner):
                 return lr
         self._eager_updates += 1
         self._update_backward()
-        if self.world > 1:
+        if self.dp:
             self.comm.allreduce(self.network.grad)
         self._update_apply()
         return lr
@@ -455,7 +461,7 @@ class PAACLearner(ActorLearner):
                                       self.rep_all[:T].reshape(N, -1), self.values, self.idx[0].view(N),
                                       self.idx[1].view(N), self.rm_h_dev, self.rm_h_dev + 4 * T * E, self.v_boot,
                                       self.gamma, self.y, self.adv, loss_terms=self.loss_terms, ws_key='train',
-                                      norm_partials=self.world == 1, boot_ws=self._boot_ws if boot_done else None)
+                                      norm_partials=not self.dp, boot_ws=self._boot_ws if boot_done else None)
         if end is not None:
             end.record()
 
@@ -480,8 +486,8 @@ class PAACLearner(ActorLearner):
 
     def _update_apply(self):
         T = self.max_local_steps
-        self.network.apply_gradients(1.0 / self.world if self.world > 1 else 1.0,
-                                     partials_ready=self.world == 1 and not self.lstm_bool)
+        self.network.apply_gradients(self.grad_scale,
+                                     partials_ready=not self.dp and not self.lstm_bool)
         if self.lstm_bool:  # the next rollout's slots 0..4 = s_{T-4} .. s_T; windows carry over
             if T >= 5:
                 self.slots[0:5].copy_(self.slots[T:T + 5])
@@ -536,7 +542,7 @@ class PAACLearner(ActorLearner):
             return run
 
         self._buckets = None
-        if self.world == 1:  # one graph; the rollout's last step launches it (_register_update)
+        if not self.dp:  # one graph; the rollout's last step launches it (_register_update)
             graphs = capture([whole])
         elif not self.lstm_bool and os.environ.get('MT_DP_BUCKETS', '1') != '0':
             # data parallel: the backward captured as its first launches, up to the one that completes
@@ -573,7 +579,7 @@ class PAACLearner(ActorLearner):
         update graph itself, right behind the bootstrap chain (mt_rollout_set_update): no host
         round trip between the last emulator step and the update. MT_UPDATE_IN_ROLLOUT=0: off."""
         if os.environ.get('MT_UPDATE_IN_ROLLOUT', '1') == '0' or self.native_step is None or self.lstm_bool \
-                or self.world > 1:
+                or self.dp:
             # (LSTM: its update also moves the frame-store slots the next rollout starts from; data
             # parallel: the learner launches the update, its all-reduces eagerly between graphs)
             return
@@ -605,9 +611,10 @@ class PAACLearner(ActorLearner):
     # ------------------------------------------------------------------------------------------
     def start(self):
         self.global_step = self.init_network()
-        if self.world > 1:
+        if self.dp:
             from . import comm
             self.comm = comm.make(self.comm_kind, self.rank, self.world, torch.cuda.current_device())
+        if self.world > 1:
             # rank 0's run is the run: its checkpoint step (resume) and its parameters / slots
             self.global_step, self.last_saving_step = comm.broadcast_scalars(
                 [self.global_step, self.last_saving_step], self.rank)
@@ -644,10 +651,13 @@ class PAACLearner(ActorLearner):
         self.summaries.log_values(self.book.total_steps, 'steps_per_episode', self.global_step)
         self.summaries.flush()
 
-    def _write_summaries_dp(self, interval=None):
+    def _write_summaries_dp(self, interval=None, final=False):
+        """final: the gather of the episodes finished since the last one (train()'s normal exit, every
+        rank), so no episode of the run is left unlogged."""
         self._summary_calls = getattr(self, '_summary_calls', 0) + 1
-        interval = interval or max(1, 2048 // self.emulator_counts)
-        if self._summary_calls % interval != 0:
+        # the reference's interval counts updates of the whole job: 2048 / (global emulator count)
+        interval = interval or max(1, 2048 // (self.emulator_counts * self.world))
+        if not final and self._summary_calls % interval != 0:
             return
         self.book.drain()
         mine = [tuple(e) for e in self.book.episodes[self._logged_episodes:]]
@@ -695,6 +705,8 @@ class PAACLearner(ActorLearner):
                     logging.info('Ran %d steps, at %f steps/s (%f steps/s avg), last 10 rewards avg %f',
                                  self.global_step, steps_per_sec, avg, last_ten)
                 self.save_vars()
+            if self.world > 1:  # (every rank: a collective) the episodes since the last gather
+                self._write_summaries_dp(final=True)
         finally:
             self.cleanup()
 

@@ -1,0 +1,90 @@
+"""Stream ordering of the data-parallel update on one GPU.
+
+paac._bucketed_update replays the backward as two graphs split at the launch that completes the
+dense / head gradients (mt_net_backward_bucket_launches) and all-reduces the two gradient buckets
+on a side stream between them, ordered by events e1 / e2 / e3; the apply graph waits for both.
+At world 1 RCCL's in-place sum is the identity, so an ordering bug would leave the result
+unchanged. Here the communicator is a stub that sleeps on the side stream (so a consumer that does
+not wait runs first) and then doubles its bucket — a two-rank sum of identical replicas — with
+the learner's 1/world fold set to 1/2. Every value of the run must then be bit-identical to the
+same learner with the RCCL communicator (a bucket doubled too early or too late, or an apply that
+does not wait, changes the gradient's direction, which the global-norm clip does not hide), and the
+dense / head bucket must already hold its final gradient when its all-reduce starts.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+UPDATES = 5
+
+
+class SlowDoublingComm(object):
+    """Side-stream all-reduce stand-in: spin ~1 ms, snapshot the bucket, then sum it with an
+    identical replica (x2)."""
+    kind = 'stub'
+    capturable = False
+
+    def __init__(self):
+        self.snaps = []
+
+    def allreduce(self, t):
+        torch.cuda._sleep(2_000_000)
+        self.snaps.append((t.data_ptr(), t.clone()))
+        t.mul_(2.0)
+
+    def broadcast(self, t, root=0):
+        pass
+
+    def close(self):
+        pass
+
+
+def _run(config, tmp_path, stub):
+    import bench
+    L, _ = bench.make_learner(config, debugging_folder=str(tmp_path) + '/', episode_len=13, dp_force=True)
+    L.start()
+    try:
+        assert L.dp and L.comm.kind == 'rccl'
+        if stub is not None:
+            L.comm.close()
+            L.comm = stub
+            L.grad_scale = 0.5
+        for _ in range(UPDATES):
+            L.book.new_update()
+            L.rollout()
+            L.update()
+        torch.cuda.synchronize()
+        assert L._buckets is not None and len(L._graphs) == 3
+        c = lambda t: t.detach().cpu().numpy().copy()
+        return dict(params=c(L.network.params), ms=c(L.network.ms), mom=c(L.network.mom), grad=c(L.network.grad),
+                    states=c(L.states), values=c(L.values), y=c(L.y), idx=L.idx_h.numpy().copy(),
+                    gs=L.global_step, split=L._buckets, grad_ptr=L.network.grad.data_ptr())
+    finally:
+        L.cleanup()
+
+
+@pytest.mark.parametrize('config', ['pong-nips', 'seaquest-nature'])
+def test_bucketed_update_stream_order(config, tmp_path):
+    ref = _run(config, tmp_path / 'rccl', None)
+    stub = SlowDoublingComm()
+    got = _run(config, tmp_path / 'stub', stub)
+    for k in ('params', 'ms', 'mom', 'states', 'values', 'y', 'idx'):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    assert got['gs'] == ref['gs']
+    # the gradient itself: the all-reduced sum of two identical replicas
+    np.testing.assert_array_equal(got['grad'], 2.0 * ref['grad'])
+    # the last update's two all-reduces: the dense / head bucket first, then the conv bucket, each
+    # already holding its final gradient (nothing wrote it after its all-reduce started)
+    k = got['split']
+    (p1, b1), (p2, b2) = stub.snaps[-2], stub.snaps[-1]
+    assert p1 == got['grad_ptr'] + 4 * k and p2 == got['grad_ptr']
+    np.testing.assert_array_equal(b1.cpu().numpy(), ref['grad'][k:])
+    np.testing.assert_array_equal(b2.cpu().numpy(), ref['grad'][:k])

@@ -61,9 +61,10 @@ def _replay(cfg, E, A, idx_all, T):
     return out
 
 
-def _run(config, tmp_path):
+def _run(config, tmp_path, dp_force=False):
     import bench
-    L, args = bench.make_learner(config, debugging_folder=str(tmp_path) + '/', episode_len=EPISODE_LEN)
+    L, args = bench.make_learner(config, debugging_folder=str(tmp_path) + '/', episode_len=EPISODE_LEN,
+                                 dp_force=dp_force)
     L.start()
     return L, args, bench.CONFIGS[config]
 
@@ -84,14 +85,26 @@ def _chunked_feats(spec, P, frames, chunk=32):
     return np.concatenate([nets.trunk_forward(spec, P, frames[c0:c0 + chunk])[0] for c0 in range(0, len(frames), chunk)])
 
 
-@pytest.mark.parametrize('config', ['pong-nips', 'breakout-nature-figar', 'seaquest-nature', 'mspacman-lstm-figar',
-                                    'breakout-pwyx-figar-rgb'])
-def test_benchmarked_path_matches_oracle(config, tmp_path):
+CASES = [('pong-nips', False), ('breakout-nature-figar', False), ('seaquest-nature', False),
+         ('mspacman-lstm-figar', False), ('breakout-pwyx-figar-rgb', False),
+         # the data-parallel update at world 1: RCCL communicator, the backward captured
+         # as two graphs around the first gradient bucket, both buckets all-reduced by RCCL on a side
+         # stream between graph replays (paac._bucketed_update), norm partials after the all-reduce,
+         # the learner (not the rollout) launching the update — everything the N-GPU run executes but
+         # the cross-rank sum, which at world 1 is the identity
+         ('pong-nips', True), ('seaquest-nature', True)]
+
+
+@pytest.mark.parametrize('config,dp', CASES, ids=['%s%s' % (c, '-dp-rccl' if d else '') for c, d in CASES])
+def test_benchmarked_path_matches_oracle(config, dp, tmp_path):
     import parity_util
-    L, args, cfg = _run(config, tmp_path)
+    L, args, cfg = _run(config, tmp_path, dp_force=dp)
     try:
         lstm = L.lstm_bool
         assert L.native_step is not None and L.boot_in_rollout and L._graph_ok()
+        assert L.dp == dp
+        if dp:
+            assert L.comm is not None and L.comm.kind == 'rccl' and L.world == 1
         E, T, A, R = L.emulator_counts, L.max_local_steps, L.num_actions, L.total_repetitions
         N = E * T
         idx_all = []
@@ -101,6 +114,8 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
             idx_all.append(L.idx_h.numpy().copy())
             L.update()
         assert L._graphs is not None  # the checked update is a graph replay
+        if dp:  # three graphs, the all-reduces of the two buckets between them on a side stream
+            assert L._buckets is not None and len(L._graphs) == 3 and not L._update_in_rollout
         # the parameters / slots the checked rollout runs with, read before it: from the third update
         # on, the rollout's last step launches the update itself (mt_rollout_set_update)
         torch.cuda.synchronize()
@@ -126,7 +141,8 @@ def test_benchmarked_path_matches_oracle(config, tmp_path):
         # argmax, the dense output)
         dev = L.network.forward_branches(L.network.lstm_workspace(E, T), 1, E, T) if lstm else \
             L.network.forward_branches(L.train_ws, 0, N)
-        assert L._update_in_rollout == (not lstm)  # the benchmarked path: the rollout launched this update
+        # the benchmarked path: the rollout launched this update (data parallel: the learner did)
+        assert L._update_in_rollout == (not lstm and not dp)
         # V(s_T): the rollout's last chain (pipelined native step) or the update's first forward (LSTM)
         v_boot, pi_all, rep_all = c(L.v_boot), c(L.pi_all), c(L.rep_all)
         grad, y, adv = L.network.get_variables('grad'), c(L.y), c(L.adv)
