@@ -623,23 +623,19 @@ def main():
             kernels.append(row('A9+A10', 'paac.py:219-231, policy_v_network.py:25-74', 'loss_bwd_kernel (n-step scan'
                                + (' + V(s_T) from the bootstrap slabs' if stacking else '') + ' + loss + head dz / dH)',
                                tl[0], loss_bytes, note='launch 1 of the update backward (bench.launch_breakdown)'))
-            import ctypes as C
-            from manette_amd import _lib
-            nb = C.c_int()
-            _lib.check(_lib.hip().mt_net_backward_bucket_launches(net._h, C.byref(nb)))
-            late = nb.value == 3  # the dense weight gradient runs beside the first conv layer's dX
             nconv = len(trunk) - 1
             if cfg['arch'] == 'NIPS' and not cfg['rgb']:  # the fused NIPS conv backward (nips_bwd.h)
                 names = ['dense dX + head dW + dense dW',
                          'nips_conv_bwd_kernel (conv2 dX, conv1 dW + db per image; conv2 dW + db per image pair)',
                          'conv1 + conv2 slab sums + global-norm partials']
             else:
-                names = ['dense dX + head dW' + ('' if late else ' + dense dW')]
+                names = ['dense dX + head dW + dense dW']
                 for i in range(nconv - 1, -1, -1):
-                    sfx = (' + dense dW' if late and i == nconv - 1 else '') + \
-                          (' + conv%d slab sum' % (i + 2) if i < nconv - 1 else '')
+                    sfx = ' + conv%d slab sum' % (i + 2) if i < nconv - 1 else ''
                     if i > 0 and cfg['arch'] == 'PWYX' and i == 1:  # its own direct dX launch (dconv.h dconv_bwd_solo)
                         names += ['conv2 dX (direct conv)', 'conv2 dW' + sfx]
+                    elif i > 0 and cfg['arch'] == 'NATURE':  # direct phase dX launch (dconv.h DBwdStrided)
+                        names += ['conv%d dX (direct phase conv)' % (i + 1), 'conv%d dW' % (i + 1) + sfx]
                     else:
                         names.append(('conv%d dX + conv%d dW' % (i + 1, i + 1) if i > 0 else 'conv1 dW') + sfx)
                 names.append('conv1 slab sum + global-norm partials')
@@ -737,6 +733,9 @@ def main():
             learner.cleanup()
             learner = None
             line['cpu_baseline'] = cpu_baseline(cfg, T, a.cpu_seconds, rank)
+            # (vs_baseline stays null: BASELINE.md publishes no number for this metric; the ratio to
+            # the CPU port timed here, on this box's host cores, is reported beside it)
+            line['vs_cpu_baseline'] = round(value / line['cpu_baseline']['value'], 1)
             # BASELINE configs[0] (Pong NIPS ec=4 ew=2, the reference's CPU-only case), a shorter sample
             c0 = cpu_baseline(CPU_CONFIG0, T, a.cpu_seconds / 2, rank)
             c0.pop('_net_ms_per_update')

@@ -76,7 +76,9 @@ int mt_net_var_info(const mt_net *net, int i, char *name, int name_len, int64_t 
                     int *ndim, size_t *offset, float *init_bound);
 int mt_net_feature_dim(const mt_net *net, int *f); /* width of the trunk output (256/512/...) */
 int mt_net_get_config(const mt_net *net, mt_net_config *cfg);
-/* Bytes of device workspace a forward/backward on `batch` rows needs. */
+/* Bytes of device workspace a forward/backward on `batch` rows needs. Zero-fill a workspace once
+ * when it is allocated: the gray NATURE stacking chain keeps per-env hand-off counters in it, which
+ * every launch leaves at zero again. */
 int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes);
 /* Diagnostics / parity: where a workspace keeps a forward value the backward branches on — kind 0:
  * conv layer `layer`'s stored output, post-activation ([rows][OH][OW][COUT] fp32; a pooled layer's
@@ -127,13 +129,14 @@ int mt_forward_rows(const mt_net *net, const float *params, const uint8_t *obs, 
 int mt_forward_trunk(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
                      size_t ws_bytes, mt_stream_t stream);
 
-/* The rollout chain's stacking trunk alone (roofline timing, parity tests): the NIPS conv kernel
- * in its in-kernel-pull form — per env, wait until ready[e * MH_READY_STRIDE] >> 3 == tag (one
- * 128-B line per env, manette_host.h), stack out = prev shifted by the push count (its low 3 bits)
- * + that many final frames (frames = [4*batch][84][84][depth],
- * env e's pushes at slots 4e..; host-mapped pinned staging or device memory) — then the dense
- * layer's split-K partials, left in ws. With every ready word already set nothing waits: the
- * kernels' own duration. NIPS only (MT_ERR_UNSUPPORTED otherwise). */
+/* The rollout chain's stacking trunk alone (roofline timing, parity tests): the conv kernel in its
+ * in-kernel-pull form — per env, wait until ready[e * MH_READY_STRIDE] >> 3 == tag (one 128-B line
+ * per env, manette_host.h), stack out = prev shifted by the push count (its low 3 bits) + that
+ * many final frames (frames = [4*batch][84][84][depth], env e's pushes at slots 4e..; host-mapped
+ * pinned staging or device memory) — then the dense layer's split-K partials, left in ws. NIPS:
+ * nips_conv_kernel<STACK> + nips_fc_kernel; gray NATURE: nature_chain_kernel (stacking conv1 ->
+ * conv2 -> conv3, per-env hand-offs in one launch) + the split-K dense GEMM. With every ready word
+ * already set nothing waits: the kernels' own duration. MT_ERR_UNSUPPORTED for the other archs. */
 int mt_forward_trunk_stacking(const mt_net *net, const float *params, const uint8_t *prev, const uint8_t *frames,
                               const uint32_t *ready, uint32_t tag, uint8_t *out, int batch, void *ws, size_t ws_bytes,
                               mt_stream_t stream);

@@ -35,7 +35,9 @@ namespace mt {
 // Forward of conv G: X = its input [B][H][W][CIN] (u8 frames for conv1), Y = the pooled output
 // [B][OH/2][OW/2][COUT] + argmax bytes (POOL, EpBiasActPool's layout and first-max rule) or the
 // activation [B][OH][OW][COUT].
-template <class G, bool U8, bool POOL_>
+// COH_IN / COH_OUT (the in-launch hand-offs of nature_chain_kernel): X read / Y written with
+// agent-scope relaxed atomics (sc1: coherent across the XCDs' L2s) instead of plain accesses.
+template <class G, bool U8, bool POOL_, bool COH_IN = false, bool COH_OUT = false>
 struct DFwd {
   static constexpr int CI = G::CIN, CO = G::COUT, KH = G::KH, KW = G::KW, PT = G::PT, PL = G::PL, S = G::S;
   static constexpr int H = G::H, W = G::W, OH = G::OH, OW = G::OW, KK = G::KK;
@@ -47,6 +49,11 @@ struct DFwd {
   uint8_t *arg;
   int act;
   float alpha;
+  // optional (the replayed rollout graph's bootstrap chain, whose dense layer is a generic GEMM):
+  // block 0 adds advance_by to advance[0] and advance[1] at its start — every reader of those
+  // sequence bases in the replay (the stacking conv1 blocks, the heads kernels) has run by then
+  uint32_t *advance = nullptr;
+  uint32_t advance_by = 0;
   __device__ __forceinline__ f32x4 wquad(int k, int n) const {  // W(k .. k+3, n), zero past KK
     f32x4 v;
 #pragma unroll
@@ -60,8 +67,27 @@ struct DFwd {
     float b;
   };
   __device__ __forceinline__ Pre pre(int, int, int n) const { return {bias[n]}; }
+  __device__ __forceinline__ f32x4 load4(const InT *q) const {
+    if constexpr (COH_IN) {
+      static_assert(!U8, "coherent loads of f32 activations");
+      const uint64_t *w = reinterpret_cast<const uint64_t *>(q);
+      const uint64_t x = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t y = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return f32x4{__uint_as_float((uint32_t)x), __uint_as_float((uint32_t)(x >> 32)), __uint_as_float((uint32_t)y),
+                   __uint_as_float((uint32_t)(y >> 32))};
+    } else {
+      return InElem<U8>::load4(q);
+    }
+  }
+  __device__ __forceinline__ void put(size_t o, float v) const {
+    if constexpr (COH_OUT)
+      __hip_atomic_store(Y + o, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      Y[o] = v;
+  }
   __device__ __forceinline__ void store(const Pre &p, int b, int u, int n, f32x4 v) const {
     if constexpr (POOL) {
+      static_assert(!COH_OUT, "coherent stores of unpooled outputs only");
       constexpr int U = (G::OH / 2) * (G::OW / 2);
       float mx = act_fwd(v[0] + p.b, act, alpha);
       int am = 0;
@@ -80,11 +106,171 @@ struct DFwd {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int px = 4 * u + q;
-        if (px < OH * OW) Y[((size_t)b * OH * OW + px) * CO + n] = act_fwd(v[q] + p.b, act, alpha);
+        if (px < OH * OW) put(((size_t)b * OH * OW + px) * CO + n, act_fwd(v[q] + p.b, act, alpha));
       }
     }
   }
 };
+
+// The NATURE rollout chain's conv1 with the A2 stacking and the in-kernel pull fused in (the NIPS
+// chain's nips_stage_rows, trunk_fused.h): each block builds its patch rows from the previous
+// state and env b's p new final frames — read from the pinned staging once env b's emulator thread
+// has published it (StackSrc::ready; edge lines of its slot group with system-scope loads), or
+// from HBM (count), or none (count == NULL: a copy of prev, slot 0 <- slot T) — converts them into
+// the f32 patch (networks.py:155's u8 * (1/255), bit for bit the unstacked loader's) and writes
+// the rows it owns to the new state slot. So env b's conv1 runs as soon as env b is emulated, not
+// after the last env. Gray frames (one u32 = 4 channels per pixel), VALID.
+template <class G, bool COH_OUT = false>
+struct DFwdStack : DFwd<G, true, false, false, COH_OUT> {
+  static_assert(G::CIN == 4 && !G::SAME && G::PT == 0 && G::PL == 0 && G::W % 4 == 0, "gray VALID conv1");
+  static constexpr bool STAGES_PATCH = true;
+  StackSrc st;
+  // rows [r0, r0 + D::RIN) of image b into the patch As; rows [r0, own_end) are the block's to
+  // write to st.out; fr: >= 4 * RIN * W bytes of LDS scratch (free until the caller's weight store)
+  template <class D>
+  __device__ __forceinline__ void stage_patch(int b, int r0, int own_end, float *As, uint8_t *fr) const {
+    constexpr int H = G::H, W = G::W, RIN = D::RIN, NT = D::NT;
+    static_assert(D::WP == W && D::WPX == W && D::CS == 4, "full-width patch rows, 4 floats per pixel");
+    static_assert(RIN % 4 == 0 && H % 4 == 0 && G::S % 4 == 0, "16-B frame chunks");
+    constexpr int PQ = RIN * W / 4;  // 4-pixel items of the patch
+    constexpr int PIT = (PQ + NT - 1) / NT;
+    const int tid = threadIdx.x;
+    const int rows = min(RIN, H - r0);  // patch rows inside the image
+    const int nq = rows * W / 4;
+    __shared__ int s_p;
+    // the previous state's rows, requested before the wait (their latency hides under it)
+    const uint4 *prev = reinterpret_cast<const uint4 *>(st.prev + ((size_t)b * H + r0) * W * 4);
+    uint4 pv[PIT];
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) pv[it] = prev[min(tid + it * NT, nq - 1)];
+    if (tid == 0) {
+      int np = 0;
+      if (st.ready) {
+        const uint32_t tag = st.tag_base ? ((*st.tag_base + st.tag) & 0x1fffffffu) : st.tag;
+        np = min(max(wait_published(st.ready, b, tag, st.status), 0), 4);  // (a timeout stacks no frame)
+      } else if (st.count) {
+        np = min(max(st.count[b], 1), 4);
+      }
+      s_p = np;
+    }
+    __syncthreads();
+    const int p = s_p;
+    // the p pushes' rows (push j of env b = frame slot 4b + j), one round trip
+    constexpr size_t F = (size_t)H * W;
+    const size_t lo = 4 * (size_t)b * F, hi = lo + 4 * F;
+    const int fq = rows * W / 16;
+    for (int q = tid; q < p * fq; q += NT) {
+      const int j = q / fq, qq = q - j * fq;
+      const size_t off = ((size_t)4 * b + j) * F + (size_t)r0 * W + 16 * (size_t)qq;
+      reinterpret_cast<uint4 *>(fr + j * RIN * W)[qq] =
+          st.ready ? ld_published16(st.frames, off, lo, hi) : *reinterpret_cast<const uint4 *>(st.frames + off);
+    }
+    __syncthreads();
+    // stack (preprocess_kernel's op: prev shifted by p channels, the p frames in the top ones),
+    // the owned rows to the new state, every row into the patch
+    uint4 *out = reinterpret_cast<uint4 *>(st.out + ((size_t)b * H + r0) * W * 4);
+    const int own_q = (own_end - r0) * W / 4;
+    const float sc = 1.0f / 255.0f;
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * NT;
+      if (PQ % NT != 0 && q >= PQ) break;
+      uint32_t wv[4] = {pv[it].x, pv[it].y, pv[it].z, pv[it].w};
+      if (q < nq) {
+        uint32_t fw[4];
+        for (int j = 0; j < p; ++j) fw[j] = reinterpret_cast<const uint32_t *>(fr + j * RIN * W)[q];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          uint32_t v = p < 4 ? wv[k] >> (8 * p) : 0u;
+          for (int j = 0; j < p; ++j) v |= ((fw[j] >> (8 * k)) & 0xffu) << (8 * (4 - p + j));
+          wv[k] = v;
+        }
+        if (q < own_q) out[q] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      } else {
+        wv[0] = wv[1] = wv[2] = wv[3] = 0u;  // (rows past the image: zero patch)
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t u = wv[k];
+        *reinterpret_cast<f32x4 *>(As + 16 * q + 4 * k) =
+            f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc, (float)((u >> 16) & 0xff) * sc,
+                  (float)(u >> 24) * sc};
+      }
+    }
+    __syncthreads();  // (fr aliases the weight buffer the caller fills next)
+  }
+};
+
+// dX of the VALID conv G by stride phases as ONE stride-1 direct conv (round 4): input pixel
+// (S qy + py, S qx + px) of phase (py, px) receives sum_{j, i < KJ} dY[qy - j][qx - i] .
+// W[py + S j][px + S i] (KJ = KH / S taps per axis). Over the phase grid q (H/S x W/S) that is a
+// stride-1 conv of dY, zero-padded KJ - 1 on each side, with a KJ x KJ kernel whose S*S*CIN output
+// channels are the phases' dX channels: n = (py S + px) CIN + ci, W'[kyp][kxp][co][n] =
+// W[py + S (KJ-1-kyp)][px + S (KJ-1-kxp)][ci][co] — so every phase reads the SAME dY patch from
+// LDS (the generic phase GEMM gathers it once per phase), and only the weights differ per output
+// channel. Its staging reads 4 consecutive co of one (tap, ci): one 16-byte load. The epilogue
+// masks by the activation derivative of X (G's input = the previous layer's output, EpMasked's
+// rule) and scatters phase pixel (qy, qx) of channel n to dX[S qy + py][S qx + px][ci].
+template <class G>
+struct DBwdStrided {
+  static constexpr int KJ = G::KH / G::S;
+  static_assert(!G::SAME && G::KH == G::KW && G::H == G::W && G::KH % G::S == 0 && G::H % G::S == 0 &&
+                    G::H / G::S == G::OH + KJ - 1 && (KJ * KJ * G::COUT) % 16 == 0,
+                "phase-separable VALID conv");
+  static constexpr int CI = G::COUT, CO = G::S * G::S * G::CIN, KH = KJ, KW = KJ;
+  static constexpr int PT = KJ - 1, PL = KJ - 1, S = 1;
+  static constexpr int H = G::OH, W = G::OW, OH = G::H / G::S, OW = G::W / G::S, KK = KJ * KJ * G::COUT;
+  static constexpr bool POOL = false;
+  using InT = float;
+  const float *X;     // dY [B][OH_G][OW_G][COUT]
+  const float *Wt;    // W of G (HWIO)
+  const float *Xact;  // G's input [B][H_G][W_G][CIN] (post-activation: the mask)
+  float *dX;          // [B][H_G][W_G][CIN]
+  int act;
+  float alpha;
+  __device__ __forceinline__ f32x4 load4(const float *q) const { return *reinterpret_cast<const f32x4 *>(q); }
+  __device__ __forceinline__ f32x4 wquad(int k, int n) const {  // W'(k .. k+3, n): 4 co of one tap
+    const int t = k / CI, c = k - t * CI;
+    const int kyp = t / KJ, kxp = t - kyp * KJ;
+    const int ph = n / G::CIN, ci = n - ph * G::CIN;
+    const int py = ph / G::S, px = ph - py * G::S;
+    const int ky = py + G::S * (KJ - 1 - kyp), kx = px + G::S * (KJ - 1 - kxp);
+    return *reinterpret_cast<const f32x4 *>(Wt + (((size_t)ky * G::KW + kx) * G::CIN + ci) * G::COUT + c);
+  }
+  // dX element of phase pixel q (< OH * OW) of channel n
+  __device__ __forceinline__ size_t index(int b, int q, int n) const {
+    const int ph = n / G::CIN, ci = n - ph * G::CIN;
+    const int py = ph / G::S, px = ph - py * G::S;
+    const int qy = q / OW, qx = q - qy * OW;
+    return (((size_t)b * G::H + G::S * qy + py) * G::W + G::S * qx + px) * G::CIN + ci;
+  }
+  struct Pre {
+    float y[4];
+  };
+  __device__ __forceinline__ Pre pre(int b, int u, int n) const {
+    Pre r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r.y[q] = Xact[index(b, min(4 * u + q, OH * OW - 1), n)];
+    return r;
+  }
+  __device__ __forceinline__ void store(const Pre &pr, int b, int u, int n, f32x4 v) const {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int px = 4 * u + q;
+      if (px < OH * OW) dX[index(b, px, n)] = v[q] * act_bwd(pr.y[q], act, alpha);
+    }
+  }
+};
+
+// problems with their own patch staging (DFwdStack) / a sequence-base advance (DFwd)
+template <class P, class = void>
+struct HasStagePatch : std::false_type {};
+template <class P>
+struct HasStagePatch<P, std::void_t<decltype(P::STAGES_PATCH)>> : std::bool_constant<P::STAGES_PATCH> {};
+template <class P, class = void>
+struct HasAdvance : std::false_type {};
+template <class P>
+struct HasAdvance<P, std::void_t<decltype(std::declval<const P &>().advance)>> : std::true_type {};
 
 // dX of the stride-1 SAME conv G (input = the pooled output of conv GJ): X = dY of G
 // [B][OH][OW][COUT], output = GJ's full-resolution conv-output gradient dact [B][GJ::OH][GJ::OW]
@@ -114,6 +300,7 @@ struct DBwdUnpool {
     float p[4];
     uint8_t a[4];
   };
+  __device__ __forceinline__ f32x4 load4(const float *q) const { return *reinterpret_cast<const f32x4 *>(q); }
   __device__ __forceinline__ Pre pre(int b, int u, int n) const {
     Pre r;
 #pragma unroll
@@ -271,6 +458,13 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
     for (int j = 0; j < D::TNW; ++j)
       pre[i][j] = p.pre(b, min(u0 + (wm * TMW + i) * 4 + g, D::U - 1), (wn * D::TNW + j) * 16 + r);
 
+  if constexpr (HasStagePatch<Pr>::value) {
+    // (the problem stages its own patch: DFwdStack; rows [oy0 S, own_end) of the new state are the
+    // block's to write — up to the next block's first row)
+    const int bi = bid - b * D::BPI;
+    const int own_end = bi + 1 < D::BPI ? min(D::H, ((4 * (u0 + D::UPB)) / D::OW) * D::S) : D::H;
+    p.template stage_patch<D>(b, oy0 * D::S, own_end, As, reinterpret_cast<uint8_t *>(Bs));
+  } else {
   // the patch: input rows oy0 - PT .. oy0 - PT + RIN - 1, columns -PL .. -PL + WP - 1 (zeros
   // outside the image), in batches of 8 quads per thread (all loads of a batch in flight)
   const auto *img = p.X + (size_t)b * D::H * D::W * D::CI;
@@ -288,8 +482,7 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
         const int pr = pix / D::WP, pc = pix - pr * D::WP;
         const int iy = oy0 * D::S - Pr::PT + pr, ix = pc - Pr::PL;
         const bool ok = (unsigned)iy < (unsigned)D::H && (unsigned)ix < (unsigned)D::W;
-        const f32x4 x = InElem<std::is_same<typename Pr::InT, uint8_t>::value>::load4(
-            img + (size_t)(ok ? iy * D::W + ix : 0) * D::CI + 4 * cq);
+        const f32x4 x = p.load4(img + (size_t)(ok ? iy * D::W + ix : 0) * D::CI + 4 * cq);
         v[t] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
         dst[t] = (D::AQ % D::NT == 0 || tid + it * D::NT < D::AQ) ? (pr * D::WPX + pc) * D::CS + 4 * cq : -1;
       }
@@ -297,6 +490,7 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
 #pragma unroll
     for (int t = 0; t < ABATCH; ++t)
       if (it0 + t < D::AIT && dst[t] >= 0) *reinterpret_cast<f32x4 *>(As + dst[t]) = v[t];
+  }
   }
 
   // lane A bases: row r of M-tile i = unit (wave's tile i, r / 4), window / quad position r % 4
@@ -383,6 +577,12 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
 template <class Pr, int WM, int WN, int TMW, int CK>
 __global__ __launch_bounds__(64 * WM * WN) void dconv_kernel(Pr p, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  if constexpr (HasAdvance<Pr>::value) {
+    if (p.advance && blockIdx.x == 0 && threadIdx.x == 0) {
+      p.advance[0] += p.advance_by;
+      p.advance[1] += p.advance_by;
+    }
+  }
   const int G = gridDim.x;
   if (ntiles > G) {
     const int t0 = (int)((long)blockIdx.x * ntiles / G), t1 = (int)((long)(blockIdx.x + 1) * ntiles / G);
@@ -432,10 +632,158 @@ struct DConvFor {
 
 template <class G, bool U8, bool POOL>
 static int conv_forward_direct(const void *X, const float *W, const float *bias, float *Y, uint8_t *arg, int B,
-                               int act, float alpha, hipStream_t s) {
+                               int act, float alpha, hipStream_t s, uint32_t *advance = nullptr,
+                               uint32_t advance_by = 0) {
   using F = DConvFor<G, POOL>;
   using Pr = DFwd<G, U8, POOL>;
-  const Pr p{reinterpret_cast<const typename Pr::InT *>(X), W, bias, Y, arg, act, alpha};
+  Pr p{reinterpret_cast<const typename Pr::InT *>(X), W, bias, Y, arg, act, alpha};
+  p.advance = advance;
+  p.advance_by = advance_by;
+  return launch_dconv<Pr, F::WM, F::WN, F::TMW, F::CK>(p, B, s);
+}
+
+// ---- the NATURE rollout chain's trunk as one dataflow launch ----------------------------------
+// conv1 (DFwdStack: each env's blocks wait for its publication), conv2 and conv3 of every env in ONE
+// grid: blocks [0, n1) are conv1 tiles, [n1, n1 + n2) conv2 tiles, then conv3, each role env-major.
+// A conv2 block of env e starts once env e's conv1 blocks have stored their activations (a per-env
+// counter), a conv3 block once env e's conv2 blocks have: env e's whole trunk runs while the
+// emulators still step the later envs, instead of conv2 / conv3 waiting behind the LAST env's
+// conv1 at two kernel boundaries. Deadlock-free: a block waits only for lower-indexed blocks (or
+// the host), and each XCD dispatches its workgroups in index order, so the lowest unfinished block
+// is always resident. The hand-off is tools/handoff_probe.hip's (0 stale of 200 launches):
+// activations stored and loaded with agent-scope (sc1) accesses (DFwd COH_OUT / COH_IN), every
+// wave's stores retired (vmcnt(0)) before the block barrier, then one relaxed agent-scope
+// increment; a consumer's lane 0 polls the counter (s_sleep; bounded ~2 s -> status, then it
+// proceeds: the host reports the error). The last conv3 block of env e resets env e's counters for
+// the next launch; with `advance` (the replayed graph's bootstrap chain) the last env to finish
+// advances the sequence bases — every conv1 block, their only reader here, has run by then.
+// Tiles: 4 waves for every role (conv2 / conv3: 4 N-tiles of one 16-row M-tile, 4 units a block,
+// so one env's conv2 spreads over 6 blocks and its conv3 over 4).
+template <class G1, class G2, class G3>
+struct NatureChain {
+  using P1 = DFwdStack<G1, true>;
+  using P2 = DFwd<G2, false, false, true, true>;
+  using P3 = DFwd<G3, false, false, true, false>;
+  using D1 = DConvCfg<P1, 4, 1, 1, 0>;
+  using D2 = DConvCfg<P2, 1, 4, 1, G2::CIN>;
+  using D3 = DConvCfg<P3, 1, 4, 1, G3::CIN>;
+  static constexpr size_t LDS = std::max(D1::LDS, std::max(D2::LDS, D3::LDS));
+  static_assert(D1::NT == 256 && D2::NT == 256 && D3::NT == 256, "one block size for every role");
+  static constexpr int BPE = D1::BPI + D2::BPI + D3::BPI;  // blocks per env
+  static constexpr int SYNC_WORDS = 4;                     // per env: conv1 / conv2 / conv3 done
+};
+
+__device__ __forceinline__ void chain_signal(uint32_t *c) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's (sc1) stores have completed
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void chain_wait(const uint32_t *c, uint32_t want, uint32_t *status) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+        if (status) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <class NC>
+__global__ __launch_bounds__(256) void nature_chain_kernel(typename NC::P1 p1, typename NC::P2 p2,
+                                                           typename NC::P3 p3, uint32_t *sync, int E,
+                                                           uint32_t *status, uint32_t *advance, uint32_t advance_by) {
+  using D1 = typename NC::D1;
+  using D2 = typename NC::D2;
+  using D3 = typename NC::D3;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int n1 = E * D1::BPI, n2 = E * D2::BPI;
+  const int bid = blockIdx.x;
+  if (bid < n1) {
+    const int t = xcd_tile(bid, n1);  // (an env's conv1 tiles on one XCD: their patch rows overlap)
+    dconv_body<typename NC::P1, 4, 1, 1, 0>(p1, t, t + 1, smem);
+    chain_signal(sync + NC::SYNC_WORDS * (t / D1::BPI));
+  } else if (bid < n1 + n2) {
+    const int t = bid - n1, e = t / D2::BPI;
+    chain_wait(sync + NC::SYNC_WORDS * e, D1::BPI, status);
+    dconv_body<typename NC::P2, 1, 4, 1, D2::CK>(p2, t, t + 1, smem);
+    chain_signal(sync + NC::SYNC_WORDS * e + 1);
+  } else {
+    const int t = bid - n1 - n2, e = t / D3::BPI;
+    uint32_t *c = sync + NC::SYNC_WORDS * e;
+    chain_wait(c + 1, D2::BPI, status);
+    dconv_body<typename NC::P3, 1, 4, 1, D3::CK>(p3, t, t + 1, smem);
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(c + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)D3::BPI - 1) {
+      // env e's last block: every block of env e is past its wait — reset for the next launch
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (advance) {
+        uint32_t *g = sync + NC::SYNC_WORDS * E;  // envs finished
+        if (__hip_atomic_fetch_add(g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)E - 1) {
+          __hip_atomic_store(g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          advance[0] += advance_by;
+          advance[1] += advance_by;
+        }
+      }
+    }
+  }
+}
+
+// The NATURE chain's trunk convs (stacking conv1 -> conv2 -> conv3) as one nature_chain_kernel
+// launch. sync: NC::SYNC_WORDS * B + 1 zero-initialised words (left zero by every launch).
+template <class G1, class G2, class G3>
+static int launch_nature_chain(const StackSrc &st, const float *W1, const float *W2, const float *W3, float *a1,
+                               float *a2, float *a3, int B, int act, float alpha, uint32_t *sync, uint32_t *advance,
+                               uint32_t advance_by, hipStream_t s) {
+  using NC = NatureChain<G1, G2, G3>;
+  static_assert(NC::LDS <= 160 * 1024, "LDS budget");
+  if (B <= 0 || !launch_allowed()) return MT_OK;
+  typename NC::P1 p1{};
+  p1.X = st.out;
+  p1.Wt = W1;
+  p1.bias = W1 + G1::KK * G1::COUT;
+  p1.Y = a1;
+  p1.act = act;
+  p1.alpha = alpha;
+  p1.st = st;
+  typename NC::P2 p2{a1, W2, W2 + G2::KK * G2::COUT, a2, nullptr, act, alpha};
+  typename NC::P3 p3{a2, W3, W3 + G3::KK * G3::COUT, a3, nullptr, act, alpha};
+  auto kern = &nature_chain_kernel<NC>;
+  static bool attr_set = false;
+  if (!attr_set && NC::LDS > 64 * 1024) {
+    MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)NC::LDS));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(B * NC::BPE)), dim3(256), NC::LDS, s, p1, p2, p3, sync, B, st.status,
+                     advance, advance_by);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+// conv1 of the stacking rollout chain (DFwdStack): the new state st.out is built and read in-kernel
+template <class G>
+static int conv_forward_stack(const StackSrc &st, const float *W, const float *bias, float *Y, int B, int act,
+                              float alpha, hipStream_t s) {
+  using F = DConvFor<G, false>;
+  using Pr = DFwdStack<G>;
+  using D = DConvCfg<Pr, F::WM, F::WN, F::TMW, F::CK>;
+  static_assert(4 * D::RIN * G::W <= 4 * D::BSZ, "frame rows fit the weight buffer they borrow");
+  Pr p{};
+  p.X = st.out;
+  p.Wt = W;
+  p.bias = bias;
+  p.Y = Y;
+  p.arg = nullptr;
+  p.act = act;
+  p.alpha = alpha;
+  p.st = st;
   return launch_dconv<Pr, F::WM, F::WN, F::TMW, F::CK>(p, B, s);
 }
 
@@ -455,6 +803,22 @@ static int conv_dgrad_unpool_solo(const float *dY, const float *Wt, const float 
                                   int B, int act, float alpha, hipStream_t s) {
   return launch_dconv<DBwdUnpool<G, GJ>, 4, 2, (G::COUT >= 64 ? 1 : 2), G::COUT>(
       DBwdUnpool<G, GJ>{dY, Wt, Pj, argj, dactj, act, alpha}, B, s);
+}
+
+// dX of a phase-separable VALID conv (NATURE conv2 / conv3) as its own 8-wave direct-conv launch
+// ahead of the layer's weight-gradient group (DBwdStrided). Tiles: 4 N-tiles per wave row (2 wave
+// rows); conv2 (128 phase channels) 2 M-tiles per wave = 2 blocks per image, conv3 (64) 3 = 1.
+template <class G>
+constexpr bool dconv_bwd_strided() {
+  if constexpr (G::SAME || G::KH % G::S != 0 || G::H % G::S != 0) return false;
+  else return G::H / G::S == G::OH + G::KH / G::S - 1 && G::COUT == 64;
+}
+template <class G>
+static int conv_dgrad_strided_solo(const float *dY, const float *Wt, const float *Xact, float *dX, int B, int act,
+                                   float alpha, hipStream_t s) {
+  using Pr = DBwdStrided<G>;
+  constexpr int TMW = G::S > 1 ? 2 : 3;
+  return launch_dconv<Pr, 2, 4, TMW, Pr::CI>(Pr{dY, Wt, Xact, dX, act, alpha}, B, s);
 }
 
 // ---- weight gradient ---------------------------------------------------------------------------

@@ -61,8 +61,20 @@ struct PwyxArch {  // networks.py:206-225: SAME convs, 2x2 pools after conv1-3
 template <class Ar, int I>
 using LayerG = std::tuple_element_t<I, typename Ar::Layers>;
 
+// gray NATURE: the rollout chain stacks in conv1 and runs its convs as one dataflow launch
+// (dconv.h nature_chain_kernel)
+template <class Ar>
+constexpr bool nature_stacking() {
+  if constexpr (Ar::LSTM || Ar::NCONV != 3) return false;
+  else return LayerG<Ar, 0>::CIN == 4 && !LayerG<Ar, 0>::SAME;
+}
+
 // The NIPS gray trunk's conv backward as one launch of per-image workgroups (nips_bwd.h) instead of
 // the layered trunk_backward.
+// Its slabs are per image (257 x 16 floats each, summed serially per column), so above this batch
+// the layered trunk_backward (split-K slabs capped at kSlabFloats) takes over: at the benchmarked
+// batches (N = E * T <= 1,280) the fused form's two slab regions stay <= 21 MB each.
+constexpr int kNipsFusedBwdMaxRows = 1280;
 template <class Ar>
 constexpr bool nips_fused_bwd() {
   if constexpr (Ar::LSTM || Ar::NCONV != 2 || Ar::FUSED_SLABS == 0) return false;
@@ -190,6 +202,7 @@ struct WsLayout {
   // parg = its window argmax bytes (pooled layers: the conv epilogue pools, EpBiasActPool), dact =
   // the gradient of the conv output (pre-activation after masking; full resolution)
   size_t act[4], pool[4], parg[4], dact[4], fcslab, H, dz, dH, wslab, wslab2, total;
+  size_t sync;  // gray NATURE: nature_chain_kernel's per-env counters (u32, zero between launches)
   int fc_splits;
 };
 
@@ -309,7 +322,8 @@ static WsLayout ws_layout(const mt_net *n, int B) {
   size_t wslab = 0;
   ws_layers<Ar>(L, off, B, wslab);
   if constexpr (nips_fused_bwd<Ar>())  // per-image conv1 slabs (wslab), per-pair conv2 slabs (wslab2)
-    wslab = std::max(wslab, std::max((size_t)B * NipsConvBwdJob::SLAB1, (size_t)((B + 1) / 2) * NipsConvBwdJob::SLAB2));
+    if (B <= kNipsFusedBwdMaxRows)
+      wslab = std::max(wslab, std::max((size_t)B * NipsConvBwdJob::SLAB1, (size_t)((B + 1) / 2) * NipsConvBwdJob::SLAB2));
   L.fc_splits = fc_splits<Ar>(B, Ar::F);
   L.fcslab = take((size_t)std::max(L.fc_splits, Ar::FUSED_SLABS) * B * Ar::F);
   L.H = take((size_t)B * Ar::F);
@@ -317,6 +331,7 @@ static WsLayout ws_layout(const mt_net *n, int B) {
   L.dH = take((size_t)B * Ar::F);
   L.wslab = take(wslab);
   L.wslab2 = take(wslab);  // ping-pong slab regions of consecutive conv layers (trunk_backward)
+  L.sync = take(nature_stacking<Ar>() ? (size_t)4 * B + 1 : 0);
   L.total = off;
   return L;
 }
@@ -977,25 +992,55 @@ static const float *layer_out(float *ws, const WsLayout &L) {
   return ws + (pooled<Ar, I>() ? L.pool[I] : L.act[I]);
 }
 
+// The layered trunk with the rollout chain's extras: st = the stacking source of conv1 (the NATURE
+// gray chain: DFwdStack, x = st->out); advance = the replayed rollout graph's sequence bases, advanced
+// by conv2's block 0 (the bootstrap chain; the NIPS chain's dense kernel does it, nips_fc_kernel).
+struct FwdExtras {
+  const StackSrc *st = nullptr;
+  uint32_t *advance = nullptr;
+  uint32_t advance_by = 0;
+  uint32_t *sync = nullptr;  // the E-row workspace's counters (WsLayout::sync): st -> nature_chain_kernel
+};
+
 template <class Ar, int I = 0>
 static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, float *ws,
-                         const WsLayout &L, hipStream_t s) {
+                         const WsLayout &L, hipStream_t s, const FwdExtras &ex = FwdExtras{}) {
   if constexpr (I < Ar::NCONV) {
     using G = LayerG<Ar, I>;
     const float *W = P + n->off_conv[I];
+    if (I == 0 && ex.st && !nature_stacking<Ar>()) {
+      set_error("the stacking conv1 is built for the NIPS and the gray NATURE trunks");
+      return MT_ERR_UNSUPPORTED;
+    }
+    if constexpr (I == 0 && nature_stacking<Ar>()) {
+      if (ex.st) {  // the rollout chain: stacking conv1 -> conv2 -> conv3 as one dataflow launch
+        if (!ex.sync) {
+          set_error("nature chain: no counter region");
+          return MT_ERR_ARG;
+        }
+        return launch_nature_chain<LayerG<Ar, 0>, LayerG<Ar, 1>, LayerG<Ar, 2>>(
+            *ex.st, W, P + n->off_conv[1], P + n->off_conv[2], ws + L.act[0], ws + L.act[1], ws + L.act[2], B,
+            n->cfg.activation, n->cfg.alpha_leaky, ex.sync, ex.advance, ex.advance_by, s);
+      }
+    }
+    if (I == 1 && ex.advance && !(Ar::NCONV == 3 && !G::SAME && G::CIN != 12)) {
+      set_error("the sequence-base advance rides on the NATURE direct conv2");
+      return MT_ERR_UNSUPPORTED;
+    }
     // PWYX / LSTM frame trunk (stride-1 SAME) and NATURE (strided VALID): direct conv, patch in LDS (dconv.h)
     // (the RGB NATURE conv1's 768-deep K with its 24-row patch exceeds the LDS: generic)
     if constexpr ((G::S == 1 && G::SAME) || (Ar::NCONV == 3 && !G::SAME && G::CIN != 12))
       MT_TRY((conv_forward_direct<G, I == 0, pooled<Ar, I>()>(
           x, W, W + G::KK * G::COUT, ws + (pooled<Ar, I>() ? L.pool[I] : L.act[I]),
-          pooled<Ar, I>() ? (uint8_t *)(ws + L.parg[I]) : nullptr, B, n->cfg.activation, n->cfg.alpha_leaky, s)));
+          pooled<Ar, I>() ? (uint8_t *)(ws + L.parg[I]) : nullptr, B, n->cfg.activation, n->cfg.alpha_leaky, s,
+          I == 1 ? ex.advance : nullptr, ex.advance_by)));
     else if constexpr (pooled<Ar, I>())
       MT_TRY((conv_forward_pool<G, I == 0>(x, W, W + G::KK * G::COUT, ws + L.pool[I], (uint8_t *)(ws + L.parg[I]), B,
                                            n->cfg.activation, n->cfg.alpha_leaky, s)));
     else
       MT_TRY((conv_forward<G, I == 0>(x, W, W + G::KK * G::COUT, ws + L.act[I], B, n->cfg.activation,
                                       n->cfg.alpha_leaky, s)));
-    return trunk_forward<Ar, I + 1>(n, P, layer_out<Ar, I>(ws, L), B, ws, L, s);
+    return trunk_forward<Ar, I + 1>(n, P, layer_out<Ar, I>(ws, L), B, ws, L, s, ex);
   }
   return MT_OK;
 }
@@ -1037,6 +1082,10 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
                                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act,
                                                            al),
                           wg.gemm, pending, extra));
+    } else if constexpr (dconv_bwd_strided<G>()) {  // direct phase dX launch (dconv.h DBwdStrided), then dW
+      MT_TRY((conv_dgrad_strided_solo<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B, act,
+                                         al, s)));
+      MT_TRY(launch_group(s, wg.gemm, pending, extra));
     } else {
       MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
                                                act, al),
@@ -1123,11 +1172,15 @@ static ActRows act_rows(const mt_net *n, float *ws, const WsLayout &L, const Tra
 template <class Ar>
 static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int B, float *ws,
                         float *v, float *pi, float *rep, const SampleArgs *smp, hipStream_t s,
-                        const TrainRows *tr = nullptr, const hipEvent_t *marks = nullptr) {
+                        const TrainRows *tr = nullptr, const hipEvent_t *marks = nullptr,
+                        const StackSrc *st = nullptr) {
   const WsLayout L = ws_layout<Ar>(n, B);
   const ActRows A = act_rows<Ar>(n, ws, L, tr);
   if (marks) MT_HIP(hipEventRecord(marks[0], s));
-  MT_TRY((trunk_forward<Ar>(n, P, obs, B, A.base, A.L, s)));
+  FwdExtras ex;
+  ex.st = st;
+  ex.sync = reinterpret_cast<uint32_t *>(ws + L.sync);
+  MT_TRY((trunk_forward<Ar>(n, P, obs, B, A.base, A.L, s, ex)));
   const float *flat = layer_out<Ar, Ar::NCONV - 1>(A.base, A.L);
   // dense layer (networks.py:57-70), split-K partial slabs; heads kernel finishes bias + act.
   const float *Wfc = P + n->off_fc;
@@ -1165,11 +1218,8 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
                         n->cfg.alpha_leaky, hp, n->cfg.softmax_temp, A.base + A.h_off, v, pi, rep,
                         smp ? *smp : SampleArgs{});
   } else {
-    if (st) {
-      set_error("stacking forward is built for the NIPS arch only");
-      return MT_ERR_ARG;
-    }
-    return forward_impl<Ar>(n, P, obs, B, ws, v, pi, rep, smp, s, tr, marks);
+    // (NATURE gray: conv1 stacks, trunk_forward refuses st for the other archs)
+    return forward_impl<Ar>(n, P, obs, B, ws, v, pi, rep, smp, s, tr, marks, st);
   }
 }
 
@@ -1188,11 +1238,12 @@ static int forward_boot_impl(const mt_net *n, const float *P, const uint8_t *obs
     return launch_nips_trunk<C>(obs, st, B, P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation,
                                 n->cfg.alpha_leaky, ws + L.act[1], nullptr, ws + L.fcslab, s, advance, advance_by);
   } else {
-    if (st || advance) {
-      set_error("stacking / replayed bootstrap is built for the NIPS arch only");
-      return MT_ERR_ARG;
-    }
-    MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s)));
+    FwdExtras ex;
+    ex.st = st;
+    ex.advance = advance;
+    ex.advance_by = advance_by;
+    ex.sync = reinterpret_cast<uint32_t *>(ws + L.sync);
+    MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s, ex)));
     const float *flat = layer_out<Ar, Ar::NCONV - 1>(ws, L);
     return launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1}, EpSlab{ws + L.fcslab, B, Ar::F},
                                B, Ar::F, Ar::FLAT, L.fc_splits, s);
@@ -1280,7 +1331,8 @@ static int backward_impl(const mt_net *n, const float *P, const uint8_t *obs, in
               kDenseBucketLaunches);
     return MT_ERR_UNSUPPORTED;
   }
-  if constexpr (nips_fused_bwd<Ar>()) return nips_conv_backward<Ar>(n, P, obs, B, ws, L, grad, s, no);
+  if constexpr (nips_fused_bwd<Ar>())
+    if (B <= kNipsFusedBwdMaxRows) return nips_conv_backward<Ar>(n, P, obs, B, ws, L, grad, s, no);
   return trunk_backward<Ar, K>(n, P, obs, B, ws, L, grad, s, SlabJob{}, no);
 }
 
@@ -1507,11 +1559,10 @@ static int trunk_infer_impl(const mt_net *n, const float *P, const uint8_t *obs,
       MT_LAUNCHED();
       return MT_OK;
     } else {
-      if (st) {
-        set_error("stacking trunk is built for the NIPS arch only");
-        return MT_ERR_UNSUPPORTED;
-      }
-      MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s)));
+      FwdExtras ex;
+      ex.st = st;
+      ex.sync = reinterpret_cast<uint32_t *>(ws + L.sync);
+      MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s, ex)));
       return launch_gemm<TileFc>(LdRowMajor{layer_out<Ar, Ar::NCONV - 1>(ws, L), Ar::FLAT},
                                  LdColMajor{Wfc, Ar::F, -1}, EpSlab{ws + L.fcslab, B, Ar::F}, B, Ar::F, Ar::FLAT,
                                  L.fc_splits, s);
@@ -1549,7 +1600,7 @@ extern "C" int mt_forward_trunk_stacking(const mt_net *net, const float *params,
       return MT_ERR_WORKSPACE;
     }
     if constexpr (Ar::LSTM) {
-      set_error("stacking trunk is built for the NIPS arch only");
+      set_error("stacking trunk is built for the NIPS and the gray NATURE archs only");
       return MT_ERR_UNSUPPORTED;
     } else {
       return trunk_infer_impl<Ar>(net, params, out, batch, (float *)ws, (hipStream_t)stream, &st);

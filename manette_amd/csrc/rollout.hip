@@ -24,7 +24,7 @@ struct mt_rollout {
                                // up to T steps ahead)
   bool zero_copy, in_place, pooled, resized, pipelined;
   bool pull;          // pipelined + resized: per-env ready words, pull kernel into HBM, tagged pairs
-  bool stack_fwd;     // pull + NIPS: the forward's conv kernel stacks (no preprocess launch)
+  bool stack_fwd;     // pull + NIPS / gray NATURE: the forward's conv(1) kernel stacks (no preprocess launch)
   bool lstm;          // LSTM arch: frame-store forward per step (mt_lstm_step_forward), nz on the device
   bool boot_slabs;    // MT_ROLLOUT_BOOT_SLABS: the bootstrap chain ends at the dense slabs (no heads)
   const uint8_t *fstore = nullptr;  // LSTM: the frame store (states = its slot 4)
@@ -158,7 +158,9 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   ro->resized = rz;
   ro->pipelined = pl;
   ro->pull = pl && rz;
-  ro->stack_fwd = ro->pull && cfg.arch == MT_ARCH_NIPS;
+  // the stacking chains: NIPS (nips_conv_kernel<STACK>) and gray NATURE (conv1 = DFwdStack): each
+  // env's conv1 waits for its own publication, no pull / preprocess kernel in front of the convs
+  ro->stack_fwd = ro->pull && (cfg.arch == MT_ARCH_NIPS || (cfg.arch == MT_ARCH_NATURE && cfg.depth == 1));
   ro->lstm = lstm;
   ro->boot_slabs = (b.flags & MT_ROLLOUT_BOOT_SLABS) != 0;
   ro->over_dev = (const float *)over_dev;
@@ -494,7 +496,7 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
   return MT_OK;
 }
 
-// The replayed rollout graph applies to the NIPS stacking chains with the bootstrap in the last
+// The replayed rollout graph applies to the stacking chains (NIPS, gray NATURE) with the bootstrap in the last
 // chain, every chain armed at step 0, after a first eager rollout (step 0's forward then takes
 // slot 0 from slot T), without trunk timing (its events are per launch).
 bool graph_eligible(const mt_rollout *ro) {

@@ -244,10 +244,10 @@ class PAACLearner(ActorLearner):
         self.native_step = h
         self._over_dev = devnet.host_device_pointer(r.over) if self.lstm_bool else None
         self.boot_in_rollout = self.pipeline  # the last step's chain runs the bootstrap forward
-        # the rollout's stacking NIPS forward (pipelined, resized staging) also carries slot T over
-        # into slot 0 at the next step 0 (mt_rollout_step): the update does not copy it
-        self.slot0_in_rollout = self.pipeline and self.staging == 'resized' and self.network.arch == 'NIPS' \
-            and not self.lstm_bool
+        # the rollout's stacking forward (pipelined, resized staging; NIPS, gray NATURE) also carries
+        # slot T over into slot 0 at the next step 0 (mt_rollout_step): the update does not copy it
+        self.slot0_in_rollout = self.pipeline and self.staging == 'resized' and not self.lstm_bool and (
+            self.network.arch == 'NIPS' or (self.network.arch == 'NATURE' and self.depth == 1))
         self._gs = C.c_int64(0)
 
     def _upload_pushes(self, total, out, prev):

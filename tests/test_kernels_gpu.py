@@ -482,15 +482,17 @@ def test_zero_copy_reads_see_host_rewrites_across_launches():
             np.testing.assert_array_equal(got[e], preprocess.stack_update(pv[e], pushes, depth), err_msg='round %d' % it)
 
 
-@pytest.mark.parametrize('E,depth', [(7, 1), (32, 1), (5, 3)])
-def test_stacking_trunk_in_kernel_pull(E, depth):
-    """mt_forward_trunk_stacking — the rollout chain's conv kernel pulling each env's frames from
-    pinned host staging behind its ready word (edge cache lines read with system-scope loads):
-    the stacked state == the A2 oracle (bit-exact), and the trunk outputs (act2 + dense partial
-    slabs) == mt_forward_trunk on that state, bit for bit."""
+@pytest.mark.parametrize('arch,E,depth', [('NIPS', 7, 1), ('NIPS', 32, 1), ('NIPS', 5, 3), ('NATURE', 7, 1),
+                                          ('NATURE', 64, 1)])
+def test_stacking_trunk_in_kernel_pull(arch, E, depth):
+    """mt_forward_trunk_stacking — the rollout chain's conv kernel (NIPS: nips_conv_kernel<STACK>;
+    gray NATURE: conv1 = the direct conv with DFwdStack's patch staging) pulling each env's frames
+    from pinned host staging behind its ready word (edge cache lines read with system-scope loads):
+    the stacked state == the A2 oracle (bit-exact), and the trunk outputs (conv activations + dense
+    partial slabs) == mt_forward_trunk on that state, bit for bit."""
     from manette_amd.network import host_device_pointer
     import ctypes as C
-    net = _net('NIPS', depth, 6, 11, seed=E)
+    net = _net(arch, depth, 6, 11, seed=E)
     rs = np.random.RandomState(30 + E + depth)
     counts = rs.randint(1, 5, E).astype(np.int32)
     counts[:2] = 4  # full slot groups: their last line borders the next env's first
@@ -517,3 +519,30 @@ def test_stacking_trunk_in_kernel_pull(E, depth):
     net.forward_trunk(out, E, ws_key='plain')
     torch.cuda.synchronize()
     assert torch.equal(ws[:ws2.numel()], ws2)
+
+
+def test_nips_backward_above_fused_cap():
+    """Above kNipsFusedBwdMaxRows (1,280 rows) the NIPS gray conv backward takes the layered
+    trunk_backward (per-image slabs would grow without bound): the gradient of 1,281 rows
+    (loss = 5/B sum of row terms) == the B-weighted sum of the fused path's gradients of rows
+    [0, 1280) and of row 1280, within fp32 reduction order."""
+    A, R = 6, 1
+    net = _net('NIPS', 1, A, R, seed=21)
+    rs = np.random.RandomState(21)
+    B = 1281
+    obs = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda()
+    a_idx = torch.from_numpy(rs.randint(0, A, B).astype(np.int32)).cuda()
+    r_idx = torch.from_numpy(rs.randint(0, R, B).astype(np.int32)).cuda()
+    y = torch.from_numpy(rs.randn(B).astype(np.float32)).cuda()
+    adv = torch.from_numpy(rs.randn(B).astype(np.float32)).cuda()
+
+    def grad(lo, hi):
+        n = hi - lo
+        v, pi, rep = net.forward(obs[lo:hi], ws_key=('cap', n))
+        net.loss_backward(obs[lo:hi], n, v, pi, rep, a_idx[lo:hi], r_idx[lo:hi], y[lo:hi], adv[lo:hi],
+                          ws_key=('cap', n))
+        torch.cuda.synchronize()
+        return net.grad.double().cpu().numpy() * n
+    whole = grad(0, B)
+    parts = grad(0, 1280) + grad(1280, B)
+    assert np.linalg.norm(whole - parts) <= 2e-5 * np.linalg.norm(parts)
