@@ -569,11 +569,16 @@ def main():
             # the rollout chain's own kernels; in the loop each conv block also waits for its env's
             # emulator (in-kernel pull), so the roofline times them with every env published
             tk_ms = iso_ms
-            kern = 'nips_conv_kernel<%d, true> (in-kernel pull) + nips_fc_kernel<%d>: the stacking rollout chain' % (
-                C_in, C_in)
+            if cfg['arch'] == 'NIPS':
+                kern = 'nips_conv_kernel<%d, true> (in-kernel pull) + nips_fc_kernel<%d>: the stacking rollout chain' % (
+                    C_in, C_in)
+                pmc_kernels = ['nips_conv_kernel<%d, true>' % C_in, 'nips_fc_kernel<%d>' % C_in]
+            else:
+                kern = ('nature_chain_kernel (stacking conv1 with in-kernel pull -> conv2 -> conv3, per-env hand-offs '
+                        'in one launch) + the split-K dense GEMM: the stacking rollout chain')
+                pmc_kernels = ['nature_chain_kernel', 'gemm_f32_kernel']
             timing = ('mt_forward_trunk_stacking (every env published, its pushes in HBM: the kernels the timed loop '
                       'runs, with nothing to wait for), ' + graph_note)
-            pmc_kernels = ['nips_conv_kernel<%d, true>' % C_in, 'nips_fc_kernel<%d>' % C_in]
         elif inloop_us is not None and not lstm:  # (LSTM: step 0's forward has 1 + 5E rows, the others E)
             tk_ms = inloop_us * 1e-3
             kern = 'trunk kernels of the rollout forward (implicit-GEMM convs + split-K dense)'
@@ -613,7 +618,8 @@ def main():
                        note='standalone mt_preprocess_resized of the E envs (%d pushes); %s' % (stack_pushes, graph_note))]
         if stacking:
             share = (med(prof['rollout_trunk']) - med(prof['plain_trunk']))
-            kernels.append({'row': 'A2 (fused)', 'kernel': 'stacking share of nips_conv_kernel<%d, true>' % C_in,
+            kernels.append({'row': 'A2 (fused)', 'kernel': 'stacking share of %s' % (
+                                'nips_conv_kernel<%d, true>' % C_in if cfg['arch'] == 'NIPS' else 'nature_chain_kernel'),
                             'us': round(share, 2), 'note': 'stacking trunk minus the same trunk on a resident state '
                             '(mt_forward_trunk): the cost of the in-kernel stack in the benchmarked chain'})
         tl = prof['train_launches']

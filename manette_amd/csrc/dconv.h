@@ -31,6 +31,16 @@
 
 namespace mt {
 
+// Probe builds (-DMT_PROBE): per env, when its publication was seen by a conv1 block (0) and when
+// its last conv1 / conv2 / conv3 block finished (1, 2, 3); s_memrealtime, read by mt_probe_read_chain
+#ifdef MT_PROBE
+static __device__ unsigned long long mt_probe_chain[512 * 4];
+#define MT_PROBE_CHAIN(e, p) \
+  if ((e) < 512) mt_probe_chain[(e) * 4 + (p)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define MT_PROBE_CHAIN(e, p)
+#endif
+
 // ---- problems ------------------------------------------------------------------------------
 // Forward of conv G: X = its input [B][H][W][CIN] (u8 frames for conv1), Y = the pooled output
 // [B][OH/2][OW/2][COUT] + argmax bytes (POOL, EpBiasActPool's layout and first-max rule) or the
@@ -49,11 +59,6 @@ struct DFwd {
   uint8_t *arg;
   int act;
   float alpha;
-  // optional (the replayed rollout graph's bootstrap chain, whose dense layer is a generic GEMM):
-  // block 0 adds advance_by to advance[0] and advance[1] at its start — every reader of those
-  // sequence bases in the replay (the stacking conv1 blocks, the heads kernels) has run by then
-  uint32_t *advance = nullptr;
-  uint32_t advance_by = 0;
   __device__ __forceinline__ f32x4 wquad(int k, int n) const {  // W(k .. k+3, n), zero past KK
     f32x4 v;
 #pragma unroll
@@ -148,6 +153,7 @@ struct DFwdStack : DFwd<G, true, false, false, COH_OUT> {
       if (st.ready) {
         const uint32_t tag = st.tag_base ? ((*st.tag_base + st.tag) & 0x1fffffffu) : st.tag;
         np = min(max(wait_published(st.ready, b, tag, st.status), 0), 4);  // (a timeout stacks no frame)
+        MT_PROBE_CHAIN(b, 0);
       } else if (st.count) {
         np = min(max(st.count[b], 1), 4);
       }
@@ -262,15 +268,11 @@ struct DBwdStrided {
   }
 };
 
-// problems with their own patch staging (DFwdStack) / a sequence-base advance (DFwd)
+// problems with their own patch staging (DFwdStack)
 template <class P, class = void>
 struct HasStagePatch : std::false_type {};
 template <class P>
 struct HasStagePatch<P, std::void_t<decltype(P::STAGES_PATCH)>> : std::bool_constant<P::STAGES_PATCH> {};
-template <class P, class = void>
-struct HasAdvance : std::false_type {};
-template <class P>
-struct HasAdvance<P, std::void_t<decltype(std::declval<const P &>().advance)>> : std::true_type {};
 
 // dX of the stride-1 SAME conv G (input = the pooled output of conv GJ): X = dY of G
 // [B][OH][OW][COUT], output = GJ's full-resolution conv-output gradient dact [B][GJ::OH][GJ::OW]
@@ -577,12 +579,6 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
 template <class Pr, int WM, int WN, int TMW, int CK>
 __global__ __launch_bounds__(64 * WM * WN) void dconv_kernel(Pr p, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  if constexpr (HasAdvance<Pr>::value) {
-    if (p.advance && blockIdx.x == 0 && threadIdx.x == 0) {
-      p.advance[0] += p.advance_by;
-      p.advance[1] += p.advance_by;
-    }
-  }
   const int G = gridDim.x;
   if (ntiles > G) {
     const int t0 = (int)((long)blockIdx.x * ntiles / G), t1 = (int)((long)(blockIdx.x + 1) * ntiles / G);
@@ -632,13 +628,10 @@ struct DConvFor {
 
 template <class G, bool U8, bool POOL>
 static int conv_forward_direct(const void *X, const float *W, const float *bias, float *Y, uint8_t *arg, int B,
-                               int act, float alpha, hipStream_t s, uint32_t *advance = nullptr,
-                               uint32_t advance_by = 0) {
+                               int act, float alpha, hipStream_t s) {
   using F = DConvFor<G, POOL>;
   using Pr = DFwd<G, U8, POOL>;
-  Pr p{reinterpret_cast<const typename Pr::InT *>(X), W, bias, Y, arg, act, alpha};
-  p.advance = advance;
-  p.advance_by = advance_by;
+  const Pr p{reinterpret_cast<const typename Pr::InT *>(X), W, bias, Y, arg, act, alpha};
   return launch_dconv<Pr, F::WM, F::WN, F::TMW, F::CK>(p, B, s);
 }
 
@@ -655,8 +648,7 @@ static int conv_forward_direct(const void *X, const float *W, const float *bias,
 // wave's stores retired (vmcnt(0)) before the block barrier, then one relaxed agent-scope
 // increment; a consumer's lane 0 polls the counter (s_sleep; bounded ~2 s -> status, then it
 // proceeds: the host reports the error). The last conv3 block of env e resets env e's counters for
-// the next launch; with `advance` (the replayed graph's bootstrap chain) the last env to finish
-// advances the sequence bases — every conv1 block, their only reader here, has run by then.
+// the next launch.
 // Tiles: 4 waves for every role (conv2 / conv3: 4 N-tiles of one 16-row M-tile, 4 units a block,
 // so one env's conv2 spreads over 6 blocks and its conv3 over 4).
 template <class G1, class G2, class G3>
@@ -673,10 +665,14 @@ struct NatureChain {
   static constexpr int SYNC_WORDS = 4;                     // per env: conv1 / conv2 / conv3 done
 };
 
-__device__ __forceinline__ void chain_signal(uint32_t *c) {
+__device__ __forceinline__ void chain_signal(uint32_t *c, uint32_t last, int e, int phase) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's (sc1) stores have completed
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == last) MT_PROBE_CHAIN(e, phase);
+    (void)old;
+  }
 }
 __device__ __forceinline__ void chain_wait(const uint32_t *c, uint32_t want, uint32_t *status) {
   if (threadIdx.x == 0) {
@@ -695,7 +691,7 @@ __device__ __forceinline__ void chain_wait(const uint32_t *c, uint32_t want, uin
 template <class NC>
 __global__ __launch_bounds__(256) void nature_chain_kernel(typename NC::P1 p1, typename NC::P2 p2,
                                                            typename NC::P3 p3, uint32_t *sync, int E,
-                                                           uint32_t *status, uint32_t *advance, uint32_t advance_by) {
+                                                           uint32_t *status) {
   using D1 = typename NC::D1;
   using D2 = typename NC::D2;
   using D3 = typename NC::D3;
@@ -705,12 +701,12 @@ __global__ __launch_bounds__(256) void nature_chain_kernel(typename NC::P1 p1, t
   if (bid < n1) {
     const int t = xcd_tile(bid, n1);  // (an env's conv1 tiles on one XCD: their patch rows overlap)
     dconv_body<typename NC::P1, 4, 1, 1, 0>(p1, t, t + 1, smem);
-    chain_signal(sync + NC::SYNC_WORDS * (t / D1::BPI));
+    chain_signal(sync + NC::SYNC_WORDS * (t / D1::BPI), D1::BPI - 1, t / D1::BPI, 1);
   } else if (bid < n1 + n2) {
     const int t = bid - n1, e = t / D2::BPI;
     chain_wait(sync + NC::SYNC_WORDS * e, D1::BPI, status);
     dconv_body<typename NC::P2, 1, 4, 1, D2::CK>(p2, t, t + 1, smem);
-    chain_signal(sync + NC::SYNC_WORDS * e + 1);
+    chain_signal(sync + NC::SYNC_WORDS * e + 1, D2::BPI - 1, e, 2);
   } else {
     const int t = bid - n1 - n2, e = t / D3::BPI;
     uint32_t *c = sync + NC::SYNC_WORDS * e;
@@ -720,27 +716,19 @@ __global__ __launch_bounds__(256) void nature_chain_kernel(typename NC::P1 p1, t
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(c + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)D3::BPI - 1) {
       // env e's last block: every block of env e is past its wait — reset for the next launch
+      MT_PROBE_CHAIN(e, 3);
       __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (advance) {
-        uint32_t *g = sync + NC::SYNC_WORDS * E;  // envs finished
-        if (__hip_atomic_fetch_add(g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)E - 1) {
-          __hip_atomic_store(g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          advance[0] += advance_by;
-          advance[1] += advance_by;
-        }
-      }
     }
   }
 }
 
 // The NATURE chain's trunk convs (stacking conv1 -> conv2 -> conv3) as one nature_chain_kernel
-// launch. sync: NC::SYNC_WORDS * B + 1 zero-initialised words (left zero by every launch).
+// launch. sync: NC::SYNC_WORDS * B zero-initialised words (left zero by every launch).
 template <class G1, class G2, class G3>
 static int launch_nature_chain(const StackSrc &st, const float *W1, const float *W2, const float *W3, float *a1,
-                               float *a2, float *a3, int B, int act, float alpha, uint32_t *sync, uint32_t *advance,
-                               uint32_t advance_by, hipStream_t s) {
+                               float *a2, float *a3, int B, int act, float alpha, uint32_t *sync, hipStream_t s) {
   using NC = NatureChain<G1, G2, G3>;
   static_assert(NC::LDS <= 160 * 1024, "LDS budget");
   if (B <= 0 || !launch_allowed()) return MT_OK;
@@ -761,30 +749,9 @@ static int launch_nature_chain(const StackSrc &st, const float *W1, const float 
                                (int)NC::LDS));
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)(B * NC::BPE)), dim3(256), NC::LDS, s, p1, p2, p3, sync, B, st.status,
-                     advance, advance_by);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(B * NC::BPE)), dim3(256), NC::LDS, s, p1, p2, p3, sync, B, st.status);
   MT_LAUNCHED();
   return MT_OK;
-}
-
-// conv1 of the stacking rollout chain (DFwdStack): the new state st.out is built and read in-kernel
-template <class G>
-static int conv_forward_stack(const StackSrc &st, const float *W, const float *bias, float *Y, int B, int act,
-                              float alpha, hipStream_t s) {
-  using F = DConvFor<G, false>;
-  using Pr = DFwdStack<G>;
-  using D = DConvCfg<Pr, F::WM, F::WN, F::TMW, F::CK>;
-  static_assert(4 * D::RIN * G::W <= 4 * D::BSZ, "frame rows fit the weight buffer they borrow");
-  Pr p{};
-  p.X = st.out;
-  p.Wt = W;
-  p.bias = bias;
-  p.Y = Y;
-  p.arg = nullptr;
-  p.act = act;
-  p.alpha = alpha;
-  p.st = st;
-  return launch_dconv<Pr, F::WM, F::WN, F::TMW, F::CK>(p, B, s);
 }
 
 // dX of stride-1 conv G unpooled into GJ's conv-output gradient: its own 8-wave launch ahead of the
@@ -808,10 +775,12 @@ static int conv_dgrad_unpool_solo(const float *dY, const float *Wt, const float 
 // dX of a phase-separable VALID conv (NATURE conv2 / conv3) as its own 8-wave direct-conv launch
 // ahead of the layer's weight-gradient group (DBwdStrided). Tiles: 4 N-tiles per wave row (2 wave
 // rows); conv2 (128 phase channels) 2 M-tiles per wave = 2 blocks per image, conv3 (64) 3 = 1.
+// Measured (round 4, E = 64): conv3 dX 32.4 + dW 18.0 us vs 43.5 for the generic group, conv2 dX
+// 42.0 + dW 27.6 vs 51.2 — the 8-wave blocks (92 / 66 KB of LDS) leave 1-2 blocks per CU over a
+// grid of 320-640: off until the tiling is redone.
 template <class G>
 constexpr bool dconv_bwd_strided() {
-  if constexpr (G::SAME || G::KH % G::S != 0 || G::H % G::S != 0) return false;
-  else return G::H / G::S == G::OH + G::KH / G::S - 1 && G::COUT == 64;
+  return false;
 }
 template <class G>
 static int conv_dgrad_strided_solo(const float *dY, const float *Wt, const float *Xact, float *dX, int B, int act,

@@ -28,6 +28,7 @@ struct LstmArch : PwyxArch<C> {
   static constexpr int F = 128;     // fc6 n_outputs
   static constexpr const char *FC = "fc6";
   static constexpr int FUSED_SLABS = 0;
+  static constexpr int FC_ROWS = 0;
 };
 
 struct LstmWs {

@@ -31,6 +31,7 @@ struct NipsArch {  // networks.py:178-192
   static constexpr int F = 256;
   static constexpr const char *FC = "fc3";
   static constexpr int FUSED_SLABS = FusedNips<C>::ROWS2;  // inference forward: trunk_fused.h
+  static constexpr int FC_ROWS = 0;                         // (the fused trunk has its own dense kernel)
   static constexpr bool LSTM = false;
 };
 template <int C>
@@ -43,6 +44,7 @@ struct NatureArch {  // networks.py:261-278
   static constexpr int F = 512;
   static constexpr const char *FC = "fc4";
   static constexpr int FUSED_SLABS = 0;  // no fused inference trunk: layered path
+  static constexpr int FC_ROWS = 7;      // dense layer by conv3 rows (row_fc_kernel)
   static constexpr bool LSTM = false;
 };
 template <int C>
@@ -55,6 +57,7 @@ struct PwyxArch {  // networks.py:206-225: SAME convs, 2x2 pools after conv1-3
   static constexpr int F = 512;
   static constexpr const char *FC = "fc5";
   static constexpr int FUSED_SLABS = 0;
+  static constexpr int FC_ROWS = 10;  // dense layer by conv4 rows (row_fc_kernel)
   static constexpr bool LSTM = false;
 };
 
@@ -281,8 +284,23 @@ static size_t conv_wgrad_slab(int B) {
 
 template <class Ar>
 static int fc_splits(int B, int F) {
+  if constexpr (Ar::FC_ROWS > 0) return Ar::FC_ROWS;  // row_fc_kernel: one slab per conv output row
   const int s = pick_splits(cdiv(B, TileFc::BM) * cdiv(F, TileFc::BN), Ar::FLAT, TileFc::BK, 128);
   return gemm_splits<TileFc>(Ar::FLAT, s);
+}
+
+// The dense layer's partial slabs [splits][B][F] of the inference forwards: the row-split kernel
+// (trunk_fused.h row_fc_kernel: one slab per conv output row, one memory round trip per block)
+// where the arch has FC_ROWS, else the split-K GEMM. advance: the replayed rollout graph's
+// sequence bases (row_fc_kernel's block 0).
+template <class Ar>
+static int launch_fc(const float *flat, int B, const float *Wfc, float *slabs, int splits, hipStream_t s,
+                     uint32_t *advance = nullptr, uint32_t advance_by = 0) {
+  if constexpr (Ar::FC_ROWS > 0)
+    return launch_row_fc<Ar::FLAT / Ar::FC_ROWS, Ar::FC_ROWS, Ar::F>(flat, B, Wfc, slabs, s, advance, advance_by);
+  else
+    return launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1}, EpSlab{slabs, B, Ar::F}, B,
+                               Ar::F, Ar::FLAT, splits, s);
 }
 
 template <class Ar, int I = 0>
@@ -331,7 +349,7 @@ static WsLayout ws_layout(const mt_net *n, int B) {
   L.dH = take((size_t)B * Ar::F);
   L.wslab = take(wslab);
   L.wslab2 = take(wslab);  // ping-pong slab regions of consecutive conv layers (trunk_backward)
-  L.sync = take(nature_stacking<Ar>() ? (size_t)4 * B + 1 : 0);
+  L.sync = take(nature_stacking<Ar>() ? (size_t)4 * B : 0);
   L.total = off;
   return L;
 }
@@ -576,6 +594,10 @@ static int launch_heads(int rows, hipStream_t s, const float *slabs, int S, int 
 #ifdef MT_PROBE
 extern "C" int mt_probe_read(unsigned long long *out, size_t n) {
   MT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(mt_probe_buf), std::min(n, sizeof(mt_probe_buf) / 8) * 8));
+  return MT_OK;
+}
+extern "C" int mt_probe_read_chain(unsigned long long *out, size_t n) {
+  MT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(mt_probe_chain), std::min(n, sizeof(mt_probe_chain) / 8) * 8));
   return MT_OK;
 }
 #endif
@@ -993,13 +1015,10 @@ static const float *layer_out(float *ws, const WsLayout &L) {
 }
 
 // The layered trunk with the rollout chain's extras: st = the stacking source of conv1 (the NATURE
-// gray chain: DFwdStack, x = st->out); advance = the replayed rollout graph's sequence bases, advanced
-// by conv2's block 0 (the bootstrap chain; the NIPS chain's dense kernel does it, nips_fc_kernel).
+// gray chain: nature_chain_kernel, x = st->out), sync = the E-row workspace's counters it uses.
 struct FwdExtras {
   const StackSrc *st = nullptr;
-  uint32_t *advance = nullptr;
-  uint32_t advance_by = 0;
-  uint32_t *sync = nullptr;  // the E-row workspace's counters (WsLayout::sync): st -> nature_chain_kernel
+  uint32_t *sync = nullptr;
 };
 
 template <class Ar, int I = 0>
@@ -1020,20 +1039,15 @@ static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, 
         }
         return launch_nature_chain<LayerG<Ar, 0>, LayerG<Ar, 1>, LayerG<Ar, 2>>(
             *ex.st, W, P + n->off_conv[1], P + n->off_conv[2], ws + L.act[0], ws + L.act[1], ws + L.act[2], B,
-            n->cfg.activation, n->cfg.alpha_leaky, ex.sync, ex.advance, ex.advance_by, s);
+            n->cfg.activation, n->cfg.alpha_leaky, ex.sync, s);
       }
-    }
-    if (I == 1 && ex.advance && !(Ar::NCONV == 3 && !G::SAME && G::CIN != 12)) {
-      set_error("the sequence-base advance rides on the NATURE direct conv2");
-      return MT_ERR_UNSUPPORTED;
     }
     // PWYX / LSTM frame trunk (stride-1 SAME) and NATURE (strided VALID): direct conv, patch in LDS (dconv.h)
     // (the RGB NATURE conv1's 768-deep K with its 24-row patch exceeds the LDS: generic)
     if constexpr ((G::S == 1 && G::SAME) || (Ar::NCONV == 3 && !G::SAME && G::CIN != 12))
       MT_TRY((conv_forward_direct<G, I == 0, pooled<Ar, I>()>(
           x, W, W + G::KK * G::COUT, ws + (pooled<Ar, I>() ? L.pool[I] : L.act[I]),
-          pooled<Ar, I>() ? (uint8_t *)(ws + L.parg[I]) : nullptr, B, n->cfg.activation, n->cfg.alpha_leaky, s,
-          I == 1 ? ex.advance : nullptr, ex.advance_by)));
+          pooled<Ar, I>() ? (uint8_t *)(ws + L.parg[I]) : nullptr, B, n->cfg.activation, n->cfg.alpha_leaky, s)));
     else if constexpr (pooled<Ar, I>())
       MT_TRY((conv_forward_pool<G, I == 0>(x, W, W + G::KK * G::COUT, ws + L.pool[I], (uint8_t *)(ws + L.parg[I]), B,
                                            n->cfg.activation, n->cfg.alpha_leaky, s)));
@@ -1184,8 +1198,7 @@ static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int
   const float *flat = layer_out<Ar, Ar::NCONV - 1>(A.base, A.L);
   // dense layer (networks.py:57-70), split-K partial slabs; heads kernel finishes bias + act.
   const float *Wfc = P + n->off_fc;
-  MT_TRY((launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1},
-                              EpSlab{ws + L.fcslab, B, Ar::F}, B, Ar::F, Ar::FLAT, L.fc_splits, s)));
+  MT_TRY((launch_fc<Ar>(flat, B, Wfc, ws + L.fcslab, L.fc_splits, s)));
   if (marks) MT_HIP(hipEventRecord(marks[1], s));
   HeadParams hp = head_params(n, P);
   return launch_heads(B, s, ws + L.fcslab, L.fc_splits, B, Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation,
@@ -1240,13 +1253,14 @@ static int forward_boot_impl(const mt_net *n, const float *P, const uint8_t *obs
   } else {
     FwdExtras ex;
     ex.st = st;
-    ex.advance = advance;
-    ex.advance_by = advance_by;
     ex.sync = reinterpret_cast<uint32_t *>(ws + L.sync);
     MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s, ex)));
-    const float *flat = layer_out<Ar, Ar::NCONV - 1>(ws, L);
-    return launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1}, EpSlab{ws + L.fcslab, B, Ar::F},
-                               B, Ar::F, Ar::FLAT, L.fc_splits, s);
+    if (advance && Ar::FC_ROWS == 0) {
+      set_error("sequence-base advance: row-split dense layers only");
+      return MT_ERR_UNSUPPORTED;
+    }
+    return launch_fc<Ar>(layer_out<Ar, Ar::NCONV - 1>(ws, L), B, Wfc, ws + L.fcslab, L.fc_splits, s, advance,
+                         advance_by);
   }
 }
 
@@ -1563,9 +1577,7 @@ static int trunk_infer_impl(const mt_net *n, const float *P, const uint8_t *obs,
       ex.st = st;
       ex.sync = reinterpret_cast<uint32_t *>(ws + L.sync);
       MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s, ex)));
-      return launch_gemm<TileFc>(LdRowMajor{layer_out<Ar, Ar::NCONV - 1>(ws, L), Ar::FLAT},
-                                 LdColMajor{Wfc, Ar::F, -1}, EpSlab{ws + L.fcslab, B, Ar::F}, B, Ar::F, Ar::FLAT,
-                                 L.fc_splits, s);
+      return launch_fc<Ar>(layer_out<Ar, Ar::NCONV - 1>(ws, L), B, Wfc, ws + L.fcslab, L.fc_splits, s);
     }
   }
 }

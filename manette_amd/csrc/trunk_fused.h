@@ -403,17 +403,22 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
   MT_PROBE_AT(0, bid, 4);
 }
 
-// Dense layer partial products: slabs[i][e][n] = sum_{f < 288} act2[e][288 i + f] Wfc[288 i + f][n].
-// Grid (F / 16, 9, ceil(B / 32)); 4 waves split the 18 K chunks of 16 (c = w + 4j), every operand
-// load of a wave issued before its first MFMA; partials added in wave order through LDS.
-// advance (replayed rollout graph whose bootstrap has no heads kernel, SampleArgs::advance): block 0
-// adds advance_by to advance[0] and advance[1] — every reader of those bases in the replay has run.
-template <int C>
-__global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ act2, int B,
-                                                      const float *__restrict__ Wfc, float *__restrict__ slabs,
-                                                      uint32_t *advance, uint32_t advance_by) {
-  using Fz = FusedNips<C>;
-  __shared__ __attribute__((aligned(16))) float red[4][Fz::FC_BM][Fz::FC_BN];
+// Dense layer partial products by trunk rows: slabs[i][e][n] = sum_{f < FEAT} x[e][FEAT i + f]
+// W[FEAT i + f][n] (x = the flattened last conv output [B][ROWS * FEAT], NHWC: row i of the conv
+// output = features [FEAT i, FEAT (i + 1))). Grid (F / 16, ROWS, ceil(B / 32)); 4 waves split the
+// FEAT / 16 K chunks of 16 (c = w + 4j), every operand load of a wave issued before its first MFMA
+// (one memory round trip, where a generic split-K GEMM block walks its K chunks one load latency
+// each: NATURE's dense layer 10 us as a TileFc GEMM at E = 64); partials added in wave order
+// through LDS. advance (replayed rollout graph whose bootstrap has no heads kernel,
+// SampleArgs::advance): block 0 adds advance_by to advance[0] and advance[1] — every reader of
+// those bases in the replay has run.
+constexpr int kRowFcBN = 16, kRowFcBM = 32;
+template <int FEAT, int ROWS, int F>
+__device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, const float *__restrict__ Wfc,
+                                            float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by) {
+  constexpr int KC = FEAT / 16, FLAT = FEAT * ROWS;
+  static_assert(FEAT % 16 == 0 && F % kRowFcBN == 0, "whole chunks and column blocks");
+  __shared__ __attribute__((aligned(16))) float red[4][kRowFcBM][kRowFcBN];
   const int pb = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
   if (advance && pb == 0 && threadIdx.x == 0) {
     advance[0] += advance_by;
@@ -422,27 +427,27 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
   const int nbk = gridDim.x * gridDim.y * gridDim.z;
   const int L = (nbk % 8 == 0) ? (pb % 8) * (nbk / 8) + pb / 8 : pb;  // XCD-aware (see the top)
   const int xb = L % gridDim.x, yz = L / gridDim.x;
-  const int n0 = xb * Fz::FC_BN, i = yz % gridDim.y, e0 = (yz / gridDim.y) * Fz::FC_BM;
+  const int n0 = xb * kRowFcBN, i = yz % gridDim.y, e0 = (yz / gridDim.y) * kRowFcBM;
   MT_PROBE_AT(1, pb, 0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  constexpr int JN = (Fz::FC_KC + 3) / 4;  // 5
+  constexpr int JN = (KC + 3) / 4;
   f32x4 a[JN][2];
   float b[JN][4];
   const int row0 = min(e0 + r, B - 1), row1 = min(e0 + 16 + r, B - 1);
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
-    const int c = min(w + 4 * j, Fz::FC_KC - 1);  // (chunks past 17 are loaded but not used)
-    const int k0 = i * Fz::FEAT + 16 * c + 4 * g;
-    a[j][0] = *reinterpret_cast<const f32x4 *>(act2 + (size_t)row0 * Fz::FLAT + k0);
-    a[j][1] = *reinterpret_cast<const f32x4 *>(act2 + (size_t)row1 * Fz::FLAT + k0);
+    const int c = min(w + 4 * j, KC - 1);  // (chunks past the row's last are loaded but not used)
+    const int k0 = i * FEAT + 16 * c + 4 * g;
+    a[j][0] = *reinterpret_cast<const f32x4 *>(x + (size_t)row0 * FLAT + k0);
+    a[j][1] = *reinterpret_cast<const f32x4 *>(x + (size_t)row1 * FLAT + k0);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) b[j][s] = Wfc[(size_t)(k0 + s) * Fz::F + n0 + r];
+    for (int s = 0; s < 4; ++s) b[j][s] = Wfc[(size_t)(k0 + s) * F + n0 + r];
   }
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
-    if (w + 4 * j < Fz::FC_KC) {
+    if (w + 4 * j < KC) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -455,12 +460,37 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
     for (int q = 0; q < 4; ++q) red[w][t * 16 + g * 4 + q][r] = acc[t][q];
   __syncthreads();
   MT_PROBE_AT(1, pb, 1);
-  for (int idx = threadIdx.x; idx < Fz::FC_BM * Fz::FC_BN; idx += 256) {
-    const int m = idx / Fz::FC_BN, n = idx - m * Fz::FC_BN;
+  for (int idx = threadIdx.x; idx < kRowFcBM * kRowFcBN; idx += 256) {
+    const int m = idx / kRowFcBN, n = idx - m * kRowFcBN;
     const float s = ((red[0][m][n] + red[1][m][n]) + red[2][m][n]) + red[3][m][n];
-    if (e0 + m < B) slabs[((size_t)i * B + e0 + m) * Fz::F + n0 + n] = s;
+    if (e0 + m < B) slabs[((size_t)i * B + e0 + m) * F + n0 + n] = s;
   }
   MT_PROBE_AT(1, pb, 2);
+}
+
+// the NIPS trunk's dense kernel (FEAT = 288 features of each of its 9 conv2 rows)
+template <int C>
+__global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ act2, int B,
+                                                      const float *__restrict__ Wfc, float *__restrict__ slabs,
+                                                      uint32_t *advance, uint32_t advance_by) {
+  using Fz = FusedNips<C>;
+  static_assert(Fz::FC_BN == kRowFcBN && Fz::FC_BM == kRowFcBM, "tile");
+  row_fc_body<Fz::FEAT, Fz::ROWS2, Fz::F>(act2, B, Wfc, slabs, advance, advance_by);
+}
+
+// the same for the layered trunks (NATURE: 7 rows of 448 features, PWYX: 10 rows of 640)
+template <int FEAT, int ROWS, int F>
+__global__ __launch_bounds__(256) void row_fc_kernel(const float *__restrict__ x, int B, const float *__restrict__ Wfc,
+                                                     float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by) {
+  row_fc_body<FEAT, ROWS, F>(x, B, Wfc, slabs, advance, advance_by);
+}
+template <int FEAT, int ROWS, int F>
+static inline int launch_row_fc(const float *x, int B, const float *Wfc, float *slabs, hipStream_t s,
+                                uint32_t *advance = nullptr, uint32_t advance_by = 0) {
+  hipLaunchKernelGGL((row_fc_kernel<FEAT, ROWS, F>), dim3(F / kRowFcBN, ROWS, (B + kRowFcBM - 1) / kRowFcBM),
+                     dim3(256), 0, s, x, B, Wfc, slabs, advance, advance_by);
+  MT_LAUNCHED();
+  return MT_OK;
 }
 
 // Throughput form of the NIPS conv trunk for large batches (gray frames, E >= kPersistMinEnvs):

@@ -81,9 +81,39 @@ def main():
     lib.mt_probe_read_rollout.argtypes = [C.c_void_p, C.c_size_t]
     _lib.check(lib.mt_probe_read_rollout(C.c_void_p(ro.ctypes.data), ro.size), 'mt_probe_read_rollout')
     R = ro.reshape(512, 4)[:E].astype(np.int64)
-    nblocks = {0: int((P[0, :, 0] != 0).sum()), 1: 16 * 9 * ((E + 31) // 32), 2: E}  # (conv: 9 or 18 per env)
-    t0 = P[0, :nblocks[0], 0].min()
     us = lambda x: x * 0.01  # 100 MHz ticks
+    if cfg['arch'] == 'NATURE':  # the dataflow chain (nature_chain_kernel) + row fc + heads
+        ch = np.zeros(512 * 4, dtype=np.uint64)
+        lib.mt_probe_read_chain.restype = C.c_int
+        lib.mt_probe_read_chain.argtypes = [C.c_void_p, C.c_size_t]
+        _lib.check(lib.mt_probe_read_chain(C.c_void_p(ch.ctypes.data), ch.size), 'mt_probe_read_chain')
+        X = ch.reshape(512, 4)[:E].astype(np.int64)
+        t_last = X[:, 0].max()
+        rel = lambda v: us(v - t_last)
+        print('chain  per env (us): conv1 done - seen med %.2f max %.2f; conv2 done - conv1 med %.2f max %.2f; '
+              'conv3 done - conv2 med %.2f max %.2f' % (
+                  us(np.median(X[:, 1] - X[:, 0])), us((X[:, 1] - X[:, 0]).max()), us(np.median(X[:, 2] - X[:, 1])),
+                  us((X[:, 2] - X[:, 1]).max()), us(np.median(X[:, 3] - X[:, 2])), us((X[:, 3] - X[:, 2]).max())))
+        print('chain  publications seen over %.2f us (first..last); relative to the last: conv1 done max %+.2f, '
+              'conv2 done max %+.2f, conv3 done max %+.2f us' % (us(t_last - X[:, 0].min()), rel(X[:, 1].max()),
+                                                                  rel(X[:, 2].max()), rel(X[:, 3].max())))
+        e_last = int(np.argmax(X[:, 0]))
+        print('chain  last env %d: seen 0, conv1 %+.2f, conv2 %+.2f, conv3 %+.2f us' % (
+            e_last, rel(X[e_last, 1]), rel(X[e_last, 2]), rel(X[e_last, 3])))
+        nfc = 32 * 7 * ((E + 31) // 32)
+        f = P[1, :nfc, :3]
+        print('fc     blocks %d start %+.2f..%+.2f end %+.2f..%+.2f us (rel. last publish), block med %.2f' % (
+            nfc, rel(f[:, 0].min()), rel(f[:, 0].max()), rel(f[:, 2].min()), rel(f[:, 2].max()),
+            us(np.median(f[:, 2] - f[:, 0]))))
+        h = P[2, :E, :4]
+        print('heads  blocks %d start %+.2f..%+.2f end %+.2f..%+.2f us; phases med: slab sum %.2f, gemv %.2f, '
+              'softmax+draw %.2f' % (E, rel(h[:, 0].min()), rel(h[:, 0].max()), rel(h[:, 3].min()), rel(h[:, 3].max()),
+                                     us(np.median(h[:, 1] - h[:, 0])), us(np.median(h[:, 2] - h[:, 1])),
+                                     us(np.median(h[:, 3] - h[:, 2]))))
+        L.cleanup()
+        return
+    nblocks = {0: int((P[0, :, 0] != 0).sum()), 1: 16 * 9 * ((E + 31) // 32), 2: E}  # (conv: 9 per env)
+    t0 = P[0, :nblocks[0], 0].min()
     if R[:, 0].any():  # a pull kernel ran (non-stacking chains)
         seen, done = R[:, 0] - t0, R[:, 1] - t0
         pstart = R[::4, 2] - t0
