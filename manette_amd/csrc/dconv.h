@@ -33,12 +33,18 @@ namespace mt {
 
 // Probe builds (-DMT_PROBE): per env, when its publication was seen by a conv1 block (0) and when
 // its last conv1 / conv2 / conv3 block finished (1, 2, 3); s_memrealtime, read by mt_probe_read_chain
+// and per block (blockIdx < 2048) of nature_chain_kernel, slots: 0 start, 1 waited (consumers) /
+// publication seen (conv1), 2 frames staged (conv1), 3 body done, 4 signal stores drained
 #ifdef MT_PROBE
 static __device__ unsigned long long mt_probe_chain[512 * 4];
+static __device__ unsigned long long mt_probe_chainblk[2048 * 8];
 #define MT_PROBE_CHAIN(e, p) \
   if ((e) < 512) mt_probe_chain[(e) * 4 + (p)] = __builtin_amdgcn_s_memrealtime()
+#define MT_PROBE_BLK(p) \
+  if (threadIdx.x == 0 && blockIdx.x < 2048) mt_probe_chainblk[blockIdx.x * 8 + (p)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define MT_PROBE_CHAIN(e, p)
+#define MT_PROBE_BLK(p)
 #endif
 
 // ---- problems ------------------------------------------------------------------------------
@@ -154,6 +160,7 @@ struct DFwdStack : DFwd<G, true, false, false, COH_OUT> {
         const uint32_t tag = st.tag_base ? ((*st.tag_base + st.tag) & 0x1fffffffu) : st.tag;
         np = min(max(wait_published(st.ready, b, tag, st.status), 0), 4);  // (a timeout stacks no frame)
         MT_PROBE_CHAIN(b, 0);
+        MT_PROBE_BLK(1);
       } else if (st.count) {
         np = min(max(st.count[b], 1), 4);
       }
@@ -172,6 +179,7 @@ struct DFwdStack : DFwd<G, true, false, false, COH_OUT> {
           st.ready ? ld_published16(st.frames, off, lo, hi) : *reinterpret_cast<const uint4 *>(st.frames + off);
     }
     __syncthreads();
+    MT_PROBE_BLK(2);
     // stack (preprocess_kernel's op: prev shifted by p channels, the p frames in the top ones),
     // the owned rows to the new state, every row into the patch
     uint4 *out = reinterpret_cast<uint4 *>(st.out + ((size_t)b * H + r0) * W * 4);
@@ -651,15 +659,23 @@ static int conv_forward_direct(const void *X, const float *W, const float *bias,
 // the next launch.
 // Tiles: 4 waves for every role (conv2 / conv3: 4 N-tiles of one 16-row M-tile, 4 units a block,
 // so one env's conv2 spreads over 6 blocks and its conv3 over 4).
-template <class G1, class G2, class G3>
+// conv2 / conv3 tiles of the chain: 1 M-tile x 4 N-tiles on 4 waves (chain_conv_tile)
+template <class Pr>
+using ChainCfg = DConvCfg<Pr, 1, 4, 1, Pr::CI>;
+
+template <class G1_, class G2_, class G3_, bool C3COH = false>
 struct NatureChain {
+  using G1 = G1_;
+  using G2 = G2_;
+  using G3 = G3_;
   using P1 = DFwdStack<G1, true>;
   using P2 = DFwd<G2, false, false, true, true>;
-  using P3 = DFwd<G3, false, false, true, false>;
+  using P3 = DFwd<G3, false, false, true, C3COH>;  // (C3COH: read by the dense role of nature_step_kernel)
   using D1 = DConvCfg<P1, 4, 1, 1, 0>;
-  using D2 = DConvCfg<P2, 1, 4, 1, G2::CIN>;
-  using D3 = DConvCfg<P3, 1, 4, 1, G3::CIN>;
-  static constexpr size_t LDS = std::max(D1::LDS, std::max(D2::LDS, D3::LDS));
+  using D2 = ChainCfg<P2>;
+  using D3 = ChainCfg<P3>;
+  // (conv2 / conv3 keep their weights in registers: only their patch in LDS)
+  static constexpr size_t LDS = std::max(D1::LDS, (size_t)std::max(D2::ASZ, D3::ASZ) * 4);
   static_assert(D1::NT == 256 && D2::NT == 256 && D3::NT == 256, "one block size for every role");
   static constexpr int BPE = D1::BPI + D2::BPI + D3::BPI;  // blocks per env
   static constexpr int SYNC_WORDS = 4;                     // per env: conv1 / conv2 / conv3 done
@@ -668,6 +684,7 @@ struct NatureChain {
 __device__ __forceinline__ void chain_signal(uint32_t *c, uint32_t last, int e, int phase) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's (sc1) stores have completed
   __syncthreads();
+  MT_PROBE_BLK(4);
   if (threadIdx.x == 0) {
     const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == last) MT_PROBE_CHAIN(e, phase);
@@ -688,30 +705,107 @@ __device__ __forceinline__ void chain_wait(const uint32_t *c, uint32_t want, uin
   __syncthreads();
 }
 
+// A conv2 / conv3 tile of the chain kernel with its weights in registers: 4 waves, wave w owns
+// N-tile w (16 output channels) over the WHOLE K, its KC B fragments loaded by the caller before
+// the hand-off wait (so their latency hides under it), one M-tile (4 units) per block. The generic
+// body stages the weights in LDS tap by tap, one barrier and one global round trip per tap: 16
+// (conv2) / 9 (conv3) of them on the per-env critical path, 4-5 us of the 5-6 us a block took.
+template <class Pr>
+__device__ __forceinline__ void chain_load_b(const Pr &p, f32x4 (&bf)[ChainCfg<Pr>::KC]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int kc = 0; kc < ChainCfg<Pr>::KC; ++kc) bf[kc] = p.wquad(16 * kc + 4 * g, 16 * w + r);
+}
+template <class Pr>
+__device__ __forceinline__ void chain_conv_tile(const Pr &p, int t, float *As, const f32x4 (&bf)[ChainCfg<Pr>::KC]) {
+  using D = ChainCfg<Pr>;
+  static_assert(D::TN == 4 && D::UPB == 4, "one M-tile x 4 N-tiles per block");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int b = t / D::BPI;
+  const int u0 = (t - b * D::BPI) * D::UPB;
+  const int oy0 = (4 * u0) / D::OW;  // output row of patch row 0
+  const typename Pr::Pre pre = p.pre(b, min(u0 + g, D::U - 1), 16 * w + r);
+  // the patch (rows oy0 - PT .., zeros outside the image), as dconv_body stages it
+  const auto *img = p.X + (size_t)b * D::H * D::W * D::CI;
+  constexpr int ABATCH = 8;
+#pragma unroll
+  for (int it0 = 0; it0 < D::AIT; it0 += ABATCH) {
+    f32x4 v[ABATCH];
+    int dst[ABATCH];
+#pragma unroll
+    for (int q = 0; q < ABATCH; ++q) {
+      const int it = it0 + q;
+      if (it < D::AIT) {
+        const int item = min(tid + it * D::NT, D::AQ - 1);
+        const int pix = item / D::QT, cq = item - pix * D::QT;
+        const int pr = pix / D::WP, pc = pix - pr * D::WP;
+        const int iy = oy0 * D::S - Pr::PT + pr, ix = pc - Pr::PL;
+        const bool ok = (unsigned)iy < (unsigned)D::H && (unsigned)ix < (unsigned)D::W;
+        const f32x4 x = p.load4(img + (size_t)(ok ? iy * D::W + ix : 0) * D::CI + 4 * cq);
+        v[q] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
+        dst[q] = (D::AQ % D::NT == 0 || tid + it * D::NT < D::AQ) ? (pr * D::WPX + pc) * D::CS + 4 * cq : -1;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < ABATCH; ++q)
+      if (it0 + q < D::AIT && dst[q] >= 0) *reinterpret_cast<f32x4 *>(As + dst[q]) = v[q];
+  }
+  // lane A base: row r of the M-tile = unit r / 4, quad position r % 4
+  int abase;
+  {
+    const int u = min(u0 + (r >> 2), D::U - 1);
+    const int px = min(4 * u + (r & 3), D::NPIX - 1);
+    const int oy = px / D::OW, ox = px - oy * D::OW;
+    abase = ((oy - oy0) * D::S * D::WPX + ox * D::S) * D::CS;
+  }
+  __syncthreads();
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kc = 0; kc < D::KC; ++kc) {
+    const int q4 = 4 * kc + g, tap = q4 / D::QT, cq = q4 - tap * D::QT;  // channel quad cq of tap `tap`
+    const int tp = min(tap, D::TAPS - 1);
+    const f32x4 a = *reinterpret_cast<const f32x4 *>(As + abase + ((tp / D::KW) * D::WPX + tp % D::KW) * D::CS + 4 * cq);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s4], bf[kc][s4], acc, 0, 0, 0);
+  }
+  if (u0 + g < D::U) p.store(pre, b, u0 + g, 16 * w + r, acc);
+}
+
+// The conv roles of block bid < E * NC::BPE. chunk_done (nature_step_kernel): env e's last conv3
+// block also counts env e done in its chunk's word (chunk_done + 4 (e / 32)).
 template <class NC>
-__global__ __launch_bounds__(256) void nature_chain_kernel(typename NC::P1 p1, typename NC::P2 p2,
-                                                           typename NC::P3 p3, uint32_t *sync, int E,
-                                                           uint32_t *status) {
+__device__ __forceinline__ void nature_conv_roles(const typename NC::P1 &p1, const typename NC::P2 &p2,
+                                                  const typename NC::P3 &p3, uint32_t *sync, int E, uint32_t *status,
+                                                  int bid, float *smem, uint32_t *chunk_done = nullptr) {
   using D1 = typename NC::D1;
   using D2 = typename NC::D2;
   using D3 = typename NC::D3;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int n1 = E * D1::BPI, n2 = E * D2::BPI;
-  const int bid = blockIdx.x;
+  MT_PROBE_BLK(0);
   if (bid < n1) {
     const int t = xcd_tile(bid, n1);  // (an env's conv1 tiles on one XCD: their patch rows overlap)
     dconv_body<typename NC::P1, 4, 1, 1, 0>(p1, t, t + 1, smem);
+    MT_PROBE_BLK(3);
     chain_signal(sync + NC::SYNC_WORDS * (t / D1::BPI), D1::BPI - 1, t / D1::BPI, 1);
   } else if (bid < n1 + n2) {
     const int t = bid - n1, e = t / D2::BPI;
+    f32x4 bf[D2::KC];
+    chain_load_b(p2, bf);
     chain_wait(sync + NC::SYNC_WORDS * e, D1::BPI, status);
-    dconv_body<typename NC::P2, 1, 4, 1, D2::CK>(p2, t, t + 1, smem);
+    MT_PROBE_BLK(1);
+    chain_conv_tile(p2, t, smem, bf);
+    MT_PROBE_BLK(3);
     chain_signal(sync + NC::SYNC_WORDS * e + 1, D2::BPI - 1, e, 2);
   } else {
     const int t = bid - n1 - n2, e = t / D3::BPI;
     uint32_t *c = sync + NC::SYNC_WORDS * e;
+    f32x4 bf[D3::KC];
+    chain_load_b(p3, bf);
     chain_wait(c + 1, D2::BPI, status);
-    dconv_body<typename NC::P3, 1, 4, 1, D3::CK>(p3, t, t + 1, smem);
+    MT_PROBE_BLK(1);
+    chain_conv_tile(p3, t, smem, bf);
+    MT_PROBE_BLK(3);
+    if (chunk_done) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (its sc1 stores, read by the dense role)
     __syncthreads();
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(c + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)D3::BPI - 1) {
@@ -720,8 +814,36 @@ __global__ __launch_bounds__(256) void nature_chain_kernel(typename NC::P1 p1, t
       __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (chunk_done) {  // (its conv3 stores retired: vmcnt(0) before the barrier above)
+        __hip_atomic_fetch_add(chunk_done + NC::SYNC_WORDS * (e / 32), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
+}
+
+template <class NC>
+__global__ __launch_bounds__(256) void nature_chain_kernel(typename NC::P1 p1, typename NC::P2 p2,
+                                                           typename NC::P3 p3, uint32_t *sync, int E,
+                                                           uint32_t *status) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  nature_conv_roles<NC>(p1, p2, p3, sync, E, status, blockIdx.x, smem);
+}
+
+template <class NC, class G1 = typename NC::G1, class G2 = typename NC::G2, class G3 = typename NC::G3>
+static void nature_chain_params(const StackSrc &st, const float *W1, const float *W2, const float *W3, float *a1,
+                                float *a2, float *a3, int act, float alpha, typename NC::P1 &p1, typename NC::P2 &p2,
+                                typename NC::P3 &p3) {
+  p1 = typename NC::P1{};
+  p1.X = st.out;
+  p1.Wt = W1;
+  p1.bias = W1 + G1::KK * G1::COUT;
+  p1.Y = a1;
+  p1.act = act;
+  p1.alpha = alpha;
+  p1.st = st;
+  p2 = typename NC::P2{a1, W2, W2 + G2::KK * G2::COUT, a2, nullptr, act, alpha};
+  p3 = typename NC::P3{a2, W3, W3 + G3::KK * G3::COUT, a3, nullptr, act, alpha};
 }
 
 // The NATURE chain's trunk convs (stacking conv1 -> conv2 -> conv3) as one nature_chain_kernel
@@ -732,16 +854,10 @@ static int launch_nature_chain(const StackSrc &st, const float *W1, const float 
   using NC = NatureChain<G1, G2, G3>;
   static_assert(NC::LDS <= 160 * 1024, "LDS budget");
   if (B <= 0 || !launch_allowed()) return MT_OK;
-  typename NC::P1 p1{};
-  p1.X = st.out;
-  p1.Wt = W1;
-  p1.bias = W1 + G1::KK * G1::COUT;
-  p1.Y = a1;
-  p1.act = act;
-  p1.alpha = alpha;
-  p1.st = st;
-  typename NC::P2 p2{a1, W2, W2 + G2::KK * G2::COUT, a2, nullptr, act, alpha};
-  typename NC::P3 p3{a2, W3, W3 + G3::KK * G3::COUT, a3, nullptr, act, alpha};
+  typename NC::P1 p1;
+  typename NC::P2 p2;
+  typename NC::P3 p3;
+  nature_chain_params<NC>(st, W1, W2, W3, a1, a2, a3, act, alpha, p1, p2, p3);
   auto kern = &nature_chain_kernel<NC>;
   static bool attr_set = false;
   if (!attr_set && NC::LDS > 64 * 1024) {

@@ -413,21 +413,35 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
 // SampleArgs::advance): block 0 adds advance_by to advance[0] and advance[1] — every reader of
 // those bases in the replay has run.
 constexpr int kRowFcBN = 16, kRowFcBM = 32;
-template <int FEAT, int ROWS, int F>
+struct NoWait {
+  __device__ __forceinline__ void operator()() const {}
+};
+// 16 bytes of a buffer another workgroup of the same launch wrote with agent-scope stores
+__device__ __forceinline__ f32x4 ld_coherent4(const float *p) {
+  const uint64_t *w = reinterpret_cast<const uint64_t *>(p);
+  const uint64_t x = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t y = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return f32x4{__uint_as_float((uint32_t)x), __uint_as_float((uint32_t)(x >> 32)), __uint_as_float((uint32_t)y),
+               __uint_as_float((uint32_t)(y >> 32))};
+}
+// Block pb of a (gx, gy, gz) = (F / 16, ROWS, env chunks) grid. COH + wait (the in-launch dense
+// role of nature_step_kernel): the weights are requested first, then wait() (the hand-off from
+// the conv3 role), then x is read and the slabs written with agent-scope (sc1) accesses.
+template <int FEAT, int ROWS, int F, bool COH = false, class Wait = NoWait>
 __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, const float *__restrict__ Wfc,
-                                            float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by) {
+                                            float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by, int pb,
+                                            int gx, int gy, int gz, const Wait &wait = Wait{}) {
   constexpr int KC = FEAT / 16, FLAT = FEAT * ROWS;
   static_assert(FEAT % 16 == 0 && F % kRowFcBN == 0, "whole chunks and column blocks");
   __shared__ __attribute__((aligned(16))) float red[4][kRowFcBM][kRowFcBN];
-  const int pb = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
   if (advance && pb == 0 && threadIdx.x == 0) {
     advance[0] += advance_by;
     advance[1] += advance_by;
   }
-  const int nbk = gridDim.x * gridDim.y * gridDim.z;
+  const int nbk = gx * gy * gz;
   const int L = (nbk % 8 == 0) ? (pb % 8) * (nbk / 8) + pb / 8 : pb;  // XCD-aware (see the top)
-  const int xb = L % gridDim.x, yz = L / gridDim.x;
-  const int n0 = xb * kRowFcBN, i = yz % gridDim.y, e0 = (yz / gridDim.y) * kRowFcBM;
+  const int xb = L % gx, yz = L / gx;
+  const int n0 = xb * kRowFcBN, i = yz % gy, e0 = (yz / gy) * kRowFcBM;
   MT_PROBE_AT(1, pb, 0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -439,10 +453,21 @@ __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, 
   for (int j = 0; j < JN; ++j) {
     const int c = min(w + 4 * j, KC - 1);  // (chunks past the row's last are loaded but not used)
     const int k0 = i * FEAT + 16 * c + 4 * g;
-    a[j][0] = *reinterpret_cast<const f32x4 *>(x + (size_t)row0 * FLAT + k0);
-    a[j][1] = *reinterpret_cast<const f32x4 *>(x + (size_t)row1 * FLAT + k0);
 #pragma unroll
     for (int s = 0; s < 4; ++s) b[j][s] = Wfc[(size_t)(k0 + s) * F + n0 + r];
+  }
+  wait();
+#pragma unroll
+  for (int j = 0; j < JN; ++j) {
+    const int c = min(w + 4 * j, KC - 1);
+    const int k0 = i * FEAT + 16 * c + 4 * g;
+    if constexpr (COH) {
+      a[j][0] = ld_coherent4(x + (size_t)row0 * FLAT + k0);
+      a[j][1] = ld_coherent4(x + (size_t)row1 * FLAT + k0);
+    } else {
+      a[j][0] = *reinterpret_cast<const f32x4 *>(x + (size_t)row0 * FLAT + k0);
+      a[j][1] = *reinterpret_cast<const f32x4 *>(x + (size_t)row1 * FLAT + k0);
+    }
   }
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -463,7 +488,13 @@ __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, 
   for (int idx = threadIdx.x; idx < kRowFcBM * kRowFcBN; idx += 256) {
     const int m = idx / kRowFcBN, n = idx - m * kRowFcBN;
     const float s = ((red[0][m][n] + red[1][m][n]) + red[2][m][n]) + red[3][m][n];
-    if (e0 + m < B) slabs[((size_t)i * B + e0 + m) * F + n0 + n] = s;
+    if (e0 + m < B) {
+      float *o = slabs + ((size_t)i * B + e0 + m) * F + n0 + n;
+      if constexpr (COH)
+        __hip_atomic_store(o, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *o = s;
+    }
   }
   MT_PROBE_AT(1, pb, 2);
 }
@@ -475,14 +506,18 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
                                                       uint32_t *advance, uint32_t advance_by) {
   using Fz = FusedNips<C>;
   static_assert(Fz::FC_BN == kRowFcBN && Fz::FC_BM == kRowFcBM, "tile");
-  row_fc_body<Fz::FEAT, Fz::ROWS2, Fz::F>(act2, B, Wfc, slabs, advance, advance_by);
+  row_fc_body<Fz::FEAT, Fz::ROWS2, Fz::F>(act2, B, Wfc, slabs, advance, advance_by,
+                                         (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gridDim.x,
+                                         gridDim.y, gridDim.z);
 }
 
 // the same for the layered trunks (NATURE: 7 rows of 448 features, PWYX: 10 rows of 640)
 template <int FEAT, int ROWS, int F>
 __global__ __launch_bounds__(256) void row_fc_kernel(const float *__restrict__ x, int B, const float *__restrict__ Wfc,
                                                      float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by) {
-  row_fc_body<FEAT, ROWS, F>(x, B, Wfc, slabs, advance, advance_by);
+  row_fc_body<FEAT, ROWS, F>(x, B, Wfc, slabs, advance, advance_by,
+                             (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gridDim.x, gridDim.y,
+                             gridDim.z);
 }
 template <int FEAT, int ROWS, int F>
 static inline int launch_row_fc(const float *x, int B, const float *Wfc, float *slabs, hipStream_t s,

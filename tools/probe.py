@@ -97,7 +97,31 @@ def main():
         print('chain  publications seen over %.2f us (first..last); relative to the last: conv1 done max %+.2f, '
               'conv2 done max %+.2f, conv3 done max %+.2f us' % (us(t_last - X[:, 0].min()), rel(X[:, 1].max()),
                                                                   rel(X[:, 2].max()), rel(X[:, 3].max())))
+        cb = np.zeros(2048 * 8, dtype=np.uint64)
+        lib.mt_probe_read_chain_blocks.restype = C.c_int
+        lib.mt_probe_read_chain_blocks.argtypes = [C.c_void_p, C.c_size_t]
+        _lib.check(lib.mt_probe_read_chain_blocks(C.c_void_p(cb.ctypes.data), cb.size), 'mt_probe_read_chain_blocks')
+        Bk = cb.reshape(2048, 8).astype(np.int64)
+        n1, n2, n3 = 7 * E, 6 * E, 4 * E
+        for name, lo, hi in (('conv1', 0, n1), ('conv2', n1, n1 + n2), ('conv3', n1 + n2, n1 + n2 + n3)):
+            b = Bk[lo:hi]
+            if name == 'conv1':
+                print('%s  block phases med (us): seen->frames staged %.2f, frames->body done %.2f, stores drained '
+                      '%.2f' % (name, us(np.median(b[:, 2] - b[:, 1])), us(np.median(b[:, 3] - b[:, 2])),
+                                us(np.median(b[:, 4] - b[:, 3]))))
+            else:
+                w = b[:, 1] - b[:, 0]
+                print('%s  block phases med (us): start->waited %.2f (max %.2f), waited->body done %.2f, stores '
+                      'drained %.2f; starts %+.2f..%+.2f rel. last publish' % (
+                          name, us(np.median(w)), us(w.max()), us(np.median(b[:, 3] - b[:, 1])),
+                          us(np.median(b[:, 4] - b[:, 3])) if name == 'conv2' else 0.0, rel(b[:, 0].min()),
+                          rel(b[:, 0].max())))
         e_last = int(np.argmax(X[:, 0]))
+        for name, lo, bpi in (('conv2', n1, 6), ('conv3', n1 + n2, 4)):
+            b = Bk[lo + bpi * e_last: lo + bpi * (e_last + 1)]
+            print('%s  last env blocks: start %s waited %s done %s (rel. last publish)' % (
+                name, ' '.join('%+.1f' % rel(x) for x in b[:, 0]), ' '.join('%+.1f' % rel(x) for x in b[:, 1]),
+                ' '.join('%+.1f' % rel(x) for x in b[:, 3])))
         print('chain  last env %d: seen 0, conv1 %+.2f, conv2 %+.2f, conv3 %+.2f us' % (
             e_last, rel(X[e_last, 1]), rel(X[e_last, 2]), rel(X[e_last, 3])))
         nfc = 32 * 7 * ((E + 31) // 32)
