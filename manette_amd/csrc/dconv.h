@@ -663,19 +663,20 @@ static int conv_forward_direct(const void *X, const float *W, const float *bias,
 template <class Pr>
 using ChainCfg = DConvCfg<Pr, 1, 4, 1, Pr::CI>;
 
-template <class G1_, class G2_, class G3_, bool C3COH = false>
+template <class G1_, class G2_, class G3_>
 struct NatureChain {
   using G1 = G1_;
   using G2 = G2_;
   using G3 = G3_;
   using P1 = DFwdStack<G1, true>;
   using P2 = DFwd<G2, false, false, true, true>;
-  using P3 = DFwd<G3, false, false, true, C3COH>;  // (C3COH: read by the dense role of nature_step_kernel)
+  using P3 = DFwd<G3, false, false, true, false>;
   using D1 = DConvCfg<P1, 4, 1, 1, 0>;
   using D2 = ChainCfg<P2>;
   using D3 = ChainCfg<P3>;
-  // (conv2 / conv3 keep their weights in registers: only their patch in LDS)
-  static constexpr size_t LDS = std::max(D1::LDS, (size_t)std::max(D2::ASZ, D3::ASZ) * 4);
+  // (every role keeps its weights in registers: only the patches in LDS, + conv1's stacked frames)
+  static constexpr size_t LDS =
+      std::max((size_t)D1::ASZ * 4 + 4 * D1::RIN * G1::W, (size_t)std::max(D2::ASZ, D3::ASZ) * 4);
   static_assert(D1::NT == 256 && D2::NT == 256 && D3::NT == 256, "one block size for every role");
   static constexpr int BPE = D1::BPI + D2::BPI + D3::BPI;  // blocks per env
   static constexpr int SYNC_WORDS = 4;                     // per env: conv1 / conv2 / conv3 done
@@ -771,12 +772,11 @@ __device__ __forceinline__ void chain_conv_tile(const Pr &p, int t, float *As, c
   if (u0 + g < D::U) p.store(pre, b, u0 + g, 16 * w + r, acc);
 }
 
-// The conv roles of block bid < E * NC::BPE. chunk_done (nature_step_kernel): env e's last conv3
-// block also counts env e done in its chunk's word (chunk_done + 4 (e / 32)).
+// The conv roles of block bid < E * NC::BPE.
 template <class NC>
 __device__ __forceinline__ void nature_conv_roles(const typename NC::P1 &p1, const typename NC::P2 &p2,
                                                   const typename NC::P3 &p3, uint32_t *sync, int E, uint32_t *status,
-                                                  int bid, float *smem, uint32_t *chunk_done = nullptr) {
+                                                  int bid, float *smem) {
   using D1 = typename NC::D1;
   using D2 = typename NC::D2;
   using D3 = typename NC::D3;
@@ -784,7 +784,15 @@ __device__ __forceinline__ void nature_conv_roles(const typename NC::P1 &p1, con
   MT_PROBE_BLK(0);
   if (bid < n1) {
     const int t = xcd_tile(bid, n1);  // (an env's conv1 tiles on one XCD: their patch rows overlap)
-    dconv_body<typename NC::P1, 4, 1, 1, 0>(p1, t, t + 1, smem);
+    f32x4 bf[2][D1::KC];
+    {
+      const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kc = 0; kc < D1::KC; ++kc) bf[j][kc] = p1.wquad(16 * kc + 4 * g, 16 * j + r);
+    }
+    chain_conv1_tile<NC>(p1, t, smem, bf);
     MT_PROBE_BLK(3);
     chain_signal(sync + NC::SYNC_WORDS * (t / D1::BPI), D1::BPI - 1, t / D1::BPI, 1);
   } else if (bid < n1 + n2) {
@@ -805,7 +813,6 @@ __device__ __forceinline__ void nature_conv_roles(const typename NC::P1 &p1, con
     MT_PROBE_BLK(1);
     chain_conv_tile(p3, t, smem, bf);
     MT_PROBE_BLK(3);
-    if (chunk_done) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (its sc1 stores, read by the dense role)
     __syncthreads();
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(c + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)D3::BPI - 1) {
@@ -814,11 +821,49 @@ __device__ __forceinline__ void nature_conv_roles(const typename NC::P1 &p1, con
       __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (chunk_done) {  // (its conv3 stores retired: vmcnt(0) before the barrier above)
-        __hip_atomic_fetch_add(chunk_done + NC::SYNC_WORDS * (e / 32), 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      }
     }
+  }
+}
+
+// The chain's conv1 tile (DFwdStack's staging) with its weights in registers too: 4 waves, wave w
+// owns M-tile w (4 units) and both 16-channel N-tiles over the whole K (KC x 2 B fragments, loaded
+// before the publication wait): no weight staging in LDS, no barrier behind the patch. fr: the
+// stacked frames' scratch, after the patch.
+template <class NC>
+__device__ __forceinline__ void chain_conv1_tile(const typename NC::P1 &p, int t, float *As,
+                                                 const f32x4 (&bf)[2][NC::D1::KC]) {
+  using D = typename NC::D1;
+  using Pr = typename NC::P1;
+  static_assert(D::WM == 4 && D::WN == 1 && D::TN == 2 && D::UPB == 16 && !D::TAPALIGNED, "conv1 tiling");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int b = t / D::BPI, bi = t - b * D::BPI;
+  const int u0 = bi * D::UPB;
+  const int oy0 = (4 * u0) / D::OW;
+  typename Pr::Pre pre[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) pre[j] = p.pre(b, min(u0 + 4 * w + g, D::U - 1), 16 * j + r);
+  const int own_end = bi + 1 < D::BPI ? min(D::H, ((4 * (u0 + D::UPB)) / D::OW) * D::S) : D::H;
+  p.template stage_patch<D>(b, oy0 * D::S, own_end, As, reinterpret_cast<uint8_t *>(As + D::ASZ));
+  int abase;
+  {
+    const int u = min(u0 + 4 * w + (r >> 2), D::U - 1);
+    const int px = min(4 * u + (r & 3), D::NPIX - 1);
+    const int oy = px / D::OW, ox = px - oy * D::OW;
+    abase = ((oy - oy0) * D::S * D::WPX + ox * D::S) * D::CS;
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int kc = 0; kc < D::KC; ++kc) {
+    const int q4 = 4 * kc + g, tap = min(q4 / D::QT, D::TAPS - 1), cq = q4 - (q4 / D::QT) * D::QT;
+    const f32x4 a = *reinterpret_cast<const f32x4 *>(As + abase + ((tap / D::KW) * D::WPX + tap % D::KW) * D::CS + 4 * cq);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s4], bf[j][kc][s4], acc[j], 0, 0, 0);
+  }
+  if (u0 + 4 * w + g < D::U) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) p.store(pre[j], b, u0 + 4 * w + g, 16 * j + r, acc[j]);
   }
 }
 

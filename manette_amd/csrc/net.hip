@@ -349,8 +349,7 @@ static WsLayout ws_layout(const mt_net *n, int B) {
   L.dH = take((size_t)B * Ar::F);
   L.wslab = take(wslab);
   L.wslab2 = take(wslab);  // ping-pong slab regions of consecutive conv layers (trunk_backward)
-  // (per env 4 words, then per chunk of 32 envs 4 words: nature_chain_kernel / nature_step_kernel)
-  L.sync = take(nature_stacking<Ar>() ? (size_t)4 * B + 4 * (size_t)cdiv(B, 32) : 0);
+  L.sync = take(nature_stacking<Ar>() ? (size_t)4 * B : 0);  // (nature_chain_kernel: 4 words per env)
   L.total = off;
   return L;
 }
@@ -439,15 +438,11 @@ __device__ __forceinline__ void head_col(const HeadParams &hp, int o, const floa
 
 __device__ uint64_t g_zero_u64 = 0;  // read in place of an absent draw counter / sequence base
 
-// COH + wait (the in-launch heads role of nature_step_kernel): everything but the slabs is requested
-// first, then wait() (the hand-off from the dense role), then the slabs are read with agent-scope
-// loads (written by other workgroups of the same launch).
-template <int FT, int SB, bool COH = false, class Wait = NoWait>
+template <int FT, int SB>
 __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs, int S, int B,
                                           const float *__restrict__ fc_b, int act, float alpha, const HeadParams &hp,
                                           float temp, float *__restrict__ H, float *__restrict__ v,
-                                          float *__restrict__ pi, float *__restrict__ rep, const SampleArgs &smp,
-                                          const Wait &wait = Wait{}) {
+                                          float *__restrict__ pi, float *__restrict__ rep, const SampleArgs &smp) {
   __shared__ float hs[256 * FT];
   __shared__ float zs[64];
   const int F = hp.F, O = 1 + hp.A + hp.R;
@@ -459,22 +454,15 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   // (1) the draw counter and the sequence base (the uniforms need them first)
   const uint64_t cnt = *(smp.counters ? smp.counters + b : &g_zero_u64);
   const uint32_t seq_base = *(smp.seq_base ? smp.seq_base : reinterpret_cast<const uint32_t *>(&g_zero_u64));
-  // (2) the slab partials of the thread's features (S = 9 for the NIPS trunk: one batch) — after
-  // (3) and the wait in the in-launch form
+  // (2) the slab partials of the thread's features (S = 9 for the NIPS trunk: one batch)
   const size_t zs_stride = (size_t)B * F;
   float t[FT][SB];
-  auto load_slabs = [&]() {
 #pragma unroll
-    for (int fi = 0; fi < FT; ++fi) {
-      const float *p = slabs + (size_t)b * F + min((int)threadIdx.x + 256 * fi, F - 1);
+  for (int fi = 0; fi < FT; ++fi) {
+    const float *p = slabs + (size_t)b * F + min((int)threadIdx.x + 256 * fi, F - 1);
 #pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        const float *q = p + (size_t)min(u, S - 1) * zs_stride;
-        t[fi][u] = COH ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
-      }
-    }
-  };
-  if constexpr (!COH) load_slabs();
+    for (int u = 0; u < SB; ++u) t[fi][u] = p[(size_t)min(u, S - 1) * zs_stride];
+  }
   // (3) dense bias, head weights and biases of this wave's first PRE outputs (o = w, w + 4, ...)
   float fb[FT];
 #pragma unroll
@@ -488,10 +476,6 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
 #pragma unroll
     for (int j = 0; j < FMAX; ++j) wpre[k][j] = wp[(size_t)min(lane + 64 * j, F - 1) * st];
     zb[k] = *bp;
-  }
-  if constexpr (COH) {
-    wait();
-    load_slabs();
   }
   if (smp.advance && b == 0 && threadIdx.x == 0) {  // the replayed rollout's last reader has run
     smp.advance[0] += smp.advance_by;
@@ -507,10 +491,7 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
 #pragma unroll
     for (int u = 0; u < SB; ++u)
       if (u < S) acc += t[fi][u];
-    for (int z = SB; z < S; ++z) {  // (S > SB)
-      const float *q = slabs + (size_t)b * F + min(f, F - 1) + (size_t)z * zs_stride;
-      acc += COH ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
-    }
+    for (int z = SB; z < S; ++z) acc += slabs[(size_t)b * F + min(f, F - 1) + (size_t)z * zs_stride];  // (S > SB)
     const float h = act_fwd(acc + fb[fi], act, alpha);
     if (f < F) {
       hs[f] = h;
@@ -606,87 +587,6 @@ static int launch_heads(int rows, hipStream_t s, const float *slabs, int S, int 
     else MT_HEADS(2, 16);
   }
 #undef MT_HEADS
-  MT_LAUNCHED();
-  return MT_OK;
-}
-
-// The whole gray-NATURE rollout step as ONE launch (round 4): nature_chain_kernel's conv roles
-// (conv3 stores with agent scope), then the row-split dense layer's blocks, then one heads block per
-// env. The dense blocks of env chunk z (32 envs) wait until every env of the chunk has finished
-// conv3, the heads block of env e until its chunk's dense blocks are done — so the dense layer and
-// the heads run right behind the last env's conv3 instead of behind two kernel boundaries, and each
-// role requests its weights (dense columns; head weights, biases, draw counter) before its wait.
-// Chunk words (after the per-env words): [conv3-done envs, dense blocks done, heads done]; the last
-// heads block of a chunk resets them. A block still waits only for lower-indexed blocks.
-template <class NC, int FT, int SB>
-__global__ __launch_bounds__(256) void nature_step_kernel(typename NC::P1 p1, typename NC::P2 p2, typename NC::P3 p3,
-                                                          uint32_t *sync, int E, uint32_t *status,
-                                                          const float *__restrict__ Wfc, float *__restrict__ slabs,
-                                                          int act, float alpha, HeadParams hp, float temp,
-                                                          float *__restrict__ H, float *__restrict__ v,
-                                                          float *__restrict__ pi, float *__restrict__ rep,
-                                                          SampleArgs smp) {
-  using G3 = typename NC::G3;
-  constexpr int ROWS = G3::OH, FEAT = G3::OW * G3::COUT;  // dense slabs by conv3 rows
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  uint32_t *chunk = sync + NC::SYNC_WORDS * E;
-  const int nconv = E * NC::BPE;
-  const int gx = hp.F / kRowFcBN, nz = (E + kRowFcBM - 1) / kRowFcBM, nfc = gx * ROWS * nz;
-  const int bid = blockIdx.x;
-  if (bid < nconv) {
-    nature_conv_roles<NC>(p1, p2, p3, sync, E, status, bid, smem, chunk);
-  } else if (bid < nconv + nfc) {
-    const int pb = bid - nconv;
-    const int L = (nfc % 8 == 0) ? (pb % 8) * (nfc / 8) + pb / 8 : pb;  // (row_fc_body's block mapping)
-    const int z = (L / gx) / ROWS;
-    uint32_t *cz = chunk + NC::SYNC_WORDS * z;
-    const auto wait = [&]() { chain_wait(cz, (uint32_t)min(kRowFcBM, E - kRowFcBM * z), status); };
-    row_fc_body<FEAT, ROWS, 512, true>(p3.Y, E, Wfc, slabs, nullptr, 0, pb, gx, ROWS, nz, wait);
-    chain_signal(cz + 1, 0xffffffffu, 0, 0);
-  } else {
-    const int e = bid - nconv - nfc, z = e / kRowFcBM;
-    uint32_t *cz = chunk + NC::SYNC_WORDS * z;
-    const auto wait = [&]() { chain_wait(cz + 1, (uint32_t)(gx * ROWS), status); };
-    heads_row<FT, SB, true>(e, slabs, ROWS, E, Wfc + (size_t)ROWS * FEAT * 512, act, alpha, hp, temp, H, v, pi, rep,
-                            smp, wait);
-    __syncthreads();
-    if (threadIdx.x == 0 && __hip_atomic_fetch_add(cz + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                                (uint32_t)min(kRowFcBM, E - kRowFcBM * z) - 1) {
-      // the chunk's last heads block: its dense blocks and heads blocks are past their waits
-      __hip_atomic_store(cz, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(cz + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(cz + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <class Ar>
-static int launch_nature_step(const mt_net *n, const float *P, const StackSrc &st, int B, float *act1, float *act2,
-                              float *act3, float *slabs, uint32_t *sync, float *H, float *v, float *pi, float *rep,
-                              const SampleArgs &smp, hipStream_t s) {
-  using NC = NatureChain<LayerG<Ar, 0>, LayerG<Ar, 1>, LayerG<Ar, 2>, true>;
-  static_assert(Ar::F == 512 && Ar::FC_ROWS == LayerG<Ar, 2>::OH, "dense slabs by conv3 rows");
-  HeadParams hp = head_params(n, P);
-  if (1 + hp.A + hp.R > kMaxHeads) {
-    set_error("heads: %d outputs > %d", 1 + hp.A + hp.R, kMaxHeads);
-    return MT_ERR_ARG;
-  }
-  typename NC::P1 p1;
-  typename NC::P2 p2;
-  typename NC::P3 p3;
-  nature_chain_params<NC>(st, P + n->off_conv[0], P + n->off_conv[1], P + n->off_conv[2], act1, act2, act3,
-                          n->cfg.activation, n->cfg.alpha_leaky, p1, p2, p3);
-  auto kern = &nature_step_kernel<NC, 2, 9>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)NC::LDS));
-    attr_set = true;
-  }
-  const int nfc = (Ar::F / kRowFcBN) * Ar::FC_ROWS * ((B + kRowFcBM - 1) / kRowFcBM);
-  hipLaunchKernelGGL(kern, dim3((unsigned)(B * NC::BPE + nfc + B)), dim3(256), NC::LDS, s, p1, p2, p3, sync, B,
-                     st.status, P + n->off_fc, slabs, n->cfg.activation, n->cfg.alpha_leaky, hp, n->cfg.softmax_temp,
-                     H, v, pi, rep, smp);
   MT_LAUNCHED();
   return MT_OK;
 }
@@ -1295,18 +1195,6 @@ static int forward_impl(const mt_net *n, const float *P, const uint8_t *obs, int
   const WsLayout L = ws_layout<Ar>(n, B);
   const ActRows A = act_rows<Ar>(n, ws, L, tr);
   if (marks) MT_HIP(hipEventRecord(marks[0], s));
-  if constexpr (nature_stacking<Ar>()) {
-    // the rollout step (stacking conv1 .. heads + draw) as one launch; the replayed graph's
-    // bootstrap with heads (SampleArgs::advance) keeps the separate launches (its heads kernel
-    // advances the sequence bases once every conv1 block has read them)
-    if (st && !(smp && smp->advance)) {
-      MT_TRY((launch_nature_step<Ar>(n, P, *st, B, A.base + A.L.act[0], A.base + A.L.act[1], A.base + A.L.act[2],
-                                     ws + L.fcslab, reinterpret_cast<uint32_t *>(ws + L.sync), A.base + A.h_off, v, pi,
-                                     rep, smp ? *smp : SampleArgs{}, s)));
-      if (marks) MT_HIP(hipEventRecord(marks[1], s));
-      return MT_OK;
-    }
-  }
   FwdExtras ex;
   ex.st = st;
   ex.sync = reinterpret_cast<uint32_t *>(ws + L.sync);

@@ -413,24 +413,11 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
 // SampleArgs::advance): block 0 adds advance_by to advance[0] and advance[1] — every reader of
 // those bases in the replay has run.
 constexpr int kRowFcBN = 16, kRowFcBM = 32;
-struct NoWait {
-  __device__ __forceinline__ void operator()() const {}
-};
-// 16 bytes of a buffer another workgroup of the same launch wrote with agent-scope stores
-__device__ __forceinline__ f32x4 ld_coherent4(const float *p) {
-  const uint64_t *w = reinterpret_cast<const uint64_t *>(p);
-  const uint64_t x = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t y = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return f32x4{__uint_as_float((uint32_t)x), __uint_as_float((uint32_t)(x >> 32)), __uint_as_float((uint32_t)y),
-               __uint_as_float((uint32_t)(y >> 32))};
-}
-// Block pb of a (gx, gy, gz) = (F / 16, ROWS, env chunks) grid. COH + wait (the in-launch dense
-// role of nature_step_kernel): the weights are requested first, then wait() (the hand-off from
-// the conv3 role), then x is read and the slabs written with agent-scope (sc1) accesses.
-template <int FEAT, int ROWS, int F, bool COH = false, class Wait = NoWait>
+// Block pb of a (gx, gy, gz) = (F / 16, ROWS, env chunks) grid.
+template <int FEAT, int ROWS, int F>
 __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, const float *__restrict__ Wfc,
                                             float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by, int pb,
-                                            int gx, int gy, int gz, const Wait &wait = Wait{}) {
+                                            int gx, int gy, int gz) {
   constexpr int KC = FEAT / 16, FLAT = FEAT * ROWS;
   static_assert(FEAT % 16 == 0 && F % kRowFcBN == 0, "whole chunks and column blocks");
   __shared__ __attribute__((aligned(16))) float red[4][kRowFcBM][kRowFcBN];
@@ -453,21 +440,10 @@ __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, 
   for (int j = 0; j < JN; ++j) {
     const int c = min(w + 4 * j, KC - 1);  // (chunks past the row's last are loaded but not used)
     const int k0 = i * FEAT + 16 * c + 4 * g;
+    a[j][0] = *reinterpret_cast<const f32x4 *>(x + (size_t)row0 * FLAT + k0);
+    a[j][1] = *reinterpret_cast<const f32x4 *>(x + (size_t)row1 * FLAT + k0);
 #pragma unroll
     for (int s = 0; s < 4; ++s) b[j][s] = Wfc[(size_t)(k0 + s) * F + n0 + r];
-  }
-  wait();
-#pragma unroll
-  for (int j = 0; j < JN; ++j) {
-    const int c = min(w + 4 * j, KC - 1);
-    const int k0 = i * FEAT + 16 * c + 4 * g;
-    if constexpr (COH) {
-      a[j][0] = ld_coherent4(x + (size_t)row0 * FLAT + k0);
-      a[j][1] = ld_coherent4(x + (size_t)row1 * FLAT + k0);
-    } else {
-      a[j][0] = *reinterpret_cast<const f32x4 *>(x + (size_t)row0 * FLAT + k0);
-      a[j][1] = *reinterpret_cast<const f32x4 *>(x + (size_t)row1 * FLAT + k0);
-    }
   }
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -488,13 +464,7 @@ __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, 
   for (int idx = threadIdx.x; idx < kRowFcBM * kRowFcBN; idx += 256) {
     const int m = idx / kRowFcBN, n = idx - m * kRowFcBN;
     const float s = ((red[0][m][n] + red[1][m][n]) + red[2][m][n]) + red[3][m][n];
-    if (e0 + m < B) {
-      float *o = slabs + ((size_t)i * B + e0 + m) * F + n0 + n;
-      if constexpr (COH)
-        __hip_atomic_store(o, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        *o = s;
-    }
+    if (e0 + m < B) slabs[((size_t)i * B + e0 + m) * F + n0 + n] = s;
   }
   MT_PROBE_AT(1, pb, 2);
 }

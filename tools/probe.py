@@ -57,8 +57,14 @@ def main():
         L.update()
     torch.cuda.synchronize()
     L.book.new_update()
-    for t in range(L.max_local_steps):  # the last chain armed is the bootstrap forward's
-        L.step(t)
+    if os.environ.get('MT_ROLLOUT_AHEAD') == '1':
+        # chains armed one step ahead (no replayed graph): stop after step T-2, so the last chain
+        # that ran is step T-1's (a rollout step's chain, not the bootstrap's)
+        for t in range(L.max_local_steps - 1):
+            L.step(t)
+    else:
+        for t in range(L.max_local_steps):  # the last chain armed is the bootstrap forward's
+            L.step(t)
     torch.cuda.synchronize()
     if a.isolated:
         E_ = cfg['ec']
