@@ -56,7 +56,8 @@ def load_pmc(config, kernels, name='pmc_trunk_%s.json'):
     d = json.load(open(path))
     total = 0
     for kern in kernels:
-        hit = [v for k, v in d.items() if k.replace('void ', '').endswith(kern)]
+        name_of = lambda k: k.replace('void ', '')
+        hit = [v for k, v in d.items() if name_of(k) == kern or name_of(k).startswith(kern + '<')]
         if not hit:
             return None
         total += hit[0]['hbm_bytes']
@@ -575,8 +576,8 @@ def main():
                 pmc_kernels = ['nips_conv_kernel<%d, true>' % C_in, 'nips_fc_kernel<%d>' % C_in]
             else:
                 kern = ('nature_chain_kernel (stacking conv1 with in-kernel pull -> conv2 -> conv3, per-env hand-offs '
-                        'in one launch) + the split-K dense GEMM: the stacking rollout chain')
-                pmc_kernels = ['nature_chain_kernel', 'gemm_f32_kernel']
+                        'in one launch) + row_fc_kernel (dense layer, one slab per conv row): the stacking rollout chain')
+                pmc_kernels = ['nature_chain_kernel', 'row_fc_kernel']
             timing = ('mt_forward_trunk_stacking (every env published, its pushes in HBM: the kernels the timed loop '
                       'runs, with nothing to wait for), ' + graph_note)
         elif inloop_us is not None and not lstm:  # (LSTM: step 0's forward has 1 + 5E rows, the others E)
@@ -640,8 +641,6 @@ def main():
                     sfx = ' + conv%d slab sum' % (i + 2) if i < nconv - 1 else ''
                     if i > 0 and cfg['arch'] == 'PWYX' and i == 1:  # its own direct dX launch (dconv.h dconv_bwd_solo)
                         names += ['conv2 dX (direct conv)', 'conv2 dW' + sfx]
-                    elif i > 0 and cfg['arch'] == 'NATURE':  # direct phase dX launch (dconv.h DBwdStrided)
-                        names += ['conv%d dX (direct phase conv)' % (i + 1), 'conv%d dW' % (i + 1) + sfx]
                     else:
                         names.append(('conv%d dX + conv%d dW' % (i + 1, i + 1) if i > 0 else 'conv1 dW') + sfx)
                 names.append('conv1 slab sum + global-norm partials')
