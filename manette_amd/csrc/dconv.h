@@ -772,6 +772,48 @@ __device__ __forceinline__ void chain_conv_tile(const Pr &p, int t, float *As, c
   if (u0 + g < D::U) p.store(pre, b, u0 + g, 16 * w + r, acc);
 }
 
+// The chain's conv1 tile (DFwdStack's staging) with its weights in registers too: 4 waves, wave w
+// owns M-tile w (4 units) and both 16-channel N-tiles over the whole K (KC x 2 B fragments, loaded
+// before the publication wait): no weight staging in LDS, no barrier behind the patch. fr: the
+// stacked frames' scratch, after the patch.
+template <class NC>
+__device__ __forceinline__ void chain_conv1_tile(const typename NC::P1 &p, int t, float *As,
+                                                 const f32x4 (&bf)[2][NC::D1::KC]) {
+  using D = typename NC::D1;
+  using Pr = typename NC::P1;
+  static_assert(D::WM == 4 && D::WN == 1 && D::TN == 2 && D::UPB == 16 && !D::TAPALIGNED, "conv1 tiling");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int b = t / D::BPI, bi = t - b * D::BPI;
+  const int u0 = bi * D::UPB;
+  const int oy0 = (4 * u0) / D::OW;
+  typename Pr::Pre pre[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) pre[j] = p.pre(b, min(u0 + 4 * w + g, D::U - 1), 16 * j + r);
+  const int own_end = bi + 1 < D::BPI ? min(D::H, ((4 * (u0 + D::UPB)) / D::OW) * D::S) : D::H;
+  p.template stage_patch<D>(b, oy0 * D::S, own_end, As, reinterpret_cast<uint8_t *>(As + D::ASZ));
+  int abase;
+  {
+    const int u = min(u0 + 4 * w + (r >> 2), D::U - 1);
+    const int px = min(4 * u + (r & 3), D::NPIX - 1);
+    const int oy = px / D::OW, ox = px - oy * D::OW;
+    abase = ((oy - oy0) * D::S * D::WPX + ox * D::S) * D::CS;
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int kc = 0; kc < D::KC; ++kc) {
+    const int q4 = 4 * kc + g, tap = min(q4 / D::QT, D::TAPS - 1), cq = q4 - (q4 / D::QT) * D::QT;
+    const f32x4 a = *reinterpret_cast<const f32x4 *>(As + abase + ((tap / D::KW) * D::WPX + tap % D::KW) * D::CS + 4 * cq);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s4], bf[j][kc][s4], acc[j], 0, 0, 0);
+  }
+  if (u0 + 4 * w + g < D::U) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) p.store(pre[j], b, u0 + 4 * w + g, 16 * j + r, acc[j]);
+  }
+}
+
 // The conv roles of block bid < E * NC::BPE.
 template <class NC>
 __device__ __forceinline__ void nature_conv_roles(const typename NC::P1 &p1, const typename NC::P2 &p2,
@@ -825,47 +867,6 @@ __device__ __forceinline__ void nature_conv_roles(const typename NC::P1 &p1, con
   }
 }
 
-// The chain's conv1 tile (DFwdStack's staging) with its weights in registers too: 4 waves, wave w
-// owns M-tile w (4 units) and both 16-channel N-tiles over the whole K (KC x 2 B fragments, loaded
-// before the publication wait): no weight staging in LDS, no barrier behind the patch. fr: the
-// stacked frames' scratch, after the patch.
-template <class NC>
-__device__ __forceinline__ void chain_conv1_tile(const typename NC::P1 &p, int t, float *As,
-                                                 const f32x4 (&bf)[2][NC::D1::KC]) {
-  using D = typename NC::D1;
-  using Pr = typename NC::P1;
-  static_assert(D::WM == 4 && D::WN == 1 && D::TN == 2 && D::UPB == 16 && !D::TAPALIGNED, "conv1 tiling");
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, g = lane >> 4;
-  const int b = t / D::BPI, bi = t - b * D::BPI;
-  const int u0 = bi * D::UPB;
-  const int oy0 = (4 * u0) / D::OW;
-  typename Pr::Pre pre[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) pre[j] = p.pre(b, min(u0 + 4 * w + g, D::U - 1), 16 * j + r);
-  const int own_end = bi + 1 < D::BPI ? min(D::H, ((4 * (u0 + D::UPB)) / D::OW) * D::S) : D::H;
-  p.template stage_patch<D>(b, oy0 * D::S, own_end, As, reinterpret_cast<uint8_t *>(As + D::ASZ));
-  int abase;
-  {
-    const int u = min(u0 + 4 * w + (r >> 2), D::U - 1);
-    const int px = min(4 * u + (r & 3), D::NPIX - 1);
-    const int oy = px / D::OW, ox = px - oy * D::OW;
-    abase = ((oy - oy0) * D::S * D::WPX + ox * D::S) * D::CS;
-  }
-  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int kc = 0; kc < D::KC; ++kc) {
-    const int q4 = 4 * kc + g, tap = min(q4 / D::QT, D::TAPS - 1), cq = q4 - (q4 / D::QT) * D::QT;
-    const f32x4 a = *reinterpret_cast<const f32x4 *>(As + abase + ((tap / D::KW) * D::WPX + tap % D::KW) * D::CS + 4 * cq);
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s4], bf[j][kc][s4], acc[j], 0, 0, 0);
-  }
-  if (u0 + 4 * w + g < D::U) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) p.store(pre[j], b, u0 + 4 * w + g, 16 * j + r, acc[j]);
-  }
-}
 
 template <class NC>
 __global__ __launch_bounds__(256) void nature_chain_kernel(typename NC::P1 p1, typename NC::P2 p2,

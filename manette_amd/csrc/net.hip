@@ -364,8 +364,11 @@ static int sum_slabs(const float *P, int S, size_t n, float *out, hipStream_t s)
 struct HeadParams {
   const float *Wc, *bc, *Wa, *ba, *Wr, *br;
   int A, R, F;
+  int nq;  // f32x4 quads of the head region [Wc, end of the parameters): critic | actor | repetition
 };
 
+// The three head (weights, biases) pairs are the last variables of every layout (add_heads), each
+// 64-float aligned, so [Wc, P + nparams) is one contiguous 256-B-aligned region.
 static HeadParams head_params(const mt_net *n, const float *P) {
   HeadParams h;
   h.F = n->F;
@@ -377,16 +380,18 @@ static HeadParams head_params(const mt_net *n, const float *P) {
   h.ba = h.Wa + (size_t)h.F * h.A;
   h.Wr = P + n->off_rep;
   h.br = h.Wr + (size_t)h.F * h.R;
+  h.nq = (int)((n->nparams - n->off_critic) / 4);
   return h;
 }
 
-// Weight of head output o (0 = critic, 1..A = actor, 1+A.. = repetition) for feature f
-// (f == F is the bias).
-__device__ __forceinline__ float head_w(const HeadParams &hp, int f, int o) {
-  if (o == 0) return f < hp.F ? hp.Wc[f] : hp.bc[0];
-  if (o <= hp.A) return f < hp.F ? hp.Wa[(size_t)f * hp.A + (o - 1)] : hp.ba[o - 1];
-  const int rr = o - 1 - hp.A;
-  return f < hp.F ? hp.Wr[(size_t)f * hp.R + rr] : hp.br[rr];
+// Head output o (0 = critic, 1..A = actor, 1+A.. = repetition) inside the head region staged in
+// LDS (heads_row): offset of its weight for feature 0, the feature stride, and its bias.
+__device__ __forceinline__ void head_col_lds(const HeadParams &hp, int o, int &base, int &stride, int &bias) {
+  const int oa = (int)(hp.Wa - hp.Wc), orr = (int)(hp.Wr - hp.Wc);
+  const bool c = o == 0, a = o <= hp.A;
+  base = c ? 0 : (a ? oa + (o - 1) : orr + (o - 1 - hp.A));
+  stride = c ? 1 : (a ? hp.A : hp.R);
+  bias = c ? hp.F : (a ? oa + hp.F * hp.A + (o - 1) : orr + hp.F * hp.R + (o - 1 - hp.A));
 }
 
 // Softmax over n logits held in lanes [0, n) of one wave (x/temp, TF: exp(x-max)/sum).
@@ -424,30 +429,25 @@ __device__ __forceinline__ int wave_draw(float p, int n, double u) {
 // Latency is everything here (32 blocks at E = 32, on the macro-step's critical chain), so every
 // global load is issued at the start, in the order it is needed — vmcnt retires loads in issue
 // order, so a wait for the first ones never waits for the later: the draw counter, then the slab
-// partials, then the dense bias, the head weights AND biases of the wave's outputs (a bias read
-// after the reduction cost one more memory round trip) — and the row's uniforms are hashed from
-// the counter while the slabs are in flight.
-// Column o of the head weights ([F][.] row-major, stride A / R for the actor / repetition heads) and
-// its bias, selected without branches (o is wave-uniform).
-__device__ __forceinline__ void head_col(const HeadParams &hp, int o, const float *&w, int &stride, const float *&bias) {
-  const bool c = o == 0, a = o <= hp.A;
-  w = c ? hp.Wc : (a ? hp.Wa + (o - 1) : hp.Wr + (o - 1 - hp.A));
-  stride = c ? 1 : (a ? hp.A : hp.R);
-  bias = c ? hp.bc : (a ? hp.ba + (o - 1) : hp.br + (o - 1 - hp.A));
-}
-
+// partials, then the dense bias, then the whole head region (every output's weights and bias) as
+// coalesced 16-B loads, staged into LDS beside h — and the row's uniforms are hashed from the
+// counter while the slabs are in flight. (Round 4: each wave used to load its outputs' weight
+// columns straight from HBM, lane f reading W[f][o] at a stride of A or R floats: one wave
+// instruction touched 16-40 cache lines, ~5,600 line requests per block for NATURE's 15 outputs
+// against ~500 for the region; the GEMV phase of the NATURE heads took 1.9 us.)
+constexpr int kHeadQ = 8;  // region quads per thread held in registers from the kernel start
 __device__ uint64_t g_zero_u64 = 0;  // read in place of an absent draw counter / sequence base
 
 template <int FT, int SB>
 __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs, int S, int B,
                                           const float *__restrict__ fc_b, int act, float alpha, const HeadParams &hp,
                                           float temp, float *__restrict__ H, float *__restrict__ v,
-                                          float *__restrict__ pi, float *__restrict__ rep, const SampleArgs &smp) {
+                                          float *__restrict__ pi, float *__restrict__ rep, const SampleArgs &smp,
+                                          float *Ws) {
   __shared__ float hs[256 * FT];
   __shared__ float zs[64];
   const int F = hp.F, O = 1 + hp.A + hp.R;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  constexpr int PRE = 6;  // 4 * PRE = 24 >= 1 + A + R of every config (more: read after the reduction)
   constexpr int FMAX = 4 * FT;
   // every load below is unconditional (clamped addresses, zeros by select): a guarded load would
   // end its basic block with a wait for it
@@ -463,20 +463,14 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
 #pragma unroll
     for (int u = 0; u < SB; ++u) t[fi][u] = p[(size_t)min(u, S - 1) * zs_stride];
   }
-  // (3) dense bias, head weights and biases of this wave's first PRE outputs (o = w, w + 4, ...)
+  // (3) dense bias, then the head region's first kHeadQ * 256 quads
   float fb[FT];
 #pragma unroll
   for (int fi = 0; fi < FT; ++fi) fb[fi] = fc_b[min((int)threadIdx.x + 256 * fi, F - 1)];
-  float wpre[PRE][FMAX], zb[PRE];
+  const f32x4 *hsrc = reinterpret_cast<const f32x4 *>(hp.Wc);
+  f32x4 wq[kHeadQ];
 #pragma unroll
-  for (int k = 0; k < PRE; ++k) {
-    const float *wp, *bp;
-    int st;
-    head_col(hp, min(w + 4 * k, O - 1), wp, st, bp);
-#pragma unroll
-    for (int j = 0; j < FMAX; ++j) wpre[k][j] = wp[(size_t)min(lane + 64 * j, F - 1) * st];
-    zb[k] = *bp;
-  }
+  for (int q = 0; q < kHeadQ; ++q) wq[q] = hsrc[min((int)threadIdx.x + 256 * q, hp.nq - 1)];
   if (smp.advance && b == 0 && threadIdx.x == 0) {  // the replayed rollout's last reader has run
     smp.advance[0] += smp.advance_by;
     smp.advance[1] += smp.advance_by;
@@ -498,25 +492,24 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
       H[(size_t)b * F + f] = h;
     }
   }
+  // the head region into LDS (the rest of a region larger than kHeadQ * 256 quads loaded here)
+  f32x4 *wdst = reinterpret_cast<f32x4 *>(Ws);
+#pragma unroll
+  for (int q = 0; q < kHeadQ; ++q)
+    if ((int)threadIdx.x + 256 * q < hp.nq) wdst[threadIdx.x + 256 * q] = wq[q];
+  for (int i = threadIdx.x + 256 * kHeadQ; i < hp.nq; i += 256) wdst[i] = hsrc[i];
   __syncthreads();
   MT_PROBE_AT(2, b, 1);
-#pragma unroll
-  for (int k = 0; k < PRE; ++k) {
-    const int o = w + 4 * k;
-    if (o < O) {
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < FMAX; ++j)
-        if (lane + 64 * j < F) acc += hs[lane + 64 * j] * wpre[k][j];
-      acc = wave_sum(acc);
-      if (lane == 0) zs[o] = acc + zb[k];
-    }
-  }
-  for (int o = w + 4 * PRE; o < O; o += 4) {
+  // logits: the same products and order as a column walk f = lane, lane + 64, ... then the bias
+  for (int o = w; o < O; o += 4) {
+    int base, stride, bias;
+    head_col_lds(hp, o, base, stride, bias);
     float acc = 0.f;
-    for (int f = lane; f < F; f += 64) acc += hs[f] * head_w(hp, f, o);
+#pragma unroll
+    for (int j = 0; j < FMAX; ++j)
+      if (lane + 64 * j < F) acc += hs[lane + 64 * j] * Ws[base + (lane + 64 * j) * stride];
     acc = wave_sum(acc);
-    if (lane == 0) zs[o] = acc + head_w(hp, F, o);
+    if (lane == 0) zs[o] = acc + Ws[bias];
   }
   __syncthreads();
   MT_PROBE_AT(2, b, 2);
@@ -560,8 +553,9 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict_
                                                         float *__restrict__ H, float *__restrict__ v,
                                                         float *__restrict__ pi,
                                                         float *__restrict__ rep, SampleArgs smp) {
+  extern __shared__ __attribute__((aligned(16))) float head_region[];
   MT_PROBE_AT(2, blockIdx.x, 0);
-  heads_row<FT, SB>(blockIdx.x, slabs, S, B, fc_b, act, alpha, hp, temp, H, v, pi, rep, smp);
+  heads_row<FT, SB>(blockIdx.x, slabs, S, B, fc_b, act, alpha, hp, temp, H, v, pi, rep, smp, head_region);
   MT_PROBE_AT(2, blockIdx.x, 3);
 }
 
@@ -574,9 +568,23 @@ static int launch_heads(int rows, hipStream_t s, const float *slabs, int S, int 
     set_error("heads: F = %d > 512 or %d outputs > %d", hp.F, 1 + hp.A + hp.R, kMaxHeads);
     return MT_ERR_ARG;
   }
-#define MT_HEADS(FT_, SB_)                                                                                 \
-  hipLaunchKernelGGL((heads_fwd_kernel<FT_, SB_>), dim3(rows), dim3(256), 0, s, slabs, S, B, fc_b, act, alpha, hp, \
-                     temp, H, v, pi, rep, smp)
+  // dynamic LDS: the head region (<= 64 outputs x 513 rows: 132 KB at most)
+  const size_t lds = (size_t)hp.nq * 16;
+  if (lds > 150 * 1024) {
+    set_error("heads: head region of %zu bytes exceeds the LDS", lds);
+    return MT_ERR_ARG;
+  }
+#define MT_HEADS(FT_, SB_)                                                                                   \
+  do {                                                                                                       \
+    static bool attr_set = false;                                                                            \
+    if (!attr_set && lds > 64 * 1024) {                                                                      \
+      MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&heads_fwd_kernel<FT_, SB_>),                \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));                   \
+      attr_set = true;                                                                                       \
+    }                                                                                                        \
+    hipLaunchKernelGGL((heads_fwd_kernel<FT_, SB_>), dim3(rows), dim3(256), lds, s, slabs, S, B, fc_b, act,    \
+                       alpha, hp, temp, H, v, pi, rep, smp);                                                 \
+  } while (0)
   if (hp.F <= 256) {
     if (S <= 1) MT_HEADS(1, 1);
     else if (S <= 9) MT_HEADS(1, 9);
@@ -646,11 +654,12 @@ struct ReturnsSrc {
 
 // V(s_T)[e] of the bootstrap (ReturnsSrc::boot_slabs): the dense layer's split-K slabs summed in
 // slab order + bias + act (heads_row's phase 1), then the critic's dot product as heads_row forms
-// it (lanes over features in 64-strides, DPP wave sum, + bias). Called by the whole block; the
-// result is in *vt (LDS) after the call. wcb: wave 0's critic weights Wc[lane + 64 j], loaded by
-// the caller at kernel start (off the slab -> dot chain).
+// it (lanes over features in 64-strides, DPP wave sum, + bias) from the head region in LDS (Ws).
+// Called by the whole block; the result is in *vt (LDS) after the call. stage(): the caller's LDS
+// stores of the head region, run after this block's slab loads are issued and before the barrier.
+template <class Stage>
 __device__ __forceinline__ void boot_value(const ReturnsSrc &rs, const HeadParams &hp, int e, int act, float alpha,
-                                           const float (&wcb)[8], float *hsb, float *vt) {
+                                           const float *Ws, float *hsb, float *vt, const Stage &stage) {
   const int F = hp.F;
   for (int f = threadIdx.x; f < F; f += 256) {
     const float *p = rs.boot_slabs + (size_t)e * F + f;
@@ -666,15 +675,16 @@ __device__ __forceinline__ void boot_value(const ReturnsSrc &rs, const HeadParam
     }
     hsb[f] = act_fwd(acc + rs.fc_b[f], act, alpha);
   }
+  stage();
   __syncthreads();
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     float acc = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (lane + 64 * j < F) acc += hsb[lane + 64 * j] * wcb[j];
+      if (lane + 64 * j < F) acc += hsb[lane + 64 * j] * Ws[lane + 64 * j];
     acc = wave_sum(acc);
-    if (lane == 0) *vt = acc + hp.bc[0];
+    if (lane == 0) *vt = acc + Ws[F];
   }
   __syncthreads();
 }
@@ -719,12 +729,16 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
   __shared__ float dzs[kMaxHeads];
   __shared__ float ya[2];
   __shared__ float buf[2 * kMaxScan];
+  extern __shared__ __attribute__((aligned(16))) float Ws[];  // the head region (HeadParams::nq quads)
   const int b = blockIdx.x;
   MT_PROBE_AT(4, b, 0);
   const int A = hp.A, R = hp.R, O = 1 + A + R, F = hp.F;
   // Every load that does not depend on the return is issued first, so its latency overlaps the
   // scan's (the rewards / masks are read over PCIe from pinned memory): the row's head inputs
-  // (threads < 64) and the dH operands H[b][f] and W[f][.] of the thread's features.
+  // (threads < 64), H[b][f] of the thread's features and the head region as coalesced 16-B loads
+  // (staged into LDS for the critic's dot product and dH; round 4: per-thread loads of W[f][.] at a
+  // stride of A or R floats made ~2,800 cache-line requests per block for NATURE's heads, queued
+  // ahead of the bootstrap slab loads).
   const int lane = threadIdx.x;
   float pa = 0.f, pr = 0.f, vb = 0.f, adv_in = 0.f, y_in = 0.f;
   int ai = 0, ri = 0;
@@ -739,24 +753,22 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
       y_in = y[b];
     }
   }
-  constexpr int FT = 2, KW = 32;  // F <= 512; A + R <= 32 (else the weights are read after the scan)
-  const bool pre = A + R <= KW;
-  float hv[FT], wc[FT], wk[FT][KW];
+  constexpr int FT = 2;  // F <= 512 in registers (more: read at the end)
+  float hv[FT];
 #pragma unroll
-  for (int fi = 0; fi < FT; ++fi) {
-    const int f = min((int)threadIdx.x + 256 * fi, F - 1);
-    hv[fi] = H[(size_t)b * F + f];
-    wc[fi] = hp.Wc[f];
+  for (int fi = 0; fi < FT; ++fi) hv[fi] = H[(size_t)b * F + min((int)threadIdx.x + 256 * fi, F - 1)];
+  const f32x4 *hsrc = reinterpret_cast<const f32x4 *>(hp.Wc);
+  f32x4 wq[kHeadQ];
 #pragma unroll
-    for (int k = 0; k < KW; ++k)
-      wk[fi][k] = !pre ? 0.f : (k < A ? hp.Wa[(size_t)f * A + k] : (k < A + R ? hp.Wr[(size_t)f * R + (k - A)] : 0.f));
-  }
-  float wcb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (rs.boot_slabs && threadIdx.x < 64) {
+  for (int q = 0; q < kHeadQ; ++q) wq[q] = hsrc[min((int)threadIdx.x + 256 * q, hp.nq - 1)];
+  auto stage = [&]() {
+    f32x4 *wdst = reinterpret_cast<f32x4 *>(Ws);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)  // (relaxed atomic: an invariant load would be sunk to its use, past two barriers)
-      wcb[j] = __hip_atomic_load(hp.Wc + min(lane + 64 * j, F - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+    for (int q = 0; q < kHeadQ; ++q)
+      if ((int)threadIdx.x + 256 * q < hp.nq) wdst[threadIdx.x + 256 * q] = wq[q];
+    for (int i = threadIdx.x + 256 * kHeadQ; i < hp.nq; i += 256) wdst[i] = hsrc[i];
+  };
+  bool staged = false;
   if (rs.r) {
     // this row's rewards / masks (pinned host memory, a PCIe round trip) requested first
     float rk = 0.f, mk = 0.f;
@@ -772,7 +784,8 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
       __shared__ float hsb[512];
       __shared__ float vts;
       const int e = b % rs.E;
-      boot_value(rs, hp, e, act, alpha, wcb, hsb, &vts);
+      boot_value(rs, hp, e, act, alpha, Ws, hsb, &vts, stage);
+      staged = true;
       vt = vts;
       if (rs.vt_out && b < rs.E && threadIdx.x == 0) rs.vt_out[e] = vt;
     } else {
@@ -782,6 +795,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
     row_return(rs, vb, b, vt, rk, mk, ya, buf);
   }
   MT_PROBE_AT(4, b, 2);
+  if (!staged) stage();  // (visible to every thread after the barrier below)
   if (threadIdx.x < 64) {
     const float ad = rs.r ? ya[1] : adv_in;
     const float yb = rs.r ? ya[0] : y_in;
@@ -804,32 +818,18 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
   __syncthreads();
   MT_PROBE_AT(4, b, 3);
   for (int o = threadIdx.x; o < O; o += 256) dz[(size_t)b * O + o] = dzs[o];
+  // dH[b][f] = act'(H) * (dz_c Wc[f] + actor terms + repetition terms), in that order
+  const int oa = (int)(hp.Wa - hp.Wc), orr = (int)(hp.Wr - hp.Wc);
+  auto dh = [&](int f, float h) {
+    float acc = dzs[0] * Ws[f];
+    for (int k = 0; k < A; ++k) acc += dzs[1 + k] * Ws[oa + f * A + k];
+    for (int k = 0; k < R; ++k) acc += dzs[1 + A + k] * Ws[orr + f * R + k];
+    dH[(size_t)b * F + f] = acc * act_bwd(h, act, alpha);
+  };
 #pragma unroll
-  for (int fi = 0; fi < FT; ++fi) {
-    const int f = threadIdx.x + 256 * fi;
-    if (f >= F) break;
-    float acc = dzs[0] * wc[fi];
-    if (pre) {
-      // same order as below: actor terms, then repetition terms
-#pragma unroll
-      for (int k = 0; k < KW; ++k)
-        if (k < A + R) acc += dzs[1 + k] * wk[fi][k];
-    } else {
-      const float *wa = hp.Wa + (size_t)f * A;
-      for (int k = 0; k < A; ++k) acc += dzs[1 + k] * wa[k];
-      const float *wr = hp.Wr + (size_t)f * R;
-      for (int k = 0; k < R; ++k) acc += dzs[1 + A + k] * wr[k];
-    }
-    dH[(size_t)b * F + f] = acc * act_bwd(hv[fi], act, alpha);
-  }
-  for (int f = threadIdx.x + 256 * FT; f < F; f += 256) {  // (F > 512: not built today)
-    float acc = dzs[0] * hp.Wc[f];
-    const float *wa = hp.Wa + (size_t)f * A;
-    for (int k = 0; k < A; ++k) acc += dzs[1 + k] * wa[k];
-    const float *wr = hp.Wr + (size_t)f * R;
-    for (int k = 0; k < R; ++k) acc += dzs[1 + A + k] * wr[k];
-    dH[(size_t)b * F + f] = acc * act_bwd(H[(size_t)b * F + f], act, alpha);
-  }
+  for (int fi = 0; fi < FT; ++fi)
+    if ((int)threadIdx.x + 256 * fi < F) dh(threadIdx.x + 256 * fi, hv[fi]);
+  for (int f = threadIdx.x + 256 * FT; f < F; f += 256) dh(f, H[(size_t)b * F + f]);  // (F > 512: not built today)
   MT_PROBE_AT(4, b, 4);
 }
 
@@ -1281,7 +1281,18 @@ static int loss_bwd_launch(const mt_net *n, const float *P, int B, float *ws, co
   const float scale = 5.0f / (float)B;
   HeadParams hp = head_params(n, P);
   if (!launch_allowed()) return MT_OK;
-  hipLaunchKernelGGL(loss_bwd_kernel, dim3(B), dim3(256), 0, s, hp, ws + L.H, pi, rep, v, a_idx, r_idx, y, adv,
+  const size_t lds = (size_t)hp.nq * 16;  // the head region (heads kernel: same bound)
+  if (lds > 150 * 1024) {
+    set_error("loss: head region of %zu bytes exceeds the LDS", lds);
+    return MT_ERR_ARG;
+  }
+  static bool attr_set = false;
+  if (!attr_set && lds > 64 * 1024) {
+    MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&loss_bwd_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3(B), dim3(256), lds, s, hp, ws + L.H, pi, rep, v, a_idx, r_idx, y, adv,
                      beta, scale, n->cfg.softmax_temp, n->cfg.activation, n->cfg.alpha_leaky, ws + L.dz, ws + L.dH,
                      loss_terms, rs);
   MT_LAUNCHED();
