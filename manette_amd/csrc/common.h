@@ -222,7 +222,11 @@ int forward_boot(const mt_net *net, const float *params, const uint8_t *obs, int
                  hipStream_t stream, const StackSrc *st = nullptr, uint32_t *advance = nullptr,
                  uint32_t advance_by = 0);
 // the native rollout's LSTM macro-step forward (lstm.h lstm_step_fwd_impl; mt_lstm_step_forward)
+// st / sync: step t > 0 of the pipelined rollout stacks its new rows in its conv1 launch (lstm.h,
+// dconv.h launch_lstm_stack_conv1), sync = lstm_stack_sync_words(E) zeroed device words
+constexpr int lstm_stack_sync_words(int E) { return 32 + 32 * E; }  // 128-B lines: tiles done, env e stacked
 int lstm_step_forward(const mt_net *net, const float *params, const uint8_t *fstore, int t, int E, int T,
                       int32_t *nz, const float *over, void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
-                      const SampleArgs *smp, hipStream_t stream, const hipEvent_t *marks = nullptr);
+                      const SampleArgs *smp, hipStream_t stream, const hipEvent_t *marks = nullptr,
+                      const StackSrc *st = nullptr, uint32_t *sync = nullptr);
 }  // namespace mt

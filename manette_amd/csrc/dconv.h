@@ -79,8 +79,13 @@ struct DFwd {
   };
   __device__ __forceinline__ Pre pre(int, int, int n) const { return {bias[n]}; }
   __device__ __forceinline__ f32x4 load4(const InT *q) const {
-    if constexpr (COH_IN) {
-      static_assert(!U8, "coherent loads of f32 activations");
+    if constexpr (COH_IN && U8) {  // (the LSTM step's stacked state, lstm_stack_conv1_kernel)
+      const uint32_t u = __hip_atomic_load(reinterpret_cast<const uint32_t *>(q), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      const float sc = 1.0f / 255.0f;  // InElem<true>::load4's arithmetic
+      return f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc, (float)((u >> 16) & 0xff) * sc,
+                   (float)(u >> 24) * sc};
+    } else if constexpr (COH_IN) {
       const uint64_t *w = reinterpret_cast<const uint64_t *>(q);
       const uint64_t x = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t y = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -912,6 +917,143 @@ static int launch_nature_chain(const StackSrc &st, const float *W1, const float 
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)(B * NC::BPE)), dim3(256), NC::LDS, s, p1, p2, p3, sync, B, st.status);
+  MT_LAUNCHED();
+  return MT_OK;
+}
+
+// ---- the LSTM rollout step's new frames: pull + stack + conv1 as one dataflow launch ----------
+// (round 4) Blocks [0, E): one per env — wait for env e's publication (StackSrc::ready), read its p
+// pushes from the pinned staging (the edge lines of its slot group system-scope, ld_published16),
+// stack them onto the previous state (preprocess_kernel's op, as DFwdStack stages it), store the
+// new state with agent-scope stores (it is also the frame store's row of env e), drain, count env e
+// stacked. Blocks [E, E + E * BPI): the layered trunk's conv1 tiles (DFwd, the same tiling and
+// arithmetic as conv_forward_direct), env-major and XCD-aware; a tile of env e polls env e's word,
+// reads the state with agent-scope loads (COH_IN) and runs the conv1 body: the step's conv1 runs
+// while the emulators still step later envs, instead of behind pull_frames_kernel ->
+// preprocess_kernel -> conv1 after the LAST env. Every env's word has its own 128-B line: with the
+// words packed (16 envs a line) the ~1,300 polling tiles delayed the env blocks' increments and the
+// launch ended ~25 us after the last publication, no earlier than the layered conv1
+// (profiles/r04_ab). Deadlock-free as nature_chain_kernel (a tile waits only for an env block, all
+// lower-indexed; bounded). sync = [tiles done][env e stacked: line 1 + e] (32-word lines); the last
+// tile resets every word for the next launch.
+template <class G>
+struct LstmStackConv1 {
+  using F = DConvFor<G, true>;
+  using P1 = DFwd<G, true, true, true, false>;
+  using D = DConvCfg<P1, F::WM, F::WN, F::TMW, F::CK>;
+  static_assert(D::NT == 256 && G::CIN == 4 && G::H == 84 && G::W == 84 && G::S == 1, "gray 84x84 conv1, 4 waves");
+  static constexpr size_t LDS = D::LDS;
+};
+
+// env e's new state (84 x 84 pixels, one u32 of 4 channels each): 16-pixel items, 256 threads
+__device__ __forceinline__ void lstm_pull_stack(const StackSrc &st, int e, uint32_t *sync) {
+  constexpr int NPIX = 84 * 84, NI = NPIX / 16, IT = (NI + 255) / 256;  // 441 items
+  const int tid = threadIdx.x;
+  __shared__ int s_p;
+  // the previous state's items requested before the wait (their latency hides under it)
+  const uint4 *prev = reinterpret_cast<const uint4 *>(st.prev + (size_t)e * NPIX * 4);
+  uint4 pv[IT][4];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = min(tid + 256 * it, NI - 1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pv[it][c] = prev[4 * i + c];
+  }
+  if (tid == 0) {
+    const uint32_t tag = st.tag_base ? ((*st.tag_base + st.tag) & 0x1fffffffu) : st.tag;
+    s_p = min(max(wait_published(st.ready, e, tag, st.status), 0), 4);  // (a timeout stacks no frame)
+    MT_PROBE_CHAIN(e, 0);
+  }
+  __syncthreads();
+  const int p = s_p;
+  // the p pushes' 16-pixel chunks (push j of env e = frame slot 4e + j), one round trip
+  const size_t F = (size_t)NPIX, lo = 4 * (size_t)e * F, hi = lo + 4 * F;
+  uint4 fv[IT][4];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = min(tid + 256 * it, NI - 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      fv[it][j] = j < p ? ld_published16(st.frames, ((size_t)4 * e + j) * F + 16 * (size_t)i, lo, hi)
+                        : make_uint4(0u, 0u, 0u, 0u);
+  }
+  uint32_t *out = reinterpret_cast<uint32_t *>(st.out + (size_t)e * NPIX * 4);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = tid + 256 * it;
+    if (NI % 256 != 0 && i >= NI) break;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {  // pixel quad c of the item: pixels 16 i + 4 c .. + 3
+      uint32_t wv[4] = {pv[it][c].x, pv[it][c].y, pv[it][c].z, pv[it][c].w};
+      uint32_t fw[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fw[j] = c == 0 ? fv[it][j].x : c == 1 ? fv[it][j].y : c == 2 ? fv[it][j].z : fv[it][j].w;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t v = p < 4 ? wv[k] >> (8 * p) : 0u;
+        for (int j = 0; j < p; ++j) v |= ((fw[j] >> (8 * k)) & 0xffu) << (8 * (4 - p + j));
+        __hip_atomic_store(out + 16 * (size_t)i + 4 * c + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's (sc1) state stores have completed
+  __syncthreads();
+  if (tid == 0) {  // env e stacked (its own 128-B line: see lstm_stack_conv1_kernel)
+    __hip_atomic_fetch_add(sync + 32 + 32 * e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    MT_PROBE_CHAIN(e, 1);
+  }
+}
+
+template <class G>
+__global__ __launch_bounds__(256) void lstm_stack_conv1_kernel(StackSrc st, typename LstmStackConv1<G>::P1 p1,
+                                                               uint32_t *sync, int E) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  using C = LstmStackConv1<G>;
+  using D = typename C::D;
+  if ((int)blockIdx.x < E) {
+    lstm_pull_stack(st, blockIdx.x, sync);
+    return;
+  }
+  const int t = xcd_tile((int)blockIdx.x - E, E * D::BPI), b = t / D::BPI;  // (an env's tiles on one XCD)
+  if (threadIdx.x == 0) {  // env b stacked (bounded wait, as chain_wait)
+    const uint32_t *w = sync + 32 + 32 * b;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      __builtin_amdgcn_s_sleep(8);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+        if (st.status) __hip_atomic_store(st.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;  // (proceed; the host reports the error)
+      }
+    }
+  }
+  __syncthreads();
+  dconv_body<typename C::P1, C::F::WM, C::F::WN, C::F::TMW, C::F::CK>(p1, t, t + 1, smem);
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(E * D::BPI) - 1) {
+    // the last tile: every tile is past its wait — reset the words for the next launch
+    __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < E; ++k) __hip_atomic_store(sync + 32 + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// pull + stack + conv1 of the E new frames of an LSTM step: st->out = the new state rows (the frame
+// store's), Y / arg = conv1's pooled output and argmax rows. sync: lstm_stack_sync_words(E) zeroed words.
+template <class G>
+static int launch_lstm_stack_conv1(const StackSrc &st, const float *W, float *Y, uint8_t *arg, int E, int act,
+                                   float alpha, uint32_t *sync, hipStream_t s) {
+  using C = LstmStackConv1<G>;
+  static_assert(C::LDS <= 160 * 1024, "LDS budget");
+  if (E <= 0 || !launch_allowed()) return MT_OK;
+  auto kern = &lstm_stack_conv1_kernel<G>;
+  static bool attr_set = false;
+  if (!attr_set && C::LDS > 64 * 1024) {
+    MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)C::LDS));
+    attr_set = true;
+  }
+  const typename C::P1 p1{st.out, W, W + G::KK * G::COUT, Y, arg, act, alpha};
+  hipLaunchKernelGGL(kern, dim3((unsigned)(E + E * C::D::BPI)), dim3(256), C::LDS, s, st, p1, sync, E);
   MT_LAUNCHED();
   return MT_OK;
 }

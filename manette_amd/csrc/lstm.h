@@ -494,16 +494,35 @@ __global__ __launch_bounds__(128) void lstm_gather_dxg_kernel(const float *__res
   dxg[(size_t)r * 128 + g] = acc;
 }
 
+// st (the native rollout's pipelined steps, gray frames): rows [row0, row0 + nrows) are the step's
+// E new states, stacked from st->prev and env e's pushes by the conv1 launch itself
+// (launch_lstm_stack_conv1: pull + stack + conv1 per env as each env is published; sync = its
+// lstm_stack_sync_words(E) zeroed words), then conv2 .. conv4 layered.
 template <class Ar>
 static int lstm_frames_fwd_impl(const mt_net *n, const float *P, const uint8_t *fstore, int row0, int nrows,
-                                int E, int T, float *ws, hipStream_t s) {
+                                int E, int T, float *ws, hipStream_t s, const StackSrc *st = nullptr,
+                                uint32_t *sync = nullptr) {
   const LstmFrameWs X = lstm_frame_layout<Ar>(n, E, T);
   MT_CHECK_ARG(row0 >= 0 && nrows >= 1 && row0 + nrows <= X.R_max, "rows [%d, %d) outside the frame store [0, %d)",
                row0, row0 + nrows, X.R_max);
   constexpr size_t FB = (size_t)84 * 84 * LayerG<Ar, 0>::CIN;
   WsLayout Ls = X.L;
   shift_rows<Ar>(Ls, (size_t)row0);
-  MT_TRY((trunk_forward<Ar>(n, P, fstore + (size_t)row0 * FB, nrows, ws, Ls, s)));
+  if (st) {
+    using G1 = LayerG<Ar, 0>;
+    if constexpr (G1::CIN == 4 && pooled<Ar, 0>()) {
+      MT_CHECK_ARG(sync && nrows == E && st->out == fstore + (size_t)row0 * FB,
+                   "stacking conv1: the step's E new rows, a counter region");
+      MT_TRY((launch_lstm_stack_conv1<G1>(*st, P + n->off_conv[0], ws + Ls.pool[0], (uint8_t *)(ws + Ls.parg[0]), E,
+                                          n->cfg.activation, n->cfg.alpha_leaky, sync, s)));
+      MT_TRY((trunk_forward<Ar, 1>(n, P, layer_out<Ar, 0>(ws, Ls), nrows, ws, Ls, s)));
+    } else {
+      set_error("stacking conv1: gray frames only");
+      return MT_ERR_UNSUPPORTED;
+    }
+  } else {
+    MT_TRY((trunk_forward<Ar>(n, P, fstore + (size_t)row0 * FB, nrows, ws, Ls, s)));
+  }
   return launch_gemm<TileFc>(LdRowMajor{layer_out<Ar, Ar::NCONV - 1>(ws, Ls), Ar::FLAT},
                              LdColMajor{P + n->off_lstm, Ar::G4, -1},
                              EpSlab{ws + X.xg + (size_t)row0 * Ar::G4, X.R_max, Ar::G4}, nrows, Ar::G4, Ar::FLAT,
@@ -543,12 +562,14 @@ static int lstm_windows_fwd_impl(const mt_net *n, const float *P, int32_t *nz_t,
 template <class Ar>
 static int lstm_step_fwd_impl(const mt_net *n, const float *P, const uint8_t *fstore, int t, int E, int T,
                               int32_t *nz, const float *over, float *ws, float *v, float *pi, float *rep,
-                              const SampleArgs *smp, hipStream_t s, const hipEvent_t *marks) {
+                              const SampleArgs *smp, hipStream_t s, const hipEvent_t *marks,
+                              const StackSrc *st = nullptr, uint32_t *sync = nullptr) {
   MT_CHECK_ARG(t >= 0 && t <= T, "step %d outside [0, %d]", t, T);
   MT_CHECK_ARG(t == 0 || over, "steps t > 0 need the episode-end flags");
   const int row0 = t == 0 ? 0 : 1 + (4 + t) * E, nrows = t == 0 ? 1 + 5 * E : E;
   if (marks) MT_HIP(hipEventRecord(marks[0], s));
-  MT_TRY((lstm_frames_fwd_impl<Ar>(n, P, fstore, row0, nrows, E, T, ws, s)));
+  MT_CHECK_ARG(!st || t > 0, "step 0 has no pushes to stack");
+  MT_TRY((lstm_frames_fwd_impl<Ar>(n, P, fstore, row0, nrows, E, T, ws, s, st, sync)));
   if (marks) MT_HIP(hipEventRecord(marks[1], s));
   return lstm_windows_fwd_impl<Ar>(n, P, nz + (size_t)t * E, t, E, T, ws, v, pi, rep, s, smp,
                                    t > 0 ? nz + (size_t)(t - 1) * E : nullptr, t > 0 ? over : nullptr);

@@ -1879,12 +1879,13 @@ extern "C" int mt_lstm_step_forward(const mt_net *net, const float *params, cons
 
 int mt::lstm_step_forward(const mt_net *net, const float *params, const uint8_t *fstore, int t, int E, int T,
                           int32_t *nz, const float *over, void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
-                          const SampleArgs *smp, hipStream_t stream, const hipEvent_t *marks) {
+                          const SampleArgs *smp, hipStream_t stream, const hipEvent_t *marks, const StackSrc *st,
+                          uint32_t *sync) {
   MT_CHECK_ARG(!smp || (smp->counters && smp->a_idx && smp->r_idx), "null sample buffer");
   MT_LSTM_ONLY(net, {
     MT_LSTM_WS(E, T);
     return lstm_step_fwd_impl<Ar>(net, params, fstore, t, E, T, nz, over, (float *)ws, v, pi, rep, smp, stream,
-                                  marks);
+                                  marks, st, sync);
   });
   return MT_OK;
 }

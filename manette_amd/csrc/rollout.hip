@@ -25,6 +25,8 @@ struct mt_rollout {
   bool zero_copy, in_place, pooled, resized, pipelined;
   bool pull;          // pipelined + resized: per-env ready words, pull kernel into HBM, tagged pairs
   bool stack_fwd;     // pull + NIPS / gray NATURE: the forward's conv(1) kernel stacks (no preprocess launch)
+  bool lstm_stack = false;     // pull + gray LSTM: each step's conv1 launch pulls + stacks (launch_lstm_stack_conv1)
+  uint32_t *lstm_sync = nullptr;  // its env queue (lstm_stack_sync_words(E), zero between launches)
   bool lstm;          // LSTM arch: frame-store forward per step (mt_lstm_step_forward), nz on the device
   bool boot_slabs;    // MT_ROLLOUT_BOOT_SLABS: the bootstrap chain ends at the dense slabs (no heads)
   const uint8_t *fstore = nullptr;  // LSTM: the frame store (states = its slot 4)
@@ -162,6 +164,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   // env's conv1 waits for its own publication, no pull / preprocess kernel in front of the convs
   ro->stack_fwd = ro->pull && (cfg.arch == MT_ARCH_NIPS || (cfg.arch == MT_ARCH_NATURE && cfg.depth == 1));
   ro->lstm = lstm;
+  ro->lstm_stack = ro->pull && lstm && cfg.depth == 1;
   ro->boot_slabs = (b.flags & MT_ROLLOUT_BOOT_SLABS) != 0;
   ro->over_dev = (const float *)over_dev;
   if (lstm) ro->fstore = b.states - (size_t)(1 + 4 * E) * 84 * 84 * 4 * cfg.depth;
@@ -180,6 +183,10 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&ro->packed_dev, ro->packed_host, 0);
     if (e == hipSuccess) e = hipMalloc((void **)&ro->frames_hbm, (size_t)4 * E * 84 * 84 * cfg.depth);
     if (e == hipSuccess) e = hipMalloc((void **)&ro->count_hbm, sizeof(int32_t) * 2 * E);  // counts; offsets 4e
+    if (e == hipSuccess && ro->lstm_stack) {
+      e = hipMalloc((void **)&ro->lstm_sync, sizeof(uint32_t) * lstm_stack_sync_words(E));
+      if (e == hipSuccess) e = hipMemset(ro->lstm_sync, 0, sizeof(uint32_t) * lstm_stack_sync_words(E));
+    }
     if (e == hipSuccess) {
       std::vector<int32_t> offs(E);
       for (int i = 0; i < E; ++i) offs[i] = 4 * i;
@@ -190,6 +197,7 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
       if (ro->packed_host) (void)hipHostFree(ro->packed_host);
       if (ro->frames_hbm) (void)hipFree(ro->frames_hbm);
       if (ro->count_hbm) (void)hipFree(ro->count_hbm);
+      if (ro->lstm_sync) (void)hipFree(ro->lstm_sync);
       delete ro;
       set_error("pinned step words: %s", hipGetErrorString(e));
       return MT_ERR_HIP;
@@ -235,6 +243,7 @@ extern "C" void mt_rollout_destroy(mt_rollout *ro) {
     (void)hipHostFree(ro->packed_host);
     (void)hipFree(ro->frames_hbm);
     (void)hipFree(ro->count_hbm);
+    if (ro->lstm_sync) (void)hipFree(ro->lstm_sync);
   }
   delete ro;
 }
@@ -398,9 +407,12 @@ int enqueue_forward(mt_rollout *ro, const float *params, int t, hipStream_t s, b
   const hipEvent_t *marks;
   MT_TRY_(next_marks(ro, &marks));
   if (ro->lstm) {  // step t's new frames + its E windows, pi / rep [T+1][E][.]
+    // (pull mode, t > 0: the step's conv1 launch pulls + stacks env by env, arm_step launched no
+    //  pull / preprocess kernel)
+    const bool stk_lstm = ro->lstm_stack && t > 0;
     MT_TRY_(lstm_step_forward(ro->net, params, ro->fstore, t, E, T, b.nz, ro->over_dev, b.ws, b.ws_bytes,
                               b.values + (size_t)t * E, b.pi + (size_t)t * E * ro->A, b.rep + (size_t)t * E * ro->R,
-                              &smp, s, marks));
+                              &smp, s, marks, stk_lstm ? &st : nullptr, ro->lstm_sync));
   } else {
     MT_TRY_(forward_sample(ro->net, params, b.states + (size_t)t * slot, E, b.ws, b.ws_bytes,
                            b.values + (size_t)t * E, b.pi + po * ro->A, b.rep + po * ro->R, &smp, true, s,
@@ -452,7 +464,7 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
   // mt_preprocess_resized
   const bool stk = ro->stack_fwd && (k < T || b.v_boot);
   if (ro->pull) {
-    if (!stk) {  // (the stacking conv kernel pulls each env itself)
+    if (!stk && !ro->lstm_stack) {  // (the stacking conv kernel pulls each env itself)
       hipLaunchKernelGGL(pull_frames_kernel, dim3((E + kPullEnvs - 1) / kPullEnvs), dim3(256), 0, s,
                          reinterpret_cast<const uint4 *>(ro->staging_dev), ro->env_ready_dev, want, ro->status_dev, E,
                          (int)(84 * 84 * ro->depth / 16), reinterpret_cast<uint4 *>(ro->frames_hbm), ro->count_hbm);
@@ -469,8 +481,14 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
   if (k < T) {
     MT_TRY_(enqueue_forward(ro, params, k, s, stk, want));
   } else if (b.v_boot && ro->lstm) {  // bootstrap V(s_T): slot 4 + T's frames + the windows of step T
+    const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
+    StackSrc st{b.states + (size_t)(T - 1) * slot, ro->staging_dev, nullptr, b.states + (size_t)T * slot};
+    st.ready = ro->env_ready_dev;
+    st.tag = want & 0x1fffffffu;
+    st.status = ro->status_dev;
     MT_TRY_(lstm_step_forward(ro->net, params, ro->fstore, T, E, T, b.nz, ro->over_dev, b.ws, b.ws_bytes, b.v_boot,
-                              b.pi + (size_t)T * E * ro->A, b.rep + (size_t)T * E * ro->R, nullptr, s));
+                              b.pi + (size_t)T * E * ro->A, b.rep + (size_t)T * E * ro->R, nullptr, s, nullptr,
+                              ro->lstm_stack ? &st : nullptr, ro->lstm_sync));
   } else if (b.v_boot) {  // bootstrap V(s_T), no draw, no train rows
     const size_t slot = (size_t)E * 84 * 84 * 4 * ro->depth;
     const size_t po = b.train_ws ? (size_t)T * E : 0;
