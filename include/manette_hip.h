@@ -135,8 +135,10 @@ int mt_forward_trunk(const mt_net *net, const float *params, const uint8_t *obs,
  * many final frames (frames = [4*batch][84][84][depth], env e's pushes at slots 4e..; host-mapped
  * pinned staging or device memory) — then the dense layer's split-K partials, left in ws. NIPS:
  * nips_conv_kernel<STACK> + nips_fc_kernel; gray NATURE: nature_chain_kernel (stacking conv1 ->
- * conv2 -> conv3, per-env hand-offs in one launch) + the split-K dense GEMM. With every ready word
- * already set nothing waits: the kernels' own duration. MT_ERR_UNSUPPORTED for the other archs. */
+ * conv2 -> conv3, per-env hand-offs in one launch) + the split-K dense GEMM; PWYX (gray or RGB):
+ * stack_conv1_kernel (per-env pull + stack blocks, then conv1 tiles per env) + conv2 .. + the dense
+ * GEMM. With every ready word already set nothing waits: the kernels' own duration.
+ * MT_ERR_UNSUPPORTED for the other archs (the LSTM steps stack in mt_rollout_step). */
 int mt_forward_trunk_stacking(const mt_net *net, const float *params, const uint8_t *prev, const uint8_t *frames,
                               const uint32_t *ready, uint32_t tag, uint8_t *out, int batch, void *ws, size_t ws_bytes,
                               mt_stream_t stream);

@@ -209,8 +209,9 @@ __device__ __forceinline__ int wait_published(const uint32_t *ready, int e, uint
   return (int)(v & 7u);
 }
 // forward (mt_forward) with the A3 draw fused into the heads kernel; smp, tr and st may be null.
-// st (NIPS inference only): the conv kernel first stacks the new state st->out (== obs) from
-// st->prev and the pushed frames (mt_preprocess_resized's op, fused into the forward).
+// st (inference only; NIPS, gray NATURE, PWYX): the conv1 launch first stacks the new state
+// st->out (== obs) from st->prev and the pushed frames (mt_preprocess_resized's op, fused into the
+// forward; PWYX: dconv.h launch_stack_conv1 with the workspace's counter region).
 // marks (optional, two events): recorded around the trunk launches (convs + dense layer; not the
 // heads), so a caller can time the trunk kernels where they really run (mt_rollout_trunk_timing).
 int forward_sample(const mt_net *net, const float *params, const uint8_t *obs, int batch, void *ws,
@@ -223,8 +224,8 @@ int forward_boot(const mt_net *net, const float *params, const uint8_t *obs, int
                  uint32_t advance_by = 0);
 // the native rollout's LSTM macro-step forward (lstm.h lstm_step_fwd_impl; mt_lstm_step_forward)
 // st / sync: step t > 0 of the pipelined rollout stacks its new rows in its conv1 launch (lstm.h,
-// dconv.h launch_lstm_stack_conv1), sync = lstm_stack_sync_words(E) zeroed device words
-constexpr int lstm_stack_sync_words(int E) { return 32 + 32 * E; }  // 128-B lines: tiles done, env e stacked
+// dconv.h launch_stack_conv1), sync = stack_conv1_sync_words(E) zeroed device words
+constexpr int stack_conv1_sync_words(int E) { return 32 + 32 * E; }  // 128-B lines: tiles done, env e stacked
 int lstm_step_forward(const mt_net *net, const float *params, const uint8_t *fstore, int t, int E, int T,
                       int32_t *nz, const float *over, void *ws, size_t ws_bytes, float *v, float *pi, float *rep,
                       const SampleArgs *smp, hipStream_t stream, const hipEvent_t *marks = nullptr,

@@ -79,7 +79,7 @@ struct DFwd {
   };
   __device__ __forceinline__ Pre pre(int, int, int n) const { return {bias[n]}; }
   __device__ __forceinline__ f32x4 load4(const InT *q) const {
-    if constexpr (COH_IN && U8) {  // (the LSTM step's stacked state, lstm_stack_conv1_kernel)
+    if constexpr (COH_IN && U8) {  // (a frame trunk's stacked state, stack_conv1_kernel)
       const uint32_t u = __hip_atomic_load(reinterpret_cast<const uint32_t *>(q), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
       const float sc = 1.0f / 255.0f;  // InElem<true>::load4's arithmetic
@@ -668,6 +668,8 @@ static int conv_forward_direct(const void *X, const float *W, const float *bias,
 template <class Pr>
 using ChainCfg = DConvCfg<Pr, 1, 4, 1, Pr::CI>;
 
+constexpr int kChainSyncWords = 96;  // nature_chain_kernel's counter words per env
+
 template <class G1_, class G2_, class G3_>
 struct NatureChain {
   using G1 = G1_;
@@ -684,7 +686,9 @@ struct NatureChain {
       std::max((size_t)D1::ASZ * 4 + 4 * D1::RIN * G1::W, (size_t)std::max(D2::ASZ, D3::ASZ) * 4);
   static_assert(D1::NT == 256 && D2::NT == 256 && D3::NT == 256, "one block size for every role");
   static constexpr int BPE = D1::BPI + D2::BPI + D3::BPI;  // blocks per env
-  static constexpr int SYNC_WORDS = 4;                     // per env: conv1 / conv2 / conv3 done
+  // per env: conv1 / conv2 / conv3 done, each counter on its own 128-B line (words 0 / 32 / 64) —
+  // polled lines shared by several envs delay the producers' increments (stack_conv1_kernel)
+  static constexpr int SYNC_WORDS = kChainSyncWords, C2 = 32, C3 = 64;
 };
 
 __device__ __forceinline__ void chain_signal(uint32_t *c, uint32_t last, int e, int phase) {
@@ -850,24 +854,24 @@ __device__ __forceinline__ void nature_conv_roles(const typename NC::P1 &p1, con
     MT_PROBE_BLK(1);
     chain_conv_tile(p2, t, smem, bf);
     MT_PROBE_BLK(3);
-    chain_signal(sync + NC::SYNC_WORDS * e + 1, D2::BPI - 1, e, 2);
+    chain_signal(sync + NC::SYNC_WORDS * e + NC::C2, D2::BPI - 1, e, 2);
   } else {
     const int t = bid - n1 - n2, e = t / D3::BPI;
     uint32_t *c = sync + NC::SYNC_WORDS * e;
     f32x4 bf[D3::KC];
     chain_load_b(p3, bf);
-    chain_wait(c + 1, D2::BPI, status);
+    chain_wait(c + NC::C2, D2::BPI, status);
     MT_PROBE_BLK(1);
     chain_conv_tile(p3, t, smem, bf);
     MT_PROBE_BLK(3);
     __syncthreads();
     if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(c + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)D3::BPI - 1) {
+        __hip_atomic_fetch_add(c + NC::C3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)D3::BPI - 1) {
       // env e's last block: every block of env e is past its wait — reset for the next launch
       MT_PROBE_CHAIN(e, 3);
       __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(c + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c + NC::C2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c + NC::C3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -921,44 +925,53 @@ static int launch_nature_chain(const StackSrc &st, const float *W1, const float 
   return MT_OK;
 }
 
-// ---- the LSTM rollout step's new frames: pull + stack + conv1 as one dataflow launch ----------
-// (round 4) Blocks [0, E): one per env — wait for env e's publication (StackSrc::ready), read its p
-// pushes from the pinned staging (the edge lines of its slot group system-scope, ld_published16),
-// stack them onto the previous state (preprocess_kernel's op, as DFwdStack stages it), store the
-// new state with agent-scope stores (it is also the frame store's row of env e), drain, count env e
-// stacked. Blocks [E, E + E * BPI): the layered trunk's conv1 tiles (DFwd, the same tiling and
-// arithmetic as conv_forward_direct), env-major and XCD-aware; a tile of env e polls env e's word,
-// reads the state with agent-scope loads (COH_IN) and runs the conv1 body: the step's conv1 runs
-// while the emulators still step later envs, instead of behind pull_frames_kernel ->
-// preprocess_kernel -> conv1 after the LAST env. Every env's word has its own 128-B line: with the
-// words packed (16 envs a line) the ~1,300 polling tiles delayed the env blocks' increments and the
-// launch ended ~25 us after the last publication, no earlier than the layered conv1
-// (profiles/r04_ab). Deadlock-free as nature_chain_kernel (a tile waits only for an env block, all
-// lower-indexed; bounded). sync = [tiles done][env e stacked: line 1 + e] (32-word lines); the last
-// tile resets every word for the next launch.
+// ---- a frame trunk's rollout step: pull + stack + conv1 as one dataflow launch ----------------
+// (round 4; the LSTM and PWYX rollouts, gray or RGB) Blocks [0, E): one per env — wait for env e's
+// publication (StackSrc::ready), read its p pushes from the pinned staging (the edge lines of its
+// slot group system-scope, ld_published16), stack them onto the previous state (preprocess_kernel's
+// op: every state word = one colour channel's 4 frames, shifted by p bytes, the p new frame bytes
+// on top), store the new state with agent-scope stores, drain, count env e stacked. Blocks
+// [E, E + E * BPI): the trunk's conv1 tiles (DFwd, the same tiling and arithmetic as
+// conv_forward_direct), env-major and XCD-aware; a tile of env e polls env e's word, reads the
+// state with agent-scope loads (COH_IN) and runs the conv1 body: the step's conv1 runs while the
+// emulators still step later envs, instead of behind pull_frames_kernel -> preprocess_kernel ->
+// conv1 after the LAST env. Every env's word has its own 128-B line: with the words packed (16
+// envs a line) the ~1,300 polling tiles delayed the env blocks' increments and the launch ended
+// ~25 us after the last publication, no earlier than the layered conv1 (profiles/r04_ab).
+// Deadlock-free as nature_chain_kernel (a tile waits only for an env block, all lower-indexed;
+// bounded). sync = [tiles done][env e stacked: line 1 + e] (32-word lines); the last tile resets
+// every word for the next launch.
 template <class G>
-struct LstmStackConv1 {
+struct StackConv1 {
   using F = DConvFor<G, true>;
   using P1 = DFwd<G, true, true, true, false>;
   using D = DConvCfg<P1, F::WM, F::WN, F::TMW, F::CK>;
-  static_assert(D::NT == 256 && G::CIN == 4 && G::H == 84 && G::W == 84 && G::S == 1, "gray 84x84 conv1, 4 waves");
+  static constexpr int DEPTH = G::CIN / 4;  // colour channels (1 gray, 3 RGB)
+  static_assert(D::NT == 256 && (G::CIN == 4 || G::CIN == 12) && G::H == 84 && G::W == 84 && G::S == 1,
+                "84x84 conv1 of 4 stacked frames, 4 waves");
   static constexpr size_t LDS = D::LDS;
 };
 
-// env e's new state (84 x 84 pixels, one u32 of 4 channels each): 16-pixel items, 256 threads
-__device__ __forceinline__ void lstm_pull_stack(const StackSrc &st, int e, uint32_t *sync) {
-  constexpr int NPIX = 84 * 84, NI = NPIX / 16, IT = (NI + 255) / 256;  // 441 items
+// env e's new state (84 x 84 x DEPTH words of 4 frames each): 16-word items (one 16-B chunk of
+// each push), 256 threads, PASS items per thread in flight
+template <int DEPTH>
+__device__ __forceinline__ void frame_pull_stack(const StackSrc &st, int e, uint32_t *sync) {
+  constexpr int NW = 84 * 84 * DEPTH, NI = NW / 16, IT = (NI + 255) / 256;  // 441 items gray, 1,323 RGB
+  constexpr int PASS = 2;
+  static_assert(NW % 16 == 0, "whole 16-B frame chunks");
   const int tid = threadIdx.x;
   __shared__ int s_p;
-  // the previous state's items requested before the wait (their latency hides under it)
-  const uint4 *prev = reinterpret_cast<const uint4 *>(st.prev + (size_t)e * NPIX * 4);
-  uint4 pv[IT][4];
+  const uint4 *prev = reinterpret_cast<const uint4 *>(st.prev + (size_t)e * NW * 4);
+  uint4 pv[PASS][4];
+  auto load_prev = [&](int it0) {
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int i = min(tid + 256 * it, NI - 1);
+    for (int q = 0; q < PASS; ++q) {
+      const int i = min(tid + 256 * (it0 + q), NI - 1);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) pv[it][c] = prev[4 * i + c];
-  }
+      for (int c = 0; c < 4; ++c) pv[q][c] = prev[4 * i + c];
+    }
+  };
+  load_prev(0);  // (the first pass's previous state requested before the wait: its latency hides under it)
   if (tid == 0) {
     const uint32_t tag = st.tag_base ? ((*st.tag_base + st.tag) & 0x1fffffffu) : st.tag;
     s_p = min(max(wait_published(st.ready, e, tag, st.status), 0), 4);  // (a timeout stacks no frame)
@@ -966,52 +979,56 @@ __device__ __forceinline__ void lstm_pull_stack(const StackSrc &st, int e, uint3
   }
   __syncthreads();
   const int p = s_p;
-  // the p pushes' 16-pixel chunks (push j of env e = frame slot 4e + j), one round trip
-  const size_t F = (size_t)NPIX, lo = 4 * (size_t)e * F, hi = lo + 4 * F;
-  uint4 fv[IT][4];
+  // push j of env e = frame slot 4e + j (NW bytes), its 16-B chunk i = state words 16 i .. 16 i + 15
+  const size_t F = (size_t)NW, lo = 4 * (size_t)e * F, hi = lo + 4 * F;
+  uint32_t *out = reinterpret_cast<uint32_t *>(st.out + (size_t)e * NW * 4);
+  for (int it0 = 0; it0 < IT; it0 += PASS) {
+    if (it0 > 0) load_prev(it0);
+    uint4 fv[PASS][4];
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int i = min(tid + 256 * it, NI - 1);
+    for (int q = 0; q < PASS; ++q) {
+      const int i = min(tid + 256 * (it0 + q), NI - 1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      fv[it][j] = j < p ? ld_published16(st.frames, ((size_t)4 * e + j) * F + 16 * (size_t)i, lo, hi)
-                        : make_uint4(0u, 0u, 0u, 0u);
-  }
-  uint32_t *out = reinterpret_cast<uint32_t *>(st.out + (size_t)e * NPIX * 4);
+      for (int j = 0; j < 4; ++j)
+        fv[q][j] = j < p ? ld_published16(st.frames, ((size_t)4 * e + j) * F + 16 * (size_t)i, lo, hi)
+                         : make_uint4(0u, 0u, 0u, 0u);
+    }
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int i = tid + 256 * it;
-    if (NI % 256 != 0 && i >= NI) break;
+    for (int q = 0; q < PASS; ++q) {
+      const int i = tid + 256 * (it0 + q);
+      if (it0 + q >= IT || i >= NI) break;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {  // pixel quad c of the item: pixels 16 i + 4 c .. + 3
-      uint32_t wv[4] = {pv[it][c].x, pv[it][c].y, pv[it][c].z, pv[it][c].w};
-      uint32_t fw[4];
+      for (int c = 0; c < 4; ++c) {  // words 16 i + 4 c .. + 3
+        const uint32_t wv[4] = {pv[q][c].x, pv[q][c].y, pv[q][c].z, pv[q][c].w};
+        uint32_t fw[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fw[j] = c == 0 ? fv[it][j].x : c == 1 ? fv[it][j].y : c == 2 ? fv[it][j].z : fv[it][j].w;
+        for (int j = 0; j < 4; ++j)
+          fw[j] = c == 0 ? fv[q][j].x : c == 1 ? fv[q][j].y : c == 2 ? fv[q][j].z : fv[q][j].w;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint32_t v = p < 4 ? wv[k] >> (8 * p) : 0u;
-        for (int j = 0; j < p; ++j) v |= ((fw[j] >> (8 * k)) & 0xffu) << (8 * (4 - p + j));
-        __hip_atomic_store(out + 16 * (size_t)i + 4 * c + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < 4; ++k) {
+          uint32_t v = p < 4 ? wv[k] >> (8 * p) : 0u;
+          for (int j = 0; j < p; ++j) v |= ((fw[j] >> (8 * k)) & 0xffu) << (8 * (4 - p + j));
+          __hip_atomic_store(out + 16 * (size_t)i + 4 * c + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's (sc1) state stores have completed
   __syncthreads();
-  if (tid == 0) {  // env e stacked (its own 128-B line: see lstm_stack_conv1_kernel)
+  if (tid == 0) {  // env e stacked (its own 128-B line: see stack_conv1_kernel)
     __hip_atomic_fetch_add(sync + 32 + 32 * e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     MT_PROBE_CHAIN(e, 1);
   }
 }
 
 template <class G>
-__global__ __launch_bounds__(256) void lstm_stack_conv1_kernel(StackSrc st, typename LstmStackConv1<G>::P1 p1,
-                                                               uint32_t *sync, int E) {
+__global__ __launch_bounds__(256) void stack_conv1_kernel(StackSrc st, typename StackConv1<G>::P1 p1, uint32_t *sync,
+                                                          int E) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  using C = LstmStackConv1<G>;
+  using C = StackConv1<G>;
   using D = typename C::D;
   if ((int)blockIdx.x < E) {
-    lstm_pull_stack(st, blockIdx.x, sync);
+    frame_pull_stack<C::DEPTH>(st, blockIdx.x, sync);
     return;
   }
   const int t = xcd_tile((int)blockIdx.x - E, E * D::BPI), b = t / D::BPI;  // (an env's tiles on one XCD)
@@ -1037,15 +1054,19 @@ __global__ __launch_bounds__(256) void lstm_stack_conv1_kernel(StackSrc st, type
   }
 }
 
-// pull + stack + conv1 of the E new frames of an LSTM step: st->out = the new state rows (the frame
-// store's), Y / arg = conv1's pooled output and argmax rows. sync: lstm_stack_sync_words(E) zeroed words.
+// pull + stack + conv1 of the E new frames of a rollout step: st->out = the new state rows, Y / arg =
+// conv1's pooled output and argmax rows. sync: stack_conv1_sync_words(E) zeroed words.
 template <class G>
-static int launch_lstm_stack_conv1(const StackSrc &st, const float *W, float *Y, uint8_t *arg, int E, int act,
-                                   float alpha, uint32_t *sync, hipStream_t s) {
-  using C = LstmStackConv1<G>;
+static int launch_stack_conv1(const StackSrc &st, const float *W, float *Y, uint8_t *arg, int E, int act, float alpha,
+                              uint32_t *sync, hipStream_t s) {
+  using C = StackConv1<G>;
   static_assert(C::LDS <= 160 * 1024, "LDS budget");
+  if (!st.ready || !st.prev || !st.frames || !st.out || !sync) {
+    set_error("stacking conv1: ready words, previous / new state, staging and a counter region");
+    return MT_ERR_ARG;
+  }
   if (E <= 0 || !launch_allowed()) return MT_OK;
-  auto kern = &lstm_stack_conv1_kernel<G>;
+  auto kern = &stack_conv1_kernel<G>;
   static bool attr_set = false;
   if (!attr_set && C::LDS > 64 * 1024) {
     MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,

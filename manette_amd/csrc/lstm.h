@@ -494,10 +494,10 @@ __global__ __launch_bounds__(128) void lstm_gather_dxg_kernel(const float *__res
   dxg[(size_t)r * 128 + g] = acc;
 }
 
-// st (the native rollout's pipelined steps, gray frames): rows [row0, row0 + nrows) are the step's
-// E new states, stacked from st->prev and env e's pushes by the conv1 launch itself
-// (launch_lstm_stack_conv1: pull + stack + conv1 per env as each env is published; sync = its
-// lstm_stack_sync_words(E) zeroed words), then conv2 .. conv4 layered.
+// st (the native rollout's pipelined steps): rows [row0, row0 + nrows) are the step's E new
+// states, stacked from st->prev and env e's pushes by the conv1 launch itself (dconv.h
+// launch_stack_conv1: pull + stack + conv1 per env as each env is published; sync = its
+// stack_conv1_sync_words(E) zeroed words), then conv2 .. conv4 layered (net.hip trunk_forward).
 template <class Ar>
 static int lstm_frames_fwd_impl(const mt_net *n, const float *P, const uint8_t *fstore, int row0, int nrows,
                                 int E, int T, float *ws, hipStream_t s, const StackSrc *st = nullptr,
@@ -508,21 +508,12 @@ static int lstm_frames_fwd_impl(const mt_net *n, const float *P, const uint8_t *
   constexpr size_t FB = (size_t)84 * 84 * LayerG<Ar, 0>::CIN;
   WsLayout Ls = X.L;
   shift_rows<Ar>(Ls, (size_t)row0);
-  if (st) {
-    using G1 = LayerG<Ar, 0>;
-    if constexpr (G1::CIN == 4 && pooled<Ar, 0>()) {
-      MT_CHECK_ARG(sync && nrows == E && st->out == fstore + (size_t)row0 * FB,
-                   "stacking conv1: the step's E new rows, a counter region");
-      MT_TRY((launch_lstm_stack_conv1<G1>(*st, P + n->off_conv[0], ws + Ls.pool[0], (uint8_t *)(ws + Ls.parg[0]), E,
-                                          n->cfg.activation, n->cfg.alpha_leaky, sync, s)));
-      MT_TRY((trunk_forward<Ar, 1>(n, P, layer_out<Ar, 0>(ws, Ls), nrows, ws, Ls, s)));
-    } else {
-      set_error("stacking conv1: gray frames only");
-      return MT_ERR_UNSUPPORTED;
-    }
-  } else {
-    MT_TRY((trunk_forward<Ar>(n, P, fstore + (size_t)row0 * FB, nrows, ws, Ls, s)));
-  }
+  MT_CHECK_ARG(!st || (sync && nrows == E && st->out == fstore + (size_t)row0 * FB),
+               "stacking conv1: the step's E new rows, a counter region");
+  FwdExtras ex;
+  ex.st = st;
+  ex.sync = sync;
+  MT_TRY((trunk_forward<Ar>(n, P, fstore + (size_t)row0 * FB, nrows, ws, Ls, s, ex)));
   return launch_gemm<TileFc>(LdRowMajor{layer_out<Ar, Ar::NCONV - 1>(ws, Ls), Ar::FLAT},
                              LdColMajor{P + n->off_lstm, Ar::G4, -1},
                              EpSlab{ws + X.xg + (size_t)row0 * Ar::G4, X.R_max, Ar::G4}, nrows, Ar::G4, Ar::FLAT,

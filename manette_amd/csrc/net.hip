@@ -87,6 +87,13 @@ template <class Ar, int I>
 constexpr bool pooled() {
   return (Ar::POOL >> I) & 1u;
 }
+// the frame trunks (PWYX, LSTM; gray or RGB): the rollout step's conv1 launch pulls + stacks each
+// env as it is published (dconv.h stack_conv1_kernel), conv2 .. layered
+template <class Ar>
+constexpr bool frame_stacking() {
+  using G = LayerG<Ar, 0>;
+  return G::S == 1 && G::SAME && pooled<Ar, 0>() && (G::CIN == 4 || G::CIN == 12) && G::H == 84 && G::W == 84;
+}
 // spatial size of layer I's output after its (optional) pool
 template <class Ar, int I>
 constexpr int out_hw() {
@@ -349,7 +356,9 @@ static WsLayout ws_layout(const mt_net *n, int B) {
   L.dH = take((size_t)B * Ar::F);
   L.wslab = take(wslab);
   L.wslab2 = take(wslab);  // ping-pong slab regions of consecutive conv layers (trunk_backward)
-  L.sync = take(nature_stacking<Ar>() ? (size_t)4 * B : 0);  // (nature_chain_kernel: 4 words per env)
+  // the rollout chains' counters (nature_chain_kernel; stack_conv1_kernel), zero between launches
+  L.sync = take(nature_stacking<Ar>() ? (size_t)kChainSyncWords * B
+                                      : frame_stacking<Ar>() && !Ar::LSTM ? (size_t)stack_conv1_sync_words(B) : 0);
   L.total = off;
   return L;
 }
@@ -1018,8 +1027,9 @@ static const float *layer_out(float *ws, const WsLayout &L) {
   return ws + (pooled<Ar, I>() ? L.pool[I] : L.act[I]);
 }
 
-// The layered trunk with the rollout chain's extras: st = the stacking source of conv1 (the NATURE
-// gray chain: nature_chain_kernel, x = st->out), sync = the E-row workspace's counters it uses.
+// The layered trunk with the rollout chain's extras: st = the stacking source of conv1 (x = st->out;
+// the NATURE gray chain: nature_chain_kernel; the frame trunks: stack_conv1_kernel, then conv2 ..
+// layered), sync = the counters it uses (zero between launches).
 struct FwdExtras {
   const StackSrc *st = nullptr;
   uint32_t *sync = nullptr;
@@ -1031,9 +1041,20 @@ static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, 
   if constexpr (I < Ar::NCONV) {
     using G = LayerG<Ar, I>;
     const float *W = P + n->off_conv[I];
-    if (I == 0 && ex.st && !nature_stacking<Ar>()) {
-      set_error("the stacking conv1 is built for the NIPS and the gray NATURE trunks");
+    if (I == 0 && ex.st && !nature_stacking<Ar>() && !frame_stacking<Ar>()) {
+      set_error("the stacking conv1 is built for the NIPS, the gray NATURE and the frame (PWYX / LSTM) trunks");
       return MT_ERR_UNSUPPORTED;
+    }
+    if constexpr (I == 0 && frame_stacking<Ar>()) {
+      if (ex.st) {  // the rollout step: pull + stack + conv1 as one dataflow launch, then conv2 ..
+        if (!ex.sync || x != ex.st->out) {
+          set_error("stacking conv1: the input must be the new state rows, with a counter region");
+          return MT_ERR_ARG;
+        }
+        MT_TRY((launch_stack_conv1<G>(*ex.st, W, ws + L.pool[0], (uint8_t *)(ws + L.parg[0]), B, n->cfg.activation,
+                                      n->cfg.alpha_leaky, ex.sync, s)));
+        return trunk_forward<Ar, 1>(n, P, layer_out<Ar, 0>(ws, L), B, ws, L, s);
+      }
     }
     if constexpr (I == 0 && nature_stacking<Ar>()) {
       if (ex.st) {  // the rollout chain: stacking conv1 -> conv2 -> conv3 as one dataflow launch
@@ -1627,7 +1648,7 @@ extern "C" int mt_forward_trunk_stacking(const mt_net *net, const float *params,
       return MT_ERR_WORKSPACE;
     }
     if constexpr (Ar::LSTM) {
-      set_error("stacking trunk is built for the NIPS and the gray NATURE archs only");
+      set_error("stacking trunk: the NIPS, gray NATURE and PWYX archs (the LSTM steps: mt_lstm_step_forward)");
       return MT_ERR_UNSUPPORTED;
     } else {
       return trunk_infer_impl<Ar>(net, params, out, batch, (float *)ws, (hipStream_t)stream, &st);

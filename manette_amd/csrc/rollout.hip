@@ -25,8 +25,9 @@ struct mt_rollout {
   bool zero_copy, in_place, pooled, resized, pipelined;
   bool pull;          // pipelined + resized: per-env ready words, pull kernel into HBM, tagged pairs
   bool stack_fwd;     // pull + NIPS / gray NATURE: the forward's conv(1) kernel stacks (no preprocess launch)
-  bool lstm_stack = false;     // pull + gray LSTM: each step's conv1 launch pulls + stacks (launch_lstm_stack_conv1)
-  uint32_t *lstm_sync = nullptr;  // its env queue (lstm_stack_sync_words(E), zero between launches)
+  bool lstm_stack = false;     // pull + LSTM: each step's conv1 launch pulls + stacks (launch_stack_conv1)
+  bool frame_stack = false;    // pull + PWYX: the same in the forward's trunk (ws counters)
+  uint32_t *lstm_sync = nullptr;  // its env queue (stack_conv1_sync_words(E), zero between launches)
   bool lstm;          // LSTM arch: frame-store forward per step (mt_lstm_step_forward), nz on the device
   bool boot_slabs;    // MT_ROLLOUT_BOOT_SLABS: the bootstrap chain ends at the dense slabs (no heads)
   const uint8_t *fstore = nullptr;  // LSTM: the frame store (states = its slot 4)
@@ -164,7 +165,8 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
   // env's conv1 waits for its own publication, no pull / preprocess kernel in front of the convs
   ro->stack_fwd = ro->pull && (cfg.arch == MT_ARCH_NIPS || (cfg.arch == MT_ARCH_NATURE && cfg.depth == 1));
   ro->lstm = lstm;
-  ro->lstm_stack = ro->pull && lstm && cfg.depth == 1;
+  ro->lstm_stack = ro->pull && lstm;
+  ro->frame_stack = ro->pull && !lstm && cfg.arch == MT_ARCH_PWYX;
   ro->boot_slabs = (b.flags & MT_ROLLOUT_BOOT_SLABS) != 0;
   ro->over_dev = (const float *)over_dev;
   if (lstm) ro->fstore = b.states - (size_t)(1 + 4 * E) * 84 * 84 * 4 * cfg.depth;
@@ -184,8 +186,8 @@ extern "C" int mt_rollout_create(const mt_net *net, int E, int T, void *runner, 
     if (e == hipSuccess) e = hipMalloc((void **)&ro->frames_hbm, (size_t)4 * E * 84 * 84 * cfg.depth);
     if (e == hipSuccess) e = hipMalloc((void **)&ro->count_hbm, sizeof(int32_t) * 2 * E);  // counts; offsets 4e
     if (e == hipSuccess && ro->lstm_stack) {
-      e = hipMalloc((void **)&ro->lstm_sync, sizeof(uint32_t) * lstm_stack_sync_words(E));
-      if (e == hipSuccess) e = hipMemset(ro->lstm_sync, 0, sizeof(uint32_t) * lstm_stack_sync_words(E));
+      e = hipMalloc((void **)&ro->lstm_sync, sizeof(uint32_t) * stack_conv1_sync_words(E));
+      if (e == hipSuccess) e = hipMemset(ro->lstm_sync, 0, sizeof(uint32_t) * stack_conv1_sync_words(E));
     }
     if (e == hipSuccess) {
       std::vector<int32_t> offs(E);
@@ -462,7 +464,7 @@ int arm_step(mt_rollout *ro, const float *params, int k, int ahead, hipStream_t 
   // pull: the pull kernel waits per env and copies the pushes into HBM; the preprocess of step
   // k-1 then reads them there — inside step k's forward conv kernel (stack_fwd, NIPS), else as
   // mt_preprocess_resized
-  const bool stk = ro->stack_fwd && (k < T || b.v_boot);
+  const bool stk = (ro->stack_fwd || ro->frame_stack) && (k < T || b.v_boot);
   if (ro->pull) {
     if (!stk && !ro->lstm_stack) {  // (the stacking conv kernel pulls each env itself)
       hipLaunchKernelGGL(pull_frames_kernel, dim3((E + kPullEnvs - 1) / kPullEnvs), dim3(256), 0, s,

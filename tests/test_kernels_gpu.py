@@ -485,10 +485,11 @@ def test_zero_copy_reads_see_host_rewrites_across_launches():
 
 
 @pytest.mark.parametrize('arch,E,depth', [('NIPS', 7, 1), ('NIPS', 32, 1), ('NIPS', 5, 3), ('NATURE', 7, 1),
-                                          ('NATURE', 64, 1)])
+                                          ('NATURE', 64, 1), ('PWYX', 7, 1), ('PWYX', 5, 3), ('PWYX', 32, 3)])
 def test_stacking_trunk_in_kernel_pull(arch, E, depth):
     """mt_forward_trunk_stacking — the rollout chain's conv kernel (NIPS: nips_conv_kernel<STACK>;
-    gray NATURE: conv1 = the direct conv with DFwdStack's patch staging) pulling each env's frames
+    gray NATURE: conv1 = the direct conv with DFwdStack's patch staging; PWYX gray / RGB:
+    stack_conv1_kernel's env blocks, then its conv1 tiles per env) pulling each env's frames
     from pinned host staging behind its ready word (edge cache lines read with system-scope loads):
     the stacked state == the A2 oracle (bit-exact), and the trunk outputs (conv activations + dense
     partial slabs) == mt_forward_trunk on that state, bit for bit."""
