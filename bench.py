@@ -469,6 +469,9 @@ def main():
     net = learner.network
     depth_ = 3 if cfg['rgb'] else 1
     stacking = getattr(learner, 'slot0_in_rollout', False)
+    # PWYX: the rollout steps' conv1 launch pulls + stacks each env (stack_conv1_kernel), so the in-loop
+    # trunk window includes the emulators: the roofline times the stacking trunk with every env published
+    frame_stack = not learner.lstm_bool and getattr(learner, 'frame_stack_in_rollout', False)
     # the update's train pass (fused returns + loss + backward of the last rollout)
     bwd = learner.train_backward if learner.lstm_bool else learner._update_backward
     prof['train_pass'] = graph_time(bwd, 20, label='train_pass')
@@ -496,7 +499,7 @@ def main():
         roll_fwd = lambda: net.forward(learner.states[0], E, out=(learner.v_boot, learner.pi_roll, learner.rep_roll),
                                        ws_key='rollout', infer=True)
         plain_trunk = lambda: net.forward_trunk(learner.states[0], E, ws_key='rollout')
-        if stacking:
+        if stacking or frame_stack:
             # the stacking rollout chain's kernels (the in-kernel-pull conv kernel + the dense
             # kernel) with every env's ready word already set and its pushes in HBM: nothing waits
             ready = torch.zeros(E, 32, dtype=torch.int32)  # MH_READY_STRIDE words per env
@@ -508,7 +511,7 @@ def main():
             roll_trunk = plain_trunk
     prof['rollout_forward'] = graph_time(roll_fwd, 20, label='rollout_forward')
     prof['rollout_trunk'] = graph_time(roll_trunk, 40, label='roofline')
-    if stacking:
+    if stacking or frame_stack:
         prof['plain_trunk'] = graph_time(plain_trunk, 40, label='plain_trunk')
     # the eager form (40 Python calls back to back between one event pair, BENCH_r02's method):
     # bounded by the host's launch rate when the box is loaded, kept to show the difference
@@ -565,7 +568,7 @@ def main():
         stack_bytes = (4 * ec - stack_pushes) * frame + stack_pushes * frame + 4 * ec * frame
         graph_note = ('hipGraph of back-to-back calls replayed 5 times between HIP event pairs on its stream '
                       '(bench.graph_time); median per call, dispatch gaps included')
-        if stacking:  # + the fused A2 stacking: the pushes read and the new state written
+        if stacking or frame_stack:  # + the fused A2 stacking: the pushes read and the new state written
             tk_bytes += stack_pushes * frame + 4 * ec * frame
             # the rollout chain's own kernels; in the loop each conv block also waits for its env's
             # emulator (in-kernel pull), so the roofline times them with every env published
@@ -574,10 +577,14 @@ def main():
                 kern = 'nips_conv_kernel<%d, true> (in-kernel pull) + nips_fc_kernel<%d>: the stacking rollout chain' % (
                     C_in, C_in)
                 pmc_kernels = ['nips_conv_kernel<%d, true>' % C_in, 'nips_fc_kernel<%d>' % C_in]
-            else:
+            elif cfg['arch'] == 'NATURE':
                 kern = ('nature_chain_kernel (stacking conv1 with in-kernel pull -> conv2 -> conv3, per-env hand-offs '
                         'in one launch) + row_fc_kernel (dense layer, one slab per conv row): the stacking rollout chain')
                 pmc_kernels = ['nature_chain_kernel', 'row_fc_kernel']
+            else:
+                kern = ('stack_conv1_kernel (per-env pull + stack blocks, then conv1 tiles per env) + conv2 .. conv4 '
+                        '(direct) + split-K dense: the stacking rollout chain')
+                pmc_kernels = None
             timing = ('mt_forward_trunk_stacking (every env published, its pushes in HBM: the kernels the timed loop '
                       'runs, with nothing to wait for), ' + graph_note)
         elif inloop_us is not None and not lstm:  # (LSTM: step 0's forward has 1 + 5E rows, the others E)
@@ -617,10 +624,11 @@ def main():
         kernels = [row('A2', 'atari_emulator.py:79-124, environment.py:58-80', 'preprocess_kernel (resized: stacking only)',
                        med(prof['stack']), stack_bytes,
                        note='standalone mt_preprocess_resized of the E envs (%d pushes); %s' % (stack_pushes, graph_note))]
-        if stacking:
+        if stacking or frame_stack:
             share = (med(prof['rollout_trunk']) - med(prof['plain_trunk']))
             kernels.append({'row': 'A2 (fused)', 'kernel': 'stacking share of %s' % (
-                                'nips_conv_kernel<%d, true>' % C_in if cfg['arch'] == 'NIPS' else 'nature_chain_kernel'),
+                                'nips_conv_kernel<%d, true>' % C_in if cfg['arch'] == 'NIPS' else
+                                'nature_chain_kernel' if cfg['arch'] == 'NATURE' else 'stack_conv1_kernel'),
                             'us': round(share, 2), 'note': 'stacking trunk minus the same trunk on a resident state '
                             '(mt_forward_trunk): the cost of the in-kernel stack in the benchmarked chain'})
         tl = prof['train_launches']
@@ -692,7 +700,7 @@ def main():
                 'note': 'event pair around each macro-step forward\'s trunk launches in the timed loop '
                         '(mt_rollout_trunk_timing, %d updates after the timed region)%s' % (
                             a.measure_updates, '; includes the conv blocks\' wait for their env\'s emulator '
-                            '(in-kernel pull)' if stacking else
+                            '(in-kernel pull)' if stacking or frame_stack else
                             '; LSTM: frame trunk + cell x-product, averaged over step 0 (1 + 5E rows), steps '
                             '1..T-1 and the bootstrap (E rows each)' if lstm else '')},
             'train_pass': {'bound': 'mfma', 'kernels': ('backward of %d windows over %d distinct frames (forward reused from the rollout)' % (N, 1 + (T + 4) * ec)) if lstm else 'fused returns + loss + backward of %d rows (forward reused from the rollout)' % N,

@@ -248,6 +248,9 @@ class PAACLearner(ActorLearner):
         # slot T over into slot 0 at the next step 0 (mt_rollout_step): the update does not copy it
         self.slot0_in_rollout = self.pipeline and self.staging == 'resized' and not self.lstm_bool and (
             self.network.arch == 'NIPS' or (self.network.arch == 'NATURE' and self.depth == 1))
+        # the frame trunks' rollout steps stack in their conv1 launch (stack_conv1_kernel; slot 0 still
+        # copied by the update)
+        self.frame_stack_in_rollout = self.pipeline and self.staging == 'resized' and self.network.arch in ('PWYX', 'LSTM')
         self._gs = C.c_int64(0)
 
     def _upload_pushes(self, total, out, prev):
