@@ -926,21 +926,23 @@ static int launch_nature_chain(const StackSrc &st, const float *W1, const float 
 }
 
 // ---- a frame trunk's rollout step: pull + stack + conv1 as one dataflow launch ----------------
-// (round 4; the LSTM and PWYX rollouts, gray or RGB) Blocks [0, E): one per env — wait for env e's
-// publication (StackSrc::ready), read its p pushes from the pinned staging (the edge lines of its
-// slot group system-scope, ld_published16), stack them onto the previous state (preprocess_kernel's
-// op: every state word = one colour channel's 4 frames, shifted by p bytes, the p new frame bytes
-// on top), store the new state with agent-scope stores, drain, count env e stacked. Blocks
-// [E, E + E * BPI): the trunk's conv1 tiles (DFwd, the same tiling and arithmetic as
-// conv_forward_direct), env-major and XCD-aware; a tile of env e polls env e's word, reads the
-// state with agent-scope loads (COH_IN) and runs the conv1 body: the step's conv1 runs while the
-// emulators still step later envs, instead of behind pull_frames_kernel -> preprocess_kernel ->
-// conv1 after the LAST env. Every env's word has its own 128-B line: with the words packed (16
-// envs a line) the ~1,300 polling tiles delayed the env blocks' increments and the launch ended
-// ~25 us after the last publication, no earlier than the layered conv1 (profiles/r04_ab).
-// Deadlock-free as nature_chain_kernel (a tile waits only for an env block, all lower-indexed;
-// bounded). sync = [tiles done][env e stacked: line 1 + e] (32-word lines); the last tile resets
-// every word for the next launch.
+// (round 4; the LSTM and PWYX rollouts, gray or RGB) Blocks [0, E * SPL): SPL per env (one 16-word
+// item per thread: 2 gray, 6 RGB) — wait for env e's publication (StackSrc::ready), read its p
+// pushes from the pinned staging (the edge lines of its slot group system-scope, ld_published16),
+// stack them onto the previous state (preprocess_kernel's op: every state word = one colour
+// channel's 4 frames, shifted by p bytes, the p new frame bytes on top), store the new state with
+// agent-scope stores, drain, count one part of env e stacked. Blocks [E * SPL, .. + E * BPI): the
+// trunk's conv1 tiles (DFwd, the same tiling and arithmetic as conv_forward_direct), env-major and
+// XCD-aware; a tile of env e polls env e's word until its SPL parts are in, reads the state with
+// agent-scope loads (COH_IN) and runs the conv1 body: the step's conv1 runs while the emulators
+// still step later envs, instead of behind pull_frames_kernel -> preprocess_kernel -> conv1 after
+// the LAST env. Every env's word has its own 128-B line: with the words packed (16 envs a line) the
+// ~1,300 polling tiles delayed the env blocks' increments and the launch ended ~25 us after the
+// last publication, no earlier than the layered conv1 (profiles/r04_ab). One block per env made
+// the last env's stack a serial ~20 us (RGB) after its publication: SPL blocks share it.
+// Deadlock-free as nature_chain_kernel (a tile waits only for stack blocks, all lower-indexed;
+// bounded). sync = [tiles done][env e: line 1 + e] (32-word lines); the last tile resets every word
+// for the next launch.
 template <class G>
 struct StackConv1 {
   using F = DConvFor<G, true>;
@@ -949,73 +951,59 @@ struct StackConv1 {
   static constexpr int DEPTH = G::CIN / 4;  // colour channels (1 gray, 3 RGB)
   static_assert(D::NT == 256 && (G::CIN == 4 || G::CIN == 12) && G::H == 84 && G::W == 84 && G::S == 1,
                 "84x84 conv1 of 4 stacked frames, 4 waves");
+  static constexpr int NI = 84 * 84 * DEPTH / 16;  // 16-word items per env: 441 gray, 1,323 RGB
+  static constexpr int SPL = (NI + 255) / 256;     // stack blocks per env
   static constexpr size_t LDS = D::LDS;
 };
 
-// env e's new state (84 x 84 x DEPTH words of 4 frames each): 16-word items (one 16-B chunk of
-// each push), 256 threads, PASS items per thread in flight
+// part `part` of env e's new state (84 x 84 x DEPTH words of 4 frames each): items part * 256 + tid,
+// a 16-word item = one 16-B chunk of each push
 template <int DEPTH>
-__device__ __forceinline__ void frame_pull_stack(const StackSrc &st, int e, uint32_t *sync) {
-  constexpr int NW = 84 * 84 * DEPTH, NI = NW / 16, IT = (NI + 255) / 256;  // 441 items gray, 1,323 RGB
-  constexpr int PASS = 2;
+__device__ __forceinline__ void frame_pull_stack(const StackSrc &st, int e, int part, uint32_t *sync) {
+  constexpr int NW = 84 * 84 * DEPTH, NI = NW / 16;
   static_assert(NW % 16 == 0, "whole 16-B frame chunks");
   const int tid = threadIdx.x;
+  const int i = part * 256 + tid;
+  const int ic = min(i, NI - 1);
   __shared__ int s_p;
+  // the previous state's item requested before the wait (its latency hides under it)
   const uint4 *prev = reinterpret_cast<const uint4 *>(st.prev + (size_t)e * NW * 4);
-  uint4 pv[PASS][4];
-  auto load_prev = [&](int it0) {
+  uint4 pv[4];
 #pragma unroll
-    for (int q = 0; q < PASS; ++q) {
-      const int i = min(tid + 256 * (it0 + q), NI - 1);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) pv[q][c] = prev[4 * i + c];
-    }
-  };
-  load_prev(0);  // (the first pass's previous state requested before the wait: its latency hides under it)
+  for (int c = 0; c < 4; ++c) pv[c] = prev[4 * ic + c];
   if (tid == 0) {
     const uint32_t tag = st.tag_base ? ((*st.tag_base + st.tag) & 0x1fffffffu) : st.tag;
     s_p = min(max(wait_published(st.ready, e, tag, st.status), 0), 4);  // (a timeout stacks no frame)
-    MT_PROBE_CHAIN(e, 0);
+    if (part == 0) MT_PROBE_CHAIN(e, 0);
   }
   __syncthreads();
   const int p = s_p;
   // push j of env e = frame slot 4e + j (NW bytes), its 16-B chunk i = state words 16 i .. 16 i + 15
   const size_t F = (size_t)NW, lo = 4 * (size_t)e * F, hi = lo + 4 * F;
-  uint32_t *out = reinterpret_cast<uint32_t *>(st.out + (size_t)e * NW * 4);
-  for (int it0 = 0; it0 < IT; it0 += PASS) {
-    if (it0 > 0) load_prev(it0);
-    uint4 fv[PASS][4];
+  uint4 fv[4];
 #pragma unroll
-    for (int q = 0; q < PASS; ++q) {
-      const int i = min(tid + 256 * (it0 + q), NI - 1);
+  for (int j = 0; j < 4; ++j)
+    fv[j] = j < p ? ld_published16(st.frames, ((size_t)4 * e + j) * F + 16 * (size_t)ic, lo, hi)
+                  : make_uint4(0u, 0u, 0u, 0u);
+  if (i < NI) {
+    uint32_t *out = reinterpret_cast<uint32_t *>(st.out + (size_t)e * NW * 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        fv[q][j] = j < p ? ld_published16(st.frames, ((size_t)4 * e + j) * F + 16 * (size_t)i, lo, hi)
-                         : make_uint4(0u, 0u, 0u, 0u);
-    }
+    for (int c = 0; c < 4; ++c) {  // words 16 i + 4 c .. + 3
+      const uint32_t wv[4] = {pv[c].x, pv[c].y, pv[c].z, pv[c].w};
+      uint32_t fw[4];
 #pragma unroll
-    for (int q = 0; q < PASS; ++q) {
-      const int i = tid + 256 * (it0 + q);
-      if (it0 + q >= IT || i >= NI) break;
+      for (int j = 0; j < 4; ++j) fw[j] = c == 0 ? fv[j].x : c == 1 ? fv[j].y : c == 2 ? fv[j].z : fv[j].w;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {  // words 16 i + 4 c .. + 3
-        const uint32_t wv[4] = {pv[q][c].x, pv[q][c].y, pv[q][c].z, pv[q][c].w};
-        uint32_t fw[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          fw[j] = c == 0 ? fv[q][j].x : c == 1 ? fv[q][j].y : c == 2 ? fv[q][j].z : fv[q][j].w;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          uint32_t v = p < 4 ? wv[k] >> (8 * p) : 0u;
-          for (int j = 0; j < p; ++j) v |= ((fw[j] >> (8 * k)) & 0xffu) << (8 * (4 - p + j));
-          __hip_atomic_store(out + 16 * (size_t)i + 4 * c + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+      for (int k = 0; k < 4; ++k) {
+        uint32_t v = p < 4 ? wv[k] >> (8 * p) : 0u;
+        for (int j = 0; j < p; ++j) v |= ((fw[j] >> (8 * k)) & 0xffu) << (8 * (4 - p + j));
+        __hip_atomic_store(out + 16 * (size_t)i + 4 * c + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's (sc1) state stores have completed
   __syncthreads();
-  if (tid == 0) {  // env e stacked (its own 128-B line: see stack_conv1_kernel)
+  if (tid == 0) {  // one part of env e stacked (its own 128-B line: see above)
     __hip_atomic_fetch_add(sync + 32 + 32 * e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     MT_PROBE_CHAIN(e, 1);
   }
@@ -1027,15 +1015,16 @@ __global__ __launch_bounds__(256) void stack_conv1_kernel(StackSrc st, typename 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using C = StackConv1<G>;
   using D = typename C::D;
-  if ((int)blockIdx.x < E) {
-    frame_pull_stack<C::DEPTH>(st, blockIdx.x, sync);
+  const int nstk = E * C::SPL;
+  if ((int)blockIdx.x < nstk) {
+    frame_pull_stack<C::DEPTH>(st, (int)blockIdx.x / C::SPL, (int)blockIdx.x % C::SPL, sync);
     return;
   }
-  const int t = xcd_tile((int)blockIdx.x - E, E * D::BPI), b = t / D::BPI;  // (an env's tiles on one XCD)
-  if (threadIdx.x == 0) {  // env b stacked (bounded wait, as chain_wait)
+  const int t = xcd_tile((int)blockIdx.x - nstk, E * D::BPI), b = t / D::BPI;  // (an env's tiles on one XCD)
+  if (threadIdx.x == 0) {  // env b's SPL parts stacked (bounded wait, as chain_wait)
     const uint32_t *w = sync + 32 + 32 * b;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)C::SPL) {
       __builtin_amdgcn_s_sleep(8);
       if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
         if (st.status) __hip_atomic_store(st.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1074,7 +1063,7 @@ static int launch_stack_conv1(const StackSrc &st, const float *W, float *Y, uint
     attr_set = true;
   }
   const typename C::P1 p1{st.out, W, W + G::KK * G::COUT, Y, arg, act, alpha};
-  hipLaunchKernelGGL(kern, dim3((unsigned)(E + E * C::D::BPI)), dim3(256), C::LDS, s, st, p1, sync, E);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(E * C::SPL + E * C::D::BPI)), dim3(256), C::LDS, s, st, p1, sync, E);
   MT_LAUNCHED();
   return MT_OK;
 }
