@@ -524,6 +524,44 @@ def test_stacking_trunk_in_kernel_pull(arch, E, depth):
     assert torch.equal(ws[:ws2.numel()], ws2)
 
 
+@pytest.mark.parametrize('arch,depth', [('NIPS', 1), ('NATURE', 1), ('PWYX', 3)])
+def test_stacking_trunk_unpublished_env_is_bounded(arch, depth):
+    """An env whose ready word never carries the launch's tag (an emulator that died): every wait
+    of the stacking chain is bounded (~2 s of s_memrealtime), so the launch drains instead of
+    hanging the GPU; the stalled env's new state is the previous one (no frame stacked, as
+    wait_published's timeout rule says) and every other env is stacked bit-exactly."""
+    import time
+    from manette_amd.network import host_device_pointer
+    import ctypes as C
+    E, stalled = 7, 3
+    net = _net(arch, depth, 6, 11, seed=3)
+    rs = np.random.RandomState(40 + depth)
+    counts = rs.randint(1, 5, E).astype(np.int32)
+    frames = torch.zeros(4 * E, 84, 84, depth, dtype=torch.uint8).pin_memory()
+    frames.numpy()[...] = rs.randint(0, 256, size=frames.shape).astype(np.uint8)
+    tag = 4242
+    ready = torch.zeros(E, 32, dtype=torch.int32).pin_memory()
+    ready.numpy()[:, 0] = (tag << 3) | counts
+    ready.numpy()[stalled, 0] = ((tag + 1) << 3) | counts[stalled]  # published for another launch
+    prev_h = rs.randint(0, 256, size=(E, 84, 84, 4 * depth)).astype(np.uint8)
+    prev = torch.from_numpy(prev_h).cuda()
+    out = torch.zeros_like(prev)
+    ws = net.workspace(E, 'stk_bounded')
+    ws.zero_()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    net.forward_trunk_stacking(prev, C.c_void_p(host_device_pointer(frames)), C.c_void_p(host_device_pointer(ready)),
+                               tag, out, E, ws_key='stk_bounded')
+    torch.cuda.synchronize()
+    assert time.time() - t0 < 30.0
+    got = out.cpu().numpy()
+    f = frames.numpy()
+    for e in range(E):
+        pushes = [] if e == stalled else [f[4 * e + j] for j in range(counts[e])]
+        want = prev_h[e] if e == stalled else preprocess.stack_update(prev_h[e], pushes, depth)
+        np.testing.assert_array_equal(got[e], want, err_msg='env %d' % e)
+
+
 def test_nips_backward_above_fused_cap():
     """Above kNipsFusedBwdMaxRows (1,280 rows) the NIPS gray conv backward takes the layered
     trunk_backward (per-image slabs would grow without bound): the gradient of 1,281 rows
