@@ -47,7 +47,9 @@ def load_pmc(config, kernels, name='pmc_trunk_%s.json'):
     """HBM bytes per roofline launch (the sum over its kernels of bytes per launch) from the
     committed PMC summary of this workload's roofline launch (profiles/pmc_trunk_<config>.json,
     written by tools/pmc_trunk.sh + tools/pmc_summary.py on tools/trunk_only.py: the same
-    kernels, grid and inputs bench.py times), or None when a kernel is missing from it."""
+    kernels, grid and inputs bench.py times), or None when a kernel is missing from it. A name
+    matches itself and its template instantiations, all of them summed (PWYX: conv2 .. conv4 are
+    three dconv_kernel<...> instantiations)."""
     if not kernels:
         return None
     path = os.path.join(ROOT, 'profiles', name % config)
@@ -60,7 +62,7 @@ def load_pmc(config, kernels, name='pmc_trunk_%s.json'):
         hit = [v for k, v in d.items() if name_of(k) == kern or name_of(k).startswith(kern + '<')]
         if not hit:
             return None
-        total += hit[0]['hbm_bytes']
+        total += sum(v['hbm_bytes'] for v in hit)
     return dict(hbm_bytes=total, source='profiles/' + name % config)
 
 
@@ -583,8 +585,8 @@ def main():
                 pmc_kernels = ['nature_chain_kernel', 'row_fc_kernel']
             else:
                 kern = ('stack_conv1_kernel (per-env pull + stack blocks, then conv1 tiles per env) + conv2 .. conv4 '
-                        '(direct) + split-K dense: the stacking rollout chain')
-                pmc_kernels = None
+                        '(dconv_kernel, direct) + row_fc_kernel (dense): the stacking rollout chain')
+                pmc_kernels = ['stack_conv1_kernel', 'dconv_kernel', 'row_fc_kernel']
             timing = ('mt_forward_trunk_stacking (every env published, its pushes in HBM: the kernels the timed loop '
                       'runs, with nothing to wait for), ' + graph_note)
         elif inloop_us is not None and not lstm:  # (LSTM: step 0's forward has 1 + 5E rows, the others E)

@@ -8,6 +8,6 @@ set -u
 TAG=${1:-meas}
 CPU_ALL=1 TAG=$TAG bash tools/bench_all.sh || exit $?
 bash tools/prof_all.sh $TAG || exit $?
-for c in ${PMC_CONFIGS:-breakout-nature-figar seaquest-nature}; do
+for c in ${PMC_CONFIGS:-breakout-nature-figar seaquest-nature breakout-pwyx-figar-rgb}; do
   bash tools/pmc_trunk.sh pmc_trunk_$c --config $c || exit $?
 done

@@ -1,6 +1,7 @@
 """The roofline launch alone (for rocprofv3 PMC / kernel-trace passes): bench.py's stacking trunk
 (mt_forward_trunk_stacking: nips_conv_kernel<C, true> in-kernel-pull form + nips_fc_kernel<C>, or
-for gray NATURE nature_chain_kernel + row_fc_kernel; every env published, pushes in HBM) at the workload's E, --reps launches back to back, random-init
+for gray NATURE nature_chain_kernel + row_fc_kernel; PWYX stack_conv1_kernel + conv2 .. conv4 +
+row_fc_kernel; every env published, pushes in HBM) at the workload's E, --reps launches back to back, random-init
 weights of the bench config.  python tools/trunk_only.py [--config pong-nips --reps 50]"""
 import argparse
 import os
@@ -21,7 +22,7 @@ def main():
     from manette_amd.network import DeviceNetwork
     from manette_amd.environment_creator import MINIMAL_ACTIONS
     cfg = bench.CONFIGS[a.config]
-    assert cfg['arch'] == 'NIPS' or (cfg['arch'] == 'NATURE' and not cfg['rgb'])
+    assert cfg['arch'] in ('NIPS', 'PWYX') or (cfg['arch'] == 'NATURE' and not cfg['rgb'])
     depth = 3 if cfg['rgb'] else 1
     E = cfg['ec']
     net = DeviceNetwork(dict(arch=cfg['arch'], rgb=cfg['rgb'], num_actions=MINIMAL_ACTIONS[cfg['game']],
