@@ -954,12 +954,16 @@ struct StackConv1 {
   static constexpr int NI = 84 * 84 * DEPTH / 16;  // 16-word items per env: 441 gray, 1,323 RGB
   static constexpr int SPL = (NI + 255) / 256;     // stack blocks per env
   static constexpr size_t LDS = D::LDS;
+  static_assert(LDS >= 256 * 17 * 4, "the stack blocks' word exchange fits the tiles' LDS");
 };
 
 // part `part` of env e's new state (84 x 84 x DEPTH words of 4 frames each): items part * 256 + tid,
-// a 16-word item = one 16-B chunk of each push
+// a 16-word item = one 16-B chunk of each push. The words go out through LDS (xs: 256 x 17 words)
+// so that each store instruction writes 256 consecutive words: a thread's own 16 words, stored
+// directly, put 4 B of every 64 B in each agent-scope store and wrote ~8x the state's bytes to HBM
+// (PMC WRITE_SIZE 30 MB per PWYX-RGB launch for a 2.7 MB state + 9 MB of conv1 output).
 template <int DEPTH>
-__device__ __forceinline__ void frame_pull_stack(const StackSrc &st, int e, int part, uint32_t *sync) {
+__device__ __forceinline__ void frame_pull_stack(const StackSrc &st, int e, int part, uint32_t *sync, uint32_t *xs) {
   constexpr int NW = 84 * 84 * DEPTH, NI = NW / 16;
   static_assert(NW % 16 == 0, "whole 16-B frame chunks");
   const int tid = threadIdx.x;
@@ -985,21 +989,27 @@ __device__ __forceinline__ void frame_pull_stack(const StackSrc &st, int e, int 
   for (int j = 0; j < 4; ++j)
     fv[j] = j < p ? ld_published16(st.frames, ((size_t)4 * e + j) * F + 16 * (size_t)ic, lo, hi)
                   : make_uint4(0u, 0u, 0u, 0u);
-  if (i < NI) {
-    uint32_t *out = reinterpret_cast<uint32_t *>(st.out + (size_t)e * NW * 4);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {  // words 16 i + 4 c .. + 3
-      const uint32_t wv[4] = {pv[c].x, pv[c].y, pv[c].z, pv[c].w};
-      uint32_t fw[4];
+  for (int c = 0; c < 4; ++c) {  // words 16 i + 4 c .. + 3 -> xs[tid * 17 + 4 c + k] (stride 17: no bank conflicts)
+    const uint32_t wv[4] = {pv[c].x, pv[c].y, pv[c].z, pv[c].w};
+    uint32_t fw[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fw[j] = c == 0 ? fv[j].x : c == 1 ? fv[j].y : c == 2 ? fv[j].z : fv[j].w;
+    for (int j = 0; j < 4; ++j) fw[j] = c == 0 ? fv[j].x : c == 1 ? fv[j].y : c == 2 ? fv[j].z : fv[j].w;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint32_t v = p < 4 ? wv[k] >> (8 * p) : 0u;
-        for (int j = 0; j < p; ++j) v |= ((fw[j] >> (8 * k)) & 0xffu) << (8 * (4 - p + j));
-        __hip_atomic_store(out + 16 * (size_t)i + 4 * c + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    for (int k = 0; k < 4; ++k) {
+      uint32_t v = p < 4 ? wv[k] >> (8 * p) : 0u;
+      for (int j = 0; j < p; ++j) v |= ((fw[j] >> (8 * k)) & 0xffu) << (8 * (4 - p + j));
+      xs[tid * 17 + 4 * c + k] = v;
     }
+  }
+  __syncthreads();
+  // word w = 256 q + tid of the part (item w / 16, word w % 16): one coalesced agent-scope store per q
+  uint32_t *out = reinterpret_cast<uint32_t *>(st.out + (size_t)e * NW * 4) + 16 * (size_t)(part * 256);
+  const int nw = 16 * min(256, NI - part * 256);  // the part's words
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int w = 256 * q + tid;
+    if (w < nw) __hip_atomic_store(out + w, xs[(w >> 4) * 17 + (w & 15)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's (sc1) state stores have completed
   __syncthreads();
@@ -1017,7 +1027,8 @@ __global__ __launch_bounds__(256) void stack_conv1_kernel(StackSrc st, typename 
   using D = typename C::D;
   const int nstk = E * C::SPL;
   if ((int)blockIdx.x < nstk) {
-    frame_pull_stack<C::DEPTH>(st, (int)blockIdx.x / C::SPL, (int)blockIdx.x % C::SPL, sync);
+    frame_pull_stack<C::DEPTH>(st, (int)blockIdx.x / C::SPL, (int)blockIdx.x % C::SPL, sync,
+                               reinterpret_cast<uint32_t *>(smem));
     return;
   }
   const int t = xcd_tile((int)blockIdx.x - nstk, E * D::BPI), b = t / D::BPI;  // (an env's tiles on one XCD)
