@@ -12,6 +12,7 @@ Workload (N=1 default): BASELINE.json configs[1], Pong NIPS ec=32 ew=8 t_max=5, 
 """
 import argparse
 import json
+import re
 import os
 import shutil
 import sys
@@ -56,6 +57,10 @@ def load_pmc(config, kernels, name='pmc_trunk_%s.json'):
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
+    if kernels == '*':  # every kernel of the roofline launch (the profiled program runs nothing else but
+        # torch's allocation fills and copies)
+        kernels = sorted({re.sub(r'^void ', '', k).split('<')[0] for k in d
+                          if not k.startswith('__amd') and 'at::native' not in k})
     total = 0
     for kern in kernels:
         name_of = lambda k: k.replace('void ', '')
@@ -369,6 +374,13 @@ def main():
     ap.add_argument('--comm', default='rccl', choices=['rccl', 'torch'],
                     help='data-parallel gradient all-reduce (torch: torch.distributed on gloo — a rehearsal of the '
                          'N > 1 path on one GPU with MT_BENCH_SHARED_GPU=1, every rank on cuda:0)')
+    ap.add_argument('--dp_force', action='store_true',
+                    help='the data-parallel update at world 1 (RCCL communicator, bucketed side-stream all-reduce '
+                         'between three update graphs, the learner launching the update): the per-GPU cost of the '
+                         'N-GPU path (paac.PAACLearner.dp)')
+    ap.add_argument('--settle_s', type=float, default=1.0,
+                    help='seconds of untimed updates before the warmup steps (host emulator threads, CPU clocks and '
+                         'the graphs reach their steady state; the 5-update warmup of a 20-update run did not)')
     ap.add_argument('--trunk_sweep', default='256,1024,4096',
                     help='extra batch sizes the trunk kernel is timed at after the run ("" = none)')
     a = ap.parse_args()
@@ -384,8 +396,9 @@ def main():
     cfg = CONFIGS[a.config]
     T = a.t_max
     learner, args = make_learner(a.config, T, a.sampling, a.seed, a.staging, a.pipeline, a.update_graph, rank,
-                                 comm=a.comm)
+                                 comm=a.comm, dp_force=a.dp_force)
     learner.start()
+    learner_dp = learner.dp
     if a.step_impl == 'python' and learner.native_step is not None:
         from manette_amd import _lib
         _lib.hip().mt_rollout_destroy(learner.native_step)
@@ -396,37 +409,62 @@ def main():
         learner.rollout()
         learner.update()
 
+    # settle: untimed updates for --settle_s seconds (every rank the same count, rank 0's), so the
+    # W warmup steps and the K timed ones start from the steady state; the graphs are captured and
+    # registered within the first 3 updates, the rest is the host side (emulator threads' caches and
+    # clocks) — a 5-update warmup left the r04 driver run ramping 603k -> 713k over its 20 updates
+    settle = 0
+    if a.settle_s > 0:
+        t_s = time.perf_counter()
+        while time.perf_counter() - t_s < a.settle_s and settle < 5000:
+            one_update()
+            settle += 1
+        if world > 1:
+            n_s = torch.tensor([settle], dtype=torch.int64)
+            dist.broadcast(n_s, 0)
+            for _ in range(int(n_s.item()) - settle):
+                one_update()
+            settle = int(n_s.item())
     for _ in range(a.warmup):
         one_update()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     stats = None
+    phase_names = ['launch_and_wait_us', 'emulators_us', 'bookkeeping_us', 'upload_enqueue_us']
     if learner.native_step is not None:
         import ctypes as C
         from manette_amd import _lib
         stats = (C.c_double * 7)()
         _lib.hip().mt_rollout_stats_ex(learner.native_step, stats, 7, 1)
+    w = max(1, a.steps // 4)  # sub-windows of the timed region
+    win_stats = []  # per sub-window: the host phases of its macro-steps (read + reset at its end)
     t0 = time.perf_counter()
     marks = []  # host clock after each update: the value of sub-windows of the timed region
-    for _ in range(a.steps):
+    for k in range(a.steps):
         one_update()
         marks.append(time.perf_counter())
+        if stats is not None and (k + 1) % w == 0:
+            _lib.hip().mt_rollout_stats_ex(learner.native_step, stats, 7, 1)
+            win_stats.append(list(stats))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if stats is not None:
         _lib.hip().mt_rollout_stats_ex(learner.native_step, stats, 7, 0)
-        n = max(stats[4], 1)
-        step_phases = {k: round(stats[i] / n, 2) for i, k in enumerate(
-            ['launch_and_wait_us', 'emulators_us', 'bookkeeping_us', 'upload_enqueue_us'])}
+        tot = [sum(ws_[i] for ws_ in win_stats) + stats[i] for i in range(7)]
+        n = max(tot[4], 1)
+        step_phases = {k: round(tot[i] / n, 2) for i, k in enumerate(phase_names)}
         # launch_and_wait = host launches (this step's forward if not armed + the chains armed
         # ahead) + the spin for this step's sampled indices
-        step_phases['of_which_enqueue_us'] = round(stats[5] / n, 2)
-        step_phases['of_which_wait_us'] = round(stats[6] / n, 2)
+        step_phases['of_which_enqueue_us'] = round(tot[5] / n, 2)
+        step_phases['of_which_wait_us'] = round(tot[6] / n, 2)
+        window_phases = [{k: round(ws_[i] / max(ws_[4], 1), 2) for i, k in enumerate(phase_names[:2])}
+                         for ws_ in win_stats]
     else:
         step_phases = None
+        window_phases = None
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -599,7 +637,7 @@ def main():
             tk_ms = iso_ms
             kern = 'mt_forward_trunk (%s)' % ('LSTM frame trunk + cell x-product' if lstm else 'layered')
             timing = 'isolated mt_forward_trunk, ' + graph_note
-            pmc_kernels = None
+            pmc_kernels = '*' if lstm else None  # (LSTM: tools/trunk_only.py runs exactly this launch)
         tk_gbs = tk_bytes / (tk_ms * 1e-3) / 1e9
         tk_tf = tk_flops / (tk_ms * 1e-3) / 1e12
         pmc = load_pmc(a.config, pmc_kernels)
@@ -661,7 +699,6 @@ def main():
                            28 * P_ + 4 * 512 + 4, note='%d params: w, ms, mom, g read (16 B) and w, ms, mom written '
                            '(12 B) per parameter; ' % P_ + graph_note))
         # the timed region in sub-windows (host clock after each update)
-        w = max(1, a.steps // 4)
         edges = [t0] + marks
         wins = [world * ec * T * w / (edges[i + w] - edges[i]) for i in range(0, a.steps - w + 1, w)]
         line = {
@@ -680,9 +717,12 @@ def main():
                     'emulator threads pool + resize each push to 84x84, the GPU stacks the 4-frame states and runs '
                     'forward, sampling, returns, backward and RMSProp; random-init weights. The emulators are '
                     'near-free, so this is an upper bound for real ALE games (learner_only isolates the GPU side)',
-            'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step, %s staging%s' % (
-                a.config, ec, cfg['ew'], T, a.sampling, a.step_impl, a.staging, ', pipelined' if a.pipeline else ''), 'arch': cfg['arch'], 'emulators_per_gpu': ec,
-                'global_emulators': ec * world, 'parallelism': 'dp%d' % world},
+            'config': {'workload': '%s ec=%d ew=%d t_max=%d per GPU, %s sampling, %s step, %s staging%s%s' % (
+                a.config, ec, cfg['ew'], T, a.sampling, a.step_impl, a.staging, ', pipelined' if a.pipeline else '',
+                ', data-parallel update forced at world 1 (RCCL)' if a.dp_force and world == 1 else ''),
+                'arch': cfg['arch'], 'emulators_per_gpu': ec,
+                'global_emulators': ec * world, 'parallelism': 'dp%d' % world,
+                'dp_update': bool(learner_dp), 'settle_updates': settle},
             # bound = the resource the trunk's arithmetic intensity binds on the roofline (fp32 ridge
             # 157.3 TFLOP/s / 8 TB/s = 19.7 FLOP/B; NIPS E=32: 52 FLOP/B -> mfma); both fractions kept
             'roofline': dict(
@@ -724,8 +764,11 @@ def main():
                                 'hbm_frac': round(fwd_bytes / (rf_ms * 1e-3) / 1e9 / MI355X_HBM_GBS, 4)},
             'value_windows': {'updates_per_window': w, 'values': [round(v, 1) for v in wins],
                               'spread': round((max(wins) - min(wins)) / float(np.median(wins)), 4),
+                              'host_phases_us': window_phases,
                               'note': 'env-steps/s of consecutive sub-windows of the timed region (host clock after '
-                                      'each update; the rollout waits on the device every macro-step)'},
+                                      'each update; the rollout waits on the device every macro-step), with each '
+                                      'window\'s per-macro-step host phases (launch_and_wait = the GPU chain as the '
+                                      'host sees it, emulators = the emulator threads)'},
         }
         if replicas is not None:
             line['replicas_identical'] = replicas

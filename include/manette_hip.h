@@ -77,8 +77,9 @@ int mt_net_var_info(const mt_net *net, int i, char *name, int name_len, int64_t 
 int mt_net_feature_dim(const mt_net *net, int *f); /* width of the trunk output (256/512/...) */
 int mt_net_get_config(const mt_net *net, mt_net_config *cfg);
 /* Bytes of device workspace a forward/backward on `batch` rows needs. Zero-fill a workspace once
- * when it is allocated: the gray NATURE stacking chain keeps per-env hand-off counters in it, which
- * every launch leaves at zero again. */
+ * when it is allocated: the stacking chains keep per-env hand-off counters in it — the gray NATURE
+ * chain (nature_chain_kernel) and the PWYX stacking conv1 launch, gray or RGB (stack_conv1_kernel) —
+ * which every launch leaves at zero again, a launch whose bounded waits timed out included. */
 int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes);
 /* Diagnostics / parity: where a workspace keeps a forward value the backward branches on — kind 0:
  * conv layer `layer`'s stored output, post-activation ([rows][OH][OW][COUT] fp32; a pooled layer's
@@ -86,7 +87,8 @@ int mt_net_workspace_bytes(const mt_net *net, int batch, size_t *bytes);
  * max-pool argmax bytes ([rows][OH/2][OW/2][COUT] uint8, the window position 0..3 of the first
  * maximum in (row, col) order that the backward routes the gradient to, TF MaxPoolGrad); kind 2:
  * the dense layer's output H ([rows][F] fp32); kind 3: the gradient of conv layer `layer`'s output
- * after a backward ([rows][OH][OW][COUT] fp32, full resolution). Byte offset and size. layout 0 = the workspace of
+ * after a backward ([rows][OH][OW][COUT] fp32, full resolution); kind 4: the stacking chains' hand-off
+ * counters (uint32 words, zero between launches; empty for an arch without them). Byte offset and size. layout 0 = the workspace of
  * mt_forward / mt_forward_rows on a = batch rows; layout 1 = the LSTM frame-store workspace of
  * (E = a, T = b), conv rows = fstore rows, H rows = the (T+1)E windows; layout 2 = the LSTM
  * mt_forward workspace of a windows, conv rows = window frames (window-major, 5 per window). */
@@ -138,10 +140,13 @@ int mt_forward_trunk(const mt_net *net, const float *params, const uint8_t *obs,
  * conv2 -> conv3, per-env hand-offs in one launch) + the split-K dense GEMM; PWYX (gray or RGB):
  * stack_conv1_kernel (per-env pull + stack blocks, then conv1 tiles per env) + conv2 .. + the dense
  * GEMM. With every ready word already set nothing waits: the kernels' own duration.
+ * Every device wait is bounded (~2 s): a wait that times out stores 1 into *status (a device-visible
+ * word, e.g. mapped pinned memory; may be NULL) and the launch drains (an env never published keeps
+ * its previous state); the caller reads *status after the stream has completed.
  * MT_ERR_UNSUPPORTED for the other archs (the LSTM steps stack in mt_rollout_step). */
 int mt_forward_trunk_stacking(const mt_net *net, const float *params, const uint8_t *prev, const uint8_t *frames,
                               const uint32_t *ready, uint32_t tag, uint8_t *out, int batch, void *ws, size_t ws_bytes,
-                              mt_stream_t stream);
+                              uint32_t *status, mt_stream_t stream);
 
 /* ---- LSTM frame-store mode (the learner's LSTM path; manette_amd/csrc/lstm.h) -------------
  * The reference feeds each step's memory window [E][5][84][84][C] (paac.py:79-83) and the train

@@ -220,67 +220,6 @@ struct DFwdStack : DFwd<G, true, false, false, COH_OUT> {
   }
 };
 
-// dX of the VALID conv G by stride phases as ONE stride-1 direct conv (round 4): input pixel
-// (S qy + py, S qx + px) of phase (py, px) receives sum_{j, i < KJ} dY[qy - j][qx - i] .
-// W[py + S j][px + S i] (KJ = KH / S taps per axis). Over the phase grid q (H/S x W/S) that is a
-// stride-1 conv of dY, zero-padded KJ - 1 on each side, with a KJ x KJ kernel whose S*S*CIN output
-// channels are the phases' dX channels: n = (py S + px) CIN + ci, W'[kyp][kxp][co][n] =
-// W[py + S (KJ-1-kyp)][px + S (KJ-1-kxp)][ci][co] — so every phase reads the SAME dY patch from
-// LDS (the generic phase GEMM gathers it once per phase), and only the weights differ per output
-// channel. Its staging reads 4 consecutive co of one (tap, ci): one 16-byte load. The epilogue
-// masks by the activation derivative of X (G's input = the previous layer's output, EpMasked's
-// rule) and scatters phase pixel (qy, qx) of channel n to dX[S qy + py][S qx + px][ci].
-template <class G>
-struct DBwdStrided {
-  static constexpr int KJ = G::KH / G::S;
-  static_assert(!G::SAME && G::KH == G::KW && G::H == G::W && G::KH % G::S == 0 && G::H % G::S == 0 &&
-                    G::H / G::S == G::OH + KJ - 1 && (KJ * KJ * G::COUT) % 16 == 0,
-                "phase-separable VALID conv");
-  static constexpr int CI = G::COUT, CO = G::S * G::S * G::CIN, KH = KJ, KW = KJ;
-  static constexpr int PT = KJ - 1, PL = KJ - 1, S = 1;
-  static constexpr int H = G::OH, W = G::OW, OH = G::H / G::S, OW = G::W / G::S, KK = KJ * KJ * G::COUT;
-  static constexpr bool POOL = false;
-  using InT = float;
-  const float *X;     // dY [B][OH_G][OW_G][COUT]
-  const float *Wt;    // W of G (HWIO)
-  const float *Xact;  // G's input [B][H_G][W_G][CIN] (post-activation: the mask)
-  float *dX;          // [B][H_G][W_G][CIN]
-  int act;
-  float alpha;
-  __device__ __forceinline__ f32x4 load4(const float *q) const { return *reinterpret_cast<const f32x4 *>(q); }
-  __device__ __forceinline__ f32x4 wquad(int k, int n) const {  // W'(k .. k+3, n): 4 co of one tap
-    const int t = k / CI, c = k - t * CI;
-    const int kyp = t / KJ, kxp = t - kyp * KJ;
-    const int ph = n / G::CIN, ci = n - ph * G::CIN;
-    const int py = ph / G::S, px = ph - py * G::S;
-    const int ky = py + G::S * (KJ - 1 - kyp), kx = px + G::S * (KJ - 1 - kxp);
-    return *reinterpret_cast<const f32x4 *>(Wt + (((size_t)ky * G::KW + kx) * G::CIN + ci) * G::COUT + c);
-  }
-  // dX element of phase pixel q (< OH * OW) of channel n
-  __device__ __forceinline__ size_t index(int b, int q, int n) const {
-    const int ph = n / G::CIN, ci = n - ph * G::CIN;
-    const int py = ph / G::S, px = ph - py * G::S;
-    const int qy = q / OW, qx = q - qy * OW;
-    return (((size_t)b * G::H + G::S * qy + py) * G::W + G::S * qx + px) * G::CIN + ci;
-  }
-  struct Pre {
-    float y[4];
-  };
-  __device__ __forceinline__ Pre pre(int b, int u, int n) const {
-    Pre r;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) r.y[q] = Xact[index(b, min(4 * u + q, OH * OW - 1), n)];
-    return r;
-  }
-  __device__ __forceinline__ void store(const Pre &pr, int b, int u, int n, f32x4 v) const {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int px = 4 * u + q;
-      if (px < OH * OW) dX[index(b, px, n)] = v[q] * act_bwd(pr.y[q], act, alpha);
-    }
-  }
-};
-
 // problems with their own patch staging (DFwdStack)
 template <class P, class = void>
 struct HasStagePatch : std::false_type {};
@@ -867,10 +806,14 @@ __device__ __forceinline__ void nature_conv_roles(const typename NC::P1 &p1, con
     __syncthreads();
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(c + NC::C3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)D3::BPI - 1) {
-      // env e's last block: every block of env e is past its wait — reset for the next launch
+      // env e's last conv3 block: reset env e's counters for the next launch. Every block adds to its
+      // counter exactly once, timed out or not, so the conv1 / conv2 counters are reset by subtracting
+      // their full counts rather than stored to zero: after a bounded wait timed out, a producer may
+      // still add AFTER this point (its consumer stopped waiting first), and the word must still read
+      // zero once the launch has drained. (C3's adds are all in: this block is the last.)
       MT_PROBE_CHAIN(e, 3);
-      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(c + NC::C2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_sub(c, (uint32_t)D1::BPI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_sub(c + NC::C2, (uint32_t)D2::BPI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c + NC::C3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -1048,9 +991,13 @@ __global__ __launch_bounds__(256) void stack_conv1_kernel(StackSrc st, typename 
   __syncthreads();
   if (threadIdx.x == 0 &&
       __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(E * D::BPI) - 1) {
-    // the last tile: every tile is past its wait — reset the words for the next launch
+    // the last tile: reset the words for the next launch. The env words by subtracting SPL (each
+    // stack block adds once): a stack block whose publication wait timed out may add after its tiles
+    // stopped waiting, i.e. after this point, and the word must still read zero once the launch has
+    // drained
     __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int k = 0; k < E; ++k) __hip_atomic_store(sync + 32 + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < E; ++k)
+      __hip_atomic_fetch_sub(sync + 32 + 32 * k, (uint32_t)C::SPL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1095,24 +1042,6 @@ static int conv_dgrad_unpool_solo(const float *dY, const float *Wt, const float 
                                   int B, int act, float alpha, hipStream_t s) {
   return launch_dconv<DBwdUnpool<G, GJ>, 4, 2, (G::COUT >= 64 ? 1 : 2), G::COUT>(
       DBwdUnpool<G, GJ>{dY, Wt, Pj, argj, dactj, act, alpha}, B, s);
-}
-
-// dX of a phase-separable VALID conv (NATURE conv2 / conv3) as its own 8-wave direct-conv launch
-// ahead of the layer's weight-gradient group (DBwdStrided). Tiles: 4 N-tiles per wave row (2 wave
-// rows); conv2 (128 phase channels) 2 M-tiles per wave = 2 blocks per image, conv3 (64) 3 = 1.
-// Measured (round 4, E = 64): conv3 dX 32.4 + dW 18.0 us vs 43.5 for the generic group, conv2 dX
-// 42.0 + dW 27.6 vs 51.2 — the 8-wave blocks (92 / 66 KB of LDS) leave 1-2 blocks per CU over a
-// grid of 320-640: off until the tiling is redone.
-template <class G>
-constexpr bool dconv_bwd_strided() {
-  return false;
-}
-template <class G>
-static int conv_dgrad_strided_solo(const float *dY, const float *Wt, const float *Xact, float *dX, int B, int act,
-                                   float alpha, hipStream_t s) {
-  using Pr = DBwdStrided<G>;
-  constexpr int TMW = G::S > 1 ? 2 : 3;
-  return launch_dconv<Pr, 2, 4, TMW, Pr::CI>(Pr{dY, Wt, Xact, dX, act, alpha}, B, s);
 }
 
 // ---- weight gradient ---------------------------------------------------------------------------

@@ -212,7 +212,7 @@ struct WsLayout {
   // parg = its window argmax bytes (pooled layers: the conv epilogue pools, EpBiasActPool), dact =
   // the gradient of the conv output (pre-activation after masking; full resolution)
   size_t act[4], pool[4], parg[4], dact[4], fcslab, H, dz, dH, wslab, wslab2, total;
-  size_t sync;  // gray NATURE: nature_chain_kernel's per-env counters (u32, zero between launches)
+  size_t sync;  // the stacking chains' counters (nature_chain_kernel, stack_conv1_kernel; u32, zero between launches)
   int fc_splits;
 };
 
@@ -1121,10 +1121,6 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
                                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act,
                                                            al),
                           wg.gemm, pending, extra));
-    } else if constexpr (dconv_bwd_strided<G>()) {  // direct phase dX launch (dconv.h DBwdStrided), then dW
-      MT_TRY((conv_dgrad_strided_solo<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B, act,
-                                         al, s)));
-      MT_TRY(launch_group(s, wg.gemm, pending, extra));
     } else {
       MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
                                                act, al),
@@ -1276,14 +1272,14 @@ static int forward_boot_impl(const mt_net *n, const float *P, const uint8_t *obs
     return launch_nips_trunk<C>(obs, st, B, P + n->off_conv[0], P + n->off_conv[1], Wfc, n->cfg.activation,
                                 n->cfg.alpha_leaky, ws + L.act[1], nullptr, ws + L.fcslab, s, advance, advance_by);
   } else {
+    if (advance && Ar::FC_ROWS == 0) {  // (refused before anything is enqueued)
+      set_error("sequence-base advance: row-split dense layers only");
+      return MT_ERR_UNSUPPORTED;
+    }
     FwdExtras ex;
     ex.st = st;
     ex.sync = reinterpret_cast<uint32_t *>(ws + L.sync);
     MT_TRY((trunk_forward<Ar>(n, P, obs, B, ws, L, s, ex)));
-    if (advance && Ar::FC_ROWS == 0) {
-      set_error("sequence-base advance: row-split dense layers only");
-      return MT_ERR_UNSUPPORTED;
-    }
     return launch_fc<Ar>(layer_out<Ar, Ar::NCONV - 1>(ws, L), B, Wfc, ws + L.fcslab, L.fc_splits, s, advance,
                          advance_by);
   }
@@ -1504,9 +1500,16 @@ extern "C" int mt_net_backward_bucket_launches(const mt_net *net, int *launches)
 // Byte range of a stored forward value in a workspace (diagnostics / parity; mt_net_workspace_region):
 // kind 0 = conv layer `layer`'s stored output (post-activation; the pooled map of a pooled layer),
 // kind 1 = a pooled layer's argmax bytes, kind 2 = the dense layer's post-activation output H,
-// kind 3 = the conv output's gradient (the backward's dY of the layer's weight gradient).
+// kind 3 = the conv output's gradient (the backward's dY of the layer's weight gradient),
+// kind 4 = the stacking chains' hand-off counters (uint32 words, zero between launches; 0 bytes when
+// the arch keeps none).
 template <class Ar, int I = 0>
 static int ws_region(const WsLayout &L, int kind, int layer, size_t rows, size_t *offset, size_t *bytes) {
+  if (kind == 4) {
+    *offset = L.sync * sizeof(float);
+    *bytes = (L.total - L.sync) * sizeof(float);
+    return MT_OK;
+  }
   if (kind == 2) {
     *offset = L.H * sizeof(float);
     *bytes = rows * Ar::F * sizeof(float);
@@ -1554,7 +1557,8 @@ static int ws_region_frames(const mt_net *net, int E, int T, int kind, int layer
 extern "C" int mt_net_workspace_region(const mt_net *net, int layout, int a, int b, int kind, int layer,
                                        size_t *offset, size_t *bytes) {
   MT_CHECK_ARG(net && offset && bytes, "null argument");
-  MT_CHECK_ARG(a >= 1 && (layout != 1 || b >= 1) && kind >= 0 && kind <= 3, "bad sizes or kind");
+  MT_CHECK_ARG(a >= 1 && (layout != 1 || b >= 1) && kind >= 0 && kind <= 4, "bad sizes or kind");
+  MT_CHECK_ARG(kind != 4 || layout == 0, "the counter region (kind 4) is in the layout-0 workspace");
   MT_ARCH_SWITCH(net, {
     if (layout == 0) {
       if constexpr (Ar::LSTM) {
@@ -1635,12 +1639,14 @@ extern "C" int mt_forward_trunk(const mt_net *net, const float *params, const ui
 
 extern "C" int mt_forward_trunk_stacking(const mt_net *net, const float *params, const uint8_t *prev,
                                          const uint8_t *frames, const uint32_t *ready, uint32_t tag, uint8_t *out,
-                                         int batch, void *ws, size_t ws_bytes, mt_stream_t stream) {
+                                         int batch, void *ws, size_t ws_bytes, uint32_t *status,
+                                         mt_stream_t stream) {
   MT_CHECK_ARG(net && params && prev && frames && ready && out && ws, "null argument");
   MT_CHECK_ARG(batch >= 1, "batch must be >= 1");
   StackSrc st{prev, frames, nullptr, out};
   st.ready = ready;
   st.tag = tag & 0x1fffffffu;
+  st.status = status;
   MT_ARCH_SWITCH(net, {
     const WsLayout L = ws_layout<Ar>(net, batch);
     if (ws_bytes < L.total * sizeof(float)) {

@@ -492,6 +492,7 @@ __global__ __launch_bounds__(256) void row_fc_kernel(const float *__restrict__ x
 template <int FEAT, int ROWS, int F>
 static inline int launch_row_fc(const float *x, int B, const float *Wfc, float *slabs, hipStream_t s,
                                 uint32_t *advance = nullptr, uint32_t advance_by = 0) {
+  if (B <= 0 || !launch_allowed()) return MT_OK;
   hipLaunchKernelGGL((row_fc_kernel<FEAT, ROWS, F>), dim3(F / kRowFcBN, ROWS, (B + kRowFcBM - 1) / kRowFcBM),
                      dim3(256), 0, s, x, B, Wfc, slabs, advance, advance_by);
   MT_LAUNCHED();

@@ -23,6 +23,23 @@ def _stream():
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+class WaitStatus(object):
+    """The word a bounded device wait sets when it times out (pinned, device-mapped: the kernels
+    store 1 with system scope and carry on, so the launch drains). check() — after the stream has
+    completed — surfaces a timeout as an MTError, as mt_rollout_step does for the rollout's own word,
+    and re-arms the word."""
+
+    def __init__(self):
+        self.word = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self.dev = host_device_pointer(self.word)
+
+    def check(self, what='device wait'):
+        if int(self.word[0]) != 0:
+            self.word[0] = 0
+            raise _lib.MTError('%s: a bounded device wait timed out (a producer never published within ~2 s)'
+                               % what)
+
+
 class DeviceNetwork(object):
     """network_conf of train.py:52-63 -> device parameters + forward / backward / update."""
 
@@ -205,13 +222,15 @@ class DeviceNetwork(object):
         check(_lib.hip().mt_forward_trunk(self._h, _ptr(self.params), _ptr(obs), int(batch), _ptr(ws), ws.numel(),
                                           _stream()), 'mt_forward_trunk')
 
-    def forward_trunk_stacking(self, prev, frames, ready, tag, out, batch, ws_key=None):
+    def forward_trunk_stacking(self, prev, frames, ready, tag, out, batch, ws_key=None, status=None):
         """mt_forward_trunk_stacking: the rollout chain's stacking trunk (in-kernel pull of each
-        env's frames behind its ready word), diagnostics / parity / roofline timing."""
+        env's frames behind its ready word), diagnostics / parity / roofline timing. status: a
+        WaitStatus whose word a timed-out device wait sets (check it once the stream completed)."""
         ws = self.workspace(batch, ws_key)
         addr = lambda x: x if isinstance(x, C.c_void_p) else _ptr(x)
         check(_lib.hip().mt_forward_trunk_stacking(self._h, _ptr(self.params), _ptr(prev), addr(frames), addr(ready),
                                                    C.c_uint32(tag), _ptr(out), int(batch), _ptr(ws), ws.numel(),
+                                                   C.c_void_p(status.dev) if status is not None else None,
                                                    _stream()), 'mt_forward_trunk_stacking')
         return ws
 

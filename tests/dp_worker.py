@@ -23,22 +23,23 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-ENVS = 16
+ENVS = {'NIPS': 16, 'LSTM': 8}  # global envs of the job per arch
 UPDATES = 4
 
 
-def _learner(out_dir, rank, world, comm='torch'):
+def _learner(out_dir, rank, world, comm='torch', arch='NIPS'):
     import train as cli
     from manette_amd.exploration_policy import ExplorationPolicy
     from manette_amd.paac import PAACLearner
     from manette_amd.synthetic import SyntheticBank
     a = cli.get_arg_parser().parse_args([])
-    ec = ENVS // world
-    a.game, a.arch, a.emulator_counts, a.emulator_workers = 'breakout', 'NIPS', ec, 2
+    ec = ENVS[arch] // world
+    a.game = 'breakout' if arch == 'NIPS' else 'ms_pacman'  # (configs[4]: MsPacman LSTM + FiGAR10)
+    a.arch, a.emulator_counts, a.emulator_workers = arch, ec, 2
     a.max_repetition, a.nb_choices = 10, 11
     a.runner, a.sampling, a.seed, a.staging, a.pipeline = 'native', 'device', 0, 'resized', True
     a.comm = comm
-    a.debugging_folder = os.path.join(out_dir, 'w%d_r%d' % (world, rank)) + '/'
+    a.debugging_folder = os.path.join(out_dir, '%s_w%d_r%d' % (arch, world, rank)) + '/'
     a.max_global_steps = 1 << 40
     a.checkpoint_interval = 1 << 40
     a.env_id_offset = rank * ec
@@ -52,9 +53,9 @@ def _learner(out_dir, rank, world, comm='torch'):
     return L
 
 
-def gpu_rank(out_dir, rank, world):
-    L = _learner(out_dir, rank, world)
-    rec = dict(params=[], states=[], gs=[])
+def gpu_rank(out_dir, rank, world, arch='NIPS'):
+    L = _learner(out_dir, rank, world, arch=arch)
+    rec = dict(params=[], states=[], gs=[], nz=[])
     params0 = L.network.params.cpu().numpy().copy()
     try:
         for _ in range(UPDATES):
@@ -65,12 +66,17 @@ def gpu_rank(out_dir, rank, world):
             rec['params'].append(L.network.params.cpu().numpy().copy())
             rec['states'].append(L.states[1:].cpu().numpy().copy())
             rec['gs'].append(L.global_step)
+            if L.lstm_bool:  # the memory windows' leading-zero counts (device-derived, paac.py:79-83)
+                rec['nz'].append(L.nz_d.cpu().numpy().copy())
         L.book.drain()
         assert L._graphs is not None  # the graph path ran
-        if world > 1:  # the data-parallel update: two gradient buckets all-reduced on a side stream
+        if world > 1 and arch != 'LSTM':  # the data-parallel update: two gradient buckets all-reduced on a side stream
             assert L._buckets is not None and len(L._graphs) == 3 and not L._update_in_rollout
-        np.savez(os.path.join(out_dir, 'w%d_r%d.npz' % (world, rank)), params0=params0, params=np.stack(rec['params']),
-                 states=np.stack(rec['states']), gs=np.array(rec['gs']),
+        elif world > 1:  # LSTM: backward | all-reduce of the whole gradient | apply (+ slot / nz carry)
+            assert L._buckets is None and len(L._graphs) == 2 and not L._update_in_rollout
+        np.savez(os.path.join(out_dir, '%s_w%d_r%d.npz' % (arch, world, rank)), params0=params0,
+                 params=np.stack(rec['params']),
+                 states=np.stack(rec['states']), gs=np.array(rec['gs']), nz=np.array(rec['nz']),
                  episodes=np.array(L.book.episodes, dtype=np.float64).reshape(-1, 3))
     finally:
         L.cleanup()
@@ -142,16 +148,17 @@ def cpu_rank(out_dir):
 
 if __name__ == '__main__':
     out_dir, mode = sys.argv[1], sys.argv[2]
+    arch = sys.argv[3] if len(sys.argv) > 3 else 'NIPS'
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if mode in ('gpu', 'resume'):
         torch.cuda.set_device(0)
     if world == 1 and mode == 'gpu':  # the single process owning every env
-        gpu_rank(out_dir, 0, 1)
+        gpu_rank(out_dir, 0, 1, arch)
         sys.exit(0)
     dist.init_process_group('gloo')
     try:
         if mode == 'gpu':
-            gpu_rank(out_dir, dist.get_rank(), world)
+            gpu_rank(out_dir, dist.get_rank(), world, arch)
         elif mode == 'resume':
             resume_rank(out_dir, dist.get_rank(), world)
         else:

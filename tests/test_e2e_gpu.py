@@ -92,7 +92,11 @@ CASES = [('pong-nips', False), ('breakout-nature-figar', False), ('seaquest-natu
          # stream between graph replays (paac._bucketed_update), norm partials after the all-reduce,
          # the learner (not the rollout) launching the update — everything the N-GPU run executes but
          # the cross-rank sum, which at world 1 is the identity
-         ('pong-nips', True), ('seaquest-nature', True)]
+         ('pong-nips', True), ('seaquest-nature', True),
+         # configs[4]'s data-parallel leg: the LSTM update as two graphs — backward |
+         # eager RCCL all-reduce of the whole gradient | apply, whose second step also moves the frame
+         # store's slots and nz behind the all-reduce (paac.py:79-83, :202-203)
+         ('mspacman-lstm-figar', True)]
 
 
 @pytest.mark.parametrize('config,dp', CASES, ids=['%s%s' % (c, '-dp-rccl' if d else '') for c, d in CASES])
@@ -114,8 +118,10 @@ def test_benchmarked_path_matches_oracle(config, dp, tmp_path):
             idx_all.append(L.idx_h.numpy().copy())
             L.update()
         assert L._graphs is not None  # the checked update is a graph replay
-        if dp:  # three graphs, the all-reduces of the two buckets between them on a side stream
+        if dp and not lstm:  # three graphs, the all-reduces of the two buckets between them on a side stream
             assert L._buckets is not None and len(L._graphs) == 3 and not L._update_in_rollout
+        elif dp:  # LSTM: backward | eager all-reduce of the whole gradient | apply (+ the slot / nz carry)
+            assert L._buckets is None and len(L._graphs) == 2 and not L._update_in_rollout
         # the parameters / slots the checked rollout runs with, read before it: from the third update
         # on, the rollout's last step launches the update itself (mt_rollout_set_update)
         torch.cuda.synchronize()

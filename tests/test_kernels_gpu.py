@@ -524,14 +524,29 @@ def test_stacking_trunk_in_kernel_pull(arch, E, depth):
     assert torch.equal(ws[:ws2.numel()], ws2)
 
 
-@pytest.mark.parametrize('arch,depth', [('NIPS', 1), ('NATURE', 1), ('PWYX', 3)])
+def _counter_words(net, ws, E):
+    """The stacking chains' hand-off counters of a workspace of E rows (mt_net_workspace_region kind 4)."""
+    import ctypes as C
+    from manette_amd import _lib
+    off, n = C.c_size_t(), C.c_size_t()
+    _lib.check(_lib.hip().mt_net_workspace_region(net._h, 0, E, 0, 4, 0, C.byref(off), C.byref(n)), 'region')
+    return ws[off.value:off.value + n.value].cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize('arch,depth', [('NIPS', 1), ('NATURE', 1), ('PWYX', 1), ('PWYX', 3)])
 def test_stacking_trunk_unpublished_env_is_bounded(arch, depth):
-    """An env whose ready word never carries the launch's tag (an emulator that died): every wait
-    of the stacking chain is bounded (~2 s of s_memrealtime), so the launch drains instead of
-    hanging the GPU; the stalled env's new state is the previous one (no frame stacked, as
-    wait_published's timeout rule says) and every other env is stacked bit-exactly."""
+    """An env whose ready word never carries the launch's tag (an emulator that died,
+    emulator_runner.py:19-42's worker that never reports back): every wait of the stacking chain is
+    bounded (~2 s of s_memrealtime), so the launch drains instead of hanging the GPU; the stalled
+    env's new state is the previous one (no frame stacked, as wait_published's timeout rule says) and
+    every other env is stacked bit-exactly. The timeout is RAISED in the status word and surfaced by
+    the host as an MTError; the hand-off counters are all zero after the stalled launch (a producer
+    whose consumer stopped waiting first still adds after the reset: the reset subtracts the full
+    counts), and a second, fully published launch on the same workspace stacks and
+    computes bit-exactly (its tiles do not pass their waits on a stale count)."""
     import time
-    from manette_amd.network import host_device_pointer
+    from manette_amd import _lib
+    from manette_amd.network import WaitStatus, host_device_pointer
     import ctypes as C
     E, stalled = 7, 3
     net = _net(arch, depth, 6, 11, seed=3)
@@ -548,18 +563,45 @@ def test_stacking_trunk_unpublished_env_is_bounded(arch, depth):
     out = torch.zeros_like(prev)
     ws = net.workspace(E, 'stk_bounded')
     ws.zero_()
+    status = WaitStatus()
+    fdev, rdev = C.c_void_p(host_device_pointer(frames)), C.c_void_p(host_device_pointer(ready))
     torch.cuda.synchronize()
     t0 = time.time()
-    net.forward_trunk_stacking(prev, C.c_void_p(host_device_pointer(frames)), C.c_void_p(host_device_pointer(ready)),
-                               tag, out, E, ws_key='stk_bounded')
+    net.forward_trunk_stacking(prev, fdev, rdev, tag, out, E, ws_key='stk_bounded', status=status)
     torch.cuda.synchronize()
     assert time.time() - t0 < 30.0
+    with pytest.raises(_lib.MTError, match='timed out'):
+        status.check('stacking trunk')
     got = out.cpu().numpy()
     f = frames.numpy()
     for e in range(E):
         pushes = [] if e == stalled else [f[4 * e + j] for j in range(counts[e])]
         want = prev_h[e] if e == stalled else preprocess.stack_update(prev_h[e], pushes, depth)
         np.testing.assert_array_equal(got[e], want, err_msg='env %d' % e)
+    words = _counter_words(net, ws, E)
+    assert (arch == 'NIPS') == (words.size == 0), words.size  # (NIPS: no in-launch hand-off)
+    assert not words.any(), np.nonzero(words)
+
+    # a second launch on the same workspace, every env published: no timeout, bit-exact
+    tag2 = tag + 7
+    counts2 = rs.randint(1, 5, E).astype(np.int32)
+    frames.numpy()[...] = rs.randint(0, 256, size=frames.shape).astype(np.uint8)
+    ready.numpy()[:, 0] = (tag2 << 3) | counts2
+    prev2_h = got
+    out2 = torch.zeros_like(prev)
+    net.forward_trunk_stacking(out, fdev, rdev, tag2, out2, E, ws_key='stk_bounded', status=status)
+    torch.cuda.synchronize()
+    status.check('second stacking trunk')
+    got2 = out2.cpu().numpy()
+    for e in range(E):
+        pushes = [f[4 * e + j] for j in range(counts2[e])]
+        np.testing.assert_array_equal(got2[e], preprocess.stack_update(prev2_h[e], pushes, depth), err_msg='env %d' % e)
+    assert not _counter_words(net, ws, E).any()
+    ws2 = net.workspace(E, 'stk_bounded_plain')
+    ws2.zero_()
+    net.forward_trunk(out2, E, ws_key='stk_bounded_plain')
+    torch.cuda.synchronize()
+    assert torch.equal(ws[:ws2.numel()], ws2)  # (the counter words included: zero in both)
 
 
 def test_nips_backward_above_fused_cap():

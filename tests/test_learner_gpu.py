@@ -164,40 +164,46 @@ def test_eval_cli_restores_training_checkpoint(tmp_path, arch, extra):
     assert any(l.startswith('Mean: ') for l in lines) and any(l.startswith('Std: ') for l in lines)
 
 
-def _dp_run(tmp_path, world, port, mode='gpu'):
+def _dp_run(tmp_path, world, port, mode='gpu', arch='NIPS'):
     script = os.path.join(ROOT, 'tests', 'dp_worker.py')
     env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world))
     procs = []
     for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK='0')
-        procs.append(subprocess.Popen([sys.executable, script, str(tmp_path), mode], env=e,
+        procs.append(subprocess.Popen([sys.executable, script, str(tmp_path), mode, arch], env=e,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=300) for p in procs]
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, o[-2000:] + e[-3000:]
     if mode != 'gpu':
         return None
-    return [np.load(os.path.join(str(tmp_path), 'w%d_r%d.npz' % (world, r))) for r in range(world)]
+    return [np.load(os.path.join(str(tmp_path), '%s_w%d_r%d.npz' % (arch, world, r))) for r in range(world)]
 
 
-def test_dp_two_ranks_equal_single_process_union(tmp_path):
-    """W=2 ranks (8 envs each, gradient summed once per update, 1/W folded into the
-    clip) == ONE process owning all 16 envs, through the product's update (graph-replayed from the
+@pytest.mark.parametrize('arch,envs,port', [('NIPS', 16, 29531), ('LSTM', 8, 29535)])
+def test_dp_two_ranks_equal_single_process_union(tmp_path, arch, envs, port):
+    """W=2 ranks (envs/2 each, gradient summed once per update, 1/W folded into the
+    clip) == ONE process owning all the envs, through the product's update (graph-replayed from the
     second update on): the device draw hashes global env ids, so both runs take the same
-    trajectory (states bit-identical per env), global_step advances by all 16 envs per macro-step
+    trajectory (states bit-identical per env), global_step advances by every env per macro-step
     on every rank (mh_book_set_shard), episodes carry the same global steps, and the parameters
     after every update agree within the fp32 reduction-order budget (the W=2 gradient is two
-    80-row sums added by the all-reduce instead of one 160-row sum)."""
-    one = _dp_run(tmp_path, 1, 29531)[0]
-    two = _dp_run(tmp_path, 2, 29533)
-    ec = 8
-    p0 = None
+    half-batch sums added by the all-reduce instead of one sum). LSTM (configs[4]'s data-parallel
+    leg): its update is backward | all-reduce of the whole gradient | apply, the
+    apply also carrying the frame store's slots and windows; the device-derived windows (nz) are
+    identical per env too (paac.py:79-83, :202-203)."""
+    one = _dp_run(tmp_path, 1, port, arch=arch)[0]
+    two = _dp_run(tmp_path, 2, port + 2, arch=arch)
+    ec = envs // 2
     for r in range(2):
         np.testing.assert_array_equal(two[r]['gs'], one['gs'])
         np.testing.assert_array_equal(two[r]['states'], one['states'][:, :, r * ec:(r + 1) * ec],
                                       err_msg='rank %d trajectory' % r)
+        if arch == 'LSTM':
+            np.testing.assert_array_equal(two[r]['nz'], one['nz'][:, :, r * ec:(r + 1) * ec],
+                                          err_msg='rank %d windows' % r)
     np.testing.assert_array_equal(two[0]['params'], two[1]['params'])  # replicas identical
-    assert one['gs'][-1] == 4 * 5 * 16
+    assert one['gs'][-1] == 4 * 5 * envs
     ep1 = sorted(map(tuple, one['episodes']))
     ep2 = sorted(map(tuple, np.concatenate([two[0]['episodes'], two[1]['episodes']])))
     assert len(ep1) > 0 and ep1 == ep2
