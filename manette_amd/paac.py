@@ -16,7 +16,8 @@ Sampling (args.sampling): 'host' = the reference's numpy multinomial stream (par
 Data parallel: one process per GPU; env ids are offset by rank (rank r owns global envs
 [r*ec, (r+1)*ec), the runners.py:17-18 split over ranks), each rank rolls out its own shard and
 the flat gradient is summed by ONE all-reduce per update (RCCL behind the C ABI, mt_allreduce,
-inside the update's hipGraph; manette_amd/comm.py); 1/world is folded into mt_clip_rmsprop, so
+issued eagerly between the update's graph replays: _bucketed_update; manette_amd/comm.py); 1/world
+is folded into mt_clip_rmsprop, so
 clip + RMSProp see the global-batch mean gradient and the replicas stay identical. The device
 draw hashes the global env id and global_step counts every env of the job (mh_book_set_shard),
 so a W-rank run takes the same trajectory and LR schedule as one process owning all W*ec envs.
