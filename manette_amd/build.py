@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 HIP_SOURCES = ['net.hip', 'misc.hip', 'rollout.hip', 'comm.hip']
-HIP_HEADERS = ['common.h', 'gemm.h', 'jobs.h', 'nips_bwd.h', 'trunk_fused.h', 'lstm.h', 'dconv.h']
+HIP_HEADERS = ['common.h', 'gemm.h', 'jobs.h', 'nips_bwd.h', 'trunk_fused.h', 'lstm.h', 'dconv.h', 'nature_bwd.h']
 HOST_SOURCES = ['runner.cpp', 'crc32c.cpp']
 HIP_LIB = os.path.join(HERE, 'libmanette_hip.so')
 PROBE_LIB = os.path.join(HERE, 'libmanette_hip_probe.so')

@@ -15,6 +15,7 @@
 #include "trunk_fused.h"
 #include "nips_bwd.h"
 #include "dconv.h"
+#include "nature_bwd.h"
 
 namespace mt {
 
@@ -1116,6 +1117,10 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
       MT_TRY((conv_dgrad_unpool_solo<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act, al, s)));
       MT_TRY(launch_group(s, wg.gemm, pending, extra));
+    } else if constexpr (stream_dx<G>()) {  // NATURE conv2: the weight-stationary streaming dX (nature_bwd.h)
+      MT_TRY(launch_group(s, DxStreamJob<G>{ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
+                                            dx_stream_groups<G>(B), act, al},
+                          wg.gemm, pending, extra));
     } else if constexpr (pooled<Ar, J>()) {
       MT_TRY(launch_group(s, conv_dgrad_unpool_job<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
                                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act,
