@@ -450,6 +450,27 @@ int mt_comm_info(const mt_comm *comm, int *rank, int *world);
 int mt_allreduce(mt_comm *comm, float *buf, size_t n, mt_stream_t stream);
 /* In-place broadcast of `bytes` bytes from rank `root`. */
 int mt_broadcast(mt_comm *comm, void *buf, size_t bytes, int root, mt_stream_t stream);
+/* Diagnostics / tests: a communicator without RCCL standing for `replicas` identical ranks. Its
+ * mt_allreduce multiplies the buffer by `replicas` at once (the in-place sum of identical replicas)
+ * and then holds the stream for delay_us microseconds; mt_broadcast is a no-op. A sum that started
+ * before its producer finished, or a consumer that did not wait for it, changes the result (the
+ * stream-order tests of the data-parallel update, tests/test_dp_gpu.py). */
+int mt_comm_init_loopback(int replicas, int delay_us, mt_comm **out);
+
+/* The data-parallel update launched by the rollout itself (the counterpart of mt_rollout_set_update
+ * for world > 1, or forced at world 1): once registered, the last macro-step of every rollout stores
+ * the LR as mt_rollout_set_update does and enqueues, with no return to the caller,
+ *   graph_execs[0] (loss + dense / head gradients: the backward's first
+ *   mt_net_backward_bucket_launches launches) on the rollout's stream;
+ *   the in-place sum of grad[split, n) (mt_allreduce) on a side stream the rollout owns, behind it;
+ *   graph_execs[1] (the rest of the conv backward) on the rollout's stream;
+ *   the sum of grad[0, split) on the side stream, behind that;
+ *   graph_execs[2] (norm partials + clip + RMSProp with inv_scale = 1/world) behind both sums.
+ * The all-reduces run beside the conv backward, as PAACLearner._bucketed_update issues them from
+ * Python (which the learner keeps for communicators outside the C ABI). graph_execs NULL
+ * unregisters; registering either form replaces the other. */
+int mt_rollout_set_update_dp(mt_rollout *ro, void *const *graph_execs, mt_comm *comm, float *grad, size_t n,
+                             size_t split, float *lr_host, double initial_lr, double annealing_steps);
 
 /* ---- small helpers ----------------------------------------------------------------------- */
 /* out[i] = sum_z parts[z*n + i] (deterministic order); used for split reductions. */

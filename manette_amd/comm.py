@@ -9,6 +9,9 @@ RcclComm   the product path: an RCCL communicator behind the C ABI (mt_comm_*, m
            torch.distributed (gloo) is only the control channel that ships rank 0's unique id.
 TorchComm  torch.distributed collectives on the existing process group: for topologies RCCL does
            not support, i.e. several ranks sharing one GPU (the world-2 tests on a 1-GPU box).
+LoopbackComm  the C-ABI communicator without RCCL (tests: x replicas + a delay, exposing stream order).
+The C-ABI communicators (RcclComm, LoopbackComm) carry `_h`, the mt_comm handle the native rollout
+launches the data-parallel update with (mt_rollout_set_update_dp).
 """
 import ctypes as C
 
@@ -58,6 +61,20 @@ class RcclComm(object):
 
     def __del__(self):
         self.close()
+
+
+class LoopbackComm(RcclComm):
+    """A communicator behind the C ABI without RCCL (mt_comm_init_loopback): its all-reduce scales
+    by `replicas` (the sum of identical replicas) and then holds the stream delay_us — the
+    stream-order tests of the data-parallel update (tests/test_dp_gpu.py) on one GPU, where RCCL's
+    one-rank sum is the identity and an ordering bug would not show."""
+    kind = 'loopback'
+
+    def __init__(self, replicas=2, delay_us=2000):
+        h = C.c_void_p()
+        check(_lib.hip().mt_comm_init_loopback(int(replicas), int(delay_us), C.byref(h)), 'mt_comm_init_loopback')
+        self._h = h
+        self.rank, self.world = 0, int(replicas)
 
 
 class TorchComm(object):

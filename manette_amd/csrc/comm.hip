@@ -8,13 +8,18 @@
 // RCCL calls, so they can be captured into the update's hipGraph (mt_graph_*).
 #include <rccl/rccl.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 static_assert(NCCL_UNIQUE_ID_BYTES == MT_COMM_UID_BYTES, "RCCL unique id size");
 
 struct mt_comm {
-  ncclComm_t comm;
-  int rank, world, device;
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1, device = 0;
+  // loopback (mt_comm_init_loopback, tests): no RCCL; the "sum" of `replicas` identical replicas
+  float replicas = 0.f;
+  uint64_t delay_ticks = 0;
 };
 
 using namespace mt;
@@ -53,10 +58,31 @@ extern "C" int mt_comm_init(const char *uid, int rank, int world, int device, mt
   return MT_OK;
 }
 
+extern "C" int mt_comm_init_loopback(int replicas, int delay_us, mt_comm **out) {
+  MT_CHECK_ARG(out, "null argument");
+  MT_CHECK_ARG(replicas >= 1 && delay_us >= 0 && delay_us <= 100000, "replicas %d / delay %d us", replicas, delay_us);
+  mt_comm *m = new mt_comm();
+  m->replicas = (float)replicas;
+  m->delay_ticks = (uint64_t)delay_us * 100;  // s_memrealtime: 100 MHz
+  *out = m;
+  return MT_OK;
+}
+
 extern "C" void mt_comm_destroy(mt_comm *comm) {
   if (!comm) return;
-  (void)ncclCommDestroy(comm->comm);
+  if (comm->comm) (void)ncclCommDestroy(comm->comm);
   delete comm;
+}
+
+// loopback all-reduce: scale by the replica count at once (a sum that started before its producer
+// finished would be overwritten), then hold the stream for delay_ticks (a consumer that does not
+// wait for the sum would run first)
+__global__ __launch_bounds__(256) void loopback_sum_kernel(float *buf, size_t n, float replicas) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) buf[i] *= replicas;
+}
+__global__ void loopback_delay_kernel(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
 extern "C" int mt_comm_info(const mt_comm *comm, int *rank, int *world) {
@@ -69,6 +95,16 @@ extern "C" int mt_comm_info(const mt_comm *comm, int *rank, int *world) {
 extern "C" int mt_allreduce(mt_comm *comm, float *buf, size_t n, mt_stream_t stream) {
   MT_CHECK_ARG(comm && (buf || n == 0), "null argument");
   if (n == 0) return MT_OK;
+  if (!comm->comm) {  // loopback
+    const int blocks = (int)std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(loopback_sum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, buf, n, comm->replicas);
+    MT_HIP(hipGetLastError());
+    if (comm->delay_ticks) {
+      hipLaunchKernelGGL(loopback_delay_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, comm->delay_ticks);
+      MT_HIP(hipGetLastError());
+    }
+    return MT_OK;
+  }
   MT_RCCL(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, comm->comm, (hipStream_t)stream));
   return MT_OK;
 }
@@ -76,7 +112,7 @@ extern "C" int mt_allreduce(mt_comm *comm, float *buf, size_t n, mt_stream_t str
 extern "C" int mt_broadcast(mt_comm *comm, void *buf, size_t bytes, int root, mt_stream_t stream) {
   MT_CHECK_ARG(comm && (buf || bytes == 0), "null argument");
   MT_CHECK_ARG(root >= 0 && root < comm->world, "root %d out of [0, %d)", root, comm->world);
-  if (bytes == 0) return MT_OK;
+  if (bytes == 0 || !comm->comm) return MT_OK;  // (loopback: the replicas are identical)
   MT_RCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm->comm, (hipStream_t)stream));
   return MT_OK;
 }

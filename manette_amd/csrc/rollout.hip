@@ -82,6 +82,14 @@ struct mt_rollout {
   hipGraphExec_t update_graph = nullptr;
   float *lr_host = nullptr;
   double initial_lr = 0.0, annealing_steps = 1.0;
+  // ... or the data-parallel update (mt_rollout_set_update_dp): three graphs with the two gradient
+  // buckets' all-reduces on a side stream between them, ordered by events
+  hipGraphExec_t dp_graph[3] = {nullptr, nullptr, nullptr};
+  mt_comm *dp_comm = nullptr;
+  float *dp_grad = nullptr;
+  size_t dp_n = 0, dp_split = 0;
+  hipStream_t dp_side = nullptr;
+  hipEvent_t dp_ev[3] = {nullptr, nullptr, nullptr};
 };
 
 using namespace mt;
@@ -234,6 +242,9 @@ extern "C" void mt_rollout_destroy(mt_rollout *ro) {
   if (ro->cap_stream) (void)hipStreamDestroy(ro->cap_stream);
   if (ro->gev) (void)hipEventDestroy(ro->gev);
   if (ro->gbase_dev) (void)hipFree(ro->gbase_dev);
+  if (ro->dp_side) (void)hipStreamDestroy(ro->dp_side);
+  for (hipEvent_t e : ro->dp_ev)
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : ro->ev) (void)hipEventDestroy(e);
   for (auto &m : ro->marks) {
     (void)hipEventDestroy(m.first);
@@ -701,14 +712,29 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   } else {
     rc = enqueue_preprocess(ro, t, total, s);
   }
-  // 6. the update right behind the bootstrap chain (mt_rollout_set_update): LR of the step reached
-  if (rc == MT_OK && t == T - 1 && ro->update_graph) {
+  // 6. the update right behind the bootstrap chain (mt_rollout_set_update / _dp): LR of the step reached
+  if (rc == MT_OK && t == T - 1 && (ro->update_graph || ro->dp_graph[0])) {
     const int64_t gs = *global_step;
     const double lr = (double)gs <= ro->annealing_steps
                           ? ro->initial_lr - ((double)gs * ro->initial_lr / ro->annealing_steps)
                           : 0.0;
     *ro->lr_host = (float)lr;  // (read by the RMSProp kernel when it runs, after this store)
-    MT_HIP(hipGraphLaunch(ro->update_graph, s));
+    if (ro->update_graph) {
+      MT_HIP(hipGraphLaunch(ro->update_graph, s));
+    } else {  // the data-parallel update (paac._bucketed_update's sequence, from here)
+      float *g = ro->dp_grad;
+      MT_HIP(hipGraphLaunch(ro->dp_graph[0], s));  // loss + dense / head gradients
+      MT_HIP(hipEventRecord(ro->dp_ev[0], s));
+      MT_HIP(hipStreamWaitEvent(ro->dp_side, ro->dp_ev[0], 0));
+      MT_TRY_(mt_allreduce(ro->dp_comm, g + ro->dp_split, ro->dp_n - ro->dp_split, ro->dp_side));
+      MT_HIP(hipGraphLaunch(ro->dp_graph[1], s));  // the rest of the conv backward
+      MT_HIP(hipEventRecord(ro->dp_ev[1], s));
+      MT_HIP(hipStreamWaitEvent(ro->dp_side, ro->dp_ev[1], 0));
+      MT_TRY_(mt_allreduce(ro->dp_comm, g, ro->dp_split, ro->dp_side));
+      MT_HIP(hipEventRecord(ro->dp_ev[2], ro->dp_side));
+      MT_HIP(hipStreamWaitEvent(s, ro->dp_ev[2], 0));
+      MT_HIP(hipGraphLaunch(ro->dp_graph[2], s));  // norm partials + clip + RMSProp
+    }
   }
   const double t4 = now_us();
   ro->acc[0] += t1 - t0;
@@ -743,6 +769,35 @@ extern "C" int mt_rollout_set_update(mt_rollout *ro, void *graph_exec, float *lr
   MT_CHECK_ARG(!graph_exec || (lr_host && annealing_steps > 0.0), "a registered update needs lr_host and annealing_steps > 0");
   MT_CHECK_ARG(!graph_exec || ro->pipelined, "the rollout launches the update only in pipelined mode");
   ro->update_graph = (hipGraphExec_t)graph_exec;
+  ro->lr_host = lr_host;
+  ro->initial_lr = initial_lr;
+  ro->annealing_steps = annealing_steps;
+  if (graph_exec) ro->dp_graph[0] = ro->dp_graph[1] = ro->dp_graph[2] = nullptr;
+  return MT_OK;
+}
+
+extern "C" int mt_rollout_set_update_dp(mt_rollout *ro, void *const *graph_execs, mt_comm *comm, float *grad, size_t n,
+                                        size_t split, float *lr_host, double initial_lr, double annealing_steps) {
+  MT_CHECK_ARG(ro, "null argument");
+  if (!graph_execs) {  // unregister
+    ro->dp_graph[0] = ro->dp_graph[1] = ro->dp_graph[2] = nullptr;
+    return MT_OK;
+  }
+  MT_CHECK_ARG(graph_execs[0] && graph_execs[1] && graph_execs[2] && comm && grad && lr_host,
+               "a registered data-parallel update needs 3 graphs, a communicator, the gradient and lr_host");
+  MT_CHECK_ARG(split <= n && annealing_steps > 0.0, "bucket split %zu of %zu, annealing steps %g", split, n,
+               annealing_steps);
+  MT_CHECK_ARG(ro->pipelined, "the rollout launches the update only in pipelined mode");
+  if (!ro->dp_side) {
+    MT_HIP(hipStreamCreateWithFlags(&ro->dp_side, hipStreamNonBlocking));
+    for (hipEvent_t &e : ro->dp_ev) MT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  for (int i = 0; i < 3; ++i) ro->dp_graph[i] = (hipGraphExec_t)graph_execs[i];
+  ro->dp_comm = comm;
+  ro->dp_grad = grad;
+  ro->dp_n = n;
+  ro->dp_split = split;
+  ro->update_graph = nullptr;
   ro->lr_host = lr_host;
   ro->initial_lr = initial_lr;
   ro->annealing_steps = annealing_steps;

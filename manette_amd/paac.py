@@ -145,7 +145,8 @@ class PAACLearner(ActorLearner):
         # replay the update as hipGraph(s) from the second update on (native pipelined step)
         self.use_update_graph = bool(getattr(args, 'update_graph', True))
         self._graphs = None
-        self._update_in_rollout = False  # mt_rollout_set_update registered (_register_update)
+        self._update_in_rollout = False  # mt_rollout_set_update(_dp) registered (_register_update)
+        self._rollout_update = None  # 'all': the rollout launches the whole update; 'first': its first graph
         self._boot_ws = None  # the rollout's workspace whose bootstrap dense slabs the loss kernel finishes
         self._eager_updates = 0
         self._buckets = None  # data parallel: flat offset splitting the two all-reduce buckets
@@ -391,6 +392,8 @@ class PAACLearner(ActorLearner):
             if np.float32(self._lr_word[0]) != np.float32(lr):
                 raise RuntimeError('native LR schedule %r != get_lr() %r at global step %d'
                                    % (float(self._lr_word[0]), lr, self.global_step))
+            if self._rollout_update == 'first':  # data parallel, Python communicator: the rollout
+                self._bucketed_update(devnet._stream(), first_launched=True)  # launched graph 1 only
             return lr
         self.network.set_lr(lr)
         if self._graph_ok():
@@ -398,8 +401,12 @@ class PAACLearner(ActorLearner):
                 self._capture_update()
             if self._graphs is not None:
                 s = devnet._stream()
-                if self._buckets is not None:  # data parallel, bucketed (see _capture_update)
+                if self._buckets is not None and len(self._graphs) == 1:  # data parallel, one graph
+                    self._launch_graph(self._graphs[0], s)
+                    self._register_update()
+                elif self._buckets is not None:  # data parallel, three graphs (see _capture_update)
                     self._bucketed_update(s)
+                    self._register_update()
                 elif len(self._graphs) > 1:  # backward | eager all-reduce | apply
                     self._launch_graph(self._graphs[0], s)
                     self.comm.allreduce(self.network.grad)
@@ -415,18 +422,21 @@ class PAACLearner(ActorLearner):
         self._update_apply()
         return lr
 
-    def _bucketed_update(self, s):
+    def _bucketed_update(self, s, first_launched=False):
         """Data-parallel update with the gradient all-reduced in two buckets on a side stream: the
         dense + head variables (the tail of the flat gradient, ~98 % of its bytes) as soon as the
         backward's second launch has written them, while the conv backward runs on the learner's
         stream, then the conv variables; clip + RMSProp wait for both. Every rollout kernel (the
         in-kernel waits) stays on the learner's stream; the side stream only ever runs the
-        all-reduces, between the update's first launch and its apply."""
+        all-reduces, between the update's first launch and its apply. first_launched: the rollout's
+        last macro-step already launched the first graph on this stream (mt_rollout_set_update), so
+        the backward starts right behind the bootstrap chain, not after the return to Python."""
         cur = torch.cuda.current_stream()
         side, (e1, e2, e3) = self._ar_stream, self._ar_events
         g1, g2, g3 = self._graphs
         grad = self.network.grad
-        self._launch_graph(g1, s)             # loss + dense dX / dW + head dW (+ the first conv layer's)
+        if not first_launched:
+            self._launch_graph(g1, s)         # loss + dense dX / dW + head dW (+ the first conv layer's)
         e1.record(cur)
         with torch.cuda.stream(side):
             side.wait_event(e1)
@@ -549,23 +559,57 @@ class PAACLearner(ActorLearner):
         if not self.dp:  # one graph; the rollout's last step launches it (_register_update)
             graphs = capture([whole])
         elif not self.lstm_bool and os.environ.get('MT_DP_BUCKETS', '1') != '0':
-            # data parallel: the backward captured as its first launches, up to the one that completes
-            # the dense / head gradients (mt_net_backward_bucket_launches), and the rest (the conv
-            # backward); the all-reduces of the two gradient buckets run eagerly on a side stream
-            # between them (_bucketed_update)
+            # data parallel: the backward's first launches, up to the one that completes the dense /
+            # head gradients (mt_net_backward_bucket_launches), then the rest (the conv backward); the
+            # all-reduce of each gradient bucket runs on the all-reduce stream as soon as its launches
+            # are done, beside the conv backward, and the apply waits for both
             n_tail = C.c_int()
             _lib.check(lib.mt_net_backward_bucket_launches(self.network._h, C.byref(n_tail)),
                        'mt_net_backward_bucket_launches')
             k = n_tail.value
-            graphs = capture([window(0, k, self._update_backward), window(k, -1, self._update_backward),
-                              self._update_apply])
             self._buckets = self._dense_offset()
             self._ar_stream = torch.cuda.Stream()
             self._ar_events = tuple(torch.cuda.Event() for _ in range(3))
+            graphs = None
+            if getattr(self.comm, 'capturable', False) and os.environ.get('MT_DP_ONE_GRAPH', '1') != '0':
+                # a C-ABI communicator: the whole sequence as ONE graph, the all-reduce stream forked and
+                # joined by events inside the capture (no host enqueue between its parts: at world 1
+                # the eager form's RCCL calls and event hops left ~18 + 28 us device gaps, profiles/r05f)
+                try:
+                    graphs = capture([lambda: self._dp_sequence(window(0, k, self._update_backward),
+                                                                window(k, -1, self._update_backward))])
+                except _lib.MTError as e:
+                    logging.warning('data-parallel update not capturable as one graph (%s): three graphs', e)
+                    graphs = None
+            if graphs is None:  # three graphs, the all-reduces issued between their replays
+                graphs = capture([window(0, k, self._update_backward), window(k, -1, self._update_backward),
+                                  self._update_apply])
         else:  # backward | eager all-reduce of the whole gradient | apply
             graphs = capture([self._update_backward, self._update_apply])
         self._graphs = graphs
         self._graph_stream = side  # keep the capture stream alive with the graphs
+
+    def _dp_sequence(self, first, rest):
+        """The bucketed data-parallel update as stream work (captured into one graph): first() = the
+        backward's launches up to the dense / head gradients, rest() = the conv backward. Each bucket's
+        in-place sum runs on the all-reduce stream behind an event as soon as its gradients are
+        complete; the apply (norm partials, clip + RMSProp) waits for both."""
+        cap = torch.cuda.current_stream()
+        ar, (e1, e2, e3) = self._ar_stream, self._ar_events
+        grad = self.network.grad
+        first()
+        e1.record(cap)
+        ar.wait_event(e1)
+        with torch.cuda.stream(ar):
+            self.comm.allreduce(grad[self._buckets:])  # dense + head bucket, beside the conv backward
+        rest()
+        e2.record(cap)
+        ar.wait_event(e2)
+        with torch.cuda.stream(ar):
+            self.comm.allreduce(grad[:self._buckets])  # conv bucket
+            e3.record(ar)
+        cap.wait_event(e3)
+        self._update_apply()
 
     def _dense_offset(self):
         """Flat-gradient offset of the first non-conv variable (the dense layer): variables are in
@@ -579,19 +623,39 @@ class PAACLearner(ActorLearner):
         _lib.check(_lib.hip().mt_graph_launch(g, s), 'mt_graph_launch')
 
     def _register_update(self):
-        """From the next rollout on, its last macro-step stores the LR and launches the (single)
-        update graph itself, right behind the bootstrap chain (mt_rollout_set_update): no host
-        round trip between the last emulator step and the update. MT_UPDATE_IN_ROLLOUT=0: off."""
+        """From the next rollout on, its last macro-step stores the LR and launches the update itself,
+        right behind the bootstrap chain: no host round trip between the last emulator step and
+        the update. Single process: the one update graph (mt_rollout_set_update). Data parallel
+        (bucketed) with a C-ABI communicator (RCCL): the one graph of _dp_sequence (all-reduces
+        forked / joined inside it), or if that could not be captured the three graphs with the
+        buckets' all-reduces on the rollout's side stream between them (mt_rollout_set_update_dp);
+        with a Python communicator (gloo rehearsals, test stubs) the rollout launches the first
+        graph and the learner the rest (_bucketed_update). MT_UPDATE_IN_ROLLOUT=0: off."""
         if os.environ.get('MT_UPDATE_IN_ROLLOUT', '1') == '0' or self.native_step is None or self.lstm_bool \
-                or self.dp:
-            # (LSTM: its update also moves the frame-store slots the next rollout starts from; data
-            # parallel: the learner launches the update, its all-reduces eagerly between graphs)
+                or (self.dp and self._buckets is None):
+            # (LSTM: its update also moves the frame-store slots the next rollout starts from; the
+            # unbucketed data-parallel update: backward | all-reduce | apply, launched by the learner)
             return
+        import ctypes as C
         from . import _lib
-        _lib.check(_lib.hip().mt_rollout_set_update(self.native_step, self._graphs[0],
-                                                    self.network._lr_host.data_ptr(),
+        lib = _lib.hip()
+        lr_ptr = self.network._lr_host.data_ptr()
+        if len(self._graphs) == 1:  # the single-process update, or the data-parallel one as one graph
+            self._rollout_update = 'all'
+        elif getattr(self.comm, '_h', None) is not None:  # three graphs, a C-ABI communicator
+            self._rollout_update = 'all'
+            gs = (C.c_void_p * 3)(*[g.value if isinstance(g, C.c_void_p) else g for g in self._graphs])
+            grad = self.network.grad
+            _lib.check(lib.mt_rollout_set_update_dp(self.native_step, gs, self.comm._h, C.c_void_p(grad.data_ptr()),
+                                                    grad.numel(), int(self._buckets), C.c_void_p(lr_ptr),
                                                     float(self.initial_lr), float(self.lr_annealing_steps)),
-                   'mt_rollout_set_update')
+                       'mt_rollout_set_update_dp')
+        else:  # three graphs, a Python communicator: the rollout launches the first
+            self._rollout_update = 'first'
+        if self._rollout_update == 'first' or len(self._graphs) == 1:
+            _lib.check(lib.mt_rollout_set_update(self.native_step, self._graphs[0], lr_ptr,
+                                                 float(self.initial_lr), float(self.lr_annealing_steps)),
+                       'mt_rollout_set_update')
         self._lr_word = self.network._lr_host.numpy()  # (the pinned word the rollout writes)
         self._update_in_rollout = True
 
@@ -599,6 +663,7 @@ class PAACLearner(ActorLearner):
         if self._update_in_rollout and self.native_step is not None:
             from . import _lib
             _lib.hip().mt_rollout_set_update(self.native_step, None, None, 0.0, 1.0)
+            _lib.hip().mt_rollout_set_update_dp(self.native_step, None, None, None, 0, 0, None, 0.0, 1.0)
         self._update_in_rollout = False
         if getattr(self, '_graphs', None):
             from . import _lib

@@ -70,8 +70,9 @@ def gpu_rank(out_dir, rank, world, arch='NIPS'):
                 rec['nz'].append(L.nz_d.cpu().numpy().copy())
         L.book.drain()
         assert L._graphs is not None  # the graph path ran
-        if world > 1 and arch != 'LSTM':  # the data-parallel update: two gradient buckets all-reduced on a side stream
-            assert L._buckets is not None and len(L._graphs) == 3 and not L._update_in_rollout
+        if world > 1 and arch != 'LSTM':  # the data-parallel update: two gradient buckets all-reduced on a side
+            # stream, the first graph launched by the rollout's last step
+            assert L._buckets is not None and len(L._graphs) == 3 and L._rollout_update == 'first' 
         elif world > 1:  # LSTM: backward | all-reduce of the whole gradient | apply (+ slot / nz carry)
             assert L._buckets is None and len(L._graphs) == 2 and not L._update_in_rollout
         np.savez(os.path.join(out_dir, '%s_w%d_r%d.npz' % (arch, world, rank)), params0=params0,

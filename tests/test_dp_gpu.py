@@ -62,7 +62,13 @@ def _run(config, tmp_path, stub):
             L.rollout()
             L.update()
         torch.cuda.synchronize()
-        assert L._buckets is not None and len(L._graphs) == 3
+        native = getattr(L.comm, '_h', None) is not None
+        one = native and os.environ.get('MT_DP_ONE_GRAPH', '1') != '0'
+        # C-ABI communicators: the rollout's last step launches the whole update — one captured graph
+        # (paac._dp_sequence) or the three graphs with the all-reduces between them
+        # (mt_rollout_set_update_dp); a Python one: the first graph, the learner the rest
+        assert L._buckets is not None and len(L._graphs) == (1 if one else 3) and L._update_in_rollout
+        assert L._rollout_update == ('all' if native else 'first')
         c = lambda t: t.detach().cpu().numpy().copy()
         return dict(params=c(L.network.params), ms=c(L.network.ms), mom=c(L.network.mom), grad=c(L.network.grad),
                     states=c(L.states), values=c(L.values), y=c(L.y), idx=L.idx_h.numpy().copy(),
@@ -73,6 +79,8 @@ def _run(config, tmp_path, stub):
 
 @pytest.mark.parametrize('config', ['pong-nips', 'seaquest-nature'])
 def test_bucketed_update_stream_order(config, tmp_path):
+    """The Python form of the bucketed update (the learner issues the all-reduces and graphs 2 and 3;
+    a Python communicator), against the RCCL run (the native form)."""
     ref = _run(config, tmp_path / 'rccl', None)
     stub = SlowDoublingComm()
     got = _run(config, tmp_path / 'stub', stub)
@@ -88,3 +96,21 @@ def test_bucketed_update_stream_order(config, tmp_path):
     assert p1 == got['grad_ptr'] + 4 * k and p2 == got['grad_ptr']
     np.testing.assert_array_equal(b1.cpu().numpy(), ref['grad'][k:])
     np.testing.assert_array_equal(b2.cpu().numpy(), ref['grad'][:k])
+
+
+@pytest.mark.parametrize('config,one_graph', [('pong-nips', True), ('seaquest-nature', True), ('pong-nips', False)])
+def test_native_bucketed_update_stream_order(config, one_graph, tmp_path, monkeypatch):
+    """The native forms — one graph with the all-reduce stream forked and joined inside it
+    (paac._dp_sequence), or the three graphs with the all-reduces enqueued between them by the
+    rollout (mt_rollout_set_update_dp; MT_DP_ONE_GRAPH=0) — with the loopback communicator of the C
+    ABI (mt_comm_init_loopback: the bucket doubled at once — a sum that started before its producer
+    finished would be overwritten — then its stream held ~2 ms, so a consumer that does not wait
+    runs first): every value bit-identical to the RCCL run, the gradient doubled."""
+    from manette_amd.comm import LoopbackComm
+    monkeypatch.setenv('MT_DP_ONE_GRAPH', '1' if one_graph else '0')
+    ref = _run(config, tmp_path / 'rccl', None)
+    got = _run(config, tmp_path / 'loopback', LoopbackComm(replicas=2, delay_us=2000))
+    for k in ('params', 'ms', 'mom', 'states', 'values', 'y', 'idx'):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    assert got['gs'] == ref['gs']
+    np.testing.assert_array_equal(got['grad'], 2.0 * ref['grad'])

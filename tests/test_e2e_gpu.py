@@ -88,10 +88,10 @@ def _chunked_feats(spec, P, frames, chunk=32):
 CASES = [('pong-nips', False), ('breakout-nature-figar', False), ('seaquest-nature', False),
          ('mspacman-lstm-figar', False), ('breakout-pwyx-figar-rgb', False),
          # the data-parallel update at world 1: RCCL communicator, the backward captured
-         # as two graphs around the first gradient bucket, both buckets all-reduced by RCCL on a side
-         # stream between graph replays (paac._bucketed_update), norm partials after the all-reduce,
-         # the learner (not the rollout) launching the update — everything the N-GPU run executes but
-         # the cross-rank sum, which at world 1 is the identity
+         # with both gradient buckets all-reduced by RCCL on their own stream beside the conv backward,
+         # forked and joined inside ONE captured graph (paac._dp_sequence), norm partials after the
+         # all-reduce, launched by the rollout's last step — everything the N-GPU run executes but the
+         # cross-rank sum, which at world 1 is the identity
          ('pong-nips', True), ('seaquest-nature', True),
          # configs[4]'s data-parallel leg: the LSTM update as two graphs — backward |
          # eager RCCL all-reduce of the whole gradient | apply, whose second step also moves the frame
@@ -118,8 +118,10 @@ def test_benchmarked_path_matches_oracle(config, dp, tmp_path):
             idx_all.append(L.idx_h.numpy().copy())
             L.update()
         assert L._graphs is not None  # the checked update is a graph replay
-        if dp and not lstm:  # three graphs, the all-reduces of the two buckets between them on a side stream
-            assert L._buckets is not None and len(L._graphs) == 3 and not L._update_in_rollout
+        if dp and not lstm:  # one graph: the backward, the two buckets' all-reduces forked onto their stream and
+            # joined before the apply (paac._dp_sequence), launched by the rollout's last step
+            assert L._buckets is not None and len(L._graphs) == 1 and L._update_in_rollout
+            assert L._rollout_update == 'all' 
         elif dp:  # LSTM: backward | eager all-reduce of the whole gradient | apply (+ the slot / nz carry)
             assert L._buckets is None and len(L._graphs) == 2 and not L._update_in_rollout
         # the parameters / slots the checked rollout runs with, read before it: from the third update
@@ -134,7 +136,7 @@ def test_benchmarked_path_matches_oracle(config, dp, tmp_path):
         torch.cuda.synchronize()
         idx_all.append(L.idx_h.numpy().copy())
         states = c(L.states)
-        if L._update_in_rollout and not L.slot0_in_rollout:  # this update's apply has already run
+        if L._update_in_rollout and not dp and not L.slot0_in_rollout:  # this update's apply has already run
             states[0] = slot0
         rm = L.rm_h.numpy().copy()
         values = c(L.values)
@@ -147,8 +149,9 @@ def test_benchmarked_path_matches_oracle(config, dp, tmp_path):
         # argmax, the dense output)
         dev = L.network.forward_branches(L.network.lstm_workspace(E, T), 1, E, T) if lstm else \
             L.network.forward_branches(L.train_ws, 0, N)
-        # the benchmarked path: the rollout launched this update (data parallel: the learner did)
-        assert L._update_in_rollout == (not lstm and not dp)
+        # the benchmarked path: the rollout launched this update (data parallel: its first graph, the
+        # learner the all-reduces and the other two)
+        assert L._update_in_rollout == (not lstm)
         # V(s_T): the rollout's last chain (pipelined native step) or the update's first forward (LSTM)
         v_boot, pi_all, rep_all = c(L.v_boot), c(L.pi_all), c(L.rep_all)
         grad, y, adv = L.network.get_variables('grad'), c(L.y), c(L.adv)
