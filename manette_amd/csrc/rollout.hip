@@ -589,6 +589,29 @@ int replay_rollout_graph(mt_rollout *ro, const float *params, hipStream_t s) {
   return MT_OK;
 }
 
+// The registered update on stream s: the single graph (mt_rollout_set_update), or the data-parallel
+// sequence (mt_rollout_set_update_dp: paac._bucketed_update's three graphs with the two gradient
+// buckets' all-reduces on the side stream between them).
+int launch_update(mt_rollout *ro, hipStream_t s) {
+  if (ro->update_graph) {
+    MT_HIP(hipGraphLaunch(ro->update_graph, s));
+    return MT_OK;
+  }
+  float *g = ro->dp_grad;
+  MT_HIP(hipGraphLaunch(ro->dp_graph[0], s));  // loss + dense / head gradients
+  MT_HIP(hipEventRecord(ro->dp_ev[0], s));
+  MT_HIP(hipStreamWaitEvent(ro->dp_side, ro->dp_ev[0], 0));
+  MT_TRY_(mt_allreduce(ro->dp_comm, g + ro->dp_split, ro->dp_n - ro->dp_split, ro->dp_side));
+  MT_HIP(hipGraphLaunch(ro->dp_graph[1], s));  // the rest of the conv backward
+  MT_HIP(hipEventRecord(ro->dp_ev[1], s));
+  MT_HIP(hipStreamWaitEvent(ro->dp_side, ro->dp_ev[1], 0));
+  MT_TRY_(mt_allreduce(ro->dp_comm, g, ro->dp_split, ro->dp_side));
+  MT_HIP(hipEventRecord(ro->dp_ev[2], ro->dp_side));
+  MT_HIP(hipStreamWaitEvent(s, ro->dp_ev[2], 0));
+  MT_HIP(hipGraphLaunch(ro->dp_graph[2], s));  // norm partials + clip + RMSProp
+  return MT_OK;
+}
+
 }  // namespace
 
 // One macro-step t (paac.py:140-205). Pipelined mode keeps the GPU ahead of the host's launch
@@ -630,6 +653,7 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   //    emulators is shorter than the launches of a chain)
   if (ro->pipelined)
     for (int k = ro->armed_upto + 1; k <= std::min(t + ro->ahead, T); ++k) MT_TRY_(arm_step(ro, params, k, k - t, s));
+  const bool update_now = (ro->update_graph || ro->dp_graph[0]) && t == T - 1;
   const double t0w = now_us();
   // 3. wait for the indices of step t (spin: a blocking wait sleeps past the chain and pays the
   //    wake-up latency)
@@ -704,7 +728,16 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
     return MT_ERR_ARG;
   }
   const double t3 = now_us();
-  // 5. release the armed chain (pipelined), or enqueue the preprocess now
+  // 5. the LR of the step reached, for a registered update (actor_learner.py:145-148; read by the
+  //    RMSProp kernel when it runs, after this store), then release the armed chain (pipelined), or
+  //    enqueue the preprocess now
+  if (update_now) {
+    const int64_t gs = *global_step;
+    const double lr = (double)gs <= ro->annealing_steps
+                          ? ro->initial_lr - ((double)gs * ro->initial_lr / ro->annealing_steps)
+                          : 0.0;
+    *ro->lr_host = (float)lr;
+  }
   int rc = MT_OK;
   if (ro->pipelined) {
     ro->seq += 1;
@@ -712,30 +745,11 @@ extern "C" int mt_rollout_step(mt_rollout *ro, const float *params, int t, int64
   } else {
     rc = enqueue_preprocess(ro, t, total, s);
   }
-  // 6. the update right behind the bootstrap chain (mt_rollout_set_update / _dp): LR of the step reached
-  if (rc == MT_OK && t == T - 1 && (ro->update_graph || ro->dp_graph[0])) {
-    const int64_t gs = *global_step;
-    const double lr = (double)gs <= ro->annealing_steps
-                          ? ro->initial_lr - ((double)gs * ro->initial_lr / ro->annealing_steps)
-                          : 0.0;
-    *ro->lr_host = (float)lr;  // (read by the RMSProp kernel when it runs, after this store)
-    if (ro->update_graph) {
-      MT_HIP(hipGraphLaunch(ro->update_graph, s));
-    } else {  // the data-parallel update (paac._bucketed_update's sequence, from here)
-      float *g = ro->dp_grad;
-      MT_HIP(hipGraphLaunch(ro->dp_graph[0], s));  // loss + dense / head gradients
-      MT_HIP(hipEventRecord(ro->dp_ev[0], s));
-      MT_HIP(hipStreamWaitEvent(ro->dp_side, ro->dp_ev[0], 0));
-      MT_TRY_(mt_allreduce(ro->dp_comm, g + ro->dp_split, ro->dp_n - ro->dp_split, ro->dp_side));
-      MT_HIP(hipGraphLaunch(ro->dp_graph[1], s));  // the rest of the conv backward
-      MT_HIP(hipEventRecord(ro->dp_ev[1], s));
-      MT_HIP(hipStreamWaitEvent(ro->dp_side, ro->dp_ev[1], 0));
-      MT_TRY_(mt_allreduce(ro->dp_comm, g, ro->dp_split, ro->dp_side));
-      MT_HIP(hipEventRecord(ro->dp_ev[2], ro->dp_side));
-      MT_HIP(hipStreamWaitEvent(s, ro->dp_ev[2], 0));
-      MT_HIP(hipGraphLaunch(ro->dp_graph[2], s));  // norm partials + clip + RMSProp
-    }
-  }
+  // 6. the update right behind the bootstrap chain (mt_rollout_set_update / _dp). (Enqueued at this
+  //    step's start instead, behind a device wait for the step word, it measured slower: the graph
+  //    launch then delays the emulators of the last step, while here it overlaps the bootstrap
+  //    chain; Pong 682-728k vs 731k, profiles/r05h.)
+  if (rc == MT_OK && update_now) MT_TRY_(launch_update(ro, s));
   const double t4 = now_us();
   ro->acc[0] += t1 - t0;
   ro->acc[1] += t2 - t1;
