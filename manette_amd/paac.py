@@ -584,8 +584,20 @@ class PAACLearner(ActorLearner):
             if graphs is None:  # three graphs, the all-reduces issued between their replays
                 graphs = capture([window(0, k, self._update_backward), window(k, -1, self._update_backward),
                                   self._update_apply])
-        else:  # backward | eager all-reduce of the whole gradient | apply
-            graphs = capture([self._update_backward, self._update_apply])
+        else:  # backward | all-reduce of the whole gradient | apply (LSTM, or MT_DP_BUCKETS=0)
+            graphs = None
+            if getattr(self.comm, 'capturable', False) and os.environ.get('MT_DP_ONE_GRAPH', '1') != '0':
+                def one():  # a C-ABI communicator: the sum captured between the two (one graph)
+                    self._update_backward()
+                    self.comm.allreduce(self.network.grad)
+                    self._update_apply()
+                try:
+                    graphs = capture([one])
+                except _lib.MTError as e:
+                    logging.warning('data-parallel update not capturable as one graph (%s): two graphs', e)
+                    graphs = None
+            if graphs is None:
+                graphs = capture([self._update_backward, self._update_apply])
         self._graphs = graphs
         self._graph_stream = side  # keep the capture stream alive with the graphs
 

@@ -122,8 +122,8 @@ def test_benchmarked_path_matches_oracle(config, dp, tmp_path):
             # joined before the apply (paac._dp_sequence), launched by the rollout's last step
             assert L._buckets is not None and len(L._graphs) == 1 and L._update_in_rollout
             assert L._rollout_update == 'all' 
-        elif dp:  # LSTM: backward | eager all-reduce of the whole gradient | apply (+ the slot / nz carry)
-            assert L._buckets is None and len(L._graphs) == 2 and not L._update_in_rollout
+        elif dp:  # LSTM: backward | all-reduce of the whole gradient | apply (+ the slot / nz carry), one graph
+            assert L._buckets is None and len(L._graphs) == 1 and not L._update_in_rollout
         # the parameters / slots the checked rollout runs with, read before it: from the third update
         # on, the rollout's last step launches the update itself (mt_rollout_set_update)
         torch.cuda.synchronize()
