@@ -149,8 +149,10 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
   const int q = g / NH;  // 0 i, 1 j, 2 f, 3 o
   float c = 0.f;
   if (g < NH) hs[g] = 0.f;
-  // the x-product slab sums of all STEPS positions first (they do not depend on h): 8 slabs x
+  // the x-product slab sums of all STEPS positions first (they do not depend on h): XB slabs x
   // STEPS loads in flight per batch instead of one load latency per slab; adds in slab order
+  // (the frame store's x-product has 50 split-K slabs: batches of 8 were 7 load round trips, most
+  // of this kernel's 13.5 us per rollout step)
   float zx[STEPS];
   size_t xoff[STEPS];
   const int z = map.zeros(b);
@@ -175,16 +177,17 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
     for (int k = 0; k < NH; ++k)
       w6c[j][k] = __hip_atomic_load(W6 + (size_t)k * F + nn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  for (int s0 = 0; s0 < S; s0 += 8) {
-    float v[STEPS][8];
+  constexpr int XB = 25;
+  for (int s0 = 0; s0 < S; s0 += XB) {
+    float v[STEPS][XB];
 #pragma unroll
     for (int t = 0; t < STEPS; ++t)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[t][u] = xg[(size_t)min(s0 + u, S - 1) * rows * G4 + xoff[t]];
+      for (int u = 0; u < XB; ++u) v[t][u] = xg[(size_t)min(s0 + u, S - 1) * rows * G4 + xoff[t]];
 #pragma unroll
     for (int t = 0; t < STEPS; ++t)
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < XB; ++u)
         if (s0 + u < S) zx[t] += v[t][u];
   }
   __syncthreads();
