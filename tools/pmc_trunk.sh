@@ -18,4 +18,9 @@ done
 python3 $R/tools/pmc_summary.py $R/gpurun_out/$NAME > $R/gpurun_out/$NAME.json
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${NAME}_trace -o run --output-format csv -- \
   python3 $R/tools/trunk_only.py "$@" > $R/gpurun_out/${NAME}_trace.log 2>&1
-echo "trace rc=$?"
+rc=$?
+echo "trace rc=$rc"
+# keep the JSON, the logs and the trace's stats; drop the raw counter / trace files (<= 64 MiB back)
+find $R/gpurun_out/${NAME}_trace -name '*kernel_stats.csv' -exec cp {} $R/gpurun_out/${NAME}_trace_stats.csv \; 2>/dev/null
+rm -rf $R/gpurun_out/$NAME $R/gpurun_out/${NAME}_trace
+exit $rc
