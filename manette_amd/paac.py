@@ -418,7 +418,15 @@ class PAACLearner(ActorLearner):
         self._eager_updates += 1
         self._update_backward()
         if self.dp:
-            self.comm.allreduce(self.network.grad)
+            grad = self.network.grad
+            if not self.lstm_bool and os.environ.get('MT_DP_BUCKETS', '1') != '0':
+                # the captured update's two bucket sums, in its order: every size the graph will
+                # replay has run (and connected its RCCL channels) before the capture
+                off = self._dense_offset()
+                self.comm.allreduce(grad[off:])
+                self.comm.allreduce(grad[:off])
+            else:
+                self.comm.allreduce(grad)
         self._update_apply()
         return lr
 
