@@ -575,7 +575,9 @@ struct DConvFor {
   static constexpr int WN = C64 ? (POOL ? 2 : 4) : (SMALLC ? 1 : 2);
   static constexpr int WM = C64 ? (POOL ? 4 : 2) : 4;
   static constexpr int TMW = SMALLC ? (G::S > 1 ? 1 : 2) : (C64 ? 1 : 2);
-  static constexpr int CK = SMALLC ? 0 : G::CIN;
+  // weight chunk: one tap for the 5x5 layers; 4 / 3 taps for the 4x4 / 3x3 ones (one tap left their
+  // blocks 16 / 9 chunk steps of 16-32 MFMAs per wave, each behind a barrier)
+  static constexpr int CK = SMALLC ? 0 : G::CIN * (G::KH == 4 ? 4 : G::KH == 3 ? 3 : 1);
 };
 
 template <class G, bool U8, bool POOL>
