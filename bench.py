@@ -413,18 +413,22 @@ def main():
     # W warmup steps and the K timed ones start from the steady state; the graphs are captured and
     # registered within the first 3 updates, the rest is the host side (emulator threads' caches and
     # clocks) — a 5-update warmup left the r04 driver run ramping 603k -> 713k over its 20 updates
+    # (world > 1: rank 0's clock decides before every update, so every rank runs the same updates —
+    # a rank that ran one update more than rank 0 would wait in its all-reduce while rank 0 waits in
+    # the next control-channel collective)
     settle = 0
     if a.settle_s > 0:
         t_s = time.perf_counter()
-        while time.perf_counter() - t_s < a.settle_s and settle < 5000:
+        while settle < 5000:
+            stop = time.perf_counter() - t_s >= a.settle_s
+            if world > 1:
+                flag = torch.tensor([1 if stop else 0], dtype=torch.int64)
+                dist.broadcast(flag, 0)
+                stop = bool(flag.item())
+            if stop:
+                break
             one_update()
             settle += 1
-        if world > 1:
-            n_s = torch.tensor([settle], dtype=torch.int64)
-            dist.broadcast(n_s, 0)
-            for _ in range(int(n_s.item()) - settle):
-                one_update()
-            settle = int(n_s.item())
     for _ in range(a.warmup):
         one_update()
     if world > 1:

@@ -18,4 +18,7 @@ echo "rocprof rc=$rc"
 db=$(find $R/gpurun_out/$NAME -name '*.db' | head -1)
 [ -z "$db" ] && { echo "no rocpd database under gpurun_out/$NAME"; exit 1; }
 python3 $R/tools/rocpd_summary.py "$db" --bench $R/gpurun_out/$NAME.log -o $R/gpurun_out/$NAME.summary.txt > /dev/null
-echo "summary rc=$?"
+rc=$?
+echo "summary rc=$rc"
+rm -rf $R/gpurun_out/$NAME  # (the summary and the log stay; gpurun copies back <= 64 MiB)
+exit $rc
