@@ -255,6 +255,30 @@ def make_learner(config, T=5, sampling='device', seed=0, staging='resized', pipe
     return learner, args
 
 
+def settle_updates(one_update, seconds, world, dist, cap=5000):
+    """Untimed updates for `seconds` of rank 0's clock; returns their count. World > 1: rank 0
+    decides before every update and broadcasts it over the control channel, so every rank runs the
+    same updates — a rank one update ahead of rank 0 would wait in that update's all-reduce while
+    rank 0 waits in the next control-channel collective (the 2-rank rehearsal hung that way when
+    each rank read its own clock)."""
+    import torch
+    n = 0
+    if seconds <= 0:
+        return 0
+    t_s = time.perf_counter()
+    while n < cap:
+        stop = time.perf_counter() - t_s >= seconds
+        if world > 1:
+            flag = torch.tensor([1 if stop else 0], dtype=torch.int64)
+            dist.broadcast(flag, 0)
+            stop = bool(flag.item())
+        if stop:
+            break
+        one_update()
+        n += 1
+    return n
+
+
 def cpu_baseline(cfg, T, seconds, rank):
     """The oracle ("port") restated reference loop on host cores: the reference's host loop and
     process runners (mp.Queue barrier) from oracle/host_loop.py, a torch-CPU fp32 network with the
@@ -413,22 +437,7 @@ def main():
     # W warmup steps and the K timed ones start from the steady state; the graphs are captured and
     # registered within the first 3 updates, the rest is the host side (emulator threads' caches and
     # clocks) — a 5-update warmup left the r04 driver run ramping 603k -> 713k over its 20 updates
-    # (world > 1: rank 0's clock decides before every update, so every rank runs the same updates —
-    # a rank that ran one update more than rank 0 would wait in its all-reduce while rank 0 waits in
-    # the next control-channel collective)
-    settle = 0
-    if a.settle_s > 0:
-        t_s = time.perf_counter()
-        while settle < 5000:
-            stop = time.perf_counter() - t_s >= a.settle_s
-            if world > 1:
-                flag = torch.tensor([1 if stop else 0], dtype=torch.int64)
-                dist.broadcast(flag, 0)
-                stop = bool(flag.item())
-            if stop:
-                break
-            one_update()
-            settle += 1
+    settle = settle_updates(one_update, a.settle_s, world, dist)
     for _ in range(a.warmup):
         one_update()
     if world > 1:
