@@ -510,14 +510,31 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   for (int i = threadIdx.x + 256 * kHeadQ; i < hp.nq; i += 256) wdst[i] = hsrc[i];
   __syncthreads();
   MT_PROBE_AT(2, b, 1);
-  // logits: the same products and order as a column walk f = lane, lane + 64, ... then the bias
-  for (int o = w; o < O; o += 4) {
+  // logits: the same products and order as a column walk f = lane, lane + 64, ... then the bias.
+  // (The wave index through readfirstlane and, for F a multiple of 64, a wave-uniform term count:
+  // a per-lane guard made each term an exec-masked block with its own LDS round trip, and the
+  // column loop a divergent one — ~0.45 us per column of a wave, probe build.)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int jn = F >> 6;
+  for (int o = wu; o < O; o += 4) {
     int base, stride, bias;
     head_col_lds(hp, o, base, stride, bias);
     float acc = 0.f;
+    if ((F & 63) == 0) {
+      float hv[FMAX], wv[FMAX];
 #pragma unroll
-    for (int j = 0; j < FMAX; ++j)
-      if (lane + 64 * j < F) acc += hs[lane + 64 * j] * Ws[base + (lane + 64 * j) * stride];
+      for (int j = 0; j < FMAX; ++j) {  // every operand of the column requested at once
+        hv[j] = hs[min(lane + 64 * j, 256 * FT - 1)];
+        wv[j] = Ws[base + min(lane + 64 * j, F - 1) * stride];
+      }
+#pragma unroll
+      for (int j = 0; j < FMAX; ++j)
+        if (j < jn) acc += hv[j] * wv[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < FMAX; ++j)
+        if (lane + 64 * j < F) acc += hs[lane + 64 * j] * Ws[base + (lane + 64 * j) * stride];
+    }
     acc = wave_sum(acc);
     if (lane == 0) zs[o] = acc + Ws[bias];
   }
