@@ -241,11 +241,11 @@ __global__ __launch_bounds__(128) void lstm_bwd_kernel(const float *__restrict__
                                                        const float *__restrict__ Kh, const float *__restrict__ gates,
                                                        const float *__restrict__ cst, float *__restrict__ dout32,
                                                        float *__restrict__ dgates) {
-  constexpr int G4 = 4 * NH;
-  __shared__ float khs[NH * G4];
+  constexpr int G4 = 4 * NH, KS = G4 + 1;  // K_h rows padded by one float: thread g's row read below
+  __shared__ float khs[NH * KS];              // is on bank (g + j) % 32, not all 32 threads on one
   __shared__ float dos[NH], dzs[G4];
   const int b = blockIdx.x, g = threadIdx.x;
-  for (int i = g; i < NH * G4; i += G4) khs[i] = Kh[i];
+  for (int i = g; i < NH * G4; i += G4) khs[(i / G4) * KS + i % G4] = Kh[i];
   // every operand of the window requested up front (relaxed atomics: plain read-only loads are
   // sunk to their use — one load latency per step and per 8 products otherwise): the projection
   // row, every step's gates and cell states; same products, same order below
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(128) void lstm_bwd_kernel(const float *__restrict__
     if (g < NH) {  // d h_{t-1} = dz K_h^T
       float a = 0.f;
 #pragma unroll 8
-      for (int j = 0; j < G4; ++j) a += dzs[j] * khs[g * G4 + j];
+      for (int j = 0; j < G4; ++j) a += dzs[j] * khs[g * KS + j];
       dh = a;
     }
     __syncthreads();
@@ -474,8 +474,15 @@ __global__ __launch_bounds__(128) void lstm_gather_dxg_kernel(const float *__res
                                                               float *__restrict__ dxg) {
   const int r = blockIdx.x, g = threadIdx.x;
   float acc = 0.f;
-  if (r == 0) {
-    for (int c = 0; c < nparts; ++c) acc += zpart[(size_t)c * 128 + g];
+  if (r == 0) {  // the zero frame: the partials in batches of 16 loads in flight, added in order
+    for (int c0 = 0; c0 < nparts; c0 += 16) {
+      float p[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) p[u] = zpart[(size_t)min(c0 + u, nparts - 1) * 128 + g];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (c0 + u < nparts) acc += p[u];
+    }
   } else {
     const int j = (r - 1) / E, e = (r - 1) % E;
     // every load first, from clamped addresses (a guarded load ends its block with a wait for it);
