@@ -41,11 +41,26 @@ __global__ void returns_kernel(const float *__restrict__ r, const float *__restr
   y[(size_t)(T - 1) * E + e] = (float)R;
   adv[(size_t)(T - 1) * E + e] = (float)(R - (double)V[(size_t)(T - 1) * E + e]);
   const double gd = gamma;  // python float (float64)
-  for (int t = T - 2; t >= 0; --t) {
-    const size_t i = (size_t)t * E + e;
-    R = (double)r[i] + (gd * R) * (double)mask[i];
-    y[i] = (float)R;
-    adv[i] = (float)(R - (double)V[i]);
+  // steps T-2 .. 0 in batches of 8 whose loads are all in flight before the scan (the rewards and
+  // masks may be pinned host memory: one PCIe round trip per step otherwise)
+  for (int t0 = T - 2; t0 >= 0; t0 -= 8) {
+    float rv[8], mv[8], vv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t i = (size_t)max(t0 - u, 0) * E + e;
+      rv[u] = r[i];
+      mv[u] = mask[i];
+      vv[u] = V[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 - u;
+      if (t < 0) break;
+      const size_t i = (size_t)t * E + e;
+      R = (double)rv[u] + (gd * R) * (double)mv[u];
+      y[i] = (float)R;
+      adv[i] = (float)(R - (double)vv[u]);
+    }
   }
 }
 
