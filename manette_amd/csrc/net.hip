@@ -684,32 +684,73 @@ struct ReturnsSrc {
 // it (lanes over features in 64-strides, DPP wave sum, + bias) from the head region in LDS (Ws).
 // Called by the whole block; the result is in *vt (LDS) after the call. stage(): the caller's LDS
 // stores of the head region, run after this block's slab loads are issued and before the barrier.
-template <class Stage>
+template <class Pre, class Stage>
 __device__ __forceinline__ void boot_value(const ReturnsSrc &rs, const HeadParams &hp, int e, int act, float alpha,
-                                           const float *Ws, float *hsb, float *vt, const Stage &stage) {
+                                           const float *Ws, float *hsb, float *vt, const Pre &pre, const Stage &stage) {
   const int F = hp.F;
-  for (int f = threadIdx.x; f < F; f += 256) {
-    const float *p = rs.boot_slabs + (size_t)e * F + f;
-    const size_t zs_stride = (size_t)rs.E * F;
-    float acc = 0.f;
-    for (int z = 0; z < rs.boot_S; z += 16) {
-      float t[16];
+  const size_t zs_stride = (size_t)rs.E * F;
+  if (F <= 512 && rs.boot_S <= 16) {
+    // every slab partial and dense bias of the thread's features requested first, THEN pre() (the
+    // caller's pinned-memory reward loads): vector loads retire in issue order, so a PCIe load
+    // issued ahead of these made the slab sum wait for it (round 5)
+    float t[2][16], fb[2];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) t[u] = p[(size_t)min(z + u, rs.boot_S - 1) * zs_stride];
+    for (int fi = 0; fi < 2; ++fi) {
+      const int fc = min((int)threadIdx.x + 256 * fi, F - 1);
+      const float *p = rs.boot_slabs + (size_t)e * F + fc;
 #pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (z + u < rs.boot_S) acc += t[u];
+      for (int u = 0; u < 16; ++u) t[fi][u] = p[(size_t)min(u, rs.boot_S - 1) * zs_stride];
+      fb[fi] = rs.fc_b[fc];
     }
-    hsb[f] = act_fwd(acc + rs.fc_b[f], act, alpha);
+    pre();
+#pragma unroll
+    for (int fi = 0; fi < 2; ++fi) {
+      const int f = threadIdx.x + 256 * fi;
+      if (f < F) {
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (u < rs.boot_S) acc += t[fi][u];
+        hsb[f] = act_fwd(acc + fb[fi], act, alpha);
+      }
+    }
+  } else {
+    pre();
+    for (int f = threadIdx.x; f < F; f += 256) {
+      const float *p = rs.boot_slabs + (size_t)e * F + f;
+      float acc = 0.f;
+      for (int z = 0; z < rs.boot_S; z += 16) {
+        float t[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) t[u] = p[(size_t)min(z + u, rs.boot_S - 1) * zs_stride];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (z + u < rs.boot_S) acc += t[u];
+      }
+      hsb[f] = act_fwd(acc + rs.fc_b[f], act, alpha);
+    }
   }
   stage();
   __syncthreads();
-  if (threadIdx.x < 64) {
+  if (threadIdx.x < 64) {  // heads_row's critic column: same products, same order
     const int lane = threadIdx.x;
     float acc = 0.f;
+    if ((F & 63) == 0) {
+      const int jn = F >> 6;
+      float hv[8], wv[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (lane + 64 * j < F) acc += hsb[lane + 64 * j] * Ws[lane + 64 * j];
+      for (int j = 0; j < 8; ++j) {
+        hv[j] = hsb[min(lane + 64 * j, 511)];
+        wv[j] = Ws[min(lane + 64 * j, F - 1)];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < jn) acc += hv[j] * wv[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (lane + 64 * j < F) acc += hsb[lane + 64 * j] * Ws[lane + 64 * j];
+    }
     acc = wave_sum(acc);
     if (lane == 0) *vt = acc + Ws[F];
   }
@@ -797,25 +838,27 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(
   };
   bool staged = false;
   if (rs.r) {
-    // this row's rewards / masks (pinned host memory, a PCIe round trip) requested first
+    // this row's rewards / masks (pinned host memory, a PCIe round trip): requested right behind the
+    // bootstrap slab loads (boot_value's pre), whose sum would otherwise wait for them
     float rk = 0.f, mk = 0.f;
-    {
+    auto rewards = [&]() {
       const int t = b / rs.E, e = b - t * rs.E;
       if ((int)threadIdx.x < rs.T - t) {
         rk = rs.r[(size_t)(t + threadIdx.x) * rs.E + e];
         mk = rs.mask[(size_t)(t + threadIdx.x) * rs.E + e];
       }
-    }
+    };
     float vt;
     if (rs.boot_slabs) {
       __shared__ float hsb[512];
       __shared__ float vts;
       const int e = b % rs.E;
-      boot_value(rs, hp, e, act, alpha, Ws, hsb, &vts, stage);
+      boot_value(rs, hp, e, act, alpha, Ws, hsb, &vts, rewards, stage);
       staged = true;
       vt = vts;
       if (rs.vt_out && b < rs.E && threadIdx.x == 0) rs.vt_out[e] = vt;
     } else {
+      rewards();
       vt = rs.VT[b % rs.E];
     }
     MT_PROBE_AT(4, b, 1);
