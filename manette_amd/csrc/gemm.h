@@ -442,6 +442,30 @@ __device__ __forceinline__ void run_group(int id, float *smem, const J1 &j1, con
   if constexpr (sizeof...(Rest) > 0) run_group(id - j1.blocks(), smem, rest...);
 }
 
+// Up to four jobs as one (a grouped launch's extra slot), blocks in argument order.
+template <class A, class B, class C = NoJob, class D = NoJob>
+struct JobPack {
+  A a;
+  B b;
+  C c{};
+  D d{};
+  __host__ __device__ int blocks() const { return a.blocks() + b.blocks() + c.blocks() + d.blocks(); }
+  size_t lds() const {
+    size_t l = 0;
+    for (size_t x : {a.blocks() ? a.lds() : 0, b.blocks() ? b.lds() : 0, c.blocks() ? c.lds() : 0,
+                     d.blocks() ? d.lds() : 0})
+      l = std::max(l, x);
+    return l;
+  }
+  __device__ __forceinline__ void run(int id, float *smem) const { run_group(id, smem, a, b, c, d); }
+};
+template <class A, class B>
+JobPack(A, B) -> JobPack<A, B>;
+template <class A, class B, class C>
+JobPack(A, B, C) -> JobPack<A, B, C>;
+template <class A, class B, class C, class D>
+JobPack(A, B, C, D) -> JobPack<A, B, C, D>;
+
 template <class... J>
 __global__ __launch_bounds__(256) void group_kernel(J... j) {
   extern __shared__ __attribute__((aligned(16))) float smem[];

@@ -586,21 +586,31 @@ static int lstm_frames_bwd_impl(const mt_net *n, const float *P, const uint8_t *
   const int W = T * E, rows = W * Ar::STEPS;
   const int act = n->cfg.activation;
   const float al = n->cfg.alpha_leaky;
-  MT_TRY(heads_backward<Ar>(n, P, W, ws, L, pi, rep, v, a_idx, r_idx, y, adv, beta, grad, loss_terms, s));
+  if (sizeof(float) * ((size_t)W + 4 * 64) > 160 * 1024) {
+    set_error("batch %d exceeds the head-gradient LDS stage", W);
+    return MT_ERR_ARG;
+  }
+  MT_TRY(loss_bwd_launch<Ar>(n, P, W, ws, L, pi, rep, v, a_idx, r_idx, y, adv, beta, loss_terms, s));
   const float *Kx = P + n->off_lstm;
   const float *Kh = Kx + (size_t)Ar::FLAT * Ar::G4;
   const float *Wp = P + n->off_proj;
   const float *W6 = P + n->off_fc;
-  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{ws + X.out32, Ar::NH, Ar::NH}, LdColMajor{ws + L.dH, Ar::F, -1},
-                                  EpStore{grad + n->off_fc, Ar::F}, Ar::NH + 1, Ar::F, W, 1, s)));
   hipLaunchKernelGGL((lstm_bwd_kernel<Ar::NH, Ar::STEPS>), dim3(W), dim3(Ar::G4), 0, s, ws + L.dH, Ar::F, W6, Wp,
                      Kh, ws + X.gates, ws + X.cst, ws + X.dout32, ws + X.dgates);
   MT_LAUNCHED();
-  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{ws + X.h5, Ar::NH, Ar::NH}, LdColMajor{ws + X.dout32, Ar::NH, -1},
-                                  EpStore{grad + n->off_proj, Ar::NH}, Ar::NH + 1, Ar::NH, W, 1, s)));
-  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{ws + X.hprev, Ar::NH, Ar::NH}, LdColMajor{ws + X.dgates, Ar::G4, -1},
-                                  EpStore{grad + n->off_lstm + (size_t)Ar::FLAT * Ar::G4, Ar::G4}, Ar::NH + 1,
-                                  Ar::G4, rows, 1, s)));
+  // the small weight gradients — K_h rows + bias [h_{t-1}, 1]^T dz, fc6 [out, 1]^T dH, the heads,
+  // the projection [h_5, 1]^T d out: a few blocks each, a serial walk of up to 10 K chunks — are off
+  // the critical path: they run beside conv4's backward (trunk_backward's extra jobs, longest walk
+  // first) instead of as four launches of their own (same products, same chunks)
+  const JobPack small{
+      gemm_job<TileDenseW>(LdColMajor{ws + X.hprev, Ar::NH, Ar::NH}, LdColMajor{ws + X.dgates, Ar::G4, -1},
+                           EpStore{grad + n->off_lstm + (size_t)Ar::FLAT * Ar::G4, Ar::G4}, Ar::NH + 1, Ar::G4, rows,
+                           1),
+      gemm_job<TileDenseW>(LdColMajor{ws + X.out32, Ar::NH, Ar::NH}, LdColMajor{ws + L.dH, Ar::F, -1},
+                           EpStore{grad + n->off_fc, Ar::F}, Ar::NH + 1, Ar::F, W, 1),
+      head_wgrad_job<Ar>(n, W, ws, L, grad),
+      gemm_job<TileDenseW>(LdColMajor{ws + X.h5, Ar::NH, Ar::NH}, LdColMajor{ws + X.dout32, Ar::NH, -1},
+                           EpStore{grad + n->off_proj, Ar::NH}, Ar::NH + 1, Ar::NH, W, 1)};
   // per-frame gate gradients (the zero frame: chunk partials first)
   hipLaunchKernelGGL(lstm_zero_partials_kernel, dim3(kZeroParts), dim3(Ar::G4), 0, s, ws + X.dgates, nz, W,
                      ws + X.zpart);
@@ -610,12 +620,14 @@ static int lstm_frames_bwd_impl(const mt_net *n, const float *P, const uint8_t *
   MT_LAUNCHED();
   constexpr int K = Ar::NCONV - 1;
   const float *flat = layer_out<Ar, K>(ws, L);
-  MT_TRY((launch_gemm<TileDenseW>(LdColMajor{flat, Ar::FLAT, -1}, LdColMajor{ws + X.dxg, Ar::G4, -1},
-                                  EpStore{grad + n->off_lstm, Ar::G4}, Ar::FLAT, Ar::G4, X.R_bwd, 1, s)));
-  MT_TRY((launch_gemm<TileDenseX>(LdRowMajor{ws + X.dxg, Ar::G4}, LdRowMajor{Kx, Ar::G4},
-                                  EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, X.R_bwd, Ar::FLAT, Ar::G4, 1,
-                                  s)));
-  return trunk_backward<Ar, K>(n, P, fstore, X.R_bwd, ws, L, grad, s);
+  // d flat = dxg K_x^T (masked by conv4's activation; the trunk's critical path, first) and the
+  // cell kernel's x rows [flat]^T dxg, one grouped launch
+  const auto dx = gemm_job<TileDenseX>(LdRowMajor{ws + X.dxg, Ar::G4}, LdRowMajor{Kx, Ar::G4},
+                                       EpMasked{ws + L.dact[K], flat, Ar::FLAT, act, al}, X.R_bwd, Ar::FLAT, Ar::G4, 1);
+  const auto kxw = gemm_job<TileDenseW>(LdColMajor{flat, Ar::FLAT, -1}, LdColMajor{ws + X.dxg, Ar::G4, -1},
+                                        EpStore{grad + n->off_lstm, Ar::G4}, Ar::FLAT, Ar::G4, X.R_bwd, 1);
+  MT_TRY(launch_group(s, dx, kxw));
+  return trunk_backward<Ar, K>(n, P, fstore, X.R_bwd, ws, L, grad, s, SlabJob{}, NormOut{}, small);
 }
 
 }  // namespace mt

@@ -1148,7 +1148,9 @@ static int trunk_forward(const mt_net *n, const float *P, const void *x, int B, 
 // Conv layers I .. 0 of the backward, top down: one grouped launch per layer — its dX (the
 // critical path, first), its dW GEMM and `pending` (the slab sum of layer I+1's dW) — then
 // conv1's slab sum. Layer I's slabs live in region I % 2 (wslab / wslab2), so the slab sum of
-// layer I+1 reads the other region while layer I's dW GEMM writes its own.
+// layer I+1 reads the other region while layer I's dW GEMM writes its own. `extra` (the LSTM's
+// small cell / fc6 weight gradients: a few blocks, each a serial K walk) leads the top layer's
+// grid, so its blocks start before the wide products fill the CUs instead of trailing them.
 // Optional global-norm partials of the whole gradient written by the backward's last launch
 // (world == 1: no all-reduce between the backward and the clip, so mt_grad_sumsq is not needed).
 struct NormOut {
@@ -1176,24 +1178,24 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
     if constexpr (pooled<Ar, J>() && G::S == 1 && G::SAME && dconv_bwd_solo<G>()) {  // direct dX launch, then dW
       MT_TRY((conv_dgrad_unpool_solo<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act, al, s)));
-      MT_TRY(launch_group(s, wg.gemm, pending, extra));
+      MT_TRY(launch_group(s, extra, wg.gemm, pending));
     } else if constexpr (stream_dx<G>()) {  // NATURE conv2: the weight-stationary streaming dX (nature_bwd.h)
-      MT_TRY(launch_group(s, DxStreamJob<G>{ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
+      MT_TRY(launch_group(s, extra, DxStreamJob<G>{ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
                                             dx_stream_groups<G>(B), act, al},
-                          wg.gemm, pending, extra));
+                          wg.gemm, pending));
     } else if constexpr (pooled<Ar, J>()) {
-      MT_TRY(launch_group(s, conv_dgrad_unpool_job<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
+      MT_TRY(launch_group(s, extra, conv_dgrad_unpool_job<G, GJ>(ws + L.dact[I], P + n->off_conv[I], ws + L.pool[J],
                                                            (const uint8_t *)(ws + L.parg[J]), ws + L.dact[J], B, act,
                                                            al),
-                          wg.gemm, pending, extra));
+                          wg.gemm, pending));
     } else {
-      MT_TRY(launch_group(s, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
+      MT_TRY(launch_group(s, extra, conv_dgrad_job<G>(ws + L.dact[I], P + n->off_conv[I], ws + L.act[J], ws + L.dact[J], B,
                                                act, al),
-                          wg.gemm, pending, extra));
+                          wg.gemm, pending));
     }
     return trunk_backward<Ar, J>(n, P, obs, B, ws, L, grad, s, wg.sum, no);
   } else {
-    MT_TRY(launch_group(s, wg.gemm, pending, extra));
+    MT_TRY(launch_group(s, extra, wg.gemm, pending));
     SlabJob last = wg.sum;
     if (no.partials && last.blocks() <= MT_NORM_PARTIALS / 2) {
       // conv1's slab sum writes the norm partials of its region, the rest of the gradient (complete
