@@ -142,17 +142,15 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
   constexpr int G4 = 4 * NH;
   __shared__ float hs[NH], as[G4], os[NH];
   const int b = blockIdx.x, g = threadIdx.x;
-  float wcol[NH];
-#pragma unroll
-  for (int k = 0; k < NH; ++k) wcol[k] = Kh[(size_t)k * G4 + g];
-  const float bias = kb[g];
   const int q = g / NH;  // 0 i, 1 j, 2 f, 3 o
   float c = 0.f;
   if (g < NH) hs[g] = 0.f;
-  // the x-product slab sums of all STEPS positions first (they do not depend on h): XB slabs x
-  // STEPS loads in flight per batch instead of one load latency per slab; adds in slab order
-  // (the frame store's x-product has 50 split-K slabs: batches of 8 were 7 load round trips, most
-  // of this kernel's 13.5 us per rollout step)
+  // Loads in the order they are consumed (a wave's loads return in issue order): the x-product
+  // slab sums of all STEPS positions first (they do not depend on h; XB slabs x STEPS loads in
+  // flight per batch, adds in slab order — the frame store's x-product has 50 split-K slabs), and
+  // behind the first batch every parameter of the recurrence and the epilogue (relaxed atomics:
+  // plain read-only loads are sunk to their use, behind the recurrence barriers — the projection
+  // bias was a load round trip of its own at the end); same products, same order below
   float zx[STEPS];
   size_t xoff[STEPS];
   const int z = map.zeros(b);
@@ -161,34 +159,41 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
     zx[t] = 0.f;
     xoff[t] = (size_t)map.row(b, t, z) * G4 + g;
   }
-  // the projection column (threads < NH) and fc6 columns of the epilogue, requested now with the
-  // slab partials (relaxed atomics: plain read-only loads are sunk to their use, behind the STEPS
-  // recurrence barriers, one load latency per 8 products there); same products, same order below
-  constexpr int NN = 1;  // fc6 columns per thread: F <= NN * G4 (the launch sites assert it)
-  float wpc[NH], w6c[NN][NH];
-  const int gp = min(g, NH - 1);
-#pragma unroll
-  for (int m = 0; m < NH; ++m)
-    wpc[m] = __hip_atomic_load(Wp + m * NH + gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-  for (int j = 0; j < NN; ++j) {
-    const int nn = min(g + G4 * j, F - 1);
-#pragma unroll
-    for (int k = 0; k < NH; ++k)
-      w6c[j][k] = __hip_atomic_load(W6 + (size_t)k * F + nn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   constexpr int XB = 25;
-  for (int s0 = 0; s0 < S; s0 += XB) {
-    float v[STEPS][XB];
+  float v[STEPS][XB];
+  auto load_batch = [&](int s0) {
 #pragma unroll
     for (int t = 0; t < STEPS; ++t)
 #pragma unroll
       for (int u = 0; u < XB; ++u) v[t][u] = xg[(size_t)min(s0 + u, S - 1) * rows * G4 + xoff[t]];
+  };
+  load_batch(0);
+  auto ld = [](const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  float wcol[NH];
+#pragma unroll
+  for (int k = 0; k < NH; ++k) wcol[k] = ld(Kh + (size_t)k * G4 + g);
+  const float bias = ld(kb + g);
+  constexpr int NN = 1;  // fc6 columns per thread: F <= NN * G4 (the launch sites assert it)
+  float wpc[NH], w6c[NN][NH];
+  const int gp = min(g, NH - 1);
+#pragma unroll
+  for (int m = 0; m < NH; ++m) wpc[m] = ld(Wp + m * NH + gp);
+  const float bpg = ld(bp + gp);
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    const int nn = min(g + G4 * j, F - 1);
+#pragma unroll
+    for (int k = 0; k < NH; ++k) w6c[j][k] = ld(W6 + (size_t)k * F + nn);
+  }
+  for (int s0 = 0;;) {
 #pragma unroll
     for (int t = 0; t < STEPS; ++t)
 #pragma unroll
       for (int u = 0; u < XB; ++u)
         if (s0 + u < S) zx[t] += v[t][u];
+    s0 += XB;
+    if (s0 >= S) break;
+    load_batch(s0);
   }
   __syncthreads();
 #pragma unroll
@@ -217,7 +222,7 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
     float o = 0.f;
 #pragma unroll
     for (int m = 0; m < NH; ++m) o += hs[m] * wpc[m];
-    o += bp[g];
+    o += bpg;
     os[g] = o;
     out32[(size_t)b * NH + g] = o;
   }
@@ -245,10 +250,13 @@ __global__ __launch_bounds__(128) void lstm_bwd_kernel(const float *__restrict__
   __shared__ float khs[NH * KS];              // is on bank (g + j) % 32, not all 32 threads on one
   __shared__ float dos[NH], dzs[G4];
   const int b = blockIdx.x, g = threadIdx.x;
-  for (int i = g; i < NH * G4; i += G4) khs[(i / G4) * KS + i % G4] = Kh[i];
-  // every operand of the window requested up front (relaxed atomics: plain read-only loads are
-  // sunk to their use — one load latency per step and per 8 products otherwise): the projection
-  // row, every step's gates and cell states; same products, same order below
+  // every operand of the window requested up front, K_h first (relaxed atomics: plain read-only
+  // loads are sunk to their use — one load latency per step and per 8 products otherwise; K_h's
+  // LDS copy was two round trips of its own before the rest were requested): K_h column g, the
+  // projection row, every step's gates and cell states; same products, same order below
+  float khv[NH];
+#pragma unroll
+  for (int k = 0; k < NH; ++k) khv[k] = __hip_atomic_load(Kh + (size_t)k * G4 + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int gc = min(g, NH - 1);
   float wpr[NH], gt[STEPS][4], cs[STEPS];
 #pragma unroll
@@ -260,21 +268,35 @@ __global__ __launch_bounds__(128) void lstm_bwd_kernel(const float *__restrict__
     for (int q = 0; q < 4; ++q) gt[t][q] = __hip_atomic_load(ga + q * NH + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     cs[t] = __hip_atomic_load(cst + (size_t)(b * STEPS + t) * NH + gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (g < NH) {  // d out = dH W6^T  (fc6 input gradient): 32 products' loads per trip, added in order
-    float a = 0.f;
-    const float *w = W6 + (size_t)g * F;
+  // d out = dH W6^T (fc6 input gradient) and each step's d h_{t-1} = dz K_h^T: NH outputs of long
+  // dot products, so all G4 = 4 NH threads take part — thread (q, o) sums quarter q of output o's
+  // terms (its loads in one trip), the quarters added in order by thread o through LDS
+  static_assert(G4 == 4 * NH && NH <= 64, "four quarter-threads per output");
+  __shared__ float part[4][NH];
+  const int q = g / NH, o = g - q * NH;
+  {
+    const int FQ = (F + 3) / 4, n0 = q * FQ, n1 = min(F, n0 + FQ);
+    const float *w = W6 + (size_t)o * F;
     const float *d = dH + (size_t)b * F;
-    for (int n0 = 0; n0 < F; n0 += 32) {
+    float a = 0.f;
+    for (int c0 = n0; c0 < n1; c0 += 32) {
       float dv[32], wv[32];
 #pragma unroll
       for (int u = 0; u < 32; ++u) {
-        dv[u] = d[min(n0 + u, F - 1)];
-        wv[u] = w[min(n0 + u, F - 1)];
+        dv[u] = d[min(c0 + u, F - 1)];
+        wv[u] = w[min(c0 + u, F - 1)];
       }
 #pragma unroll
       for (int u = 0; u < 32; ++u)
-        if (n0 + u < F) a += dv[u] * wv[u];
+        if (c0 + u < n1) a += dv[u] * wv[u];
     }
+    part[q][o] = a;
+  }
+#pragma unroll
+  for (int k = 0; k < NH; ++k) khs[k * KS + g] = khv[k];  // (after the dot's loads: one round trip)
+  __syncthreads();
+  if (g < NH) {
+    const float a = ((part[0][g] + part[1][g]) + part[2][g]) + part[3][g];
     dos[g] = a;
     dout32[(size_t)b * NH + g] = a;
   }
@@ -288,6 +310,7 @@ __global__ __launch_bounds__(128) void lstm_bwd_kernel(const float *__restrict__
   for (int t = STEPS - 1; t >= 0; --t) {
     const int row = b * STEPS + t;
     if (g < NH) {
+      if (t < STEPS - 1) dh = ((part[0][g] + part[1][g]) + part[2][g]) + part[3][g];
       const float si = gt[t][0], tj = gt[t][1], sf = gt[t][2], so = gt[t][3];
       const float c = cs[t];
       const float cp = t > 0 ? cs[t > 0 ? t - 1 : 0] : 0.f;
@@ -305,11 +328,11 @@ __global__ __launch_bounds__(128) void lstm_bwd_kernel(const float *__restrict__
     }
     __syncthreads();
     dgates[(size_t)row * G4 + g] = dzs[g];
-    if (g < NH) {  // d h_{t-1} = dz K_h^T
+    if (t > 0) {  // d h_{t-1} = dz K_h^T: quarter q of output o's terms
       float a = 0.f;
 #pragma unroll 8
-      for (int j = 0; j < G4; ++j) a += dzs[j] * khs[g * KS + j];
-      dh = a;
+      for (int j = q * NH; j < (q + 1) * NH; ++j) a += dzs[j] * khs[o * KS + j];
+      part[q][o] = a;
     }
     __syncthreads();
   }
