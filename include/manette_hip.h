@@ -167,7 +167,9 @@ int mt_forward_trunk_stacking(const mt_net *net, const float *params, const uint
  *    rollout (mt_rollout_*) runs the same forward with the draw fused into its heads kernel;
  *  - mt_lstm_frames_backward: loss + gradient of the T*E windows of steps 0..T-1 (the train
  *    step of paac.py:254-256) from the rollout's activations (unchanged parameters), with pi,
- *    rep, v [T*E] the rollout outputs; back-propagates through each distinct frame once. */
+ *    rep, v [T*E] the rollout outputs; back-propagates through each distinct frame once.
+ *    norm_partials (optional, [MT_NORM_PARTIALS]): as mt_returns_loss_backward's — the global-norm
+ *    partials of the whole gradient from the backward's last launch (no mt_grad_sumsq needed). */
 int mt_lstm_frames_workspace_bytes(const mt_net *net, int E, int T, size_t *bytes);
 int mt_lstm_frames_forward(const mt_net *net, const float *params, const uint8_t *fstore, int row0, int nrows,
                            int E, int T, void *ws, size_t ws_bytes, mt_stream_t stream);
@@ -180,7 +182,7 @@ int mt_lstm_frames_backward(const mt_net *net, const float *params, const uint8_
                             int E, int T, void *ws, size_t ws_bytes, const float *pi, const float *rep,
                             const float *v, const int32_t *a_idx, const int32_t *r_idx, const float *y,
                             const float *adv, float entropy_beta, float *grad, float *loss_terms,
-                            mt_stream_t stream);
+                            float *norm_partials, mt_stream_t stream);
 
 /* ---- device multinomial sampling (perf mode of A3) -----------------------------------------
  * Replaces ExplorationPolicy.multinomial_choose (exploration_policy.py:108-116) with an

@@ -73,7 +73,7 @@ _HIP_SIGS = {
     'mt_lstm_frames_forward': (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),
     'mt_lstm_windows_forward': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P, _P, _P, _P]),
     'mt_lstm_step_forward': (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _SZ, _P, _P, _P, _P]),
-    'mt_lstm_frames_backward': (_I, [_P, _P, _P, _P, _I, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
+    'mt_lstm_frames_backward': (_I, [_P, _P, _P, _P, _I, _I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P]),
     'mt_forward_rows': (_I, [_P, _P, _P, _I, _P, _SZ, _P, _SZ, _I, _I, _P, _P, _P, _P]),
     'mt_forward_trunk': (_I, [_P, _P, _P, _I, _P, _SZ, _P]),
     'mt_forward_trunk_stacking': (_I, [_P, _P, _P, _P, _P, C.c_uint32, _P, _I, _P, _SZ, _P, _P]),

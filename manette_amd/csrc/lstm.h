@@ -603,7 +603,8 @@ template <class Ar>
 static int lstm_frames_bwd_impl(const mt_net *n, const float *P, const uint8_t *fstore, const int32_t *nz, int E,
                                 int T, float *ws, const float *pi, const float *rep, const float *v,
                                 const int32_t *a_idx, const int32_t *r_idx, const float *y, const float *adv,
-                                float beta, float *grad, float *loss_terms, hipStream_t s) {
+                                float beta, float *grad, float *loss_terms, hipStream_t s,
+                                const NormOut &no = NormOut{}) {
   const LstmFrameWs X = lstm_frame_layout<Ar>(n, E, T);
   const WsLayout &L = X.L;
   const int W = T * E, rows = W * Ar::STEPS;
@@ -650,7 +651,7 @@ static int lstm_frames_bwd_impl(const mt_net *n, const float *P, const uint8_t *
   const auto kxw = gemm_job<TileDenseW>(LdColMajor{flat, Ar::FLAT, -1}, LdColMajor{ws + X.dxg, Ar::G4, -1},
                                         EpStore{grad + n->off_lstm, Ar::G4}, Ar::FLAT, Ar::G4, X.R_bwd, 1);
   MT_TRY(launch_group(s, dx, kxw));
-  return trunk_backward<Ar, K>(n, P, fstore, X.R_bwd, ws, L, grad, s, SlabJob{}, NormOut{}, small);
+  return trunk_backward<Ar, K>(n, P, fstore, X.R_bwd, ws, L, grad, s, SlabJob{}, no, small);
 }
 
 }  // namespace mt

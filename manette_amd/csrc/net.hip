@@ -1988,14 +1988,17 @@ extern "C" int mt_lstm_frames_backward(const mt_net *net, const float *params, c
                                        const int32_t *nz, int E, int T, void *ws, size_t ws_bytes, const float *pi,
                                        const float *rep, const float *v, const int32_t *a_idx, const int32_t *r_idx,
                                        const float *y, const float *adv, float entropy_beta, float *grad,
-                                       float *loss_terms, mt_stream_t stream) {
+                                       float *loss_terms, float *norm_partials, mt_stream_t stream) {
   MT_CHECK_ARG(net && params && fstore && nz && ws && pi && rep && v && a_idx && r_idx && y && adv && grad,
                "null argument");
   MT_CHECK_ARG(E >= 1 && T >= 1, "E and T must be >= 1");
   MT_LSTM_ONLY(net, {
     MT_LSTM_WS(E, T);
+    NormOut no;
+    no.partials = norm_partials;
+    no.n = net->nparams;
     return lstm_frames_bwd_impl<Ar>(net, params, fstore, nz, E, T, (float *)ws, pi, rep, v, a_idx, r_idx, y, adv,
-                                    entropy_beta, grad, loss_terms, (hipStream_t)stream);
+                                    entropy_beta, grad, loss_terms, (hipStream_t)stream, no);
   });
   return MT_OK;
 }

@@ -275,13 +275,15 @@ class DeviceNetwork(object):
                                               _stream()), 'mt_lstm_step_forward')
         return v, pi, rep
 
-    def lstm_frames_backward(self, fstore, nz, E, T, pi, rep, v, a_idx, r_idx, y, adv, loss_terms=None):
-        """Gradient of the T*E windows of the last rollout into self.grad."""
+    def lstm_frames_backward(self, fstore, nz, E, T, pi, rep, v, a_idx, r_idx, y, adv, loss_terms=None,
+                             norm_partials=False):
+        """Gradient of the T*E windows of the last rollout into self.grad. norm_partials: as
+        returns_loss_backward's (the global-norm partials left in self.partials; single process)."""
         ws = self.lstm_workspace(E, T)
         check(_lib.hip().mt_lstm_frames_backward(
             self._h, _ptr(self.params), _ptr(fstore), _ptr(nz), int(E), int(T), _ptr(ws), ws.numel(), _ptr(pi),
             _ptr(rep), _ptr(v), _ptr(a_idx), _ptr(r_idx), _ptr(y), _ptr(adv), self.beta, _ptr(self.grad),
-            _ptr(loss_terms), _stream()), 'mt_lstm_frames_backward')
+            _ptr(loss_terms), _ptr(self.partials if norm_partials else None), _stream()), 'mt_lstm_frames_backward')
         return self.grad
 
     def loss_backward(self, obs, B, v, pi, rep, a_idx, r_idx, y, adv, loss_terms=None, ws_key=None):

@@ -497,7 +497,7 @@ class PAACLearner(ActorLearner):
             # through each distinct frame once
             net.lstm_frames_backward(self.fstore, self.nz_d[:T], E, T, self.pi_all[:T], self.rep_all[:T],
                                      self.values, self.idx[0].view(N), self.idx[1].view(N), self.y.view(N),
-                                     self.adv.view(N), loss_terms=self.loss_terms)
+                                     self.adv.view(N), loss_terms=self.loss_terms, norm_partials=not self.dp)
             return
         # the rollout's forwards already left every row's activations in the train workspace
         # (mt_forward_rows, row t*E + e as paac.py:236)
@@ -508,8 +508,7 @@ class PAACLearner(ActorLearner):
 
     def _update_apply(self):
         T = self.max_local_steps
-        self.network.apply_gradients(self.grad_scale,
-                                     partials_ready=not self.dp and not self.lstm_bool)
+        self.network.apply_gradients(self.grad_scale, partials_ready=not self.dp)
         if self.lstm_bool:  # the next rollout's slots 0..4 = s_{T-4} .. s_T; windows carry over
             if T >= 5:
                 self.slots[0:5].copy_(self.slots[T:T + 5])
