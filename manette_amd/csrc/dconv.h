@@ -1059,6 +1059,17 @@ static int conv_dgrad_unpool_solo(const float *dY, const float *Wt, const float 
 // offset from a per-lane base (the (tap, ci) of row 16 m + r is decomposed once).
 constexpr size_t kDwSlabCap = (size_t)4 << 20;  // slab floats (the generic path's kSlabFloats)
 
+// Small-channel patches (conv1: 4 / 12 u8 channels): no channel pad (16-B pixel quads, one LDS store
+// each) and the patch row stride padded instead, to the first whose offset puts lane group g = 1 on
+// the other 16 banks — an A read of these M-tiles spans several taps of one row, so a channel pad
+// cannot separate the groups (bank model of the A reads: 3.7 -> 2.9 LDS cycles per read gray, 3.9
+// -> 2.3 RGB)
+constexpr int dw_row_stride(int cs, int wp) {
+  int w = wp;
+  while ((w * cs) % 32 != 16) ++w;
+  return w;
+}
+
 constexpr int dw_pad(int c, int wd) {  // channel stride whose row stride wd * cs puts lane group g = 1
   int best = c, bd = 99;               // on the other 16 banks (|(wd cs) % 32 - 16| smallest)
   for (int p = 0; p < 16; ++p) {
@@ -1089,8 +1100,10 @@ struct DWCfg {
   static constexpr int KQ = WPAD / 4;              // 16-k steps per chunk
   static constexpr int WP = (WPAD - 1) * S + KW;   // patch columns
   static constexpr int RIN = (R - 1) * S + KH;     // patch rows
-  static constexpr int CS = dw_pad(CIN, S * WP), COS = dw_pad(COUT, WPAD);
-  static constexpr int XSZ = (RIN * WP * CS + 3) / 4 * 4, YSZ = R * WPAD * COS;
+  static constexpr bool SMALLC = CIN < 16 && CIN % 4 == 0 && S == 1;
+  static constexpr int CS = SMALLC ? CIN : dw_pad(CIN, S * WP), COS = dw_pad(COUT, WPAD);
+  static constexpr int WPX = SMALLC ? dw_row_stride(CS, WP) : WP;  // patch row stride (pixels)
+  static constexpr int XSZ = (RIN * WPX * CS + 3) / 4 * 4, YSZ = R * WPAD * COS;
   static constexpr size_t LDS = (size_t)(XSZ + YSZ) * 4;
   static constexpr int XQ = RIN * WP * (CIN / 4), YQ = R * WPAD * (COUT / 4);  // quads per chunk
   static constexpr int XIT = (XQ + 255) / 256, YIT = (YQ + 255) / 256;
@@ -1124,7 +1137,7 @@ struct DWgradJob {
     for (int i = 0; i < TMW; ++i) {
       const int row = min(16 * (tg * D::MPB + wm + D::WROWS * i) + r, D::KK - 1);  // (rows >= KK: not stored)
       const int t = row / D::CIN, ci = row - t * D::CIN, ky = t / D::KW, kx = t - ky * D::KW;
-      abase[i] = ((g * D::S + ky) * D::WP + kx) * D::CS + ci;
+      abase[i] = ((g * D::S + ky) * D::WPX + kx) * D::CS + ci;
     }
     const int bbase = g * D::WPAD * D::COS + 16 * j + r;
 
@@ -1160,9 +1173,14 @@ struct DWgradJob {
         const int item = tid + 256 * it;
         if (D::XQ % 256 == 0 || item < D::XQ) {
           const int pix = item / (D::CIN / 4), cq = item - pix * (D::CIN / 4);
-          float *d = Xs + pix * D::CS + 4 * cq;  // (CS % 4 may be != 0: four dword stores)
+          const int pr = pix / D::WP, pc = pix - pr * D::WP;
+          float *d = Xs + (pr * D::WPX + pc) * D::CS + 4 * cq;
+          if constexpr (D::CS % 4 == 0) {
+            *reinterpret_cast<f32x4 *>(d) = xr[it];
+          } else {  // (four dword stores)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) d[e] = xr[it][e];
+            for (int e = 0; e < 4; ++e) d[e] = xr[it][e];
+          }
         }
       }
 #pragma unroll
