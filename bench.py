@@ -227,7 +227,7 @@ def build_args(cfg, T, sampling, seed, debugging_folder=None):
 
 
 def make_learner(config, T=5, sampling='device', seed=0, staging='resized', pipeline=True, update_graph=True,
-                 rank=0, debugging_folder=None, episode_len=None, comm='rccl', dp_force=False):
+                 rank=0, debugging_folder=None, episode_len=None, comm='rccl', dp_force=False, pin_threads='auto'):
     """The benchmarked learner of `config` (BASELINE.json configs[1..4]; tests/test_e2e_gpu.py
     checks exactly this path against the oracle). episode_len: a shorter synthetic episode (tests
     exercise resets); None = the synthetic default. dp_force: the data-parallel update (bucketed
@@ -243,6 +243,7 @@ def make_learner(config, T=5, sampling='device', seed=0, staging='resized', pipe
     args.update_graph = update_graph
     args.comm = comm
     args.dp_force = dp_force
+    args.pin_threads = pin_threads
     np.random.seed(1234 + rank)
     explo = ExplorationPolicy(args)
     net_creator, env_creator = train_cli.get_network_and_environment_creator(args, explo)
@@ -402,6 +403,9 @@ def main():
                     help='the data-parallel update at world 1 (RCCL communicator, bucketed side-stream all-reduce '
                          'between three update graphs, the learner launching the update): the per-GPU cost of the '
                          'N-GPU path (paac.PAACLearner.dp)')
+    ap.add_argument('--pin_threads', default='auto', choices=['auto', 'on', 'off'],
+                    help='host-thread placement (manette_amd/placement.py); auto: pinned when several ranks share '
+                         'the node')
     ap.add_argument('--settle_s', type=float, default=1.0,
                     help='seconds of untimed updates before the warmup steps (host emulator threads, CPU clocks and '
                          'the graphs reach their steady state; the 5-update warmup of a 20-update run did not)')
@@ -420,7 +424,7 @@ def main():
     cfg = CONFIGS[a.config]
     T = a.t_max
     learner, args = make_learner(a.config, T, a.sampling, a.seed, a.staging, a.pipeline, a.update_graph, rank,
-                                 comm=a.comm, dp_force=a.dp_force)
+                                 comm=a.comm, dp_force=a.dp_force, pin_threads=a.pin_threads)
     learner.start()
     learner_dp = learner.dp
     if a.step_impl == 'python' and learner.native_step is not None:
@@ -437,6 +441,11 @@ def main():
     # W warmup steps and the K timed ones start from the steady state; the graphs are captured and
     # registered within the first 3 updates, the rest is the host side (emulator threads' caches and
     # clocks) — a 5-update warmup left the r04 driver run ramping 603k -> 713k over its 20 updates
+    if world > 1 or learner_dp:  # the first update's all-reduce, bounded like the communicator's setup
+        from manette_amd import comm as comm_
+        with comm_.Deadline('the first data-parallel update (all-reduce of the gradient)', rank, world):
+            one_update()
+            torch.cuda.synchronize()
     settle = settle_updates(one_update, a.settle_s, world, dist)
     for _ in range(a.warmup):
         one_update()
@@ -450,6 +459,9 @@ def main():
         from manette_amd import _lib
         stats = (C.c_double * 7)()
         _lib.hip().mt_rollout_stats_ex(learner.native_step, stats, 7, 1)
+    runner_stats = getattr(learner.runners, 'stats', None)  # (native runner) host-phase split
+    if runner_stats:
+        runner_stats(reset=True)
     w = max(1, a.steps // 4)  # sub-windows of the timed region
     win_stats = []  # per sub-window: the host phases of its macro-steps (read + reset at its end)
     t0 = time.perf_counter()
@@ -464,6 +476,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    emu_split = runner_stats() if runner_stats else None
     if stats is not None:
         _lib.hip().mt_rollout_stats_ex(learner.native_step, stats, 7, 0)
         tot = [sum(ws_[i] for ws_ in win_stats) + stats[i] for i in range(7)]
@@ -482,6 +495,14 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    # host-thread placement of every rank (manette_amd/placement.py): cores, threads, pinning
+    from manette_amd import placement as placement_
+    threads = placement_.report(learner.placement) if learner.placement else None
+    if world > 1:
+        every_threads = [None] * world
+        dist.all_gather_object(every_threads, threads)
+    else:
+        every_threads = [threads]
     # ---- measurements after the timed region (none of them is part of `value`) ----------------
     prof = {}
     # (1) roofline kernels where the timed loop runs them: the native rollout records an event
@@ -528,8 +549,8 @@ def main():
     # the update's train pass (fused returns + loss + backward of the last rollout)
     bwd = learner.train_backward if learner.lstm_bool else learner._update_backward
     prof['train_pass'] = graph_time(bwd, 20, label='train_pass')
-    # (the LSTM backward has launches outside the budgeted grouped launches: no breakdown)
-    prof['train_launches'] = None if learner.lstm_bool else launch_breakdown(bwd)[0]
+    # launch by launch (mt_launch_window numbers every launch of the backward, LSTM included)
+    prof['train_launches'] = launch_breakdown(bwd)[0]
     # A11: clip + RMSProp alone (the norm partials the backward left; world > 1 adds mt_grad_sumsq)
     prof['clip_rmsprop'] = graph_time(lambda: net.apply_gradients(partials_ready=True), 40, label='clip_rmsprop')
     gen = torch.Generator(device='cuda').manual_seed(11)
@@ -544,6 +565,24 @@ def main():
     from manette_amd import network as devnet_
     prof['stack'] = graph_time(lambda: devnet_.preprocess(pushes, offs, cnt_d, E, depth_, None, None, learner.states[0],
                                                           stk_out, resized=True), 40, label='stack')
+    # A2 on the GPU in full (the north star's placement): each push's two raw screens -> frame-pool max
+    # -> nearest 84x84 -> stack (mt_preprocess), reading (a) whole 210x160 screens in HBM, (b) the 84
+    # screen rows the resize reads from pinned host memory over PCIe in place (the zero_copy staging)
+    from manette_amd.environment import ROW_LUT as ROW_LUT_
+    raw_hbm = torch.randint(0, 256, (4 * E, 2, 210, 160 * depth_), dtype=torch.uint8, device='cuda', generator=gen)
+    rows_d = torch.from_numpy(ROW_LUT_.astype(np.int32)).cuda()
+    ident_d = torch.arange(84, dtype=torch.int32, device='cuda')
+    cols_d = learner.col_lut
+    prof['preprocess_raw_hbm'] = graph_time(
+        lambda: devnet_.preprocess(raw_hbm, offs, cnt_d, E, depth_, rows_d, cols_d, learner.states[0], stk_out,
+                                   src_rows=210), 40, label='preprocess_raw_hbm')
+    raw_pin = torch.empty((4 * E, 2, 84, 160 * depth_), dtype=torch.uint8, pin_memory=True)
+    raw_pin.copy_(raw_hbm[:, :, :84].cpu())
+    raw_pin_dev = devnet_.host_device_pointer(raw_pin)
+    prof['preprocess_raw_pinned'] = graph_time(
+        lambda: devnet_.preprocess(raw_pin_dev, offs, cnt_d, E, depth_, ident_d, cols_d, learner.states[0], stk_out,
+                                   src_rows=84), 40, label='preprocess_raw_pinned')
+    del raw_hbm
     if learner.lstm_bool:  # a step's new frames (trunk + cell x-product), + its E windows
         roll_fwd = lambda: learner._lstm_forward(1, learner.v_boot)
         roll_trunk = lambda: net.lstm_frames_forward(learner.fstore, 1 + 5 * E, E, E, T)
@@ -677,30 +716,56 @@ def main():
         kernels = [row('A2', 'atari_emulator.py:79-124, environment.py:58-80', 'preprocess_kernel (resized: stacking only)',
                        med(prof['stack']), stack_bytes,
                        note='standalone mt_preprocess_resized of the E envs (%d pushes); %s' % (stack_pushes, graph_note))]
-        if stacking or frame_stack:
+        # the whole A2 on the GPU: per push the 84 screen rows the nearest resize reads, of both screens
+        # (2 x 84 x 160 x depth B: whole lines, the kernel's 16-B loads), + the stack's bytes
+        raw_bytes = stack_pushes * 2 * 84 * 160 * depth + stack_bytes - stack_pushes * frame
+        kernels.append(row('A2 (GPU pool + resize + stack, HBM)', 'atari_emulator.py:79-124, environment.py:58-80',
+                           'preprocess_kernel (mt_preprocess: 2 raw 210x160 screens per push -> max -> nearest '
+                           '84x84 -> 4-frame stack)', med(prof['preprocess_raw_hbm']), raw_bytes,
+                           note='raw screens resident in HBM; the same E envs and pushes as A2; ' + graph_note))
+        pin_row = row('A2 (GPU pool + resize + stack, pinned host)', 'atari_emulator.py:79-124',
+                      'preprocess_kernel (mt_preprocess on the zero_copy staging: the 84 resize rows of both screens '
+                      'read over PCIe in place)', med(prof['preprocess_raw_pinned']), raw_bytes,
+                      note='the bytes cross PCIe (achieved_gbs is the PCIe-inclusive rate; frac vs HBM is not its '
+                           'bound); ' + graph_note)
+        kernels.append(pin_row)
+        if (stacking or frame_stack) and cfg['arch'] == 'NIPS':
+            # (NIPS only: its plain trunk is the same kernel without the stack, nips_conv_kernel<C, false>;
+            # NATURE's / PWYX's plain trunks are other kernels — the layered direct convs — so a difference
+            # of the two would not be the stack's cost: round 5 printed -1.57 us for Seaquest)
             share = (med(prof['rollout_trunk']) - med(prof['plain_trunk']))
-            kernels.append({'row': 'A2 (fused)', 'kernel': 'stacking share of %s' % (
-                                'nips_conv_kernel<%d, true>' % C_in if cfg['arch'] == 'NIPS' else
-                                'nature_chain_kernel' if cfg['arch'] == 'NATURE' else 'stack_conv1_kernel'),
-                            'us': round(share, 2), 'note': 'stacking trunk minus the same trunk on a resident state '
-                            '(mt_forward_trunk): the cost of the in-kernel stack in the benchmarked chain'})
+            kernels.append({'row': 'A2 (fused)', 'kernel': 'stacking share of nips_conv_kernel<%d, true>' % C_in,
+                            'us': round(share, 2), 'note': 'stacking trunk minus the same kernel on a resident state '
+                            '(nips_conv_kernel<%d, false> + the dense kernel): the cost of the in-kernel stack in '
+                            'the benchmarked chain' % C_in})
         tl = prof['train_launches']
         if tl:
             boot = 4 * 9 * ec * F_ if stacking else 0
             loss_bytes = 4 * N * (2 * F_ + 2 * O_ + 4 + 6) + 4 * (F_ + 1) * O_ + boot
-            kernels.append(row('A9+A10', 'paac.py:219-231, policy_v_network.py:25-74', 'loss_bwd_kernel (n-step scan'
-                               + (' + V(s_T) from the bootstrap slabs' if stacking else '') + ' + loss + head dz / dH)',
+            loss_name = ('loss_bwd_kernel (loss + head dz / dH of the T*E windows; the LSTM update runs the n-step '
+                         'scan in returns_kernel before its backward)' if lstm else
+                         'loss_bwd_kernel (n-step scan' + (' + V(s_T) from the bootstrap slabs' if stacking else '')
+                         + ' + loss + head dz / dH)')
+            kernels.append(row('A10' if lstm else 'A9+A10', 'paac.py:219-231, policy_v_network.py:25-74', loss_name,
                                tl[0], loss_bytes, note='launch 1 of the update backward (bench.launch_breakdown)'))
-            nconv = len(trunk) - 1
+            nconv = sum(1 for l in layers if l[0] == 'conv')
             if cfg['arch'] == 'NIPS' and not cfg['rgb']:  # the fused NIPS conv backward (nips_bwd.h)
                 names = ['dense dX + head dW + dense dW',
                          'nips_conv_bwd_kernel (conv2 dX, conv1 dW + db per image; conv2 dW + db per image pair)',
                          'conv1 + conv2 slab sums + global-norm partials']
             else:
-                names = ['dense dX + head dW + dense dW']
+                if lstm:  # mt_lstm_frames_backward (lstm.h lstm_frames_bwd_impl), then the frame trunk's
+                    names = ['lstm_bwd_kernel (BPTT of the T*E windows, dz of the gates)',
+                             'lstm_zero_partials_kernel (the zero frame\'s gate-gradient partials)',
+                             'lstm_gather_dxg_kernel (per-frame gate-gradient sums)',
+                             'd flat = dxg K_x^T (conv4 act mask) + K_x dW']
+                else:
+                    names = ['dense dX + head dW + dense dW']
                 for i in range(nconv - 1, -1, -1):
                     sfx = ' + conv%d slab sum' % (i + 2) if i < nconv - 1 else ''
-                    if i > 0 and cfg['arch'] == 'PWYX' and i == 1:  # its own direct dX launch (dconv.h dconv_bwd_solo)
+                    if lstm and i == nconv - 1:
+                        sfx += ' + K_h / fc6 / heads / projection dW (leading jobs)'
+                    if i > 0 and cfg['arch'] in ('PWYX', 'LSTM') and i == 1:  # its own direct dX (dconv_bwd_solo)
                         names += ['conv2 dX (direct conv)', 'conv2 dW' + sfx]
                     else:
                         names.append(('conv%d dX + conv%d dW' % (i + 1, i + 1) if i > 0 else 'conv1 dW') + sfx)
@@ -783,6 +848,12 @@ def main():
                                       'window\'s per-macro-step host phases (launch_and_wait = the GPU chain as the '
                                       'host sees it, emulators = the emulator threads)'},
         }
+        line['host_threads'] = {'per_rank': every_threads,
+                                'note': 'emulator worker threads + the host thread of each rank: its cpu slice '
+                                        '(the allowed cpus on its GPU\'s NUMA node, split between the local ranks '
+                                        'sharing it), the cores it may use (slice, container quota / local ranks), '
+                                        'ew after the oversubscription cap, and whether they were pinned '
+                                        '(--pin_threads auto: only with several ranks per node)'}
         if replicas is not None:
             line['replicas_identical'] = replicas
         if allreduce is not None:
@@ -799,6 +870,16 @@ def main():
                  'flop_frac': round(Eb * per_env_flops / (ms * 1e-3) / 1e12 / MI355X_FP32_TFLOPS, 4)}
                 for Eb, ms in sweep]
         if step_phases:
+            if emu_split:  # what the emulator threads spend per step (averaged over workers)
+                step_phases['emulator_threads'] = {
+                    'staging_us_per_worker': round(emu_split['stage_us'], 2),
+                    'busy_us_per_worker': round(emu_split['busy_us'], 2),
+                    'workers': learner.workers,
+                    'note': 'per worker per macro-step: staging = %s; busy = the whole step phase (staging + '
+                            'the synthetic emulation, FiGAR repeats and per-env publication); emulators_us = the '
+                            'step\'s wall time to its last worker' % (
+                                'frame pool + nearest resize + streaming copy of each push\'s 84x84 frame'
+                                if a.staging == 'resized' else 'the copy of the staged screen rows')}
             line['macro_step_host_us'] = step_phases
         if world == 1 and not a.no_cpu_baseline:
             learner.cleanup()

@@ -427,7 +427,8 @@ int mt_rollout_trunk_timing(mt_rollout *ro, int enable, double *sum_us, int64_t 
  * into *lr_host (the pinned LR word the RMSProp kernel reads) and launches graph_exec (the update:
  * loss backward [, all-reduce], clip + RMSProp) on the rollout's stream, right behind the bootstrap
  * chain: the update then starts with no host round trip after the last emulator step (the caller
- * must not launch it again). graph_exec NULL unregisters (before destroying the graph). */
+ * must not launch it again). graph_exec NULL unregisters every registered update, this form's and a
+ * data-parallel one (mt_rollout_set_update_dp), before the graphs are destroyed. */
 int mt_rollout_set_update(mt_rollout *ro, void *graph_exec, float *lr_host, double initial_lr,
                           double annealing_steps);
 
@@ -479,7 +480,7 @@ int mt_rollout_set_update_dp(mt_rollout *ro, void *const *graph_execs, mt_comm *
 int mt_sum_slabs(const float *parts, int nslabs, size_t n, float *out, mt_stream_t stream);
 
 /* Launch window: after mt_launch_window(first, count), first >= 0, the library numbers its grouped
- * launches and loss-kernel launches from 0 in issue order and issues only those with index in
+ * launches, loss-kernel launches and every launch of mt_lstm_frames_backward from 0 in issue order and issues only those with index in
  * [first, first + count) (count < 0: no upper end); the others return MT_OK without launching.
  * mt_launch_window(-1, -1), the default, turns it off. Used while CAPTURING: one
  * mt_returns_loss_backward* call recorded as two graphs, [0, 2) = the loss + the dense / head

@@ -51,6 +51,21 @@ int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_rep, int n_re
                      const uint8_t *screens, int ring, size_t frame_bytes, const float *rewards,
                      int reward_len, int episode_len, const int32_t *row_select, int n_rows,
                      int flags, mh_runner **out);
+/* Thread placement of the worker pool (one process per GPU sharing a node's cores; the reference's
+ * runners.py:11-18 starts `ew` processes and leaves placement to the OS): worker w is pinned to
+ * cpus[w] (w < n_cpus; the caller passes cores of its GPU's NUMA node not used by its own thread),
+ * and idle workers spin spin_us microseconds of wall time before sleeping on the generation word
+ * (2000 by default; the learner lowers it when the node's cores are oversubscribed). */
+int mh_runner_set_threads(mh_runner *r, const int32_t *cpus, int n_cpus, int spin_us);
+/* Diagnostics: out[w] = the one cpu worker w may run on, or -1 when several are allowed; returns
+ * the worker count (or -1 on error). */
+int mh_runner_thread_cpus(mh_runner *r, int32_t *out, int n);
+/* Host-phase split of the steps since the last reset (diagnostics, bench.py): out[0] = worker time
+ * in staging per worker per step (us: the frame pool + resize + the streaming copy of resized
+ * staging, or the row copies of the other modes), out[1] = worker time in the whole step phase per
+ * worker per step (us; the rest is the synthetic emulation and the per-env publication), out[2] =
+ * steps counted. reset != 0 zeroes the counters after reading. */
+int mh_runner_stats(mh_runner *r, double *out, int n, int reset);
 /* The resize's column LUT (84 source columns, increasing) for MH_RUNNER_RESIZED. */
 int mh_runner_set_col_lut(mh_runner *r, const int32_t *col_lut, int n_cols);
 void mh_runner_destroy(mh_runner *r);

@@ -129,6 +129,9 @@ _HOST_SIGS = {
     'mh_runner_env_state': (_I, [_P, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     'mh_crc32c': (C.c_uint32, [_P, _SZ, C.c_uint32]),
     'mh_runner_set_col_lut': (_I, [_P, _P, _I]),
+    'mh_runner_set_threads': (_I, [_P, _P, _I, _I]),
+    'mh_runner_thread_cpus': (_I, [_P, _P, _I]),
+    'mh_runner_stats': (_I, [_P, _P, _I, _I]),
     'mh_runner_set_ready': (_I, [_P, _P, C.c_uint32]),
     'mh_runner_step_begin': (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
     'mh_runner_step_end': (_I, [_P, C.POINTER(_I)]),

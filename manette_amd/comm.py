@@ -14,11 +14,52 @@ The C-ABI communicators (RcclComm, LoopbackComm) carry `_h`, the mt_comm handle 
 launches the data-parallel update with (mt_rollout_set_update_dp).
 """
 import ctypes as C
+import os
+import sys
+import threading
+import time
 
 import torch
 
 from . import _lib
 from ._lib import check
+
+# Bound on the communicator's setup and on the first update's all-reduce (seconds): RCCL's init and
+# collectives block until every rank arrives, so a rank that never starts (or died) would hang the
+# whole job; past this bound the process prints what it waited for and exits with status 3.
+DEFAULT_TIMEOUT_S = 300.0
+
+
+class Deadline(object):
+    """Context manager: if the block has not finished within `seconds` (MT_COMM_TIMEOUT_S, default
+    DEFAULT_TIMEOUT_S), a watchdog thread writes '<what> did not complete ...' to stderr and ends
+    the process with os._exit(exit_code) — a blocked RCCL call cannot be interrupted from Python,
+    and a non-zero exit is what the launcher (torch.distributed.run) turns into a failed job."""
+
+    def __init__(self, what, rank=0, world=1, seconds=None, exit_code=3):
+        self.what, self.rank, self.world, self.exit_code = what, rank, world, exit_code
+        self.seconds = float(os.environ.get('MT_COMM_TIMEOUT_S', DEFAULT_TIMEOUT_S)) if seconds is None else seconds
+        self._done = threading.Event()
+        self._t = None
+
+    def _watch(self):
+        if not self._done.wait(self.seconds):
+            sys.stderr.write('manette: %s did not complete within %.0f s on rank %d of %d (a rank never arrived '
+                             'or died): exiting\n' % (self.what, self.seconds, self.rank, self.world))
+            sys.stderr.flush()
+            os._exit(self.exit_code)
+
+    def __enter__(self):
+        self._t0 = time.perf_counter()
+        self._t = threading.Thread(target=self._watch, name='manette-deadline', daemon=True)
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._done.set()
+        self._t.join()
+        self.elapsed = time.perf_counter() - self._t0
+        return False
 
 
 def _stream():
@@ -35,12 +76,13 @@ class RcclComm(object):
         uid = C.create_string_buffer(_lib.MT_COMM_UID_BYTES)
         if rank == 0:
             check(lib.mt_comm_unique_id(uid), 'mt_comm_unique_id')
-        if world > 1:
-            box = [uid.raw if rank == 0 else None]
-            dist.broadcast_object_list(box, src=0)
-            C.memmove(uid, box[0], _lib.MT_COMM_UID_BYTES)
         h = C.c_void_p()
-        check(lib.mt_comm_init(uid, int(rank), int(world), int(device_index), C.byref(h)), 'mt_comm_init')
+        with Deadline('RCCL communicator setup (unique id exchange + mt_comm_init)', rank, world):
+            if world > 1:
+                box = [uid.raw if rank == 0 else None]
+                dist.broadcast_object_list(box, src=0)
+                C.memmove(uid, box[0], _lib.MT_COMM_UID_BYTES)
+            check(lib.mt_comm_init(uid, int(rank), int(world), int(device_index), C.byref(h)), 'mt_comm_init')
         self._h = h
         self.rank, self.world = rank, world
 

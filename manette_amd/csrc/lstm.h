@@ -619,9 +619,13 @@ static int lstm_frames_bwd_impl(const mt_net *n, const float *P, const uint8_t *
   const float *Kh = Kx + (size_t)Ar::FLAT * Ar::G4;
   const float *Wp = P + n->off_proj;
   const float *W6 = P + n->off_fc;
-  hipLaunchKernelGGL((lstm_bwd_kernel<Ar::NH, Ar::STEPS>), dim3(W), dim3(Ar::G4), 0, s, ws + L.dH, Ar::F, W6, Wp,
-                     Kh, ws + X.gates, ws + X.cst, ws + X.dout32, ws + X.dgates);
-  MT_LAUNCHED();
+  // (every launch of the frames backward is numbered by the launch window, so bench.py times it
+  // launch by launch: bench.launch_breakdown)
+  if (launch_allowed()) {
+    hipLaunchKernelGGL((lstm_bwd_kernel<Ar::NH, Ar::STEPS>), dim3(W), dim3(Ar::G4), 0, s, ws + L.dH, Ar::F, W6, Wp,
+                       Kh, ws + X.gates, ws + X.cst, ws + X.dout32, ws + X.dgates);
+    MT_LAUNCHED();
+  }
   // the small weight gradients — K_h rows + bias [h_{t-1}, 1]^T dz, fc6 [out, 1]^T dH, the heads,
   // the projection [h_5, 1]^T d out: a few blocks each, a serial walk of up to 10 K chunks — are off
   // the critical path: they run beside conv4's backward (trunk_backward's extra jobs, longest walk
@@ -636,12 +640,16 @@ static int lstm_frames_bwd_impl(const mt_net *n, const float *P, const uint8_t *
       gemm_job<TileDenseW>(LdColMajor{ws + X.h5, Ar::NH, Ar::NH}, LdColMajor{ws + X.dout32, Ar::NH, -1},
                            EpStore{grad + n->off_proj, Ar::NH}, Ar::NH + 1, Ar::NH, W, 1)};
   // per-frame gate gradients (the zero frame: chunk partials first)
-  hipLaunchKernelGGL(lstm_zero_partials_kernel, dim3(kZeroParts), dim3(Ar::G4), 0, s, ws + X.dgates, nz, W,
-                     ws + X.zpart);
-  MT_LAUNCHED();
-  hipLaunchKernelGGL(lstm_gather_dxg_kernel, dim3(X.R_bwd), dim3(Ar::G4), 0, s, ws + X.dgates, nz, T, E,
-                     ws + X.zpart, kZeroParts, ws + X.dxg);
-  MT_LAUNCHED();
+  if (launch_allowed()) {
+    hipLaunchKernelGGL(lstm_zero_partials_kernel, dim3(kZeroParts), dim3(Ar::G4), 0, s, ws + X.dgates, nz, W,
+                       ws + X.zpart);
+    MT_LAUNCHED();
+  }
+  if (launch_allowed()) {
+    hipLaunchKernelGGL(lstm_gather_dxg_kernel, dim3(X.R_bwd), dim3(Ar::G4), 0, s, ws + X.dgates, nz, T, E,
+                       ws + X.zpart, kZeroParts, ws + X.dxg);
+    MT_LAUNCHED();
+  }
   constexpr int K = Ar::NCONV - 1;
   const float *flat = layer_out<Ar, K>(ws, L);
   // d flat = dxg K_x^T (masked by conv4's activation; the trunk's critical path, first) and the

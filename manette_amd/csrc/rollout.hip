@@ -786,7 +786,9 @@ extern "C" int mt_rollout_set_update(mt_rollout *ro, void *graph_exec, float *lr
   ro->lr_host = lr_host;
   ro->initial_lr = initial_lr;
   ro->annealing_steps = annealing_steps;
-  if (graph_exec) ro->dp_graph[0] = ro->dp_graph[1] = ro->dp_graph[2] = nullptr;
+  // registering replaces a data-parallel update; unregistering (NULL) clears both forms, so no
+  // registered update is left behind whose LR word was just set to NULL
+  ro->dp_graph[0] = ro->dp_graph[1] = ro->dp_graph[2] = nullptr;
   return MT_OK;
 }
 

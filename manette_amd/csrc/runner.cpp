@@ -33,6 +33,9 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include "../../include/manette_host.h"
 
 namespace {
@@ -148,6 +151,9 @@ struct mh_runner {
   uint32_t *ready = nullptr;
   uint32_t ready_value = 0;
   bool busy = false;  // mh_runner_step_begin dispatched, mh_runner_step_end not yet called
+  // host-phase split of a step (mh_runner_stats): worker time in stage_env (frame pool + resize +
+  // the streaming copy into the staging) and worker time in the whole phase, summed over workers
+  std::atomic<int64_t> stage_ns{0}, busy_ns{0}, stat_steps{0};
   bool nt_stores = true;  // resized frames: streaming stores (plain stores measured the same on the box)
 
   int block_begin(int w) const { return (int)((int64_t)E * w / W); }
@@ -171,7 +177,25 @@ struct mh_runner {
     e.steps = 0;
   }
 
+  static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
   void run_phase(int w) {
+    const int64_t t0 = now_ns();
+    int64_t st = 0;
+    run_phase_(w, st);
+    busy_ns.fetch_add(now_ns() - t0, std::memory_order_relaxed);
+    stage_ns.fetch_add(st, std::memory_order_relaxed);
+    if (w == 0 && phase == 1) stat_steps.fetch_add(1, std::memory_order_relaxed);
+  }
+  // a stage_env call, timed into st
+  void stage_timed(int i, int64_t &st) {
+    const int64_t t0 = now_ns();
+    stage_env(i);
+    st += now_ns() - t0;
+  }
+  void run_phase_(int w, int64_t &st) {
     const int b0 = block_begin(w), b1 = block_end(w);
     if (phase == 0) {
       for (int i = b0; i < b1; ++i) {
@@ -199,7 +223,7 @@ struct mh_runner {
           push_count[i] = std::min(e.npush, 4);
         }
         if (per_env) {  // stage env i now and publish it (sfence: the streaming stores first)
-          stage_env(i);
+          stage_timed(i, st);
           _mm_sfence();
           __atomic_store_n(ready + (size_t)i * MH_READY_STRIDE, (ready_value << 3) | (uint32_t)std::min(e.npush, 4),
                            __ATOMIC_RELEASE);
@@ -220,7 +244,7 @@ struct mh_runner {
       return;
     }
     if (phase == 0 || phase == 2 || fixed) {
-      for (int i = b0; i < b1; ++i) stage_env(i);
+      for (int i = b0; i < b1; ++i) stage_timed(i, st);
       _mm_sfence();  // streaming stores visible before the phase is reported done
     }
   }
@@ -275,7 +299,10 @@ struct mh_runner {
   // regular pause between two emulator steps is the update (the learner's backward + RMSProp and
   // the next rollout's first forward, ~0.1 ms), and a futex wake-up there cost ~10 us on the
   // critical path of every update (a fixed spin count measured ~85 us of pause on the box).
+  // mh_runner_set_threads lowers it when the host's cores are oversubscribed (several ranks' worker
+  // pools on one node), so an idle pool yields its cores to the other ranks' emulator threads.
   static constexpr int64_t kSpinUs = 2000;
+  std::atomic<int64_t> spin_us{kSpinUs};
   void worker(int w) {
     uint32_t seen = 0;
     for (;;) {
@@ -283,10 +310,10 @@ struct mh_runner {
       int spins = 0;
       uint32_t g;
       auto t0 = std::chrono::steady_clock::now();
+      const int64_t spin = spin_us.load(std::memory_order_relaxed);
       while ((g = gen.load(std::memory_order_acquire)) == seen) {
         cpu_relax();
-        if ((++spins & 255) == 0 &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs))
+        if ((++spins & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin))
           gen.wait(seen, std::memory_order_acquire);
       }
       seen = g;
@@ -382,6 +409,66 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
   for (int w = 0; w < r->W; ++w) r->threads.emplace_back([r, w] { r->worker(w); });
   *out = r;
   return 0;
+}
+
+extern "C" int mh_runner_set_threads(mh_runner *r, const int32_t *cpus, int n_cpus, int spin_us) {
+  if (!r || (n_cpus > 0 && !cpus) || n_cpus < 0 || spin_us < 0) {
+    set_error("null argument or negative count");
+    return 1;
+  }
+  for (int i = 0; i < n_cpus; ++i)
+    if (cpus[i] < 0 || cpus[i] >= CPU_SETSIZE) {
+      set_error("cpu %d out of range", cpus[i]);
+      return 1;
+    }
+  for (int w = 0; w < n_cpus && w < r->W; ++w) {  // (n_cpus < W: workers W.. keep their mask)
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(cpus[w], &set);
+    const int rc = pthread_setaffinity_np(r->threads[w].native_handle(), sizeof(set), &set);
+    if (rc != 0) {
+      set_error("pthread_setaffinity_np(worker %d, cpu %d) failed: %d", w, cpus[w], rc);
+      return 1;
+    }
+  }
+  r->spin_us.store(spin_us, std::memory_order_relaxed);
+  return 0;
+}
+
+extern "C" int mh_runner_stats(mh_runner *r, double *out, int n, int reset) {
+  if (!r || (n > 0 && !out)) {
+    set_error("null argument");
+    return 1;
+  }
+  const double steps = (double)r->stat_steps.load(), w = (double)r->W;
+  const double v[3] = {steps > 0 ? 1e-3 * (double)r->stage_ns.load() / (w * steps) : 0.0,
+                       steps > 0 ? 1e-3 * (double)r->busy_ns.load() / (w * steps) : 0.0, steps};
+  for (int i = 0; i < n && i < 3; ++i) out[i] = v[i];
+  if (reset) {
+    r->stage_ns.store(0);
+    r->busy_ns.store(0);
+    r->stat_steps.store(0);
+  }
+  return 0;
+}
+
+extern "C" int mh_runner_thread_cpus(mh_runner *r, int32_t *out, int n) {
+  if (!r || (n > 0 && !out)) {
+    set_error("null argument");
+    return -1;
+  }
+  for (int w = 0; w < n && w < r->W; ++w) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (pthread_getaffinity_np(r->threads[w].native_handle(), sizeof(set), &set) != 0) {
+      set_error("pthread_getaffinity_np(worker %d) failed", w);
+      return -1;
+    }
+    out[w] = CPU_COUNT(&set) == 1 ? -2 : -1;  // -1: several cpus allowed
+    for (int c = 0; c < CPU_SETSIZE && out[w] == -2; ++c)
+      if (CPU_ISSET(c, &set)) out[w] = c;
+  }
+  return r->W;
 }
 
 extern "C" int mh_runner_set_col_lut(mh_runner *r, const int32_t *col_lut, int n_cols) {

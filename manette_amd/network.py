@@ -391,10 +391,11 @@ def preprocess(raw, push_offset, push_count, E, depth, row_lut, col_lut, prev, o
     rows: 210 = whole screens with the resize LUT, 84 = runner-selected rows, identity LUT).
     pooled: raw holds one screen per push, the frame-pool max already taken (mt_preprocess_pooled);
     resized: raw holds each push's final 84x84 frame (mt_preprocess_resized, stacking only)."""
+    rp = C.c_void_p(raw) if isinstance(raw, int) else _ptr(raw)  # (int: a pinned buffer's device address)
     if resized:
-        check(_lib.hip().mt_preprocess_resized(_ptr(raw), _ptr(push_offset), _ptr(push_count), E, depth, _ptr(prev),
+        check(_lib.hip().mt_preprocess_resized(rp, _ptr(push_offset), _ptr(push_count), E, depth, _ptr(prev),
                                                _ptr(out), _stream()), 'mt_preprocess_resized')
         return
     name = 'mt_preprocess_pooled' if pooled else 'mt_preprocess'
-    check(getattr(_lib.hip(), name)(_ptr(raw), _ptr(push_offset), _ptr(push_count), E, depth, int(src_rows),
+    check(getattr(_lib.hip(), name)(rp, _ptr(push_offset), _ptr(push_count), E, depth, int(src_rows),
                                     _ptr(row_lut), _ptr(col_lut), _ptr(prev), _ptr(out), _stream()), name)

@@ -51,6 +51,7 @@ class PAACLearner(ActorLearner):
         self.seed = int(getattr(args, 'seed', 0))
         super(PAACLearner, self).__init__(network_creator, environment_creator, explo_policy, args)
         self.workers = args.emulator_workers
+        self.pin_threads = getattr(args, 'pin_threads', 'auto')
         self.total_repetitions = args.nb_choices
         self.lstm_bool = (args.arch == 'LSTM')
         self.tab_rep = explo_policy.tab_rep
@@ -140,6 +141,7 @@ class PAACLearner(ActorLearner):
         self.boot_in_rollout = False
         self.slot0_in_rollout = False
         self.runners = None
+        self.placement = None    # host-thread plan of the native runner (_plan_threads)
         self.profile = None      # name -> [(start_event, end_event)] when profiling (bench.py)
         self.sample_seed = (self.seed * 1000003 + 1) & 0xffffffffffff  # rank-independent: rows are global
         # replay the update as hipGraph(s) from the second update on (native pipelined step)
@@ -154,9 +156,25 @@ class PAACLearner(ActorLearner):
         self._logged_episodes = 0
 
     # ------------------------------------------------------------------------------------------
+    def _plan_threads(self):
+        """This rank's host-thread placement (manette_amd/placement.py): the emulator worker count
+        (capped when the node's cores are oversubscribed), their cpus and idle spin."""
+        from . import placement
+        lw = int(os.environ.get('LOCAL_WORLD_SIZE', '1'))
+        lr = int(os.environ.get('LOCAL_RANK', '0'))
+        mode = self.pin_threads
+        if mode == 'off' or (mode == 'auto' and lw <= 1):
+            topo = dict(allowed=sorted(os.sched_getaffinity(0)), quota=placement.cgroup_cpu_limit())
+        else:
+            topo = placement.topology(lw)
+        return placement.plan(self.workers, self.emulator_counts, min(lr, lw - 1), lw, mode=mode, **topo)
+
     def _start_runners(self):
         E, C = self.emulator_counts, self.C
         if self.runner_kind == 'native':
+            from . import placement
+            self.placement = self._plan_threads()
+            self.workers = self.placement['ew_used']
             bank = self.environment_creator.create_bank(0, E)
             self.bank = bank
             self.in_place = self.staging == 'in_place'
@@ -184,6 +202,9 @@ class PAACLearner(ActorLearner):
                                          dtype=torch.uint8, device=self.dev)
                 total = self.runners.reset()
                 self._upload_pushes(total, self.states[0], self.states[0].clone())
+            if self.placement['pinned']:
+                self.runners.set_threads(self.placement['worker_cpus'], self.placement['spin_us'])
+                placement.apply_main(self.placement)
             if self.sampling == 'device':
                 self._make_native_step()
         else:
@@ -704,11 +725,13 @@ class PAACLearner(ActorLearner):
             self.comm = comm.make(self.comm_kind, self.rank, self.world, torch.cuda.current_device())
         if self.world > 1:
             # rank 0's run is the run: its checkpoint step (resume) and its parameters / slots
-            self.global_step, self.last_saving_step = comm.broadcast_scalars(
-                [self.global_step, self.last_saving_step], self.rank)
-            for t in (self.network.params, self.network.ms, self.network.mom):
-                self.comm.broadcast(t, 0)
-            torch.cuda.current_stream().synchronize()
+            # (bounded: the first collectives on the communicator, comm.Deadline)
+            with comm.Deadline('start-of-run broadcast of rank 0\'s parameters', self.rank, self.world):
+                self.global_step, self.last_saving_step = comm.broadcast_scalars(
+                    [self.global_step, self.last_saving_step], self.rank)
+                for t in (self.network.params, self.network.ms, self.network.mom):
+                    self.comm.broadcast(t, 0)
+                torch.cuda.current_stream().synchronize()
         self.global_step_start = self.global_step
         self._start_runners()
         if self.lstm_bool:  # memory = zeros except memory[:, -1] = initial state (paac.py:109-112)
@@ -779,8 +802,15 @@ class PAACLearner(ActorLearner):
             while self.global_step < self.max_global_steps:
                 loop_start_time = time.time()
                 self.book.new_update()
-                self.rollout()
-                self.update()
+                if counter == 0 and self.world > 1:  # the first all-reduce, bounded (comm.Deadline)
+                    from . import comm
+                    with comm.Deadline('the first data-parallel update', self.rank, self.world):
+                        self.rollout()
+                        self.update()
+                        torch.cuda.synchronize()
+                else:
+                    self.rollout()
+                    self.update()
                 self.write_summaries()
                 counter += 1
                 if counter % max(1, 2048 // self.emulator_counts) == 0:

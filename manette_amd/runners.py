@@ -114,6 +114,28 @@ class NativeRunners(object):
         _lib.check_host(_lib.host().mh_runner_env_state(self._h, e, C.byref(k), C.byref(s)))
         return k.value, s.value
 
+    def set_threads(self, cpus, spin_us=2000):
+        """Pin worker w to cpus[w] and set the idle spin before the futex sleep
+        (mh_runner_set_threads; manette_amd/placement.py plans both per rank)."""
+        c = np.ascontiguousarray(np.asarray(list(cpus), dtype=np.int32))
+        _lib.check_host(_lib.host().mh_runner_set_threads(self._h, c.ctypes.data_as(C.c_void_p), len(c), int(spin_us)),
+                        'mh_runner_set_threads')
+
+    def stats(self, reset=False):
+        """(staging us, busy us) per worker per step and the step count since the last reset
+        (mh_runner_stats): staging = frame pool + resize + copy into the pinned staging."""
+        out = (C.c_double * 3)()
+        _lib.check_host(_lib.host().mh_runner_stats(self._h, out, 3, int(bool(reset))), 'mh_runner_stats')
+        return dict(stage_us=out[0], busy_us=out[1], steps=int(out[2]))
+
+    def thread_cpus(self):
+        """Per worker: the one cpu it may run on, or -1 (several allowed)."""
+        out = np.zeros(256, np.int32)
+        n = _lib.host().mh_runner_thread_cpus(self._h, out.ctypes.data_as(C.c_void_p), len(out))
+        if n < 0:
+            raise RuntimeError(_lib.host().mh_last_error().decode())
+        return [int(x) for x in out[:n]]
+
     def stop(self):
         if getattr(self, '_h', None):
             _lib.host().mh_runner_destroy(self._h)

@@ -1,4 +1,4 @@
-"""bench.settle_updates at world 2 (gloo, CPU): every rank runs the same number of untimed updates,
+"""bench.settle_updates at world 2 and 8 (gloo, CPU): every rank runs the same number of untimed updates,
 whatever its own clock says. Each fake update all-reduces like the data-parallel update does; ranks
 that stopped on their own clocks drifted by one update and hung in mismatched collectives (the
 round-5 2-rank rehearsal)."""
@@ -39,9 +39,10 @@ def _worker(rank, world, port, seconds, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(120)
-def test_settle_updates_same_count_on_every_rank():
-    world, port = 2, 29000 + os.getpid() % 1000
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize('world', [2, 8])  # 8: the driver's N-GPU run (one gloo rank per GPU)
+def test_settle_updates_same_count_on_every_rank(world):
+    port = 29000 + os.getpid() % 1000 + 7 * world
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, port, 0.3, out), nprocs=world, join=True)

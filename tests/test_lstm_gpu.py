@@ -265,3 +265,43 @@ def test_lstm_learner_memory_windows(tmp_path, pipeline):
         assert np.isfinite(p1).all() and not np.array_equal(p0, p1)
     finally:
         L.cleanup()
+
+
+@pytest.mark.parametrize('E,T', [(8, 5), (5, 3)])
+def test_lstm_frames_backward_norm_partials(E, T):
+    """mt_lstm_frames_backward with norm_partials (the single-GPU LSTM update, paac.py's
+    partials_ready path): the same gradient bit for bit as without, and the partials its last
+    launch leaves add up to the global norm of that gradient (actor_learner.py:59-63; oracle:
+    float64) — the small K_h / fc6 / head / projection gradients ride in conv4's grouped launch,
+    so a partial summed before they were complete would show here, whether or not a clip fires."""
+    from oracle import optim
+    A, R, act, depth = 9, 11, 'relu', 1
+    net = _net(depth, A, R, seed=E * 7 + T, act=act)
+    rs = np.random.RandomState(E * 31 + T)
+    fstore = rs.randint(0, 256, size=(1 + (T + 5) * E, 84, 84, 4 * depth)).astype(np.uint8)
+    fstore[0] = 0
+    nz = rs.choice([0, 0, 0, 1, 2, 4, 5], size=(T + 1, E)).astype(np.int32)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    fs_d, nz_d = d(fstore), d(nz)
+    net.lstm_frames_forward(fs_d, 0, 1 + 5 * E, E, T)
+    for t in range(1, T + 1):
+        net.lstm_frames_forward(fs_d, 1 + (4 + t) * E, E, E, T)
+    v = torch.zeros(T + 1, E, device='cuda')
+    pi = torch.zeros(T + 1, E, A, device='cuda')
+    rep = torch.zeros(T + 1, E, R, device='cuda')
+    for t in range(T + 1):
+        net.lstm_windows_forward(nz_d[t], t, E, T, out=(v[t], pi[t], rep[t]))
+    N = T * E
+    args = (d(rs.randint(0, A, size=N).astype(np.int32)), d(rs.randint(0, R, size=N).astype(np.int32)),
+            d(rs.randn(N).astype(np.float32)), d(rs.randn(N).astype(np.float32)))
+    net.grad.zero_()
+    net.lstm_frames_backward(fs_d, nz_d[:T], E, T, pi[:T], rep[:T], v[:T], *args)
+    g0 = net.grad.clone()
+    net.grad.zero_()
+    net.partials.fill_(float('nan'))
+    net.lstm_frames_backward(fs_d, nz_d[:T], E, T, pi[:T], rep[:T], v[:T], *args, norm_partials=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(net.grad.cpu().numpy(), g0.cpu().numpy())
+    norm = float(np.sqrt(net.partials.double().sum().item()))
+    ref = optim.global_norm([g0.cpu().numpy()])
+    assert np.isfinite(norm) and abs(norm - ref) <= 1e-5 * ref, (norm, ref)

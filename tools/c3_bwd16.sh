@@ -1,0 +1,9 @@
+# r06: 16-wave nips_conv_bwd_kernel — parity subset, kernel-trace A/B (old vs new), bench A/B; then the
+# new bench rows (LSTM launch breakdown, raw-screen preprocess, emulator split) on pong + lstm
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python -u -m pytest tests/test_e2e_gpu.py tests/test_kernels_gpu.py tests/test_lstm_gpu.py -x -q --timeout 120 --timeout-method thread -k "pong or NIPS or norm_partials" > gpurun_out/r06c3_tests.log 2>&1 && \
+REPS=20 CONFIG=pong-nips VARIANTS="old" bash tools/variant_prof.sh && \
+cp manette_amd/libmanette_hip.so manette_amd/libmanette_hip_new.so && REPS=20 CONFIG=pong-nips VARIANTS="new" bash tools/variant_prof.sh && \
+VARIANTS="old base" CONFIGS="pong-nips" N=2 TAG=r06c3 bash tools/ab_lib.sh && \
+timeout -k 10 300 python bench.py --config mspacman-lstm-figar --no_cpu_baseline --trunk_sweep= --steps 20 > gpurun_out/r06c3_lstm.log 2>&1
