@@ -771,8 +771,9 @@ def main():
                         names.append(('conv%d dX + conv%d dW' % (i + 1, i + 1) if i > 0 else 'conv1 dW') + sfx)
                 names.append('conv1 slab sum + global-norm partials')
             for k, us in enumerate(tl[1:]):
-                kernels.append(row('A10', 'actor_learner.py:49', 'group_kernel: ' + (names[k] if k < len(names) else
-                                                                                      'launch %d' % (k + 2)), us))
+                nm = names[k] if k < len(names) else 'launch %d' % (k + 2)
+                kernels.append(row('A10', 'actor_learner.py:49', nm if nm.startswith(('lstm_', 'nips_conv_bwd_kernel'))
+                                   else 'group_kernel: ' + nm, us))
         kernels.append(row('A11', 'actor_learner.py:55-74', 'clip_rmsprop_kernel', med(prof['clip_rmsprop']),
                            28 * P_ + 4 * 512 + 4, note='%d params: w, ms, mom, g read (16 B) and w, ms, mom written '
                            '(12 B) per parameter; ' % P_ + graph_note))

@@ -442,14 +442,18 @@ __device__ __forceinline__ void run_group(int id, float *smem, const J1 &j1, con
   if constexpr (sizeof...(Rest) > 0) run_group(id - j1.blocks(), smem, rest...);
 }
 
-// Up to four jobs as one (a grouped launch's extra slot), blocks in argument order.
+// Up to four jobs as one (a grouped launch's extra slot), blocks in argument order. The pack's
+// block count is rounded up to a multiple of 8 (the padding blocks return at once): it leads its
+// grouped launch, and the jobs after it place their tiles by xcd_tile(id & 7 = the hardware XCD),
+// which holds only when every job before them starts at a multiple of 8.
 template <class A, class B, class C = NoJob, class D = NoJob>
 struct JobPack {
   A a;
   B b;
   C c{};
   D d{};
-  __host__ __device__ int blocks() const { return a.blocks() + b.blocks() + c.blocks() + d.blocks(); }
+  __host__ __device__ int used() const { return a.blocks() + b.blocks() + c.blocks() + d.blocks(); }
+  __host__ __device__ int blocks() const { return (used() + 7) & ~7; }
   size_t lds() const {
     size_t l = 0;
     for (size_t x : {a.blocks() ? a.lds() : 0, b.blocks() ? b.lds() : 0, c.blocks() ? c.lds() : 0,
@@ -457,7 +461,9 @@ struct JobPack {
       l = std::max(l, x);
     return l;
   }
-  __device__ __forceinline__ void run(int id, float *smem) const { run_group(id, smem, a, b, c, d); }
+  __device__ __forceinline__ void run(int id, float *smem) const {
+    if (id < used()) run_group(id, smem, a, b, c, d);
+  }
 };
 template <class A, class B>
 JobPack(A, B) -> JobPack<A, B>;

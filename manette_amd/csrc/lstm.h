@@ -253,7 +253,10 @@ __global__ __launch_bounds__(128) void lstm_bwd_kernel(const float *__restrict__
   // every operand of the window requested up front, K_h first (relaxed atomics: plain read-only
   // loads are sunk to their use — one load latency per step and per 8 products otherwise; K_h's
   // LDS copy was two round trips of its own before the rest were requested): K_h column g, the
-  // projection row, every step's gates and cell states; same products, same order below
+  // projection row, every step's gates and cell states; the same products as the round-4 kernel,
+  // but the two long dot products below are summed in four quarters added ((p0 + p1) + p2) + p3
+  // (round 5), not in one sequential walk: an fp32 reduction order of its own (the oracle checks it
+  // at the gradient tolerance; nothing is pinned to the old order)
   float khv[NH];
 #pragma unroll
   for (int k = 0; k < NH; ++k) khv[k] = __hip_atomic_load(Kh + (size_t)k * G4 + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

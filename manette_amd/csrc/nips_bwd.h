@@ -12,25 +12,18 @@
 // W2 (32 KB from L2), dact1 (25.6 KB written: the workspace keeps the layered path's contents)
 // and the slabs.
 //
-// All products on v_mfma_f32_16x16x4_f32 (fp32). 16 waves, 4 per SIMD (one block per CU holds 138
-// KB of LDS; round 5 ran 8 waves, 2 per SIMD, and the image blocks issued their 624 MFMAs per SIMD
-// at ~55 % of the MFMA rate — PMC: 5.7 VALU per MFMA, half the LDS cycles bank conflicts — so the
-// other waves of a SIMD now cover one wave's operand reads and dependent-MFMA latency). Lane (r, g)
-// = (lane & 15, lane >> 4); an MFMA takes A[r][k_g], B[k_g][r] and accumulates C[4g + i][r] in acc[i].
-// Waves w, w + 4, w + 8, w + 12 share SIMD w & 3.
-//   conv2 dX: wave w = stride phase (py, px) = ((w & 3) >> 1, w & 1) of the 20x20 input (one phase
-//     per SIMD), tiles 2 (w >> 2) .. +1 of its 100 phase pixels (qy, qx) (7 tiles of 16: the last
-//     wave of a SIMD takes one), K = (a, b, co) = 2x2x32:
+// All products on v_mfma_f32_16x16x4_f32 (fp32). 8 waves (2 per SIMD: one block per CU holds 138 KB
+// of LDS, and the second wave's MFMAs issue while the first waits on LDS). Lane (r, g) = (lane & 15,
+// lane >> 4); an MFMA takes A[r][k_g], B[k_g][r] and accumulates C[4g + i][r] in acc[i].
+//   conv2 dX: wave w = stride phase (py, px) = ((w & 3) >> 1, w & 1) of the 20x20 input, half w >> 2
+//     of its rows = the 100 phase pixels (qy, qx) (tiles 0-3 / 4-6 of 16), K = (a, b, co) = 2x2x32:
 //     dX[2qy+py][2qx+px][ci] = sum dY2[qy-a][qx-b][co] W2[py+2a][px+2b][ci][co] (dY2 zero-bordered).
-//   conv1 dW: rows kr = (ky, kx, ci) (16 tiles: wave w = tile (ky, kx half) = (w >> 1, w & 1)), K =
-//     the 400 output pixels:
+//   conv1 dW: rows kr = (ky, kx, ci) (16 tiles: ky = w, kx half = tile), K = the 400 output pixels:
 //     dW1[kr][co] = (sum_p X[4oy+ky][4ox+kx][ci] dact1[p][co]) / 255 (the integer-valued frame bytes
 //     are exact in fp32; the scale is applied once to the sum); the frame is stored split by the
 //     stride phase (ky & 3, kx & 3) so 4 consecutive pixels are 4 consecutive bytes.
-//   conv2 dW (pair blocks): rows kr = (ky, kx, ci) (16 tiles, wave w = tile (w >> 2, w & 3), x 2
-//     channel halves), K = the 81 output pixels (+3 zero) of each image:
-//     dW2[kr][co] = sum_p act1[2oy+ky][2ox+kx][ci] dY2[p][co].
-// Every output's products are added in the same order as the 8-wave form's (bit-identical).
+//   conv2 dW (pair blocks): rows kr = (ky, kx, ci) (16 tiles x 2 channel halves, 4 per wave), K =
+//     the 81 output pixels (+3 zero) of each image: dW2[kr][co] = sum_p act1[2oy+ky][2ox+kx][ci] dY2[p][co].
 //   bias rows: the column sums of the B operands the waves already hold (dact1 in conv1 dW, dY2 in
 //     conv2 dW), reduced over the 4 lane groups by shuffles.
 #pragma once
@@ -49,8 +42,7 @@ struct NipsConvBwdJob {
   int B = 0, act = 0;
   float alpha = 0.f;
 
-  static constexpr int NT = 1024;
-  static constexpr int YU = (648 + NT - 1) / NT, AU = (1600 + NT - 1) / NT;  // dY2 / act1 quads per thread
+  static constexpr int NT = 512;
   static constexpr int XROW = 24;                // bytes per row of a phase plane (21 used)
   static constexpr int XPLANE = 21 * XROW;       // (ky & 3, kx & 3, ci) plane: 21 x 24 bytes
   static constexpr int X_BYTES = 64 * XPLANE;    // 32256
@@ -70,7 +62,7 @@ struct NipsConvBwdJob {
   // dY2 of image b into the zero-bordered [11][11][DS] map and act1 into the transposed [16][PS]
   // map: load() issues the global loads, store() writes LDS (callers issue every load first)
   struct DyAct {
-    f32x4 yv[YU], av[AU];
+    f32x4 yv[2], av[4];
   };
   __device__ __forceinline__ DyAct load_dy_act(int b) const {
     const int tid = threadIdx.x;
@@ -78,9 +70,9 @@ struct NipsConvBwdJob {
     const f32x4 *as = reinterpret_cast<const f32x4 *>(act1 + (size_t)b * 400 * 16);
     DyAct d;
 #pragma unroll
-    for (int u = 0; u < YU; ++u) d.yv[u] = ys[min(tid + NT * u, 647)];
+    for (int u = 0; u < 2; ++u) d.yv[u] = ys[min(tid + NT * u, 647)];
 #pragma unroll
-    for (int u = 0; u < AU; ++u) d.av[u] = as[min(tid + NT * u, 1599)];
+    for (int u = 0; u < 4; ++u) d.av[u] = as[min(tid + NT * u, 1599)];
     return d;
   }
   __device__ __forceinline__ void store_dy_act(const DyAct &d, float *dyp, float *a1t) const {
@@ -91,7 +83,7 @@ struct NipsConvBwdJob {
         *reinterpret_cast<f32x4 *>(dyp + p * DS + 4 * (i & 7)) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int u = 0; u < YU; ++u) {
+    for (int u = 0; u < 2; ++u) {
       const int i = tid + NT * u;
       if (i < 648) {
         const int p = i >> 3, oy = p / 9, ox = p - 9 * oy;
@@ -99,7 +91,7 @@ struct NipsConvBwdJob {
       }
     }
 #pragma unroll
-    for (int u = 0; u < AU; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int i = tid + NT * u;
       if (i < 1600) {
         const int p = i >> 2, c = 4 * (i & 3);
@@ -136,10 +128,9 @@ struct NipsConvBwdJob {
       for (int v = 0; v < 4; ++v) xv[v] = xs[y * 21 + min(4 * jq + v, 20)];
     }
     const f32x4 *wsrc = reinterpret_cast<const f32x4 *>(W2);
-    constexpr int WU = 2048 / NT;  // W2 quads per thread
-    f32x4 wv[WU];
+    f32x4 wv[4];
 #pragma unroll
-    for (int u = 0; u < WU; ++u) wv[u] = wsrc[tid + NT * u];
+    for (int u = 0; u < 4; ++u) wv[u] = wsrc[tid + NT * u];
     const DyAct da = load_dy_act(b);
     store_dy_act(da, dyp, a1t);
     if (tid < 84 * 6) {
@@ -157,52 +148,52 @@ struct NipsConvBwdJob {
       }
     }
 #pragma unroll
-    for (int u = 0; u < WU; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int i = tid + NT * u;
       *reinterpret_cast<f32x4 *>(w2s + (i >> 3) * WS + 4 * (i & 7)) = wv[u];
     }
     __syncthreads();
     MT_PROBE_AT(3, b, 1);
 
-    // ---- conv2 dX of stride phase w & 3, row tiles 2h, 2h+1 (h = w >> 2; tile 7 is empty) ----
+    // ---- conv2 dX of stride phase w & 3, row tiles 4h .. 4h+3 (h = w >> 2; tile 7 is empty) ----
     {
-      const int ph = w & 3, py = ph >> 1, px = ph & 1, t0 = 2 * (w >> 2);
-      const int nt = (w >> 2) == 3 ? 1 : 2;  // (wave-uniform)
-      int off[2];
+      const int ph = w & 3, py = ph >> 1, px = ph & 1, t0 = 4 * (w >> 2);
+      const int nt = w >> 2 ? 3 : 4;  // (wave-uniform)
+      int off[4];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < 4; ++t) {
         const int q = min(16 * (t0 + t) + r, 99), qy = q / 10, qx = q - 10 * qy;
         off[t] = ((qy + 1) * 11 + qx + 1) * DS + 4 * g;
       }
       // chunk kc = (a, b, co half): B = W2[py+2a][px+2b][ci = r][co0 + 4g ..], A = dY2 rows
-      auto frags = [&](int kc, f32x4 &bf, f32x4 (&af)[2]) {
+      auto frags = [&](int kc, f32x4 &bf, f32x4 (&af)[4]) {
         const int ab = kc >> 1, a = ab >> 1, bb = ab & 1, co0 = (kc & 1) * 16;
         bf = *reinterpret_cast<const f32x4 *>(w2s + (((py + 2 * a) * 4 + px + 2 * bb) * 16 + r) * WS + co0 + 4 * g);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) af[t] = *reinterpret_cast<const f32x4 *>(dyp + off[t] - (a * 11 + bb) * DS + co0);
+        for (int t = 0; t < 4; ++t) af[t] = *reinterpret_cast<const f32x4 *>(dyp + off[t] - (a * 11 + bb) * DS + co0);
       };
-      f32x4 acc[2];
+      f32x4 acc[4];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 bf, af[2];
+      for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 bf, af[4];
       frags(0, bf, af);
 #pragma unroll
       for (int kc = 0; kc < 8; ++kc) {
-        f32x4 bn, an[2];
+        f32x4 bn, an[4];
         if (kc + 1 < 8) frags(kc + 1, bn, an);  // next chunk's operands in flight under these MFMAs
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
+          for (int t = 0; t < 4; ++t)
             if (t < nt) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[t][s], bf[s], acc[t], 0, 0, 0);
         if (kc + 1 < 8) {
           bf = bn;
 #pragma unroll
-          for (int t = 0; t < 2; ++t) af[t] = an[t];
+          for (int t = 0; t < 4; ++t) af[t] = an[t];
         }
       }
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int q = 16 * (t0 + t) + 4 * g + i;
@@ -218,41 +209,45 @@ struct NipsConvBwdJob {
     __syncthreads();
     MT_PROBE_AT(3, b, 2);
 
-    // ---- conv1 dW: tile m = w (ky = w >> 1, kx = 4 (w & 1) + (r >> 2), ci = r & 3); db1 from the
+    // ---- conv1 dW: tiles m = 2w + mt (ky = w, kx = 4 mt + (r >> 2), ci = r & 3); db1 from the
     //      B fragments every wave reads (wave 0 writes it) ----
     {
-      const int ky = w >> 1, kh = w & 1;  // (wave-uniform)
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
       float db = 0.f;  // lane (r, g): dact1[co = r] over pixels 16 kc + 4 g .. + 3
       // the lane's plane row base: plane (ky & 3, kx & 3 = r >> 2, ci = r & 3), row offset ky >> 2
-      const uint8_t *pl = xq + ((ky & 3) * 16 + r) * XPLANE + (ky >> 2) * XROW;
+      const uint8_t *pl = xq + ((w & 3) * 16 + r) * XPLANE + (w >> 2) * XROW;
       // fragments of chunk kc: pixels p0 .. p0+3 = 16 kc + 4 g .. (one row: 20 % 4 == 0)
-      auto frag = [&](int kc, f32x4 &bf, uint32_t &u) {
+      auto frag = [&](int kc, f32x4 &bf, uint32_t &u0, uint32_t &u1) {
         const int p0 = 16 * kc + 4 * g, oy = p0 / 20, ox0 = p0 - 20 * oy;
         bf = *reinterpret_cast<const f32x4 *>(dat + r * PS + p0);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(pl + oy * XROW + ox0);
-        // kx >> 2 = 1: the same plane one byte further
-        u = kh ? __builtin_amdgcn_alignbyte(src[1], src[0], 1) : src[0];
+        u0 = src[0];                                           // kx >> 2 = 0
+        u1 = __builtin_amdgcn_alignbyte(src[1], src[0], 1);  // kx >> 2 = 1: one byte further
       };
       f32x4 bf;
-      uint32_t u;
-      frag(0, bf, u);
+      uint32_t u0, u1;
+      frag(0, bf, u0, u1);
 #pragma unroll 5
       for (int kc = 0; kc < 25; ++kc) {
         f32x4 bn;
-        uint32_t un;
-        frag(min(kc + 1, 24), bn, un);  // next chunk's operands in flight under this chunk's MFMAs
+        uint32_t n0, n1;
+        frag(min(kc + 1, 24), bn, n0, n1);  // next chunk's operands in flight under this chunk's MFMAs
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)((u >> (8 * s)) & 255u), bf[s], acc, 0, 0, 0);
+        for (int s = 0; s < 4; ++s) {
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)((u0 >> (8 * s)) & 255u), bf[s], acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)((u1 >> (8 * s)) & 255u), bf[s], acc[1], 0, 0, 0);
+        }
         db += (bf[0] + bf[1]) + (bf[2] + bf[3]);
         bf = bn;
-        u = un;
+        u0 = n0;
+        u1 = n1;
       }
       const float sc = 1.0f / 255.0f;  // networks.py:155
       float *o = slab1 + (size_t)b * SLAB1;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o[(16 * w + 4 * g + i) * 16 + r] = acc[i] * sc;
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[(16 * (2 * w + mt) + 4 * g + i) * 16 + r] = acc[mt][i] * sc;
       db += __shfl_xor(db, 16, 64);
       db += __shfl_xor(db, 32, 64);
       if (w == 0 && lane < 16) o[256 * 16 + r] = db;
@@ -273,9 +268,11 @@ struct NipsConvBwdJob {
     if (nimg == 2) store_dy_act(d1, dyp[1], a1t[1]);
     __syncthreads();
     MT_PROBE_AT(3, B + q, 1);
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) acc[mt][0] = acc[mt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     float db0 = 0.f, db1 = 0.f;  // lane (r, g): dY2[co = r / 16 + r] over the pixels 4 j + g
-    const int ky = w >> 2, kx = w & 3;
+    const int ky = w >> 1, kx0 = 2 * (w & 1);
     for (int im = 0; im < nimg; ++im) {
       const float *dy = dyp[im], *at = a1t[im];
 #pragma unroll 3
@@ -283,18 +280,23 @@ struct NipsConvBwdJob {
         const int p = 4 * j + g, pc = min(p, 80), oy = pc / 9, ox = pc - 9 * oy;
         const int yo = p < 81 ? ((oy + 1) * 11 + ox + 1) * DS : 0;  // pixel (0, 0) of the border: zeros
         const float b0 = dy[yo + r], b1 = dy[yo + 16 + r];
-        const float a0 = at[r * PS + (2 * oy + ky) * 20 + 2 * ox + kx];
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[1], 0, 0, 0);
+        const float *ap = at + r * PS + (2 * oy + ky) * 20 + 2 * ox + kx0;
+        const float a0 = ap[0], a1 = ap[1];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
         db0 += b0;
         db1 += b1;
       }
     }
     float *o = slab2 + (size_t)q * SLAB2;
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o[(16 * w + 4 * g + i) * 32 + 16 * n + r] = acc[n][i];
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[(16 * (2 * w + mt) + 4 * g + i) * 32 + 16 * n + r] = acc[mt][n][i];
     db0 += __shfl_xor(db0, 16, 64);
     db0 += __shfl_xor(db0, 32, 64);
     db1 += __shfl_xor(db1, 16, 64);

@@ -71,20 +71,23 @@ struct FusedNips {
   static constexpr int M1 = ROWS1 * OW1;  // conv1 pixels of a block (80)
   static constexpr int MT1 = (M1 + 15) / 16;  // m-tiles (5)
   static constexpr int KC1 = KK1 / 16, KC2 = KK2 / 16;
-  // conv kernel waves. Gray frames: conv1's M-tiles x 2 K-halves ("units": each output is the
-  // sum of 2 partials; 10 waves for 5 tiles), conv2 = 2 N-tiles x 4 K-quarters on 8 of them, 4
-  // partials; the former 8-wave K-split (every wave all 5 tiles over 1/8 of K) spent ~1.1 us per
-  // block writing and reducing 8 partials per output. RGB: 4 waves splitting K (its 3x input rows
+  // conv kernel waves. Gray frames: 8 waves, 2 per SIMD (waves w and w + 4 share SIMD w & 3).
+  // conv1 "units": M-tiles 0-3 x 2 K-halves on waves 0-7 (32 MFMAs each), M-tile 4 x 4 K-quarters
+  // on waves 0-3 (16 more each), so every SIMD issues 80 of the block's 320 conv1 MFMAs (round 5 ran
+  // 10 waves, tiles 0-4 x 2 K-halves: SIMDs 0 and 1 held three units, 96 MFMAs, beside 64 — the
+  // probe put the conv1 phase at 3.1 us, 1.7 of them MFMA issue); conv2 = 2 N-tiles x 4 K-quarters,
+  // 4 partials. (The former 8-wave K-split — every wave all 5 tiles over 1/8 of K — spent ~1.1 us per
+  // block writing and reducing 8 partials per output.) RGB: 4 waves splitting K (its 3x input rows
   // would not fit 64 KB of LDS beside more waves' partials).
-  static constexpr int NW = C == 4 ? 10 : 4, NT = 64 * NW;
+  static constexpr int NW = C == 4 ? 8 : 4, NT = 64 * NW;
   static constexpr bool UNITS = C == 4;
-  static constexpr int U1 = UNITS ? 2 * MT1 : 0;  // conv1 units (waves 0 .. U1-1)
-  static_assert(UNITS ? (C == 4 && KC1 == 16 && KC2 == 16 && U1 <= NW && NW >= 8)
+  static constexpr int U1 = UNITS ? 2 * (MT1 - 1) + 4 : 0;  // conv1 partial slots: 8 half units + 4 quarters
+  static_assert(UNITS ? (C == 4 && KC1 == 16 && KC2 == 16 && MT1 == 5 && NW == 8)
                       : (KC1 % NW == 0 && KC2 % NW == 0), "K chunks split over the waves");
   static constexpr int IN_BYTES = RIN * 84 * C;
   static constexpr int FR_BYTES = RIN * 84 * D;  // the block's rows of one new frame
   // LDS (floats unless noted)
-  static constexpr int RED_UNITS = (U1 > 8 ? U1 : 8) * 16 * CO1;  // conv1's or conv2's partials
+  static constexpr int RED_UNITS = (U1 > 8 ? U1 : 8) * 16 * CO1;  // conv1's (12 slots) or conv2's partials
   static constexpr int RED_FLOATS = UNITS ? (RED_UNITS > FR_BYTES ? RED_UNITS : FR_BYTES)
                                           : NW * MT1 * 16 * CO1;  // >= conv2's partials
   static_assert(4 * FR_BYTES <= RED_FLOATS * 4, "staged frames alias the reduction buffer");
@@ -95,7 +98,10 @@ struct FusedNips {
   static constexpr int W1T_FLOATS = UNITS ? CO1 * W1P : 0;
   static constexpr size_t LDS_BYTES = IN_BYTES + sizeof(float) * (RED_FLOATS + M1 * A1S + W1T_FLOATS);
   // fc kernel
-  static constexpr int FC_BN = 16, FC_BM = 32, FC_KC = FEAT / 16;  // 18 K chunks of 16
+  // fc tile: 16 columns x 16 envs (round 5: 32 envs; the block's 54 KB of operands at ~70 GB/s per CU
+  // from L2 / MALL and its 40 dependent MFMAs per wave were the 2.3 us block — half the envs per block
+  // halves both, the column block's weights are read by two adjacent blocks of one XCD)
+  static constexpr int FC_BN = 16, FC_BM = 16, FC_KC = FEAT / 16;  // 18 K chunks of 16
 };
 
 // Stage input rows 8i..8i+19 of env e into xin. STACK: build them from the previous state and
@@ -171,6 +177,43 @@ __device__ __forceinline__ void nips_stage_rows(const uint8_t *__restrict__ obs,
   }
 }
 
+// One conv1 unit of the gray kernel: M-tile t (16 of the block's 80 conv1 pixels) over the NCH K
+// chunks c0 .. c0 + NCH - 1 (chunk c = (ky, kx) pairs 4c .. 4c + 3, the 4 channels of each), every
+// LDS operand read first (NCH words + NCH weight fragments in flight), then the converts and the
+// MFMAs on two accumulators (even / odd chunks: independent chains), added at the end.
+template <int C, int NCH>
+__device__ __forceinline__ f32x4 nips_conv1_unit(const uint8_t *xin, const float *w1t, int t, int c0, int r, int g) {
+  using Fz = FusedNips<C>;
+  f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  const float sc = 1.0f / 255.0f;
+  const int m = min(t * 16 + r, Fz::M1 - 1);
+  const int orow = m / Fz::OW1, ox = m - orow * Fz::OW1;
+  const uint8_t *xb = xin + ((4 * orow) * 84 + 4 * ox) * C;
+  uint32_t au[NCH];
+  f32x4 bw[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int kpos = 4 * (c0 + j) + g;  // (ky, kx) of k0 = 16 c + 4 g (C = 4: the 4 channels)
+    au[j] = *reinterpret_cast<const uint32_t *>(xb + ((kpos >> 3) * 84 + (kpos & 7)) * C);
+    bw[j] = *reinterpret_cast<const f32x4 *>(w1t + r * Fz::W1P + 16 * (c0 + j) + 4 * g);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them to save VGPRs)
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const uint32_t u = au[j];
+    const f32x4 a = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc, (float)((u >> 16) & 0xff) * sc,
+                          (float)(u >> 24) * sc};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (j & 1)
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[j][s], acc1, 0, 0, 0);
+      else
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[j][s], acc0, 0, 0, 0);
+    }
+  }
+  return acc0 + acc1;
+}
+
 // conv1 -> conv2 of conv2 row i of env e; writes act2 [B][2592] row e's 288 features of row i.
 // act1 (optional): [B][20][20][16] conv1 activations (rows of a train workspace, mt_forward_rows);
 // block (e, i) writes conv1 rows 2i, 2i+1 (the last block also 18, 19), so each value is written
@@ -232,43 +275,18 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
 
   // ---- conv1 (VALID 8x8 stride 4): M = 4 rows x 20 columns, N = 16, K = 64*C ----
   if constexpr (Fz::UNITS) {
-    // unit w < U1: M-tile t = w / 2, K-half kh = w % 2 (K chunks 8kh .. 8kh+7)
-    if (w < Fz::U1) {
-    const int t = w >> 1, kh = w & 1;
-    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;  // even / odd chunks: independent MFMA chains
-    const float sc = 1.0f / 255.0f;
-    const int m = min(t * 16 + r, Fz::M1 - 1);
-    const int orow = m / Fz::OW1, ox = m - orow * Fz::OW1;
-    const uint8_t *xb = xin + ((4 * orow) * 84 + 4 * ox) * C;
-    // every LDS operand read of the unit first (8 words + 8 weight fragments in flight), then the
-    // converts and the 32 MFMAs: the reads' latency is paid once, not once per chunk
-    uint32_t au[8];
-    f32x4 bw[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int kpos = 4 * (8 * kh + j) + g;  // (ky, kx) of k0 = 16 c + 4 g (C = 4: the 4 channels)
-      au[j] = *reinterpret_cast<const uint32_t *>(xb + ((kpos >> 3) * 84 + (kpos & 7)) * C);
-      bw[j] = *reinterpret_cast<const f32x4 *>(w1t + r * Fz::W1P + 16 * (8 * kh + j) + 4 * g);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them to save VGPRs)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t u = au[j];
-      const f32x4 a = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc, (float)((u >> 16) & 0xff) * sc,
-                            (float)(u >> 24) * sc};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        if (j & 1)
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[j][s], acc1, 0, 0, 0);
-        else
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[j][s], acc0, 0, 0, 0);
-      }
-    }
+    // wave w: M-tile w >> 1, K-half w & 1 (K chunks 8 kh .. 8 kh + 7) -> slot w; waves 0..3 also
+    // M-tile 4, K-quarter w (chunks 4w .. 4w + 3) -> slot 8 + w
+    const int wu = __builtin_amdgcn_readfirstlane(w);  // (wave-uniform: scalar branches)
+    const f32x4 acc = nips_conv1_unit<C, 8>(xin, w1t, wu >> 1, 8 * (wu & 1), r, g);
+    f32x4 acc4 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (wu < 4) acc4 = nips_conv1_unit<C, 4>(xin, w1t, 4, 4 * wu, r, g);
     MT_PROBE_AT(0, bid, 6);
-    const f32x4 acc = acc0 + acc1;
 #pragma unroll
     for (int q = 0; q < 4; ++q) red[(w * 16 + g * 4 + q) * Fz::CO1 + r] = acc[q];
-    }
+    if (wu < 4)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[((8 + w) * 16 + g * 4 + q) * Fz::CO1 + r] = acc4[q];
   } else   {
     f32x4 acc[Fz::MT1];
 #pragma unroll
@@ -321,9 +339,13 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
     for (int idx = threadIdx.x; idx < Fz::M1 * Fz::CO1; idx += Fz::NT) {
       const int m = idx / Fz::CO1, n = idx - m * Fz::CO1;
       float s;
-      if constexpr (Fz::UNITS) {  // units 2t (K-half 0) + 2t+1 of tile t = m / 16
+      if constexpr (Fz::UNITS) {  // tiles 0-3: K-halves 2t + 2t+1; tile 4: K-quarters 8..11 in order
         const int t = m >> 4, rr = m & 15;
-        s = red[((2 * t) * 16 + rr) * Fz::CO1 + n] + red[((2 * t + 1) * 16 + rr) * Fz::CO1 + n];
+        if (t < 4)
+          s = red[((2 * t) * 16 + rr) * Fz::CO1 + n] + red[((2 * t + 1) * 16 + rr) * Fz::CO1 + n];
+        else
+          s = ((red[(8 * 16 + rr) * Fz::CO1 + n] + red[(9 * 16 + rr) * Fz::CO1 + n]) + red[(10 * 16 + rr) * Fz::CO1 + n]) +
+              red[(11 * 16 + rr) * Fz::CO1 + n];
       } else {
         s = red[idx];
 #pragma unroll
@@ -413,14 +435,14 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
 // SampleArgs::advance): block 0 adds advance_by to advance[0] and advance[1] — every reader of
 // those bases in the replay has run.
 constexpr int kRowFcBN = 16, kRowFcBM = 32;
-// Block pb of a (gx, gy, gz) = (F / 16, ROWS, env chunks) grid.
-template <int FEAT, int ROWS, int F>
+// Block pb of a (gx, gy, gz) = (F / 16, ROWS, env chunks of BM) grid.
+template <int FEAT, int ROWS, int F, int BM = kRowFcBM>
 __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, const float *__restrict__ Wfc,
                                             float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by, int pb,
                                             int gx, int gy, int gz) {
-  constexpr int KC = FEAT / 16, FLAT = FEAT * ROWS;
-  static_assert(FEAT % 16 == 0 && F % kRowFcBN == 0, "whole chunks and column blocks");
-  __shared__ __attribute__((aligned(16))) float red[4][kRowFcBM][kRowFcBN];
+  constexpr int KC = FEAT / 16, FLAT = FEAT * ROWS, MT = BM / 16;
+  static_assert(FEAT % 16 == 0 && F % kRowFcBN == 0 && BM % 16 == 0, "whole chunks, column blocks, M-tiles");
+  __shared__ __attribute__((aligned(16))) float red[4][BM][kRowFcBN];
   if (advance && pb == 0 && threadIdx.x == 0) {
     advance[0] += advance_by;
     advance[1] += advance_by;
@@ -432,40 +454,44 @@ __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, 
   // weights come from HBM once, not once per 32 envs (PMC: Breakout NATURE row_fc 15.0 MB per call)
   const int zc = L % gz, xy = L / gz;
   const int xb = xy % gx, i = xy / gx;
-  const int n0 = xb * kRowFcBN, e0 = zc * kRowFcBM;
+  const int n0 = xb * kRowFcBN, e0 = zc * BM;
   MT_PROBE_AT(1, pb, 0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   constexpr int JN = (KC + 3) / 4;
-  f32x4 a[JN][2];
+  f32x4 a[JN][MT];
   float b[JN][4];
-  const int row0 = min(e0 + r, B - 1), row1 = min(e0 + 16 + r, B - 1);
+  int rowt[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) rowt[t] = min(e0 + 16 * t + r, B - 1);
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
     const int c = min(w + 4 * j, KC - 1);  // (chunks past the row's last are loaded but not used)
     const int k0 = i * FEAT + 16 * c + 4 * g;
-    a[j][0] = *reinterpret_cast<const f32x4 *>(x + (size_t)row0 * FLAT + k0);
-    a[j][1] = *reinterpret_cast<const f32x4 *>(x + (size_t)row1 * FLAT + k0);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) a[j][t] = *reinterpret_cast<const f32x4 *>(x + (size_t)rowt[t] * FLAT + k0);
 #pragma unroll
     for (int s = 0; s < 4; ++s) b[j][s] = Wfc[(size_t)(k0 + s) * F + n0 + r];
   }
-  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
     if (w + 4 * j < KC) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][t][s], b[j][s], acc[t], 0, 0, 0);
+        for (int t = 0; t < MT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][t][s], b[j][s], acc[t], 0, 0, 0);
     }
   }
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int q = 0; q < 4; ++q) red[w][t * 16 + g * 4 + q][r] = acc[t][q];
   __syncthreads();
   MT_PROBE_AT(1, pb, 1);
-  for (int idx = threadIdx.x; idx < kRowFcBM * kRowFcBN; idx += 256) {
+  for (int idx = threadIdx.x; idx < BM * kRowFcBN; idx += 256) {
     const int m = idx / kRowFcBN, n = idx - m * kRowFcBN;
     const float s = ((red[0][m][n] + red[1][m][n]) + red[2][m][n]) + red[3][m][n];
     if (e0 + m < B) slabs[((size_t)i * B + e0 + m) * F + n0 + n] = s;
@@ -479,8 +505,8 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
                                                       const float *__restrict__ Wfc, float *__restrict__ slabs,
                                                       uint32_t *advance, uint32_t advance_by) {
   using Fz = FusedNips<C>;
-  static_assert(Fz::FC_BN == kRowFcBN && Fz::FC_BM == kRowFcBM, "tile");
-  row_fc_body<Fz::FEAT, Fz::ROWS2, Fz::F>(act2, B, Wfc, slabs, advance, advance_by,
+  static_assert(Fz::FC_BN == kRowFcBN, "tile");
+  row_fc_body<Fz::FEAT, Fz::ROWS2, Fz::F, Fz::FC_BM>(act2, B, Wfc, slabs, advance, advance_by,
                                          (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gridDim.x,
                                          gridDim.y, gridDim.z);
 }

@@ -136,7 +136,9 @@ def test_benchmarked_path_matches_oracle(config, dp, tmp_path):
         torch.cuda.synchronize()
         idx_all.append(L.idx_h.numpy().copy())
         states = c(L.states)
-        if L._update_in_rollout and not dp and not L.slot0_in_rollout:  # this update's apply has already run
+        # the rollout's last step launched this update (data parallel too: the one-graph form), so its
+        # apply — and, without slot0_in_rollout, the slot T -> 0 copy — already ran: restore slot 0
+        if L._update_in_rollout and not L.slot0_in_rollout:
             states[0] = slot0
         rm = L.rm_h.numpy().copy()
         values = c(L.values)
@@ -149,8 +151,8 @@ def test_benchmarked_path_matches_oracle(config, dp, tmp_path):
         # argmax, the dense output)
         dev = L.network.forward_branches(L.network.lstm_workspace(E, T), 1, E, T) if lstm else \
             L.network.forward_branches(L.train_ws, 0, N)
-        # the benchmarked path: the rollout launched this update (data parallel: its first graph, the
-        # learner the all-reduces and the other two)
+        # the benchmarked path: the rollout launched this update — the whole update, data parallel
+        # included (one graph: backward, both buckets' all-reduces forked and joined, apply; 'all')
         assert L._update_in_rollout == (not lstm)
         # V(s_T): the rollout's last chain (pipelined native step) or the update's first forward (LSTM)
         v_boot, pi_all, rep_all = c(L.v_boot), c(L.pi_all), c(L.rep_all)
