@@ -75,11 +75,20 @@ struct mh_runner {
   // job
   std::atomic<uint32_t> gen{0};
   std::atomic<int> arrived{0};
+  // dynamic env dealing of a per-env-publication step: every worker bumps it once per env, so it has
+  // a 128-B block to itself (the adjacent-line prefetcher pairs 64-B lines): sharing a line with the
+  // resize's read-only fields (depth, shuf) made every bump a miss in every other worker's gather
+  // loop — 3x the staging time on the box (r06h)
+  alignas(128) std::atomic<int> next_env{0};
+  char next_env_pad[128 - sizeof(std::atomic<int>)];
   std::atomic<bool> quit{false};
   bool fixed = false;
   bool pooled = false;  // stage max(f0, f1) of each push (one screen per slot)
   bool resized = false;  // stage the final 84x84 frame of each push (pool + nearest resize)
   int depth = 1;
+  // resize: source rows whose lines are prefetched ahead of the row being gathered (MH_PREFETCH_ROWS,
+  // default 1; the synthetic screens come from a 2 MB ring per env, so each push's rows miss the caches)
+  int prefetch_rows = 1;
   std::vector<int32_t> cols;             // resize column LUT (84)
   // resize column gather, per 16-byte output chunk c of a row (84*depth bytes): the source bytes
   // lie in [chunk_base[c], chunk_base[c] + 48); shuf[c][v] picks them out of source vector v
@@ -104,7 +113,7 @@ struct mh_runner {
     const int rb = (int)row_bytes, ob = 84 * depth;
     alignas(16) uint8_t m[480 + 64];
     for (int x = rb; x < rb + 64; x += 16) _mm_store_si128(reinterpret_cast<__m128i *>(m + x), _mm_setzero_si128());
-    constexpr int PD = 1;  // rows prefetched ahead
+    const int PD = prefetch_rows;  // rows prefetched ahead
     auto prefetch_row = [&](int q) {
       const uint8_t *na = s0 + (size_t)rows[q] * row_bytes, *nb = s1 + (size_t)rows[q] * row_bytes;
       for (int x = 0; x < rb; x += 64) {
@@ -153,7 +162,11 @@ struct mh_runner {
   bool busy = false;  // mh_runner_step_begin dispatched, mh_runner_step_end not yet called
   // host-phase split of a step (mh_runner_stats): worker time in stage_env (frame pool + resize +
   // the streaming copy into the staging) and worker time in the whole phase, summed over workers
-  std::atomic<int64_t> stage_ns{0}, busy_ns{0}, stat_steps{0};
+  // (own 128-B block: bumped by each worker at the end of its phase, while others still read the
+  // per-step fields above)
+  alignas(128) std::atomic<int64_t> stage_ns{0};
+  std::atomic<int64_t> busy_ns{0}, stat_steps{0};
+  char stats_pad[128 - 3 * sizeof(std::atomic<int64_t>)];
   bool nt_stores = true;  // resized frames: streaming stores (plain stores measured the same on the box)
 
   int block_begin(int w) const { return (int)((int64_t)E * w / W); }
@@ -204,7 +217,15 @@ struct mh_runner {
       }
     } else if (phase == 1) {
       const bool per_env = ready && fixed && !frame_idx;
-      for (int i = b0; i < b1; ++i) {
+      // per-env publication (the pipelined rollout): envs are dealt dynamically, the next one to the
+      // first free worker (next_env), instead of static blocks of E / W — an env's work varies (FiGAR
+      // repeats: 1-4 pushes; cache misses on its screens), and a static block's slowest worker set
+      // the last publication (Breakout FiGAR: 35.7 us mean worker busy time vs a 44.3 us step, r06).
+      // Each env's outputs (staging slots 4e.., push count, reward, over, ready word) are its own, so
+      // the assignment changes nothing they hold. The other modes keep the blocks: their staging
+      // pass below re-walks the worker's block after the step.
+      int i = per_env ? next_env.fetch_add(1, std::memory_order_relaxed) : b0;
+      for (; i < (per_env ? E : b1); i = per_env ? next_env.fetch_add(1, std::memory_order_relaxed) : i + 1) {
         Env &e = env[i];
         e.npush = 0;
         int left = tab[r_idx[i]];  // Action.init_from_list (exploration_policy.py:13-17)
@@ -277,7 +298,12 @@ struct mh_runner {
         for (size_t q = 0; q < nr; ++q) {
           const size_t so = (rows.empty() ? q : (size_t)rows[q]) * row_bytes;
           uint8_t *dq = d + q * row_bytes;
-          for (size_t x = 0; x < row_bytes; ++x) dq[x] = std::max(s0[so + x], s1[so + x]);
+          // SSE max, streamed to the staging (non-temporal: the GPU reads these lines over PCIe while
+          // this thread works on, and must not snoop them out of its cache — as the resized frames)
+          for (size_t x = 0; x < row_bytes; x += 16)
+            _mm_stream_si128(reinterpret_cast<__m128i *>(dq + x),
+                             _mm_max_epu8(_mm_loadu_si128(reinterpret_cast<const __m128i *>(s0 + so + x)),
+                                          _mm_loadu_si128(reinterpret_cast<const __m128i *>(s1 + so + x))));
         }
         continue;
       }
@@ -329,6 +355,7 @@ struct mh_runner {
   }
   void dispatch_begin(int ph) {
     phase = ph;
+    next_env.store(0, std::memory_order_relaxed);  // (published to the workers by gen's release)
     arrived.store(0, std::memory_order_relaxed);
     gen.fetch_add(1, std::memory_order_acq_rel);
     gen.notify_all();
@@ -371,6 +398,10 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
     set_error("bad sizes");
     return 1;
   }
+  if ((flags & MH_RUNNER_POOLED) && (frame_bytes / 210) % 16 != 0) {
+    set_error("pooled staging needs screen rows of a multiple of 16 bytes (SSE max)");
+    return 1;
+  }
   if ((flags & MH_RUNNER_RESIZED) && (n_rows != 84 || (flags & MH_RUNNER_POOLED))) {
     set_error("resized staging needs the 84-row row_select (and excludes pooled)");
     return 1;
@@ -401,6 +432,7 @@ extern "C" int mh_runner_create(int n_envs, int n_workers, const int32_t *tab_re
   if (r->resized) r->sfb = (size_t)84 * 84 * r->depth;
   r->reward_len = reward_len;
   r->episode_len = episode_len;
+  if (const char *pd = std::getenv("MH_PREFETCH_ROWS")) r->prefetch_rows = std::max(0, std::min(84, std::atoi(pd)));
   r->env.resize(n_envs);
   for (int i = 0; i < n_envs; ++i) {
     r->env[i].screens = screens + (size_t)i * ring * frame_bytes;
@@ -525,6 +557,10 @@ extern "C" int mh_runner_reset(mh_runner *r, uint8_t *staging, int32_t *push_off
     set_error("null argument");
     return 1;
   }
+  if ((r->pooled || r->resized) && (reinterpret_cast<uintptr_t>(staging) & 15) != 0) {
+    set_error("pooled / resized staging must be 16-byte aligned (streaming stores)");
+    return 1;
+  }
   r->staging = staging;
   r->push_offset = push_offset;
   r->push_count = push_count;
@@ -560,6 +596,10 @@ extern "C" int mh_runner_step_begin(mh_runner *r, const int32_t *a_idx, const in
   }
   if (r->busy) {
     set_error("a step is already in flight");
+    return 1;
+  }
+  if ((r->pooled || r->resized) && (reinterpret_cast<uintptr_t>(staging) & 15) != 0) {
+    set_error("pooled / resized staging must be 16-byte aligned (streaming stores)");
     return 1;
   }
   const int nr = (int)r->tab.size();
@@ -614,6 +654,10 @@ extern "C" int mh_runner_step(mh_runner *r, const int32_t *a_idx, const int32_t 
   }
   if (r->busy) {
     set_error("a step is already in flight");
+    return 1;
+  }
+  if ((r->pooled || r->resized) && (reinterpret_cast<uintptr_t>(staging) & 15) != 0) {
+    set_error("pooled / resized staging must be 16-byte aligned (streaming stores)");
     return 1;
   }
   const int nr = (int)r->tab.size();

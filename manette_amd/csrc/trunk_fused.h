@@ -512,18 +512,21 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
 }
 
 // the same for the layered trunks (NATURE: 7 rows of 448 features, PWYX: 10 rows of 640)
+#ifndef MT_ROWFC_BM
+#define MT_ROWFC_BM 32  // env rows per block of the layered trunks' dense layer (experiment knob)
+#endif
 template <int FEAT, int ROWS, int F>
 __global__ __launch_bounds__(256) void row_fc_kernel(const float *__restrict__ x, int B, const float *__restrict__ Wfc,
                                                      float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by) {
-  row_fc_body<FEAT, ROWS, F>(x, B, Wfc, slabs, advance, advance_by,
-                             (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gridDim.x, gridDim.y,
-                             gridDim.z);
+  row_fc_body<FEAT, ROWS, F, MT_ROWFC_BM>(x, B, Wfc, slabs, advance, advance_by,
+                                          (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gridDim.x,
+                                          gridDim.y, gridDim.z);
 }
 template <int FEAT, int ROWS, int F>
 static inline int launch_row_fc(const float *x, int B, const float *Wfc, float *slabs, hipStream_t s,
                                 uint32_t *advance = nullptr, uint32_t advance_by = 0) {
   if (B <= 0 || !launch_allowed()) return MT_OK;
-  hipLaunchKernelGGL((row_fc_kernel<FEAT, ROWS, F>), dim3(F / kRowFcBN, ROWS, (B + kRowFcBM - 1) / kRowFcBM),
+  hipLaunchKernelGGL((row_fc_kernel<FEAT, ROWS, F>), dim3(F / kRowFcBN, ROWS, (B + MT_ROWFC_BM - 1) / MT_ROWFC_BM),
                      dim3(256), 0, s, x, B, Wfc, slabs, advance, advance_by);
   MT_LAUNCHED();
   return MT_OK;

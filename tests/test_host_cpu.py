@@ -350,3 +350,41 @@ def test_emulator_count_scope():
         train.shard_emulators(30, 'global', 8, 0)
     a = train.get_arg_parser().parse_args(['--ec_scope', 'global', '-ec', '256'])
     assert a.ec_scope == 'global' and a.emulator_counts == 256 and a.sampling == 'host'
+
+
+@pytest.mark.parametrize('workers', [1, 3, 8])
+def test_native_runner_per_env_publication_matches_blocks(workers):
+    """With per-env ready words (the pipelined rollout's mode) the workers take envs dynamically
+    (next free worker, runner.cpp next_env); every env's staging slots, push count, reward, episode
+    flag and ready word equal the statically blocked step's (mh_runner_step without ready words)."""
+    import ctypes as C
+    from manette_amd import _lib
+    from manette_amd.environment import COL_LUT, ROW_LUT
+    from manette_amd.runners import NativeRunners
+    from manette_amd.synthetic import SyntheticBank
+    E = 11
+    tab = opol.tab_repetitions(10, 11)
+    bank = SyntheticBank(4, E, episode_len=6)
+    kw = dict(row_select=ROW_LUT, fixed_slots=True, resized=True, col_lut=COL_LUT)
+    a, b = NativeRunners(bank, 2, tab, **kw), NativeRunners(bank, workers, tab, **kw)
+    ready = np.zeros(E * 32, np.uint32)  # MH_READY_STRIDE words per env
+    lib = _lib.host()
+    try:
+        na, nb = a.reset(), b.reset()
+        rs = np.random.RandomState(workers)
+        for step in range(12):
+            act, rep = rs.randint(0, 6, E).astype(np.int32), rs.randint(0, 11, E).astype(np.int32)
+            _lib.check_host(lib.mh_runner_set_ready(b._h, ready.ctypes.data_as(C.c_void_p), 100 + step),
+                            'mh_runner_set_ready')
+            na, nb = a.step(act, rep), b.step(act, rep)
+            assert na == nb
+            np.testing.assert_array_equal(a.push_meta.numpy(), b.push_meta.numpy())
+            np.testing.assert_array_equal(a.staging.numpy(), b.staging.numpy())
+            np.testing.assert_array_equal(a.reward.numpy(), b.reward.numpy())
+            np.testing.assert_array_equal(a.over.numpy(), b.over.numpy())
+            words = ready.reshape(E, 32)[:, 0]
+            np.testing.assert_array_equal(words, ((100 + step) << 3) | a.push_count.numpy().astype(np.uint32))
+        _lib.check_host(lib.mh_runner_set_ready(b._h, None, 0), 'mh_runner_set_ready')
+    finally:
+        a.stop()
+        b.stop()

@@ -28,7 +28,14 @@ for _ in range(50):
     r.step(a, rr)
 n = 2000
 busy = 0.0
-for _ in range(n):
+# READY=1: per-env ready words (the pipelined rollout's mode: per-env publication, dynamic env dealing)
+ready = np.zeros(E * 32, np.uint32) if os.environ.get('READY') == '1' else None
+if ready is not None:
+    import ctypes as C
+    from manette_amd import _lib
+for k in range(n):
+    if ready is not None:
+        _lib.check_host(_lib.host().mh_runner_set_ready(r._h, ready.ctypes.data_as(C.c_void_p), k + 1), 'ready')
     t = time.perf_counter()
     r.step(a, rr)
     t1 = time.perf_counter()
