@@ -431,6 +431,9 @@ int mt_rollout_trunk_timing(mt_rollout *ro, int enable, double *sum_us, int64_t 
  * data-parallel one (mt_rollout_set_update_dp), before the graphs are destroyed. */
 int mt_rollout_set_update(mt_rollout *ro, void *graph_exec, float *lr_host, double initial_lr,
                           double annealing_steps);
+/* Diagnostics: the update the rollout launches — *form = 0 none, 1 mt_rollout_set_update's graph,
+ * 2 mt_rollout_set_update_dp's three graphs. */
+int mt_rollout_update_form(const mt_rollout *ro, int *form);
 
 /* ---- data-parallel communicator (RCCL over xGMI; manette_amd/csrc/comm.hip) ----------------
  * The reference has no collective: its only shard unit is the contiguous env split of

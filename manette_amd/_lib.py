@@ -104,6 +104,7 @@ _HIP_SIGS = {
     'mt_rollout_host_trace': (_I, [_P, _P, _I, _P]),
     'mt_rollout_trunk_timing': (_I, [_P, _I, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     'mt_rollout_set_update': (_I, [_P, _P, _P, C.c_double, C.c_double]),
+    'mt_rollout_update_form': (_I, [_P, C.POINTER(_I)]),
     'mt_rollout_set_update_dp': (_I, [_P, _P, _P, _P, _SZ, _SZ, _P, C.c_double, C.c_double]),
     'mt_comm_unique_id': (_I, [C.c_char_p]),
     'mt_comm_init': (_I, [C.c_char_p, _I, _I, _I, C.POINTER(_P)]),

@@ -792,6 +792,12 @@ extern "C" int mt_rollout_set_update(mt_rollout *ro, void *graph_exec, float *lr
   return MT_OK;
 }
 
+extern "C" int mt_rollout_update_form(const mt_rollout *ro, int *form) {
+  MT_CHECK_ARG(ro && form, "null argument");
+  *form = ro->dp_graph[0] ? 2 : (ro->update_graph ? 1 : 0);
+  return MT_OK;
+}
+
 extern "C" int mt_rollout_set_update_dp(mt_rollout *ro, void *const *graph_execs, mt_comm *comm, float *grad, size_t n,
                                         size_t split, float *lr_host, double initial_lr, double annealing_steps) {
   MT_CHECK_ARG(ro, "null argument");

@@ -75,12 +75,6 @@ struct mh_runner {
   // job
   std::atomic<uint32_t> gen{0};
   std::atomic<int> arrived{0};
-  // dynamic env dealing of a per-env-publication step: every worker bumps it once per env, so it has
-  // a 128-B block to itself (the adjacent-line prefetcher pairs 64-B lines): sharing a line with the
-  // resize's read-only fields (depth, shuf) made every bump a miss in every other worker's gather
-  // loop — 3x the staging time on the box (r06h)
-  alignas(128) std::atomic<int> next_env{0};
-  char next_env_pad[128 - sizeof(std::atomic<int>)];
   std::atomic<bool> quit{false};
   bool fixed = false;
   bool pooled = false;  // stage max(f0, f1) of each push (one screen per slot)
@@ -169,6 +163,11 @@ struct mh_runner {
   char stats_pad[128 - 3 * sizeof(std::atomic<int64_t>)];
   bool nt_stores = true;  // resized frames: streaming stores (plain stores measured the same on the box)
 
+  // Static env blocks: a worker keeps the same envs every step. (Round 6 dealt the envs of a
+  // per-env-publication step dynamically, the next env to the first free worker, to balance FiGAR's
+  // 1-4 pushes per env: the staging time per worker doubled on the box — Breakout 44 -> 80 us, Pong
+  // 7.5 -> 9.5-12.7 us, profiles/r06h — each env's screens and state were then read by a different
+  // core, often on another CCD, instead of from the L3 its worker had left them in.)
   int block_begin(int w) const { return (int)((int64_t)E * w / W); }
   int block_end(int w) const { return (int)((int64_t)E * (w + 1) / W); }
 
@@ -217,15 +216,7 @@ struct mh_runner {
       }
     } else if (phase == 1) {
       const bool per_env = ready && fixed && !frame_idx;
-      // per-env publication (the pipelined rollout): envs are dealt dynamically, the next one to the
-      // first free worker (next_env), instead of static blocks of E / W — an env's work varies (FiGAR
-      // repeats: 1-4 pushes; cache misses on its screens), and a static block's slowest worker set
-      // the last publication (Breakout FiGAR: 35.7 us mean worker busy time vs a 44.3 us step, r06).
-      // Each env's outputs (staging slots 4e.., push count, reward, over, ready word) are its own, so
-      // the assignment changes nothing they hold. The other modes keep the blocks: their staging
-      // pass below re-walks the worker's block after the step.
-      int i = per_env ? next_env.fetch_add(1, std::memory_order_relaxed) : b0;
-      for (; i < (per_env ? E : b1); i = per_env ? next_env.fetch_add(1, std::memory_order_relaxed) : i + 1) {
+      for (int i = b0; i < b1; ++i) {
         Env &e = env[i];
         e.npush = 0;
         int left = tab[r_idx[i]];  // Action.init_from_list (exploration_policy.py:13-17)
@@ -355,7 +346,6 @@ struct mh_runner {
   }
   void dispatch_begin(int ph) {
     phase = ph;
-    next_env.store(0, std::memory_order_relaxed);  // (published to the workers by gen's release)
     arrived.store(0, std::memory_order_relaxed);
     gen.fetch_add(1, std::memory_order_acq_rel);
     gen.notify_all();

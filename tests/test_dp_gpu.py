@@ -114,3 +114,60 @@ def test_native_bucketed_update_stream_order(config, one_graph, tmp_path, monkey
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     assert got['gs'] == ref['gs']
     np.testing.assert_array_equal(got['grad'], 2.0 * ref['grad'])
+
+
+def test_rollout_update_registration_order(tmp_path):
+    """mt_rollout_set_update / _set_update_dp: registering either form replaces the
+    other; unregistering with mt_rollout_set_update(NULL) clears both (a step must never launch a
+    data-parallel update whose LR word was just unregistered); _set_update_dp(NULL) clears only the
+    data-parallel form."""
+    import ctypes as C
+    import bench
+    from manette_amd import _lib
+    L, _ = bench.make_learner('pong-nips', debugging_folder=str(tmp_path) + '/', episode_len=13)
+    L.start()
+    lib = _lib.hip()
+    form = C.c_int(-1)
+
+    def current():
+        _lib.check(lib.mt_rollout_update_form(L.native_step, C.byref(form)), 'mt_rollout_update_form')
+        return form.value
+    try:
+        for _ in range(3):
+            L.book.new_update()
+            L.rollout()
+            L.update()
+        torch.cuda.synchronize()
+        assert L._update_in_rollout and current() == 1
+        g = L._graphs[0]
+        g = g.value if isinstance(g, C.c_void_p) else g
+        lr = C.c_void_p(L.network._lr_host.data_ptr())
+        grad = L.network.grad
+        from manette_amd.comm import LoopbackComm
+        comm = LoopbackComm(replicas=1, delay_us=0)
+        try:
+            gs = (C.c_void_p * 3)(g, g, g)  # (registered only: nothing is launched here)
+            _lib.check(lib.mt_rollout_set_update_dp(L.native_step, gs, comm._h, C.c_void_p(grad.data_ptr()),
+                                                    grad.numel(), 16, lr, 0.0224, 8e7), 'set_update_dp')
+            assert current() == 2
+            _lib.check(lib.mt_rollout_set_update(L.native_step, None, None, 0.0, 0.0), 'set_update(NULL)')
+            assert current() == 0  # both forms cleared
+            _lib.check(lib.mt_rollout_set_update(L.native_step, g, lr, 0.0224, 8e7), 'set_update')
+            assert current() == 1
+            _lib.check(lib.mt_rollout_set_update_dp(L.native_step, None, None, None, 0, 0, None, 0.0, 0.0),
+                       'set_update_dp(NULL)')
+            assert current() == 1  # the single form stays
+            _lib.check(lib.mt_rollout_set_update_dp(L.native_step, gs, comm._h, C.c_void_p(grad.data_ptr()),
+                                                    grad.numel(), 16, lr, 0.0224, 8e7), 'set_update_dp')
+            assert current() == 2  # replaces the single form
+            _lib.check(lib.mt_rollout_set_update(L.native_step, g, lr, 0.0224, 8e7), 'set_update')
+            assert current() == 1
+        finally:
+            comm.close()
+        # the registered single-process update still runs the learner's rollout + update
+        L.book.new_update()
+        L.rollout()
+        L.update()
+        torch.cuda.synchronize()
+    finally:
+        L.cleanup()

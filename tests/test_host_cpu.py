@@ -354,9 +354,9 @@ def test_emulator_count_scope():
 
 @pytest.mark.parametrize('workers', [1, 3, 8])
 def test_native_runner_per_env_publication_matches_blocks(workers):
-    """With per-env ready words (the pipelined rollout's mode) the workers take envs dynamically
-    (next free worker, runner.cpp next_env); every env's staging slots, push count, reward, episode
-    flag and ready word equal the statically blocked step's (mh_runner_step without ready words)."""
+    """With per-env ready words (the pipelined rollout's mode: each env staged and published as soon
+    as it is stepped) every env's staging slots, push count, reward, episode flag and ready word
+    equal the step without ready words (staging after the step), whatever the worker count."""
     import ctypes as C
     from manette_amd import _lib
     from manette_amd.environment import COL_LUT, ROW_LUT

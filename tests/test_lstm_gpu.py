@@ -305,3 +305,47 @@ def test_lstm_frames_backward_norm_partials(E, T):
     norm = float(np.sqrt(net.partials.double().sum().item()))
     ref = optim.global_norm([g0.cpu().numpy()])
     assert np.isfinite(norm) and abs(norm - ref) <= 1e-5 * ref, (norm, ref)
+
+
+def test_lstm_frames_backward_launch_by_launch():
+    """Every launch of mt_lstm_frames_backward is numbered by the launch window (bench.py times the
+    LSTM train pass launch by launch): the backward issued as windows [0, k) then [k, ...) leaves
+    the same gradient, bit for bit, as one call, and the windows count every launch."""
+    import ctypes as C
+    from manette_amd import _lib
+    E, T, A, R, depth = 6, 5, 9, 11, 1
+    net = _net(depth, A, R, seed=77, act='relu')
+    rs = np.random.RandomState(78)
+    fstore = rs.randint(0, 256, size=(1 + (T + 5) * E, 84, 84, 4 * depth)).astype(np.uint8)
+    fstore[0] = 0
+    nz = rs.choice([0, 0, 1, 3, 5], size=(T + 1, E)).astype(np.int32)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    fs_d, nz_d = d(fstore), d(nz)
+    net.lstm_frames_forward(fs_d, 0, 1 + 5 * E, E, T)
+    for t in range(1, T + 1):
+        net.lstm_frames_forward(fs_d, 1 + (4 + t) * E, E, E, T)
+    v = torch.zeros(T + 1, E, device='cuda')
+    pi = torch.zeros(T + 1, E, A, device='cuda')
+    rep = torch.zeros(T + 1, E, R, device='cuda')
+    for t in range(T + 1):
+        net.lstm_windows_forward(nz_d[t], t, E, T, out=(v[t], pi[t], rep[t]))
+    N = T * E
+    args = (d(rs.randint(0, A, size=N).astype(np.int32)), d(rs.randint(0, R, size=N).astype(np.int32)),
+            d(rs.randn(N).astype(np.float32)), d(rs.randn(N).astype(np.float32)))
+    bwd = lambda: net.lstm_frames_backward(fs_d, nz_d[:T], E, T, pi[:T], rep[:T], v[:T], *args)
+    lib = _lib.hip()
+    net.grad.zero_()
+    lib.mt_launch_window(0, -1)
+    bwd()
+    total = lib.mt_launch_window(-1, -1)
+    g0 = net.grad.clone()
+    assert total >= 9  # loss, BPTT, zero-frame partials, gather, d flat, 4 conv launches, the last slab sum
+    for k in (1, 3, 5, total - 1):
+        net.grad.zero_()
+        lib.mt_launch_window(0, k)
+        bwd()
+        assert lib.mt_launch_window(k, -1) == total
+        bwd()
+        lib.mt_launch_window(-1, -1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(net.grad.cpu().numpy(), g0.cpu().numpy(), err_msg='split at %d' % k)
