@@ -403,7 +403,7 @@ def main():
                     help='the data-parallel update at world 1 (RCCL communicator, bucketed side-stream all-reduce '
                          'between three update graphs, the learner launching the update): the per-GPU cost of the '
                          'N-GPU path (paac.PAACLearner.dp)')
-    ap.add_argument('--pin_threads', default='auto', choices=['auto', 'on', 'off'],
+    ap.add_argument('--pin_threads', default='auto', choices=['auto', 'slice', 'pin', 'on', 'off'],
                     help='host-thread placement (manette_amd/placement.py); auto: pinned when several ranks share '
                          'the node')
     ap.add_argument('--settle_s', type=float, default=1.0,

@@ -163,7 +163,7 @@ class PAACLearner(ActorLearner):
         lw = int(os.environ.get('LOCAL_WORLD_SIZE', '1'))
         lr = int(os.environ.get('LOCAL_RANK', '0'))
         mode = self.pin_threads
-        if mode == 'off' or (mode == 'auto' and lw <= 1):
+        if mode == 'off' or (mode == 'auto' and lw <= 1):  # (nothing placed: no topology reads)
             topo = dict(allowed=sorted(os.sched_getaffinity(0)), quota=placement.cgroup_cpu_limit())
         else:
             topo = placement.topology(lw)
@@ -175,6 +175,7 @@ class PAACLearner(ActorLearner):
             from . import placement
             self.placement = self._plan_threads()
             self.workers = self.placement['ew_used']
+            placement.apply_before_workers(self.placement)  # ('slice': the workers inherit the rank's cpus)
             bank = self.environment_creator.create_bank(0, E)
             self.bank = bank
             self.in_place = self.staging == 'in_place'
@@ -202,7 +203,7 @@ class PAACLearner(ActorLearner):
                                          dtype=torch.uint8, device=self.dev)
                 total = self.runners.reset()
                 self._upload_pushes(total, self.states[0], self.states[0].clone())
-            if self.placement['pinned']:
+            if self.placement['pinned'] or self.placement['sliced']:  # ('slice': no worker cpus, the spin only)
                 self.runners.set_threads(self.placement['worker_cpus'], self.placement['spin_us'])
                 placement.apply_main(self.placement)
             if self.sampling == 'device':

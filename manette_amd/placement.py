@@ -13,11 +13,20 @@ on the macro-step's critical path. plan() decides, per rank:
     it, ew is capped to budget - 1 (at least 1; the env -> worker split changes, every env's
     trajectory does not) and idle workers spin 50 us instead of 2 ms before sleeping, so an idle
     pool yields its cores to the other ranks' pools;
-  * the pinning: the host thread on the slice's first cpu (plus any cpus no worker takes), worker w
-    on the next ones (mh_runner_set_threads).
+  * the placement itself, by mode:
+      'slice': the rank's host thread and every thread it starts afterwards (the emulator workers)
+               may run anywhere in the rank's slice — NUMA-local, disjoint from the other ranks, and
+               the scheduler still moves a thread off a core another process keeps busy;
+      'pin':   the host thread on the slice's first cpu (plus any cpus no worker takes), worker w on
+               the next ones, one cpu each (mh_runner_set_threads);
+      'auto':  'slice' when several ranks share the node, else 'off' (the scheduler's placement);
+      'off':   nothing changed ('on' is an alias of 'pin').
+    One cpu per thread measured badly on the shared 1-GPU boxes (profiles/r06pin: Breakout FiGAR
+    273-278k pinned vs 342-523k unpinned, its workers' staging 122-126 vs 32-67 us per step: a pinned
+    worker cannot leave a core another tenant keeps busy), so the default keeps the scheduler free
+    inside the rank's slice.
 plan() is a pure function of the topology it is given (tests/test_placement_cpu.py); topology()
-reads it from /proc, /sys and torch on the running host. Mode 'auto' pins only when several ranks
-share the node (the 1-GPU bench keeps the scheduler's placement); 'on' / 'off' force it.
+reads it from /proc, /sys and torch on the running host.
 """
 import math
 import os
@@ -122,31 +131,42 @@ def plan(ew, E, local_rank, local_world, allowed, quota=None, node_of_rank=None,
     budget = len(mine)
     if quota:  # the container's CPU quota, shared by every local rank
         budget = min(budget, max(1, int(math.floor(quota / max(local_world, 1)))))
-    pinned = mode == 'on' or (mode == 'auto' and local_world > 1)
+    if mode == 'on':
+        mode = 'pin'
+    eff = ('slice' if local_world > 1 else 'off') if mode == 'auto' else mode
+    pinned, sliced = eff == 'pin', eff == 'slice'
+    placed = pinned or sliced
     oversub = budget < ew_req + 1
-    ew_used = max(1, min(ew_req, budget - 1)) if (pinned and oversub) else ew_req
-    spin = SPIN_US_OVERSUB if oversub and pinned else SPIN_US
+    ew_used = max(1, min(ew_req, budget - 1)) if (placed and oversub) else ew_req
+    spin = SPIN_US_OVERSUB if oversub and placed else SPIN_US
     if len(mine) >= ew_used + 1:
         main_cpus = [mine[0]] + mine[1 + ew_used:]
         worker_cpus = mine[1:1 + ew_used]
     else:  # fewer cpus than threads: workers round-robin over the slice, the host thread on all of it
         main_cpus = list(mine)
         worker_cpus = [mine[(1 + w) % len(mine)] for w in range(ew_used)]
-    return dict(mode=mode, pinned=pinned, numa_node=me, local_rank=local_rank, local_world=local_world,
-                cpus=format_cpulist(mine), cores_per_rank=budget, quota=quota, ew_requested=int(ew),
-                ew_used=ew_used, threads_per_rank=ew_used + 1, oversubscribed=oversub, spin_us=spin,
-                worker_cpus=worker_cpus if pinned else [], main_cpus=main_cpus if pinned else [])
+    return dict(mode=mode, placement=eff, pinned=pinned, sliced=sliced, numa_node=me, local_rank=local_rank,
+                local_world=local_world, cpus=format_cpulist(mine), cores_per_rank=budget, quota=quota,
+                ew_requested=int(ew), ew_used=ew_used, threads_per_rank=ew_used + 1, oversubscribed=oversub,
+                spin_us=spin, worker_cpus=worker_cpus if pinned else [],
+                main_cpus=main_cpus if pinned else (list(mine) if sliced else []))
+
+
+def apply_before_workers(p):
+    """'slice': restrict the calling (host) thread to the rank's slice before the emulator workers
+    start, so they inherit it (threads started later do too)."""
+    if p['sliced'] and p['main_cpus']:
+        os.sched_setaffinity(0, set(p['main_cpus']))
 
 
 def apply_main(p):
-    """Pin the calling (host) thread to the plan's main cpus (threads it starts later inherit the
-    mask); no-op when the plan is not pinned."""
+    """'pin': the calling (host) thread onto its cpus, after the workers were pinned to theirs."""
     if p['pinned'] and p['main_cpus']:
         os.sched_setaffinity(0, set(p['main_cpus']))
 
 
 def report(p):
     """The plan's fields for the bench line (no cpu lists of the workers)."""
-    keys = ('mode', 'pinned', 'numa_node', 'local_world', 'cpus', 'cores_per_rank', 'quota', 'ew_requested',
+    keys = ('mode', 'placement', 'numa_node', 'local_world', 'cpus', 'cores_per_rank', 'quota', 'ew_requested',
             'ew_used', 'threads_per_rank', 'oversubscribed', 'spin_us')
     return {k: p[k] for k in keys}

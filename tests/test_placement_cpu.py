@@ -38,10 +38,12 @@ def test_eight_ranks_get_disjoint_slices_on_their_gpus_node():
         assert set(cpus) <= set(topo['node_cpus'][node])  # next to its GPU's PCIe root
         assert not (set(cpus) & seen)                     # no core shared with another rank
         seen |= set(cpus)
-        assert p['pinned'] and not p['oversubscribed'] and p['ew_used'] == 8 and p['spin_us'] == pl.SPIN_US
-        assert len(p['worker_cpus']) == 8 and len(set(p['worker_cpus'])) == 8
-        assert set(p['worker_cpus']) <= set(cpus) and p['main_cpus'][0] not in p['worker_cpus']
-        assert set(p['main_cpus']) | set(p['worker_cpus']) == set(cpus)
+        assert p['sliced'] and not p['pinned'] and not p['oversubscribed'] and p['ew_used'] == 8
+        assert p['spin_us'] == pl.SPIN_US and p['worker_cpus'] == [] and p['main_cpus'] == cpus
+        q = pl.plan(8, 32, r, 8, mode='pin', **topo)  # one cpu per thread
+        assert q['pinned'] and len(q['worker_cpus']) == 8 and len(set(q['worker_cpus'])) == 8
+        assert set(q['worker_cpus']) <= set(cpus) and q['main_cpus'][0] not in q['worker_cpus']
+        assert set(q['main_cpus']) | set(q['worker_cpus']) == set(cpus)
     assert len(seen) == 128
 
 
@@ -49,9 +51,9 @@ def test_oversubscribed_node_caps_ew_and_shortens_the_spin():
     # 32 allowed cpus for 8 ranks: 4 each, so ew 8 -> 3 (3 workers + the host thread)
     plans = [pl.plan(8, 32, r, 8, **_eight_gpu_node(allowed=list(range(16)) + list(range(64, 80)))) for r in range(8)]
     for p in plans:
-        assert p['cores_per_rank'] == 4 and p['oversubscribed']
+        assert p['cores_per_rank'] == 4 and p['oversubscribed'] and p['sliced']
         assert p['ew_used'] == 3 and p['threads_per_rank'] == 4 and p['spin_us'] == pl.SPIN_US_OVERSUB
-        assert len(set(p['worker_cpus'])) == 3
+        assert len(p['main_cpus']) == 4
     # the container's quota binds before the slice: 16 cpus' worth for 8 ranks -> 2 each -> ew 1
     p = pl.plan(8, 32, 5, 8, **_eight_gpu_node(quota=16.0))
     assert p['cores_per_rank'] == 2 and p['ew_used'] == 1 and p['oversubscribed']
@@ -59,12 +61,15 @@ def test_oversubscribed_node_caps_ew_and_shortens_the_spin():
 
 def test_single_rank_auto_leaves_the_scheduler_alone():
     p = pl.plan(8, 32, 0, 1, allowed=list(range(8)), quota=None)
-    assert not p['pinned'] and p['ew_used'] == 8 and p['worker_cpus'] == [] and p['main_cpus'] == []
+    assert not p['pinned'] and not p['sliced'] and p['placement'] == 'off'
+    assert p['ew_used'] == 8 and p['worker_cpus'] == [] and p['main_cpus'] == []
     assert p['oversubscribed'] and p['spin_us'] == pl.SPIN_US  # (reported, not acted on)
-    p = pl.plan(8, 32, 0, 1, allowed=list(range(16)), quota=None, mode='on')
+    p = pl.plan(8, 32, 0, 1, allowed=list(range(16)), quota=None, mode='on')  # ('on' = 'pin')
     assert p['pinned'] and p['ew_used'] == 8 and len(p['worker_cpus']) == 8
+    p = pl.plan(8, 32, 0, 1, allowed=list(range(16)), quota=None, mode='slice')
+    assert p['sliced'] and p['main_cpus'] == list(range(16)) and p['ew_used'] == 8
     p = pl.plan(8, 32, 3, 8, mode='off', **_eight_gpu_node())
-    assert not p['pinned'] and p['ew_used'] == 8
+    assert not p['pinned'] and not p['sliced'] and p['ew_used'] == 8
 
 
 def test_unknown_topology_splits_the_allowed_cpus():

@@ -171,7 +171,7 @@ def get_arg_parser():
     parser.add_argument('--comm', default='rccl', choices=['rccl', 'torch'], help='data-parallel gradient all-reduce: '
                         'rccl = RCCL behind the C ABI (mt_allreduce, one GPU per rank); torch = torch.distributed on '
                         'the process group (ranks sharing a GPU, tests)', dest='comm')
-    parser.add_argument('--pin_threads', default='auto', choices=['auto', 'on', 'off'], help='native runner '
+    parser.add_argument('--pin_threads', default='auto', choices=['auto', 'slice', 'pin', 'on', 'off'], help='native runner '
                         'thread placement (manette_amd/placement.py): pin the emulator threads and the host thread '
                         'to cores of the GPU\'s NUMA node, capping -ew when the node\'s cores are oversubscribed; '
                         'auto = only when several ranks share the node', dest='pin_threads')
