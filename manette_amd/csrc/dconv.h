@@ -1085,6 +1085,7 @@ constexpr int dw_pad(int c, int wd) {  // channel stride whose row stride wd * c
 template <class G, bool U8, int TMW_>
 struct DWCfg {
   static_assert((G::S == 1 && G::SAME) || !G::SAME, "stride-1 SAME or VALID conv");
+  using Geom = G;
   static constexpr int CIN = G::CIN, COUT = G::COUT, KH = G::KH, KW = G::KW, H = G::H, W = G::W, S = G::S;
   static constexpr int OH = G::OH, OW = G::OW;  // (input H x W, output OH x OW)
   static constexpr int KK = G::KK, TMW = TMW_;
@@ -1108,6 +1109,198 @@ struct DWCfg {
   static constexpr int XQ = RIN * WP * (CIN / 4), YQ = R * WPAD * (COUT / 4);  // quads per chunk
   static constexpr int XIT = (XQ + 255) / 256, YIT = (YQ + 255) / 256;
   static constexpr size_t SLAB = (size_t)(KK + 1) * COUT;
+  // Row-mapped staging (ROWMAP): wave w stages patch rows w, w + 4, ... and dY row w of a chunk; lane
+  // l takes the row's quads l + 64 k, so its pixel (l / CQ + k PXK) and channel quad (l % CQ) are
+  // fixed for the whole job: the global offsets are computed once, row validity is wave-uniform (a
+  // zero-length buffer descriptor) and out-of-image columns read zero through the descriptor's range
+  // check (offset 0x80000000). Per chunk a quad costs its load and its LDS store, nothing else.
+  // (LUX lanes of a wave take patch quads: 63 for the RGB conv1's 3 quads per pixel, lane 63 idle)
+  static constexpr int CQ = CIN / 4, CQO = COUT / 4;
+  static constexpr bool ROWMAP = S == 1 && G::SAME && RIN % 4 == 0 && CQ <= 16 && 64 % CQO == 0;
+  static constexpr int LUX = 64 - 64 % CQ;
+  static constexpr int XROWS = RIN / 4, QRX = WP * CQ, KX = (QRX + LUX - 1) / LUX, PXK = LUX / CQ;
+  static constexpr int QRY = WPAD * CQO, KY = (QRY + 63) / 64, PYK = 64 / CQO;
+  // k steps whose every lane is inside the image and the row (one shared offset + k stride)
+  static constexpr bool x_inner(int k) { return k * PXK >= G::PL && (k + 1) * PXK <= G::PL + W && (k + 1) * LUX <= QRX; }
+  static constexpr bool y_inner(int k) { return (k + 1) * PYK <= OW && (k + 1) * 64 <= QRY; }
+};
+
+// Item-mapped chunk staging of DWgradJob (any layer): thread t stages items t, t + 256, ... of the
+// chunk's flat (pixel, channel quad) lists, each decomposed per chunk.
+template <class D, bool U8>
+struct DwItemStage {
+  using G = typename D::Geom;
+  using InT = typename InElem<U8>::T;
+  const InT *X;
+  const float *dY;
+  float *Xs, *Ys;
+  f32x4 xr[D::XIT], yr[D::YIT];
+  __device__ DwItemStage(const InT *X_, const float *dY_, float *Xs_, float *Ys_) : X(X_), dY(dY_), Xs(Xs_), Ys(Ys_) {}
+  __device__ __forceinline__ void load(int c) {
+    const int tid = threadIdx.x;
+    const int b = c / D::RG, y0 = (c - b * D::RG) * D::R;
+    const InT *xi = X + (size_t)b * D::H * D::W * D::CIN;
+    const float *yi = dY + (size_t)b * D::OH * D::OW * D::COUT;
+#pragma unroll
+    for (int it = 0; it < D::XIT; ++it) {
+      const int item = min(tid + 256 * it, D::XQ - 1);
+      const int pix = item / (D::CIN / 4), cq = item - pix * (D::CIN / 4);
+      const int pr = pix / D::WP, pc = pix - pr * D::WP;
+      const int iy = y0 * D::S - G::PT + pr, ix = pc - G::PL;
+      const bool ok = (unsigned)iy < (unsigned)D::H && (unsigned)ix < (unsigned)D::W;
+      const f32x4 v = InElem<U8>::load4(xi + (size_t)(ok ? iy * D::W + ix : 0) * D::CIN + 4 * cq);
+      xr[it] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int it = 0; it < D::YIT; ++it) {
+      const int item = min(tid + 256 * it, D::YQ - 1);
+      const int pix = item / (D::COUT / 4), cq = item - pix * (D::COUT / 4);
+      const int pr = pix / D::WPAD, pc = pix - pr * D::WPAD;
+      const int oy = y0 + pr;
+      const bool ok = oy < D::OH && pc < D::OW;
+      const f32x4 v = *reinterpret_cast<const f32x4 *>(yi + (size_t)(ok ? oy * D::OW + pc : 0) * D::COUT + 4 * cq);
+      yr[it] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __device__ __forceinline__ void store() {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int it = 0; it < D::XIT; ++it) {
+      const int item = tid + 256 * it;
+      if (D::XQ % 256 == 0 || item < D::XQ) {
+        const int pix = item / (D::CIN / 4), cq = item - pix * (D::CIN / 4);
+        const int pr = pix / D::WP, pc = pix - pr * D::WP;
+        float *d = Xs + (pr * D::WPX + pc) * D::CS + 4 * cq;
+        if constexpr (D::CS % 4 == 0) {
+          *reinterpret_cast<f32x4 *>(d) = xr[it];
+        } else {  // (four dword stores)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d[e] = xr[it][e];
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < D::YIT; ++it) {
+      const int item = tid + 256 * it;
+      if (D::YQ % 256 == 0 || item < D::YQ) {
+        const int pix = item / (D::COUT / 4), cq = item - pix * (D::COUT / 4);
+        float *d = Ys + pix * D::COS + 4 * cq;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[e] = yr[it][e];
+      }
+    }
+  }
+};
+
+// Row-mapped chunk staging (DWCfg::ROWMAP): wave w stages patch rows w + 4 h and dY row w; every
+// per-lane offset is computed once in the constructor.
+template <class D, bool U8>
+struct DwRowStage {
+  using G = typename D::Geom;
+  using InT = typename InElem<U8>::T;
+  using XV = typename std::conditional<U8, uint32_t, f32x4>::type;  // (u8: the raw 4 bytes until the store)
+  static constexpr uint32_t kOut = 0x80000000u;                     // an offset past any range: reads zero
+  static constexpr int kRsrc3 = 0x00020000;                         // gfx9 raw buffer: 32-bit data format
+  // the first inner k step of the patch / dY rows (-1: none); inner k = its offset + (k - K0) strides
+  static constexpr int XK0 = [] { for (int k = 0; k < D::KX; ++k) if (D::x_inner(k)) return k; return -1; }();
+  static constexpr int YK0 = [] { for (int k = 0; k < D::KY; ++k) if (D::y_inner(k)) return k; return -1; }();
+  const InT *X;
+  const float *dY;
+  float *Xs, *Ys;
+  int w, lane;
+  uint32_t xo_in, xo[D::KX], yo_in, yo[D::KY];  // (xo / yo: the edge k steps; *_in: the inner ones' base)
+  int xl, yl;                                   // LDS bases of the lane's first quad (row w)
+  XV xr[D::XROWS * D::KX];
+  f32x4 yr[D::KY];
+  __device__ DwRowStage(const InT *X_, const float *dY_, float *Xs_, float *Ys_) : X(X_), dY(dY_), Xs(Xs_), Ys(Ys_) {
+    w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    lane = threadIdx.x & 63;
+    constexpr int EB = (int)sizeof(InT);
+    const int px = lane / D::CQ, cq = lane - px * D::CQ;  // patch column (at k = 0) and channel quad
+    xo_in = (uint32_t)(((px + (XK0 < 0 ? 0 : XK0) * D::PXK - G::PL) * D::CIN + 4 * cq) * EB);
+#pragma unroll
+    for (int k = 0; k < D::KX; ++k) {
+      const int pc = px + k * D::PXK, ix = pc - G::PL;
+      const bool ok = lane < D::LUX && lane + D::LUX * k < D::QRX && ix >= 0 && ix < D::W;
+      xo[k] = ok ? (uint32_t)((ix * D::CIN + 4 * cq) * EB) : kOut;
+    }
+    const int py = lane / D::CQO, co = lane - py * D::CQO;
+    yo_in = (uint32_t)(((py + (YK0 < 0 ? 0 : YK0) * D::PYK) * D::COUT + 4 * co) * 4);
+#pragma unroll
+    for (int k = 0; k < D::KY; ++k) {
+      const int pc = py + k * D::PYK;
+      const bool ok = lane + 64 * k < D::QRY && pc < D::OW;
+      yo[k] = ok ? (uint32_t)((pc * D::COUT + 4 * co) * 4) : kOut;
+    }
+    xl = (w * D::WPX + px) * D::CS + 4 * cq;
+    yl = (w * D::WPAD + py) * D::COS + 4 * co;
+  }
+  __device__ __forceinline__ void load(int c) {
+    const int b = c / D::RG, y0 = (c - b * D::RG) * D::R;
+    const InT *xi = X + (size_t)b * D::H * D::W * D::CIN;
+#pragma unroll
+    for (int h = 0; h < D::XROWS; ++h) {
+      const int iy = y0 - G::PT + w + 4 * h;
+      const bool rok = (unsigned)iy < (unsigned)D::H;  // (wave-uniform)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(xi + (size_t)(rok ? iy : 0) * D::W * D::CIN), (short)0, rok ? D::W * D::CIN * (int)sizeof(InT) : 0,
+          kRsrc3);
+#pragma unroll
+      for (int k = 0; k < D::KX; ++k) {
+        const bool inner = D::x_inner(k);
+        const uint32_t vo = inner ? xo_in : xo[k];
+        const int so = inner ? (k - XK0) * D::PXK * D::CIN * (int)sizeof(InT) : 0;
+        if constexpr (U8)
+          xr[h * D::KX + k] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0);
+        else
+          xr[h * D::KX + k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
+      }
+    }
+    const int oy = y0 + w;
+    const bool rok = oy < D::OH;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(dY + ((size_t)b * D::OH + (rok ? oy : 0)) * D::OW * D::COUT), (short)0, rok ? D::OW * D::COUT * 4 : 0,
+        kRsrc3);
+#pragma unroll
+    for (int k = 0; k < D::KY; ++k) {
+      const bool inner = D::y_inner(k);
+      const uint32_t vo = inner ? yo_in : yo[k];
+      const int so = inner ? (k - YK0) * D::PYK * D::COUT * 4 : 0;
+      yr[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
+    }
+  }
+  __device__ __forceinline__ void store() {
+#pragma unroll
+    for (int h = 0; h < D::XROWS; ++h)
+#pragma unroll
+      for (int k = 0; k < D::KX; ++k) {
+        if (((k + 1) * D::LUX > D::QRX || D::LUX < 64) && (lane >= D::LUX || lane + D::LUX * k >= D::QRX))
+          continue;  // (the row's last, partial k step; the idle lane)
+        float *d = Xs + xl + (4 * h * D::WPX + k * D::PXK) * D::CS;
+        f32x4 v;
+        if constexpr (U8) {
+          const uint32_t u = xr[h * D::KX + k];
+          const float sc = 1.0f / 255.0f;  // InElem<true>::load4's arithmetic
+          v = f32x4{(float)(u & 0xff) * sc, (float)((u >> 8) & 0xff) * sc, (float)((u >> 16) & 0xff) * sc,
+                    (float)(u >> 24) * sc};
+        } else {
+          v = xr[h * D::KX + k];
+        }
+        if constexpr (D::CS % 4 == 0) {
+          *reinterpret_cast<f32x4 *>(d) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d[e] = v[e];
+        }
+      }
+#pragma unroll
+    for (int k = 0; k < D::KY; ++k) {
+      if ((k + 1) * 64 > D::QRY && lane + 64 * k >= D::QRY) continue;
+      float *d = Ys + yl + k * D::PYK * D::COS;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] = yr[k][e];
+    }
+  }
 };
 
 template <class G, bool U8, int TMW>
@@ -1141,59 +1334,9 @@ struct DWgradJob {
     }
     const int bbase = g * D::WPAD * D::COS + 16 * j + r;
 
-    f32x4 xr[D::XIT], yr[D::YIT];
-    auto load = [&](int c) {
-      const int b = c / D::RG, y0 = (c - b * D::RG) * D::R;
-      const InT *xi = X + (size_t)b * D::H * D::W * D::CIN;
-      const float *yi = dY + (size_t)b * D::OH * D::OW * D::COUT;
-#pragma unroll
-      for (int it = 0; it < D::XIT; ++it) {
-        const int item = min(tid + 256 * it, D::XQ - 1);
-        const int pix = item / (D::CIN / 4), cq = item - pix * (D::CIN / 4);
-        const int pr = pix / D::WP, pc = pix - pr * D::WP;
-        const int iy = y0 * D::S - G::PT + pr, ix = pc - G::PL;
-        const bool ok = (unsigned)iy < (unsigned)D::H && (unsigned)ix < (unsigned)D::W;
-        const f32x4 v = InElem<U8>::load4(xi + (size_t)(ok ? iy * D::W + ix : 0) * D::CIN + 4 * cq);
-        xr[it] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int it = 0; it < D::YIT; ++it) {
-        const int item = min(tid + 256 * it, D::YQ - 1);
-        const int pix = item / (D::COUT / 4), cq = item - pix * (D::COUT / 4);
-        const int pr = pix / D::WPAD, pc = pix - pr * D::WPAD;
-        const int oy = y0 + pr;
-        const bool ok = oy < D::OH && pc < D::OW;
-        const f32x4 v = *reinterpret_cast<const f32x4 *>(yi + (size_t)(ok ? oy * D::OW + pc : 0) * D::COUT + 4 * cq);
-        yr[it] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    };
-    auto store = [&]() {
-#pragma unroll
-      for (int it = 0; it < D::XIT; ++it) {
-        const int item = tid + 256 * it;
-        if (D::XQ % 256 == 0 || item < D::XQ) {
-          const int pix = item / (D::CIN / 4), cq = item - pix * (D::CIN / 4);
-          const int pr = pix / D::WP, pc = pix - pr * D::WP;
-          float *d = Xs + (pr * D::WPX + pc) * D::CS + 4 * cq;
-          if constexpr (D::CS % 4 == 0) {
-            *reinterpret_cast<f32x4 *>(d) = xr[it];
-          } else {  // (four dword stores)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) d[e] = xr[it][e];
-          }
-        }
-      }
-#pragma unroll
-      for (int it = 0; it < D::YIT; ++it) {
-        const int item = tid + 256 * it;
-        if (D::YQ % 256 == 0 || item < D::YQ) {
-          const int pix = item / (D::COUT / 4), cq = item - pix * (D::COUT / 4);
-          float *d = Ys + pix * D::COS + 4 * cq;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) d[e] = yr[it][e];
-        }
-      }
-    };
+    typename std::conditional<D::ROWMAP, DwRowStage<D, U8>, DwItemStage<D, U8>>::type st(X, dY, Xs, Ys);
+    auto load = [&](int c) { st.load(c); };
+    auto store = [&]() { st.store(); };
 
     f32x4 acc[TMW];
 #pragma unroll
