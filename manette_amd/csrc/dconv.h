@@ -364,28 +364,31 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
   const int r = lane & 15, g = lane >> 4;
 
   // weight chunk c -> registers, and into LDS in fragment order [kc][n-tile][lane = 16 g + r][s]
-  f32x4 wr[D::BIT];
-  auto wload = [&](int c) {
+  // (chunked weights: two chunks in flight in registers — chunk c + 2's loads are issued before
+  // chunk c is multiplied, so a chunk's L2 round trip spans two chunks' MFMAs, not one)
+  f32x4 wr[D::BIT], wr2[D::NCH > 1 ? D::BIT : 1];
+  // (no branches: a thread past the chunk's items loads and stores the last item again — the same
+  // value to the same address — so the waits before these loads and stores count outstanding
+  // loads instead of draining them at an exec-mask join)
+  auto wload_to = [&](int c, f32x4 *dstr) {
 #pragma unroll
     for (int it = 0; it < D::BIT; ++it) {
-      const int item = tid + it * D::NT;
-      if (D::BITEMS % D::NT == 0 || item < D::BITEMS) {
-        const int kq = item / D::CO, n = item - kq * D::CO;
-        wr[it] = p.wquad(c * D::CK + 4 * kq, n);
-      }
+      const int item = min(tid + it * D::NT, D::BITEMS - 1);
+      const int kq = item / D::CO, n = item - kq * D::CO;
+      dstr[it] = p.wquad(c * D::CK + 4 * kq, n);
     }
   };
-  auto wstore = [&](float *dst) {
+  auto wload = [&](int c) { wload_to(c, wr); };
+  auto wstore_from = [&](float *dst, const f32x4 *srcr) {
 #pragma unroll
     for (int it = 0; it < D::BIT; ++it) {
-      const int item = tid + it * D::NT;
-      if (D::BITEMS % D::NT == 0 || item < D::BITEMS) {
-        const int kq = item / D::CO, n = item - kq * D::CO;
-        const int kcl = kq >> 2, gg = kq & 3, j = n >> 4, rr = n & 15;
-        *reinterpret_cast<f32x4 *>(dst + ((kcl * D::TN + j) * 64 + gg * 16 + rr) * 4) = wr[it];
-      }
+      const int item = min(tid + it * D::NT, D::BITEMS - 1);
+      const int kq = item / D::CO, n = item - kq * D::CO;
+      const int kcl = kq >> 2, gg = kq & 3, j = n >> 4, rr = n & 15;
+      *reinterpret_cast<f32x4 *>(dst + ((kcl * D::TN + j) * 64 + gg * 16 + rr) * 4) = srcr[it];
     }
   };
+  auto wstore = [&](float *dst) { wstore_from(dst, wr); };
   // A offsets of the k-chunks (one chunk: K not tap-aligned, small CI): tap and channel quad of
   // quad index 4 kc + g (past the last tap: any tap, its weights are zero)
   int aoffs[D::TAPALIGNED ? 1 : D::KC];
@@ -398,7 +401,10 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
     }
   }
   wload(0);
-  if constexpr (D::NCH > 1) t1 = t0 + 1;  // (chunked weights: one tile per block, no loop)
+  if constexpr (D::NCH > 1) {
+    wload_to(1, wr2);
+    t1 = t0 + 1;  // (chunked weights: one tile per block, no loop)
+  }
   for (int bid = t0; bid < t1; ++bid) {
   const int b = bid / D::BPI;
   const int u0 = (bid - b * D::BPI) * D::UPB;
@@ -502,14 +508,23 @@ __device__ __forceinline__ void dconv_body(const Pr &p, int t0, int t1, float *s
   if constexpr (D::NCH == 1) {
     compute(Bs, 0);
   } else {
-    for (int c = 0; c < D::NCH; ++c) {
-      const bool more = c + 1 < D::NCH;
-      if (more) wload(c + 1);
-      compute(Bs + (c & 1) * D::BSZ, c);
-      if (more) {
-        wstore(Bs + ((c + 1) & 1) * D::BSZ);
-        __syncthreads();
-      }
+    // LDS buffer c & 1 holds chunk c; registers: wr = chunk c + 2 (even c), wr2 = chunk c + 1 / c + 3.
+    // One barrier per chunk: buffer (c + 1) & 1 was last read by chunk c - 1, before the last barrier.
+    // (sched_barrier: keeps each chunk's loads at the top of its iteration; the scheduler otherwise
+    // sinks them below the MFMAs, to just before the barrier, and the next store waits them out)
+    for (int c = 0; c < D::NCH; c += 2) {
+      if (c + 2 < D::NCH) wload_to(c + 2, wr);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(Bs, c);
+      if (c + 1 >= D::NCH) break;
+      wstore_from(Bs + D::BSZ, wr2);
+      __syncthreads();
+      if (c + 3 < D::NCH) wload_to(c + 3, wr2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(Bs + D::BSZ, c + 1);
+      if (c + 2 >= D::NCH) break;
+      wstore_from(Bs, wr);
+      __syncthreads();
     }
   }
 

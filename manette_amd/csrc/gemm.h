@@ -805,18 +805,70 @@ struct LdIm2colT {
 
 // Backward-data of a conv, A side: rows = input pixels (b, iy, ix), gk = (ky, kx, co);
 // A = dY[b][oy][ox][co] with oy = (iy + PT - ky)/S when that divides and lands in range. KMAJOR.
+// Stride 1 (every tap lands): a k state per item (LdConvBwdAKs) — the (oy, ox) the item's tap
+// lands on and its channel, stepped by BK per chunk — and one buffer load whose offset is pushed
+// past the descriptor's range when the tap falls outside dY (reads zero): a few VALU per quad
+// instead of the (tap, channel) divisions, clamps and selects of fetch_ctx. The caller keeps
+// dY under 2^31 bytes (trunk_backward).
 template <class G>
-struct LdConvBwdA {
-  static constexpr bool KMAJOR = true;
+struct LdConvBwdACtx {
   const float *dY;  // [B][OH][OW][COUT]
-  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
-    return row0 + rows <= nrows && k0 + bk <= ke;
-  }
-  // Row context: the image of input pixel m and (iy + PT, ix + PL).
   struct Ctx {
     const float *img;
     int ty0, tx0;
   };
+};
+template <class G, bool KSOK = G::S == 1>
+struct LdConvBwdAKs : LdConvBwdACtx<G> {};
+template <class G>
+struct LdConvBwdAKs<G, true> : LdConvBwdACtx<G> {
+  using Ctx = typename LdConvBwdACtx<G>::Ctx;
+  using LdConvBwdACtx<G>::dY;
+  struct KS {
+    int ty, tx, kx, co;  // (ty, tx): the output pixel tap (ky, kx) of the item's row lands on
+  };
+  __device__ __forceinline__ KS ks(const Ctx &c, int k) const {
+    const int ky = k / (G::KW * G::COUT);
+    const int r2 = k - ky * (G::KW * G::COUT);
+    const int kx = r2 / G::COUT, co = r2 - kx * G::COUT;
+    return {c.ty0 - ky, c.tx0 - kx, kx, co};
+  }
+  template <int BK>
+  __device__ __forceinline__ void next(KS &s) const {
+    constexpr int DT = BK / G::COUT, DC = BK % G::COUT;
+    if constexpr (DC != 0) {
+      s.co += DC;
+      const bool c = s.co >= G::COUT;
+      s.co -= c ? G::COUT : 0;
+      s.kx += c ? 1 : 0;
+      s.tx -= c ? 1 : 0;
+    }
+    s.kx += DT;
+    s.tx -= DT;
+#pragma unroll
+    for (int w = 0; w < 1 + DT / G::KW; ++w) {  // tap-row carries: (ky + 1, kx - KW)
+      const bool c = s.kx >= G::KW;
+      s.kx -= c ? G::KW : 0;
+      s.tx += c ? G::KW : 0;
+      s.ty -= c ? 1 : 0;
+    }
+  }
+  __device__ __forceinline__ f32x4 fetch_ks(const Ctx &c, const KS &s) const {
+    const bool ok = (unsigned)s.ty < (unsigned)G::OH && (unsigned)s.tx < (unsigned)G::OW;
+    const uint32_t off = (uint32_t)((c.img - dY) + (s.ty * G::OW + s.tx) * G::COUT + s.co) * 4u;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)dY, (short)0, 0x7ffffff0, 0x00020000);
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off : 0x80000000u, 0, 0));
+  }
+};
+template <class G>
+struct LdConvBwdA : LdConvBwdAKs<G> {
+  static constexpr bool KMAJOR = true;
+  using Ctx = typename LdConvBwdACtx<G>::Ctx;
+  using LdConvBwdACtx<G>::dY;
+  __device__ __forceinline__ bool interior(int row0, int rows, int k0, int bk, int ke, int nrows) const {
+    return row0 + rows <= nrows && k0 + bk <= ke;
+  }
+  // Row context: the image of input pixel m and (iy + PT, ix + PL).
   __device__ __forceinline__ Ctx ctx(int m) const {
     const int b = m / (G::H * G::W);
     const int rem = m - b * (G::H * G::W);
@@ -869,6 +921,28 @@ struct LdConvBwdB {
     const float *p;
   };
   __device__ __forceinline__ Ctx ctx(int ci) const { return {Wt + (size_t)ci * G::COUT}; }
+  // k state: the item's tap and channel, stepped by BK per chunk
+  struct KS {
+    int tap, co;
+  };
+  __device__ __forceinline__ KS ks(const Ctx &, int k) const {
+    const int tap = k / G::COUT;
+    return {tap, k - tap * G::COUT};
+  }
+  template <int BK>
+  __device__ __forceinline__ void next(KS &s) const {
+    constexpr int DT = BK / G::COUT, DC = BK % G::COUT;
+    if constexpr (DC != 0) {
+      s.co += DC;
+      const bool c = s.co >= G::COUT;
+      s.co -= c ? G::COUT : 0;
+      s.tap += c ? 1 : 0;
+    }
+    s.tap += DT;
+  }
+  __device__ __forceinline__ f32x4 fetch_ks(const Ctx &c, const KS &s) const {
+    return *reinterpret_cast<const f32x4 *>(c.p + (size_t)(s.tap * G::CIN * G::COUT + s.co));
+  }
   __device__ __forceinline__ f32x4 fetch_ctx(const Ctx &c, int k) const {
     const int ky = k / (G::KW * G::COUT);
     const int r2 = k - ky * (G::KW * G::COUT);

@@ -1170,6 +1170,10 @@ static int trunk_backward(const mt_net *n, const float *P, const uint8_t *obs, i
     set_error("batch %d too large for the conv %d weight gradient", B, I);
     return MT_ERR_ARG;
   }
+  if ((size_t)B * G::OH * G::OW * G::COUT * 4 >= ((size_t)1 << 31) - 16) {  // LdConvBwdA's 32-bit byte offsets
+    set_error("batch %d too large for the conv %d input gradient", B, I);
+    return MT_ERR_ARG;
+  }
   const auto wg = conv_wgrad_jobs_sel<G, I == 0>(x, ws + L.dact[I], ws + (I % 2 ? L.wslab2 : L.wslab),
                                              grad + n->off_conv[I], B);
   if constexpr (I > 0) {
