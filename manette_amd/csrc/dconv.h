@@ -1072,7 +1072,7 @@ static int conv_dgrad_unpool_solo(const float *dY, const float *Wt, const float 
 // the chunk, x = 4 kc + s): lane (r, g) of M-tile m reads X[row g + ky][x + s + kx][ci] and
 // dY[row g][x + s][co] — two LDS reads per MFMA-operand pair, each a ds_read_b32 at an immediate
 // offset from a per-lane base (the (tap, ci) of row 16 m + r is decomposed once).
-constexpr size_t kDwSlabCap = (size_t)4 << 20;  // slab floats (the generic path's kSlabFloats)
+constexpr size_t kDwSlabCap = (size_t)8 << 20;  // slab floats (2x the generic path's kSlabFloats)
 
 // Small-channel patches (conv1: 4 / 12 u8 channels): no channel pad (16-B pixel quads, one LDS store
 // each) and the patch row stride padded instead, to the first whose offset puts lane group g = 1 on
@@ -1409,12 +1409,16 @@ constexpr bool dconv_wgrad() {
   return G::S == 1 && G::SAME && G::KH == 5;
 }
 // M-tiles per wave: 5 (4 for 64 output channels), or for a short K (the gray conv1: 7 M-tiles of
-// (tap, ci) rows) just enough for one tap group — 5 would leave 3 of its 10 tile slots empty
+// (tap, ci) rows) just enough for one tap group — 5 would leave 3 of its 10 tile slots empty. The
+// 32 -> 32 layer (50 M-tiles): 13 per wave, two tap groups of 26 tiles, each staged chunk feeding
+// 2.6x the MFMAs (236 VGPRs; with kDwSlabCap at 8M floats, 256 splits): conv2 dW 238.7 -> 232.6 us
+// (LSTM), 137.1 -> 133.7 us (PWYX-RGB), profiles/r06dw13
 template <class G>
 constexpr int dw_tmw() {
   constexpr int mt = (G::KK + 15) / 16, wrows = 4 / (G::COUT / 16);
   if (G::COUT >= 64) return 4;
   if (mt <= 5 * wrows) return (mt + wrows - 1) / wrows;
+  if (G::CIN == 32 && mt == 50) return 13;
   constexpr int w5 = (mt + 5 * wrows - 1) / (5 * wrows) * 5 * wrows - mt;  // empty tile slots at 5
   constexpr int w4 = (mt + 4 * wrows - 1) / (4 * wrows) * 4 * wrows - mt;  // and at 4
   return w4 < w5 ? 4 : 5;
