@@ -1057,8 +1057,11 @@ constexpr bool dconv_bwd_solo() {
 template <class G, class GJ>
 static int conv_dgrad_unpool_solo(const float *dY, const float *Wt, const float *Pj, const uint8_t *argj, float *dactj,
                                   int B, int act, float alpha, hipStream_t s) {
-  return launch_dconv<DBwdUnpool<G, GJ>, 4, 2, (G::COUT >= 64 ? 1 : 2), G::COUT>(
-      DBwdUnpool<G, GJ>{dY, Wt, Pj, argj, dactj, act, alpha}, B, s);
+  // 8 waves of one M-tile x both N-tiles (two accumulators per wave, the A fragment read once for
+  // both): LSTM conv2 dX 257.1 -> 248.0 us against 4 x 2 waves of two M-tiles x one N-tile; 4 waves
+  // of 2 x 2 tiles 256.6, 5-tap weight chunks 292.2 (profiles/r06dxc)
+  return launch_dconv<DBwdUnpool<G, GJ>, 8, 1, 1, G::COUT>(DBwdUnpool<G, GJ>{dY, Wt, Pj, argj, dactj, act, alpha}, B,
+                                                           s);
 }
 
 // ---- weight gradient ---------------------------------------------------------------------------
