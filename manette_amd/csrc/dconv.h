@@ -578,18 +578,21 @@ static int launch_dconv(const Pr &p, int B, hipStream_t s) {
 // conv4 128) ----------------------------------------------------------------------------------
 //  conv1 (CIN 4 / 12, the whole K in one chunk): 4 waves, 2 M-tiles per wave (8-wave blocks measured
 //    no faster); the strided NATURE conv1 1 M-tile;
-//  conv2 (32 -> 32): 8-wave blocks (two N halves), two blocks per CU: four waves per SIMD hide the
-//    per-chunk barrier (PWYX-RGB E=32 33.4 vs 36.7 us, LSTM 161 frames 143.6 vs 157.5 us,
-//    profiles/r03i); 2 M-tiles per wave; one tap (CIN k) per weight chunk (5-tap chunks: no faster);
+//  conv2 (32 -> 32): 8-wave blocks, two blocks per CU: four waves per SIMD hide the per-chunk
+//    barrier (PWYX-RGB E=32 33.4 vs 36.7 us, LSTM 161 frames 143.6 vs 157.5 us, profiles/r03i); one
+//    M-tile x both N-tiles per wave (round 6: the A fragment read once for two accumulators; LSTM
+//    trunk 72.5 -> 71.1 us against 4 x 2 waves of 2 M-tiles x 1 N-tile, profiles/r06fwd — the same
+//    8 x 1 layout on the 64-channel layers measured 4-17 % slower); one tap (CIN k) per weight chunk
+//    (5-tap chunks: no faster);
 //  64 output channels (conv3, conv4, NATURE conv2 / conv3): 8-wave blocks for the small grids
 //    (18.2 -> 15.3 us and 11.0 -> 10.1 us), 1 M-tile per wave.
 template <class G, bool POOL>
 struct DConvFor {
   static constexpr bool SMALLC = G::CIN % 16 != 0;  // conv1: the whole K in one chunk
   static constexpr bool C64 = G::COUT >= 64;
-  static constexpr int WN = C64 ? (POOL ? 2 : 4) : (SMALLC ? 1 : 2);
-  static constexpr int WM = C64 ? (POOL ? 4 : 2) : 4;
-  static constexpr int TMW = SMALLC ? (G::S > 1 ? 1 : 2) : (C64 ? 1 : 2);
+  static constexpr int WN = C64 ? (POOL ? 2 : 4) : 1;
+  static constexpr int WM = C64 ? (POOL ? 4 : 2) : (SMALLC ? 4 : 8);
+  static constexpr int TMW = SMALLC ? (G::S > 1 ? 1 : 2) : 1;
   // weight chunk: one tap for the 5x5 layers; 4 / 3 taps for the 4x4 / 3x3 ones (one tap left their
   // blocks 16 / 9 chunk steps of 16-32 MFMAs per wave, each behind a barrier)
   static constexpr int CK = SMALLC ? 0 : G::CIN * (G::KH == 4 ? 4 : G::KH == 3 ? 3 : 1);
