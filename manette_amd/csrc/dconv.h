@@ -1414,16 +1414,17 @@ template <class G>
 constexpr bool dconv_wgrad() {
   return G::S == 1 && G::SAME && G::KH == 5;
 }
-// M-tiles per wave: 5 (4 for 64 output channels), or for a short K (the gray conv1: 7 M-tiles of
-// (tap, ci) rows) just enough for one tap group — 5 would leave 3 of its 10 tile slots empty. The
-// 32 -> 32 layer (50 M-tiles): 13 per wave, two tap groups of 26 tiles, each staged chunk feeding
-// 2.6x the MFMAs (236 VGPRs; with kDwSlabCap at 8M floats, 256 splits): conv2 dW 238.7 -> 232.6 us
-// (LSTM), 137.1 -> 133.7 us (PWYX-RGB), profiles/r06dw13
+// M-tiles per wave: every M-tile of the layer in one tap group when that takes at most 10 per wave
+// (the gray conv1's 7 M-tiles of (tap, ci) rows: 4; the RGB conv1's 19: 10, 232 VGPRs — each staged
+// chunk then feeds all of them: RGB conv1 dW 225.3 -> 195.0 us, profiles/r06rgb); the 32 -> 32
+// layer (50 M-tiles): 13 per wave, two tap groups of 26 tiles (236 VGPRs; with kDwSlabCap at 8M
+// floats, 256 splits): conv2 dW 238.7 -> 232.6 us (LSTM), 137.1 -> 133.7 us (PWYX-RGB),
+// profiles/r06dw13; otherwise 5 (4 for 64 output channels)
 template <class G>
 constexpr int dw_tmw() {
   constexpr int mt = (G::KK + 15) / 16, wrows = 4 / (G::COUT / 16);
   if (G::COUT >= 64) return 4;
-  if (mt <= 5 * wrows) return (mt + wrows - 1) / wrows;
+  if ((mt + wrows - 1) / wrows <= 10) return (mt + wrows - 1) / wrows;
   if (G::CIN == 32 && mt == 50) return 13;
   constexpr int w5 = (mt + 5 * wrows - 1) / (5 * wrows) * 5 * wrows - mt;  // empty tile slots at 5
   constexpr int w4 = (mt + 4 * wrows - 1) / (4 * wrows) * 4 * wrows - mt;  // and at 4
