@@ -809,7 +809,9 @@ struct LdIm2colT {
 // lands on and its channel, stepped by BK per chunk — and one buffer load whose offset is pushed
 // past the descriptor's range when the tap falls outside dY (reads zero): a few VALU per quad
 // instead of the (tap, channel) divisions, clamps and selects of fetch_ctx. The caller keeps
-// dY under 2^31 bytes (trunk_backward).
+// dY under 2^31 bytes (trunk_backward). Only for CIN >= 64: the thin CIN-32 tile (Tile<64, 32, 4, 1>)
+// goes from 128 to 136 VGPRs with it, a wave per SIMD less (LSTM conv3 group 186.9 vs 180.3 us
+// without, profiles/r06ks).
 template <class G>
 struct LdConvBwdACtx {
   const float *dY;  // [B][OH][OW][COUT]
@@ -818,7 +820,7 @@ struct LdConvBwdACtx {
     int ty0, tx0;
   };
 };
-template <class G, bool KSOK = G::S == 1>
+template <class G, bool KSOK = G::S == 1 && G::CIN >= 64>
 struct LdConvBwdAKs : LdConvBwdACtx<G> {};
 template <class G>
 struct LdConvBwdAKs<G, true> : LdConvBwdACtx<G> {
