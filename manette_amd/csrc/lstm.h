@@ -131,14 +131,21 @@ struct XgRows {
 };
 
 // One workgroup (128 threads) per window b. xg: split-K slabs of x_t K_x, [S][rows][128].
-template <int NH, int STEPS>
+// XS (the native rollout's macro-steps, lstm_step_fwd_impl): a per-frame cache xsum[rows][128] of
+// the slab sums. Step 0 (XS 1) sums every position from its slabs, as XS 0 does, and stores each
+// window's frame rows, block 0 also the zero frame's (row 0); steps t > 0 (XS 2) sum only position
+// 4 — the frame the step's frames forward just computed — and read positions 0..3 from the cache:
+// those frames were summed earlier in the same rollout under the same parameters, in the same
+// slab order, so the values are the ones XS 0 would compute (50 loads per thread instead of 250).
+template <int NH, int STEPS, int XS = 0>
 __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__ xg, int S, int rows, XgRows map,
                                                        const float *__restrict__ Kh, const float *__restrict__ kb,
                                                        const float *__restrict__ Wp, const float *__restrict__ bp,
                                                        const float *__restrict__ W6, int F, float forget_bias,
                                                        float *__restrict__ gates, float *__restrict__ cst,
                                                        float *__restrict__ hprev, float *__restrict__ h5,
-                                                       float *__restrict__ out32, float *__restrict__ slab6) {
+                                                       float *__restrict__ out32, float *__restrict__ slab6,
+                                                       float *__restrict__ xsum = nullptr) {
   constexpr int G4 = 4 * NH;
   __shared__ float hs[NH], as[G4], os[NH];
   const int b = blockIdx.x, g = threadIdx.x;
@@ -159,11 +166,15 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
     zx[t] = 0.f;
     xoff[t] = (size_t)map.row(b, t, z) * G4 + g;
   }
+  constexpr int T0 = XS == 2 ? STEPS - 1 : 0;  // first position summed from the slabs
+  float xc[STEPS];                             // (XS 2: the cached sums of positions 0 .. T0 - 1)
+#pragma unroll
+  for (int t = 0; t < T0; ++t) xc[t] = xsum[xoff[t]];
   constexpr int XB = 25;
   float v[STEPS][XB];
   auto load_batch = [&](int s0) {
 #pragma unroll
-    for (int t = 0; t < STEPS; ++t)
+    for (int t = T0; t < STEPS; ++t)
 #pragma unroll
       for (int u = 0; u < XB; ++u) v[t][u] = xg[(size_t)min(s0 + u, S - 1) * rows * G4 + xoff[t]];
   };
@@ -187,13 +198,33 @@ __global__ __launch_bounds__(128) void lstm_fwd_kernel(const float *__restrict__
   }
   for (int s0 = 0;;) {
 #pragma unroll
-    for (int t = 0; t < STEPS; ++t)
+    for (int t = T0; t < STEPS; ++t)
 #pragma unroll
       for (int u = 0; u < XB; ++u)
         if (s0 + u < S) zx[t] += v[t][u];
     s0 += XB;
     if (s0 >= S) break;
     load_batch(s0);
+  }
+#pragma unroll
+  for (int t = 0; t < T0; ++t) zx[t] = xc[t];
+  if constexpr (XS != 0) {  // (rows of one step are distinct per window, but for the zero frame: same value)
+#pragma unroll
+    for (int t = T0; t < STEPS; ++t) xsum[xoff[t]] = zx[t];
+  }
+  if constexpr (XS == 1) {
+    if (b == 0) {  // the zero frame, whether or not window 0 reads it (later steps' leading zeros do)
+      float z0 = 0.f;
+      for (int s0 = 0; s0 < S; s0 += XB) {
+        float w0[XB];
+#pragma unroll
+        for (int u = 0; u < XB; ++u) w0[u] = xg[(size_t)min(s0 + u, S - 1) * rows * G4 + g];
+#pragma unroll
+        for (int u = 0; u < XB; ++u)
+          if (s0 + u < S) z0 += w0[u];
+      }
+      xsum[g] = z0;
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -420,7 +451,7 @@ static int lstm_backward_impl(const mt_net *n, const float *P, const uint8_t *ob
 // ---------------------------------------------------------------------------------------------
 struct LstmFrameWs {
   WsLayout L;
-  size_t xg, dxg, zpart, slab6, gates, cst, hprev, h5, out32, dout32, dgates;
+  size_t xg, xsum, dxg, zpart, slab6, gates, cst, hprev, h5, out32, dout32, dgates;
   int S, R_max, R_bwd, W;
 };
 
@@ -451,6 +482,7 @@ static LstmFrameWs lstm_frame_layout(const mt_net *n, int E, int T) {
   X.S = gemm_splits<TileFc>(Ar::FLAT, s);
   const size_t W = X.W, WT = (size_t)T * E;
   X.xg = take((size_t)X.S * X.R_max * Ar::G4);
+  X.xsum = take((size_t)X.R_max * Ar::G4);
   X.dxg = take((size_t)X.R_max * Ar::G4);
   X.zpart = take((size_t)kZeroParts * Ar::G4);
   X.slab6 = take(W * Ar::F);
@@ -556,11 +588,13 @@ static int lstm_frames_fwd_impl(const mt_net *n, const float *P, const uint8_t *
                              X.S, s);
 }
 
+// xs: the per-frame x-product sum cache (lstm_fwd_kernel XS; the native rollout's macro-steps only,
+// whose step t > 0 follows steps 0 .. t - 1 of the same rollout under the same parameters)
 template <class Ar>
 static int lstm_windows_fwd_impl(const mt_net *n, const float *P, int32_t *nz_t, int t, int E, int T,
                                  float *ws, float *v, float *pi, float *rep, hipStream_t s,
                                  const SampleArgs *smp = nullptr, const int32_t *nz_prev = nullptr,
-                                 const float *over = nullptr) {
+                                 const float *over = nullptr, bool xs = false) {
   MT_CHECK_ARG(t >= 0 && t <= T, "step %d outside [0, %d]", t, T);
   const LstmFrameWs X = lstm_frame_layout<Ar>(n, E, T);
   const size_t w0 = (size_t)t * E;
@@ -568,11 +602,13 @@ static int lstm_windows_fwd_impl(const mt_net *n, const float *P, int32_t *nz_t,
   const float *Wp = P + n->off_proj;
   const float *W6 = P + n->off_fc;
   static_assert(Ar::F <= Ar::G4, "lstm_fwd_kernel: one fc6 column per thread");
-  hipLaunchKernelGGL((lstm_fwd_kernel<Ar::NH, Ar::STEPS>), dim3(E), dim3(Ar::G4), 0, s, ws + X.xg, X.S, X.R_max,
-                     XgRows{nz_t, t, E, nz_prev, over}, Kh, Kh + Ar::NH * Ar::G4, Wp, Wp + Ar::NH * Ar::NH, W6, Ar::F, 1.0f,
+  auto kern = !xs ? &lstm_fwd_kernel<Ar::NH, Ar::STEPS, 0>
+                  : (t == 0 ? &lstm_fwd_kernel<Ar::NH, Ar::STEPS, 1> : &lstm_fwd_kernel<Ar::NH, Ar::STEPS, 2>);
+  hipLaunchKernelGGL(kern, dim3(E), dim3(Ar::G4), 0, s, ws + X.xg, X.S, X.R_max, XgRows{nz_t, t, E, nz_prev, over}, Kh,
+                     Kh + Ar::NH * Ar::G4, Wp, Wp + Ar::NH * Ar::NH, W6, Ar::F, 1.0f,
                      ws + X.gates + w0 * Ar::STEPS * Ar::G4, ws + X.cst + w0 * Ar::STEPS * Ar::NH,
                      ws + X.hprev + w0 * Ar::STEPS * Ar::NH, ws + X.h5 + w0 * Ar::NH, ws + X.out32 + w0 * Ar::NH,
-                     ws + X.slab6 + w0 * Ar::F);
+                     ws + X.slab6 + w0 * Ar::F, xs ? ws + X.xsum : nullptr);
   MT_LAUNCHED();
   HeadParams hp = head_params(n, P);
   return launch_heads(E, s, ws + X.slab6 + w0 * Ar::F, 1, E, W6 + (size_t)Ar::NH * Ar::F, n->cfg.activation,
@@ -599,7 +635,7 @@ static int lstm_step_fwd_impl(const mt_net *n, const float *P, const uint8_t *fs
   MT_TRY((lstm_frames_fwd_impl<Ar>(n, P, fstore, row0, nrows, E, T, ws, s, st, sync)));
   if (marks) MT_HIP(hipEventRecord(marks[1], s));
   return lstm_windows_fwd_impl<Ar>(n, P, nz + (size_t)t * E, t, E, T, ws, v, pi, rep, s, smp,
-                                   t > 0 ? nz + (size_t)(t - 1) * E : nullptr, t > 0 ? over : nullptr);
+                                   t > 0 ? nz + (size_t)(t - 1) * E : nullptr, t > 0 ? over : nullptr, true);
 }
 
 template <class Ar>
