@@ -164,7 +164,10 @@ int mt_forward_trunk_stacking(const mt_net *net, const float *params, const uint
  *    + windows_forward of step t, with nz[t] derived on the device for t > 0 (nz [T+1][E]:
  *    nz[t][e] = over[e] != 0 ? 5 : max(nz[t-1][e] - 1, 0), `over` = step t-1's episode-end
  *    flags, device-readable — paac.py:173-174 update_memory, :202-203 the reset); the native
- *    rollout (mt_rollout_*) runs the same forward with the draw fused into its heads kernel;
+ *    rollout (mt_rollout_*) runs the same forward with the draw fused into its heads kernel.
+ *    Steps run in order within a rollout (t > 0 after steps 0 .. t-1 on the same ws and
+ *    parameters): step 0 stores each frame's x-product sum in ws, steps t > 0 read the 4 older
+ *    frames' sums from there (mt_lstm_windows_forward always sums every frame from its slabs);
  *  - mt_lstm_frames_backward: loss + gradient of the T*E windows of steps 0..T-1 (the train
  *    step of paac.py:254-256) from the rollout's activations (unchanged parameters), with pi,
  *    rep, v [T*E] the rollout outputs; back-propagates through each distinct frame once.
