@@ -584,14 +584,17 @@ static int launch_dconv(const Pr &p, int B, hipStream_t s) {
 //    trunk 72.5 -> 71.1 us against 4 x 2 waves of 2 M-tiles x 1 N-tile, profiles/r06fwd — the same
 //    8 x 1 layout on the 64-channel layers measured 4-17 % slower); one tap (CIN k) per weight chunk
 //    (5-tap chunks: no faster);
-//  64 output channels (conv3, conv4, NATURE conv2 / conv3): 8-wave blocks for the small grids
-//    (18.2 -> 15.3 us and 11.0 -> 10.1 us), 1 M-tile per wave.
+//  64 output channels (conv3, conv4, NATURE conv2 / conv3): 8-wave blocks for the pooled conv3
+//    (18.2 -> 15.3 us), 1 M-tile per wave; the unpooled conv4 (10 x 10 outputs) on 4 waves of one
+//    M-tile x one N-tile, 4 units a block — twice the blocks of the 8-wave form, which round 3
+//    preferred over the 4-wave 2 x 2 one (11.0 -> 10.1 us): LSTM trunk 71.0 -> 69.4 us, PWYX-RGB
+//    113.4 -> 111.9 us (profiles/r06fwd64; smaller conv3 tiles measured 5-14 % slower).
 template <class G, bool POOL>
 struct DConvFor {
   static constexpr bool SMALLC = G::CIN % 16 != 0;  // conv1: the whole K in one chunk
   static constexpr bool C64 = G::COUT >= 64;
   static constexpr int WN = C64 ? (POOL ? 2 : 4) : 1;
-  static constexpr int WM = C64 ? (POOL ? 4 : 2) : (SMALLC ? 4 : 8);
+  static constexpr int WM = C64 ? (POOL ? 4 : 1) : (SMALLC ? 4 : 8);
   static constexpr int TMW = SMALLC ? (G::S > 1 ? 1 : 2) : 1;
   // weight chunk: one tap for the 5x5 layers; 4 / 3 taps for the 4x4 / 3x3 ones (one tap left their
   // blocks 16 / 9 chunk steps of 16-32 MFMAs per wave, each behind a barrier)
