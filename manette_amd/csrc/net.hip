@@ -245,9 +245,11 @@ template <class G>
 using TileConvFwd = typename TileFor<G::COUT, conv_bk<G::KK>()>::T;
 template <class G>
 using TileConvWgrad = typename TileFor<G::COUT, 64>::T;
-// dX: BK 64 = half the LDS of 128, twice the resident workgroups (LSTM conv2 dX -5 %, Pong conv2 dX -7 %)
+// dX: BK 64 = half the LDS of 128, twice the resident workgroups (LSTM conv2 dX -5 %, Pong conv2 dX -7 %);
+// 32 for the 64-channel inputs (LSTM conv4 group 59.6 -> 56.1 us, NATURE conv3 39.6 -> 38.7; the thin
+// CIN-32 tile is slower at 32: LSTM conv3 181.6 -> 190.8, profiles/r06dg)
 template <class G>
-using TileConvDgrad = typename TileFor<G::CIN, 64>::T;
+using TileConvDgrad = typename TileFor<G::CIN, G::CIN >= 64 ? 32 : 64>::T;
 
 using TileFc = Tile<32, 64, 2, 2, 64>;       // dense forward, M = batch (small), split-K
 // dense dW (GEMM-K = batch: 160 = 2 chunks at ec=32) and dX (GEMM-K = F, M = batch): latency-bound
