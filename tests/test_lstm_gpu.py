@@ -201,6 +201,45 @@ def test_lstm_frame_store_parity(E, T, depth):
     np.testing.assert_allclose(terms.cpu().numpy(), aux['terms'], rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize('E,T,depth', [(4, 5, 1), (3, 2, 3)])
+def test_lstm_step_forward_xsum_cache_bit_exact(E, T, depth):
+    """mt_lstm_step_forward's per-frame x-product sums (step 0 stores every frame's, steps t > 0 read
+    the four older window positions from the cache, lstm.h XS) give exactly what the uncached
+    mt_lstm_windows_forward computes from the slabs — over two rollouts with a parameter change
+    between them (the cache is rebuilt at step 0), episode ends inside the rollout and leading
+    zero frames."""
+    A, R = 9, 11
+    net = _net(depth, A, R, seed=7 * E + T)
+    rs = np.random.RandomState(31 * E + T)
+    C = 4 * depth
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    for rollout in range(2):
+        fstore = rs.randint(0, 256, size=(1 + (T + 5) * E, 84, 84, C)).astype(np.uint8)
+        fstore[0] = 0
+        fs_d = d(fstore)
+        nz = np.zeros((T + 1, E), np.int32)
+        nz[0] = rs.choice([0, 0, 2, 5], size=E)
+        over = rs.rand(T + 1, E) < 0.3  # step t-1's episode ends, read by step t
+        nz_d = d(nz)
+        over_d = d(over.astype(np.float32))
+        got = [tuple(torch.zeros(*sh, device='cuda') for sh in ((E,), (E, A), (E, R))) for _ in range(T + 1)]
+        for t in range(T + 1):
+            net.lstm_step_forward(fs_d, t, E, T, nz_d, over_d[t - 1] if t > 0 else None, out=got[t])
+        torch.cuda.synchronize()
+        # the uncached windows over the same frame store (every row's x-product is in the workspace)
+        # and the nz the steps derived on the device
+        nz_dev = nz_d.clone()
+        for t in range(T + 1):
+            ref = tuple(torch.zeros(*sh, device='cuda') for sh in ((E,), (E, A), (E, R)))
+            net.lstm_windows_forward(nz_dev[t].contiguous(), t, E, T, out=ref)
+            torch.cuda.synchronize()
+            for a, b in zip(got[t], ref):
+                np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+        if rollout == 0:  # new parameters: the next rollout's step 0 must rebuild the cache
+            with torch.no_grad():
+                net.params.mul_(0.97).add_(0.001)
+
+
 @pytest.mark.parametrize('pipeline', [True, False])
 def test_lstm_learner_memory_windows(tmp_path, pipeline):
     """The learner's LSTM windows (frame store + nz, read at every step and by the train
