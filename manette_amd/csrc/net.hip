@@ -31,7 +31,7 @@ struct NipsArch {  // networks.py:178-192
   static constexpr int FLAT = 9 * 9 * 32;  // 2592
   static constexpr int F = 256;
   static constexpr const char *FC = "fc3";
-  static constexpr int FUSED_SLABS = FusedNips<C>::ROWS2;  // inference forward: trunk_fused.h
+  static constexpr int FUSED_SLABS = FusedNips<C>::FC_SPLITS;  // inference forward: trunk_fused.h
   static constexpr int FC_ROWS = 0;                         // (the fused trunk has its own dense kernel)
   static constexpr bool LSTM = false;
 };
@@ -1321,7 +1321,7 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
     MT_LAUNCHED();
     if (marks) MT_HIP(hipEventRecord(marks[1], s));
     HeadParams hp = head_params(n, P);
-    return launch_heads(B, s, ws + L.fcslab, Fz::ROWS2, B, Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation,
+    return launch_heads(B, s, ws + L.fcslab, Fz::FC_SPLITS, B, Wfc + (size_t)Ar::FLAT * Ar::F, n->cfg.activation,
                         n->cfg.alpha_leaky, hp, n->cfg.softmax_temp, A.base + A.h_off, v, pi, rep,
                         smp ? *smp : SampleArgs{});
   } else {
@@ -1332,7 +1332,7 @@ static int forward_infer_impl(const mt_net *n, const float *P, const uint8_t *ob
 
 // Bootstrap forward without its heads (mt_rollout's last chain with MT_ROLLOUT_BOOT_SLABS): the
 // trunk + the dense layer's split-K slabs left in ws (ws_layout(B).fcslab; NIPS: the fused trunk's
-// ROWS2 slabs, else fc_splits), whose sum, bias, act and critic the update's loss kernel takes
+// FC_SPLITS slabs, else fc_splits), whose sum, bias, act and critic the update's loss kernel takes
 // (mt_returns_loss_backward_boot). st: the NIPS stacking source; advance: the replayed rollout's
 // sequence bases (the fused dense kernel advances them).
 template <class Ar>

@@ -16,9 +16,9 @@
 //    rollout chain) each block waits for ITS env's publication by the emulator thread and reads
 //    the frames from the pinned staging itself: an env's convs run while the later envs are still
 //    being emulated, with no pull kernel and no kernel boundary in front of them.
-// 2. nips_fc_kernel — the dense layer as a real GEMM: block = (16 output columns, conv2 row i,
-//    32 envs); slab[i][e][n] = sum_{f < 288} act2[e][288 i + f] Wfc[288 i + f][n] on MFMA. Each
-//    fc weight is read once per 32 envs (the former one-launch trunk streamed the row's 295 KB
+// 2. nips_fc_kernel — the dense layer as a real GEMM: block = (16 output columns, K-split i of 8,
+//    16 envs); slab[i][e][n] = sum over split i's features f of act2[e][f] Wfc[f][n] on MFMA. Each
+//    fc weight is read once per 16 envs (the former one-launch trunk streamed the row's 295 KB
 //    weight chunk through every (env, row) block: 85 MB of L2 -> CU traffic at E = 32).
 //
 // Convs and fc run on v_mfma_f32_16x16x4_f32 (exact fp32) with the 4 waves splitting K; the 4
@@ -102,6 +102,10 @@ struct FusedNips {
   // from L2 / MALL and its 40 dependent MFMAs per wave were the 2.3 us block — half the envs per block
   // halves both, the column block's weights are read by two adjacent blocks of one XCD)
   static constexpr int FC_BN = 16, FC_BM = 16, FC_KC = FEAT / 16;  // 18 K chunks of 16
+  // K-splits of the dense layer = the slabs the heads kernel sums: 8 (20-21 chunks of 16 each), so
+  // E = 32 takes 16 x 8 x 2 = 256 blocks — one per CU — where 9 (one per conv2 row) put two of its
+  // 288 blocks on 32 CUs (block 1.7 us, 2.5 us on those)
+  static constexpr int FC_SPLITS = 8;
 };
 
 // Stage input rows 8i..8i+19 of env e into xin. STACK: build them from the previous state and
@@ -436,11 +440,14 @@ __global__ __launch_bounds__(FusedNips<C>::NT) void nips_conv_kernel(const uint8
 // those bases in the replay has run.
 constexpr int kRowFcBN = 16, kRowFcBM = 32;
 // Block pb of a (gx, gy, gz) = (F / 16, ROWS, env chunks of BM) grid.
-template <int FEAT, int ROWS, int F, int BM = kRowFcBM>
+// SPLITS: K-splits (slabs) of the FLAT = FEAT x ROWS inputs, split i = 16-wide chunks
+// [TC i / SPLITS, TC (i + 1) / SPLITS) — one conv output row each when SPLITS = ROWS
+template <int FEAT, int ROWS, int F, int BM = kRowFcBM, int SPLITS = ROWS>
 __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, const float *__restrict__ Wfc,
                                             float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by, int pb,
                                             int gx, int gy, int gz) {
-  constexpr int KC = FEAT / 16, FLAT = FEAT * ROWS, MT = BM / 16;
+  constexpr int FLAT = FEAT * ROWS, TC = FLAT / 16, MT = BM / 16;
+  constexpr int KC = (TC + SPLITS - 1) / SPLITS;  // chunks of the longest split
   static_assert(FEAT % 16 == 0 && F % kRowFcBN == 0 && BM % 16 == 0, "whole chunks, column blocks, M-tiles");
   __shared__ __attribute__((aligned(16))) float red[4][BM][kRowFcBN];
   if (advance && pb == 0 && threadIdx.x == 0) {
@@ -455,6 +462,7 @@ __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, 
   const int zc = L % gz, xy = L / gz;
   const int xb = xy % gx, i = xy / gx;
   const int n0 = xb * kRowFcBN, e0 = zc * BM;
+  const int c0 = (TC * i) / SPLITS, c1 = (TC * (i + 1)) / SPLITS;  // the split's chunks
   MT_PROBE_AT(1, pb, 0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -466,8 +474,8 @@ __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, 
   for (int t = 0; t < MT; ++t) rowt[t] = min(e0 + 16 * t + r, B - 1);
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
-    const int c = min(w + 4 * j, KC - 1);  // (chunks past the row's last are loaded but not used)
-    const int k0 = i * FEAT + 16 * c + 4 * g;
+    const int c = min(c0 + w + 4 * j, c1 - 1);  // (chunks past the split's last are loaded but not used)
+    const int k0 = 16 * c + 4 * g;
 #pragma unroll
     for (int t = 0; t < MT; ++t) a[j][t] = *reinterpret_cast<const f32x4 *>(x + (size_t)rowt[t] * FLAT + k0);
 #pragma unroll
@@ -478,7 +486,7 @@ __device__ __forceinline__ void row_fc_body(const float *__restrict__ x, int B, 
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
-    if (w + 4 * j < KC) {
+    if (c0 + w + 4 * j < c1) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -506,7 +514,7 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
                                                       uint32_t *advance, uint32_t advance_by) {
   using Fz = FusedNips<C>;
   static_assert(Fz::FC_BN == kRowFcBN, "tile");
-  row_fc_body<Fz::FEAT, Fz::ROWS2, Fz::F, Fz::FC_BM>(act2, B, Wfc, slabs, advance, advance_by,
+  row_fc_body<Fz::FEAT, Fz::ROWS2, Fz::F, Fz::FC_BM, Fz::FC_SPLITS>(act2, B, Wfc, slabs, advance, advance_by,
                                          (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gridDim.x,
                                          gridDim.y, gridDim.z);
 }
@@ -722,15 +730,23 @@ static inline int launch_nips_trunk(const uint8_t *obs, const StackSrc *st, int 
     hipLaunchKernelGGL(nips_conv_persist_kernel, dim3(std::min(B, cus)), dim3(PersistNips::NT), PersistNips::LDS, s,
                        obs, B, W1, W2, act, alpha, act2, act1);
     MT_LAUNCHED();
-    // the dense layer as a 64 x 64-tile GEMM in 9 K-splits of 288 (the slab count the heads kernel
-    // sums): nips_fc_kernel's 16-column blocks would re-read act2 16 times at this batch
-    return launch_gemm<Tile<64, 64, 2, 2, 96>>(LdRowMajor{act2, Fz::FLAT}, LdColMajor{Wfc, Fz::F, -1},
-                                               EpSlab{slabs, B, Fz::F}, B, Fz::F, Fz::FLAT, Fz::ROWS2, s);
+    // the dense layer as a 64 x 64-tile GEMM in FC_SPLITS K-splits (the slab count the heads kernel
+    // sums: 8 of 352 / 128 with 32-deep chunks): nips_fc_kernel's 16-column blocks would re-read act2
+    // 16 times at this batch
+    using TP = Tile<64, 64, 2, 2, 32>;
+    static_assert(Fz::FLAT % TP::BK == 0, "whole chunks");
+    if (gemm_splits<TP>(Fz::FLAT, Fz::FC_SPLITS) != Fz::FC_SPLITS) {
+      set_error("persistent NIPS trunk: %d dense K-splits, the heads sum %d", gemm_splits<TP>(Fz::FLAT, Fz::FC_SPLITS),
+                Fz::FC_SPLITS);
+      return MT_ERR_ARG;
+    }
+    return launch_gemm<TP>(LdRowMajor{act2, Fz::FLAT}, LdColMajor{Wfc, Fz::F, -1}, EpSlab{slabs, B, Fz::F}, B, Fz::F,
+                           Fz::FLAT, Fz::FC_SPLITS, s);
   } else {
     hipLaunchKernelGGL((nips_conv_kernel<C, false>), dim3(Fz::BPE * B), dim3(Fz::NT), Fz::LDS_BYTES, s, obs,
                        StackSrc{}, B, W1, W2, act, alpha, act2, act1);
   }
-  hipLaunchKernelGGL(nips_fc_kernel<C>, dim3(Fz::F / Fz::FC_BN, Fz::ROWS2, (B + Fz::FC_BM - 1) / Fz::FC_BM),
+  hipLaunchKernelGGL(nips_fc_kernel<C>, dim3(Fz::F / Fz::FC_BN, Fz::FC_SPLITS, (B + Fz::FC_BM - 1) / Fz::FC_BM),
                      dim3(256), 0, s, act2, B, Wfc, slabs, advance, advance_by);
   return MT_OK;
 }

@@ -20,6 +20,6 @@ def test_probe_build_runs_the_rollout_chain():
     assert out.returncode == 0, out.stderr[-2000:]
     lines = out.stdout.splitlines()
     # every kernel of the chain recorded its blocks' phases (conv: 9 blocks per env)
-    for name, blocks in (('conv', 9 * 32), ('fc', 16 * 9 * 2), ('heads', 32)):  # (fc: 16-env tiles)
+    for name, blocks in (('conv', 9 * 32), ('fc', 16 * 8 * 2), ('heads', 32)):  # (fc: 8 K-splits x 16-env tiles)
         hit = [ln for ln in lines if ln.startswith(name + ' ') and 'blocks' in ln]
         assert hit and int(hit[0].split()[2]) == blocks, (name, lines)

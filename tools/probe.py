@@ -142,7 +142,7 @@ def main():
                                      us(np.median(h[:, 3] - h[:, 2]))))
         L.cleanup()
         return
-    nblocks = {0: int((P[0, :, 0] != 0).sum()), 1: 16 * 9 * ((E + 15) // 16), 2: E}  # (conv: 9 per env; fc: 16-env tiles)
+    nblocks = {0: int((P[0, :, 0] != 0).sum()), 1: 16 * 8 * ((E + 15) // 16), 2: E}  # (conv: 9 per env; fc: 8 K-splits x 16-env tiles)
     t0 = P[0, :nblocks[0], 0].min()
     if R[:, 0].any():  # a pull kernel ran (non-stacking chains)
         seen, done = R[:, 0] - t0, R[:, 1] - t0
