@@ -46,6 +46,9 @@ struct NatureArch {  // networks.py:261-278
   static constexpr const char *FC = "fc4";
   static constexpr int FUSED_SLABS = 0;  // no fused inference trunk: layered path
   static constexpr int FC_ROWS = 7;      // dense layer by conv3 rows (row_fc_kernel)
+  // its K-splits (= slabs): 8, 512 blocks at E = 32 / 64 (two per CU) instead of 7 rows' 448
+  // (Breakout isolated step forward 39.5 -> 38.5 us; 4 splits, 256 blocks: slower; profiles/r06fcs)
+  static constexpr int FC_SPLITS = 8;
   static constexpr bool LSTM = false;
 };
 template <int C>
@@ -59,6 +62,7 @@ struct PwyxArch {  // networks.py:206-225: SAME convs, 2x2 pools after conv1-3
   static constexpr const char *FC = "fc5";
   static constexpr int FUSED_SLABS = 0;
   static constexpr int FC_ROWS = 10;  // dense layer by conv4 rows (row_fc_kernel)
+  static constexpr int FC_SPLITS = 8;  // its K-splits: 512 blocks at E = 32 (10: 640), as NATURE's
   static constexpr bool LSTM = false;
 };
 
@@ -294,7 +298,7 @@ static size_t conv_wgrad_slab(int B) {
 
 template <class Ar>
 static int fc_splits(int B, int F) {
-  if constexpr (Ar::FC_ROWS > 0) return Ar::FC_ROWS;  // row_fc_kernel: one slab per conv output row
+  if constexpr (Ar::FC_ROWS > 0) return Ar::FC_SPLITS;  // row_fc_kernel's K-splits
   const int s = pick_splits(cdiv(B, TileFc::BM) * cdiv(F, TileFc::BN), Ar::FLAT, TileFc::BK, 128);
   return gemm_splits<TileFc>(Ar::FLAT, s);
 }
@@ -307,7 +311,8 @@ template <class Ar>
 static int launch_fc(const float *flat, int B, const float *Wfc, float *slabs, int splits, hipStream_t s,
                      uint32_t *advance = nullptr, uint32_t advance_by = 0) {
   if constexpr (Ar::FC_ROWS > 0)
-    return launch_row_fc<Ar::FLAT / Ar::FC_ROWS, Ar::FC_ROWS, Ar::F>(flat, B, Wfc, slabs, s, advance, advance_by);
+    return launch_row_fc<Ar::FLAT / Ar::FC_ROWS, Ar::FC_ROWS, Ar::F, Ar::FC_SPLITS>(flat, B, Wfc, slabs, s, advance,
+                                                                                  advance_by);
   else
     return launch_gemm<TileFc>(LdRowMajor{flat, Ar::FLAT}, LdColMajor{Wfc, Ar::F, -1}, EpSlab{slabs, B, Ar::F}, B,
                                Ar::F, Ar::FLAT, splits, s);

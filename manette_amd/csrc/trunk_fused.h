@@ -523,23 +523,24 @@ __global__ __launch_bounds__(256) void nips_fc_kernel(const float *__restrict__ 
 // of BM env rows: 16 up to 32 envs (the 16-env tiles of the NIPS dense kernel: Seaquest E = 32 5.24
 // -> 4.95 us, PWYX-RGB 8.86 -> 8.04 us per launch), 32 beyond (Breakout E = 64: 6.95 vs 7.28 us with
 // 16: its column block's weights would be read by four blocks instead of two; profiles/r06rf)
-template <int FEAT, int ROWS, int F, int BM>
+template <int FEAT, int ROWS, int F, int BM, int SPLITS = ROWS>
 __global__ __launch_bounds__(256) void row_fc_kernel(const float *__restrict__ x, int B, const float *__restrict__ Wfc,
                                                      float *__restrict__ slabs, uint32_t *advance, uint32_t advance_by) {
-  row_fc_body<FEAT, ROWS, F, BM>(x, B, Wfc, slabs, advance, advance_by,
+  row_fc_body<FEAT, ROWS, F, BM, SPLITS>(x, B, Wfc, slabs, advance, advance_by,
                                  (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, gridDim.x, gridDim.y,
                                  gridDim.z);
 }
-template <int FEAT, int ROWS, int F>
+template <int FEAT, int ROWS, int F, int SPLITS = ROWS>
 static inline int launch_row_fc(const float *x, int B, const float *Wfc, float *slabs, hipStream_t s,
                                 uint32_t *advance = nullptr, uint32_t advance_by = 0) {
   if (B <= 0 || !launch_allowed()) return MT_OK;
   if (B <= 32)
-    hipLaunchKernelGGL((row_fc_kernel<FEAT, ROWS, F, 16>), dim3(F / kRowFcBN, ROWS, (B + 15) / 16), dim3(256), 0, s,
-                       x, B, Wfc, slabs, advance, advance_by);
+    hipLaunchKernelGGL((row_fc_kernel<FEAT, ROWS, F, 16, SPLITS>), dim3(F / kRowFcBN, SPLITS, (B + 15) / 16), dim3(256),
+                       0, s, x, B, Wfc, slabs, advance, advance_by);
   else
-    hipLaunchKernelGGL((row_fc_kernel<FEAT, ROWS, F, kRowFcBM>), dim3(F / kRowFcBN, ROWS, (B + kRowFcBM - 1) / kRowFcBM),
-                       dim3(256), 0, s, x, B, Wfc, slabs, advance, advance_by);
+    hipLaunchKernelGGL((row_fc_kernel<FEAT, ROWS, F, kRowFcBM, SPLITS>),
+                       dim3(F / kRowFcBN, SPLITS, (B + kRowFcBM - 1) / kRowFcBM), dim3(256), 0, s, x, B, Wfc, slabs,
+                       advance, advance_by);
   MT_LAUNCHED();
   return MT_OK;
 }

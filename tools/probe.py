@@ -130,7 +130,7 @@ def main():
                 ' '.join('%+.1f' % rel(x) for x in b[:, 3])))
         print('chain  last env %d: seen 0, conv1 %+.2f, conv2 %+.2f, conv3 %+.2f us' % (
             e_last, rel(X[e_last, 1]), rel(X[e_last, 2]), rel(X[e_last, 3])))
-        nfc = 32 * 7 * ((E + 15) // 16 if E <= 32 else (E + 31) // 32)  # (row_fc tiles: 16 envs up to E = 32)
+        nfc = 32 * 8 * ((E + 15) // 16 if E <= 32 else (E + 31) // 32)  # (row_fc: 8 K-splits, 16-env tiles up to E = 32)
         f = P[1, :nfc, :3]
         print('fc     blocks %d start %+.2f..%+.2f end %+.2f..%+.2f us (rel. last publish), block med %.2f' % (
             nfc, rel(f[:, 0].min()), rel(f[:, 0].max()), rel(f[:, 2].min()), rel(f[:, 2].max()),
