@@ -10,4 +10,5 @@ for c in ${CONFIGS:-pong-nips breakout-nature-figar seaquest-nature breakout-pwy
   rc=$?
   echo "$c rc=$rc"
   case $rc in 124|137|134|139) echo "fault-like exit in $c, stopping"; exit $rc;; esac
+  sleep 5  # (the previous line's CPU-baseline worker processes finish exiting before the next timed region)
 done
