@@ -523,27 +523,54 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   // column loop a divergent one — ~0.45 us per column of a wave, probe build.)
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const int jn = F >> 6;
-  for (int o = wu; o < O; o += 4) {
-    int base, stride, bias;
-    head_col_lds(hp, o, base, stride, bias);
-    float acc = 0.f;
-    if ((F & 63) == 0) {
-      float hv[FMAX], wv[FMAX];
+  if ((F & 63) == 0) {
+    // The wave's features read once; outputs o and o + 4 per pass, every operand of both columns
+    // (and their biases) requested at once. Lane offsets by 24-bit multiplies and wave-uniform term
+    // offsets (j clamped to the last real term): the per-term 32-bit multiplies were quarter-rate,
+    // and the bias a dependent LDS round trip after the reduction (round 6: 1.8 us for Seaquest's
+    // 20 outputs, probe build).
+    float hv[FMAX];
 #pragma unroll
-      for (int j = 0; j < FMAX; ++j) {  // every operand of the column requested at once
-        hv[j] = hs[min(lane + 64 * j, 256 * FT - 1)];
-        wv[j] = Ws[base + min(lane + 64 * j, F - 1) * stride];
+    for (int j = 0; j < FMAX; ++j) hv[j] = hs[min(lane + 64 * j, 256 * FT - 1)];
+    for (int o0 = wu; o0 < O; o0 += 8) {
+      const int o1 = o0 + 4 < O ? o0 + 4 : o0;
+      int b0, s0, c0, b1, s1, c1;
+      head_col_lds(hp, o0, b0, s0, c0);
+      head_col_lds(hp, o1, b1, s1, c1);
+      const int l0 = b0 + __mul24(lane, s0), l1 = b1 + __mul24(lane, s1);
+      float w0[FMAX], w1[FMAX];
+#pragma unroll
+      for (int j = 0; j < FMAX; ++j) {
+        const int jj = min(j, jn - 1);
+        w0[j] = Ws[l0 + jj * 64 * s0];
+        w1[j] = Ws[l1 + jj * 64 * s1];
       }
+      const float bias0 = Ws[c0], bias1 = Ws[c1];
+      float a0 = 0.f, a1 = 0.f;
 #pragma unroll
       for (int j = 0; j < FMAX; ++j)
-        if (j < jn) acc += hv[j] * wv[j];
-    } else {
+        if (j < jn) {
+          a0 += hv[j] * w0[j];
+          a1 += hv[j] * w1[j];
+        }
+      a0 = wave_sum(a0);
+      a1 = wave_sum(a1);
+      if (lane == 0) {
+        zs[o0] = a0 + bias0;
+        if (o1 != o0) zs[o1] = a1 + bias1;
+      }
+    }
+  } else {
+    for (int o = wu; o < O; o += 4) {
+      int base, stride, bias;
+      head_col_lds(hp, o, base, stride, bias);
+      float acc = 0.f;
 #pragma unroll
       for (int j = 0; j < FMAX; ++j)
         if (lane + 64 * j < F) acc += hs[lane + 64 * j] * Ws[base + (lane + 64 * j) * stride];
+      acc = wave_sum(acc);
+      if (lane == 0) zs[o] = acc + Ws[bias];
     }
-    acc = wave_sum(acc);
-    if (lane == 0) zs[o] = acc + Ws[bias];
   }
   __syncthreads();
   MT_PROBE_AT(2, b, 2);
