@@ -404,11 +404,14 @@ static HeadParams head_params(const mt_net *n, const float *P) {
 // Head output o (0 = critic, 1..A = actor, 1+A.. = repetition) inside the head region staged in
 // LDS (heads_row): offset of its weight for feature 0, the feature stride, and its bias.
 __device__ __forceinline__ void head_col_lds(const HeadParams &hp, int o, int &base, int &stride, int &bias) {
+  // selects only (no branches): o is wave-uniform, so these are a few scalar instructions
   const int oa = (int)(hp.Wa - hp.Wc), orr = (int)(hp.Wr - hp.Wc);
   const bool c = o == 0, a = o <= hp.A;
-  base = c ? 0 : (a ? oa + (o - 1) : orr + (o - 1 - hp.A));
-  stride = c ? 1 : (a ? hp.A : hp.R);
-  bias = c ? hp.F : (a ? oa + hp.F * hp.A + (o - 1) : orr + hp.F * hp.R + (o - 1 - hp.A));
+  const int k = a ? o - 1 : o - 1 - hp.A;  // column within the actor / repetition block
+  const int w0 = a ? oa : orr, st = a ? hp.A : hp.R;
+  base = c ? 0 : w0 + k;
+  stride = c ? 1 : st;
+  bias = c ? hp.F : w0 + hp.F * st + k;
 }
 
 // Softmax over n logits held in lanes [0, n) of one wave (x/temp, TF: exp(x-max)/sum).
