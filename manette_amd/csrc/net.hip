@@ -483,14 +483,17 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
 #pragma unroll
     for (int u = 0; u < SB; ++u) t[fi][u] = p[(size_t)min(u, S - 1) * zs_stride];
   }
-  // (3) dense bias, then the head region's first kHeadQ * 256 quads
+  // (3) dense bias, then the head region's first KQ * 256 quads (F > 256: 11, so the whole region of
+  // an A = 18, R = 1 head set (Seaquest, 2,593 quads) is requested here — the remainder loop below
+  // was a second global round trip, ~0.5 us)
+  constexpr int KQ = FT == 1 ? kHeadQ : 11;
   float fb[FT];
 #pragma unroll
   for (int fi = 0; fi < FT; ++fi) fb[fi] = fc_b[min((int)threadIdx.x + 256 * fi, F - 1)];
   const f32x4 *hsrc = reinterpret_cast<const f32x4 *>(hp.Wc);
-  f32x4 wq[kHeadQ];
+  f32x4 wq[KQ];
 #pragma unroll
-  for (int q = 0; q < kHeadQ; ++q) wq[q] = hsrc[min((int)threadIdx.x + 256 * q, hp.nq - 1)];
+  for (int q = 0; q < KQ; ++q) wq[q] = hsrc[min((int)threadIdx.x + 256 * q, hp.nq - 1)];
   if (smp.advance && b == 0 && threadIdx.x == 0) {  // the replayed rollout's last reader has run
     smp.advance[0] += smp.advance_by;
     smp.advance[1] += smp.advance_by;
@@ -512,12 +515,12 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
       H[(size_t)b * F + f] = h;
     }
   }
-  // the head region into LDS (the rest of a region larger than kHeadQ * 256 quads loaded here)
+  // the head region into LDS (the rest of a region larger than KQ * 256 quads loaded here)
   f32x4 *wdst = reinterpret_cast<f32x4 *>(Ws);
 #pragma unroll
-  for (int q = 0; q < kHeadQ; ++q)
+  for (int q = 0; q < KQ; ++q)
     if ((int)threadIdx.x + 256 * q < hp.nq) wdst[threadIdx.x + 256 * q] = wq[q];
-  for (int i = threadIdx.x + 256 * kHeadQ; i < hp.nq; i += 256) wdst[i] = hsrc[i];
+  for (int i = threadIdx.x + 256 * KQ; i < hp.nq; i += 256) wdst[i] = hsrc[i];
   __syncthreads();
   MT_PROBE_AT(2, b, 1);
   // logits: the same products and order as a column walk f = lane, lane + 64, ... then the bias.
