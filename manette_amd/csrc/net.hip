@@ -439,11 +439,11 @@ __device__ __forceinline__ int wave_draw(float p, int n, double u) {
   return res;
 }
 
-// One workgroup per row b (4 waves):
+// One workgroup per row b (NT / 64 waves: 4 for F <= 256, 8 for F <= 512):
 //  1. h = act(sum_z slabs[z][b] + b_fc) — the split-K dense layer finished here
-//     (networks.py:57-70); every thread owns F/256 features;
+//     (networks.py:57-70); every thread owns F/NT features;
 //  2. logits_o = [h, 1] . W_o for the 1+A+R head outputs (policy_v_network.py:22, :31, :47):
-//     wave w takes outputs o = w, w+4, ...; lanes split F and reduce with DPP;
+//     wave w takes outputs o = w, w + NW, ...; lanes split F and reduce with DPP;
 //  3. wave 0: v = logit_0, pi = softmax(logits_A / temp), rep = softmax(logits_R / temp);
 //  4. rollout path (smp.counters != null): wave 0 draws (a, r) for the row (A3, common.h).
 // Latency is everything here (32 blocks at E = 32, on the macro-step's critical chain), so every
@@ -458,17 +458,18 @@ __device__ __forceinline__ int wave_draw(float p, int n, double u) {
 constexpr int kHeadQ = 8;  // region quads per thread held in registers from the kernel start
 __device__ uint64_t g_zero_u64 = 0;  // read in place of an absent draw counter / sequence base
 
-template <int FT, int SB>
+template <int FT, int SB, int NT>
 __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs, int S, int B,
                                           const float *__restrict__ fc_b, int act, float alpha, const HeadParams &hp,
                                           float temp, float *__restrict__ H, float *__restrict__ v,
                                           float *__restrict__ pi, float *__restrict__ rep, const SampleArgs &smp,
                                           float *Ws) {
-  __shared__ float hs[256 * FT];
+  __shared__ float hs[NT * FT];
   __shared__ float zs[64];
   const int F = hp.F, O = 1 + hp.A + hp.R;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  constexpr int FMAX = 4 * FT;
+  constexpr int FMAX = NT * FT / 64;  // feature terms per lane of a column walk
+  constexpr int NW = NT / 64;
   // every load below is unconditional (clamped addresses, zeros by select): a guarded load would
   // end its basic block with a wait for it
   // (1) the draw counter and the sequence base (the uniforms need them first)
@@ -479,21 +480,21 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   float t[FT][SB];
 #pragma unroll
   for (int fi = 0; fi < FT; ++fi) {
-    const float *p = slabs + (size_t)b * F + min((int)threadIdx.x + 256 * fi, F - 1);
+    const float *p = slabs + (size_t)b * F + min((int)threadIdx.x + NT * fi, F - 1);
 #pragma unroll
     for (int u = 0; u < SB; ++u) t[fi][u] = p[(size_t)min(u, S - 1) * zs_stride];
   }
-  // (3) dense bias, then the head region's first KQ * 256 quads (F > 256: 11, so the whole region of
-  // an A = 18, R = 1 head set (Seaquest, 2,593 quads) is requested here — the remainder loop below
-  // was a second global round trip, ~0.5 us)
-  constexpr int KQ = FT == 1 ? kHeadQ : 11;
+  // (3) dense bias, then the head region's first KQ * NT quads (F > 256 on 512 threads: 6, so the
+  // whole region of an A = 18, R = 1 head set (Seaquest, 2,593 quads) is requested here — the
+  // remainder loop below was a second global round trip, ~0.5 us)
+  constexpr int KQ = NT == 512 ? 6 : kHeadQ;
   float fb[FT];
 #pragma unroll
-  for (int fi = 0; fi < FT; ++fi) fb[fi] = fc_b[min((int)threadIdx.x + 256 * fi, F - 1)];
+  for (int fi = 0; fi < FT; ++fi) fb[fi] = fc_b[min((int)threadIdx.x + NT * fi, F - 1)];
   const f32x4 *hsrc = reinterpret_cast<const f32x4 *>(hp.Wc);
   f32x4 wq[KQ];
 #pragma unroll
-  for (int q = 0; q < KQ; ++q) wq[q] = hsrc[min((int)threadIdx.x + 256 * q, hp.nq - 1)];
+  for (int q = 0; q < KQ; ++q) wq[q] = hsrc[min((int)threadIdx.x + NT * q, hp.nq - 1)];
   if (smp.advance && b == 0 && threadIdx.x == 0) {  // the replayed rollout's last reader has run
     smp.advance[0] += smp.advance_by;
     smp.advance[1] += smp.advance_by;
@@ -503,7 +504,7 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   // slab sum in slab order + bias + activation
 #pragma unroll
   for (int fi = 0; fi < FT; ++fi) {
-    const int f = threadIdx.x + 256 * fi;
+    const int f = threadIdx.x + NT * fi;
     float acc = 0.f;
 #pragma unroll
     for (int u = 0; u < SB; ++u)
@@ -515,12 +516,12 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
       H[(size_t)b * F + f] = h;
     }
   }
-  // the head region into LDS (the rest of a region larger than KQ * 256 quads loaded here)
+  // the head region into LDS (the rest of a region larger than KQ * NT quads loaded here)
   f32x4 *wdst = reinterpret_cast<f32x4 *>(Ws);
 #pragma unroll
   for (int q = 0; q < KQ; ++q)
-    if ((int)threadIdx.x + 256 * q < hp.nq) wdst[threadIdx.x + 256 * q] = wq[q];
-  for (int i = threadIdx.x + 256 * KQ; i < hp.nq; i += 256) wdst[i] = hsrc[i];
+    if ((int)threadIdx.x + NT * q < hp.nq) wdst[threadIdx.x + NT * q] = wq[q];
+  for (int i = threadIdx.x + NT * KQ; i < hp.nq; i += NT) wdst[i] = hsrc[i];
   __syncthreads();
   MT_PROBE_AT(2, b, 1);
   // logits: the same products and order as a column walk f = lane, lane + 64, ... then the bias.
@@ -530,16 +531,16 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const int jn = F >> 6;
   if ((F & 63) == 0) {
-    // The wave's features read once; outputs o and o + 4 per pass, every operand of both columns
+    // The wave's features read once; outputs o and o + NW per pass, every operand of both columns
     // (and their biases) requested at once. Lane offsets by 24-bit multiplies and wave-uniform term
     // offsets (j clamped to the last real term): the per-term 32-bit multiplies were quarter-rate,
     // and the bias a dependent LDS round trip after the reduction (round 6: 1.8 us for Seaquest's
     // 20 outputs, probe build).
     float hv[FMAX];
 #pragma unroll
-    for (int j = 0; j < FMAX; ++j) hv[j] = hs[min(lane + 64 * j, 256 * FT - 1)];
-    for (int o0 = wu; o0 < O; o0 += 8) {
-      const int o1 = o0 + 4 < O ? o0 + 4 : o0;
+    for (int j = 0; j < FMAX; ++j) hv[j] = hs[min(lane + 64 * j, NT * FT - 1)];
+    for (int o0 = wu; o0 < O; o0 += 2 * NW) {
+      const int o1 = o0 + NW < O ? o0 + NW : o0;
       int b0, s0, c0, b1, s1, c1;
       head_col_lds(hp, o0, b0, s0, c0);
       head_col_lds(hp, o1, b1, s1, c1);
@@ -567,7 +568,7 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
       }
     }
   } else {
-    for (int o = wu; o < O; o += 4) {
+    for (int o = wu; o < O; o += NW) {
       int base, stride, bias;
       head_col_lds(hp, o, base, stride, bias);
       float acc = 0.f;
@@ -613,8 +614,8 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   }
 }
 
-template <int FT, int SB>
-__global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict__ slabs, int S, int B,
+template <int FT, int SB, int NT>
+__global__ __launch_bounds__(NT) void heads_fwd_kernel(const float *__restrict__ slabs, int S, int B,
                                                         const float *__restrict__ fc_b, int act,
                                                         float alpha, HeadParams hp, float temp,
                                                         float *__restrict__ H, float *__restrict__ v,
@@ -622,12 +623,13 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float *__restrict_
                                                         float *__restrict__ rep, SampleArgs smp) {
   extern __shared__ __attribute__((aligned(16))) float head_region[];
   MT_PROBE_AT(2, blockIdx.x, 0);
-  heads_row<FT, SB>(blockIdx.x, slabs, S, B, fc_b, act, alpha, hp, temp, H, v, pi, rep, smp, head_region);
+  heads_row<FT, SB, NT>(blockIdx.x, slabs, S, B, fc_b, act, alpha, hp, temp, H, v, pi, rep, smp, head_region);
   MT_PROBE_AT(2, blockIdx.x, 3);
 }
 
-// heads_fwd_kernel for F features (<= 512) and S slabs: the instantiation whose register arrays
-// hold exactly the row's features (FT = F / 256 rounded up) and slabs (SB >= S, else one batch of 16).
+// heads_fwd_kernel for F features (<= 512) and S slabs: one feature per thread (256 threads for
+// F <= 256, 512 above: the GEMV is instruction-issue bound with one wave per SIMD, so 8 waves take
+// fewer output passes each — round 6) and SB >= S slabs in registers (else one batch of 16).
 static int launch_heads(int rows, hipStream_t s, const float *slabs, int S, int B, const float *fc_b, int act,
                         float alpha, const HeadParams &hp, float temp, float *H, float *v, float *pi, float *rep,
                         const SampleArgs &smp) {
@@ -641,25 +643,25 @@ static int launch_heads(int rows, hipStream_t s, const float *slabs, int S, int 
     set_error("heads: head region of %zu bytes exceeds the LDS", lds);
     return MT_ERR_ARG;
   }
-#define MT_HEADS(FT_, SB_)                                                                                   \
+#define MT_HEADS(FT_, SB_, NT_)                                                                              \
   do {                                                                                                       \
     static bool attr_set = false;                                                                            \
     if (!attr_set && lds > 64 * 1024) {                                                                      \
-      MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&heads_fwd_kernel<FT_, SB_>),                \
+      MT_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&heads_fwd_kernel<FT_, SB_, NT_>),           \
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));                   \
       attr_set = true;                                                                                       \
     }                                                                                                        \
-    hipLaunchKernelGGL((heads_fwd_kernel<FT_, SB_>), dim3(rows), dim3(256), lds, s, slabs, S, B, fc_b, act,    \
-                       alpha, hp, temp, H, v, pi, rep, smp);                                                 \
+    hipLaunchKernelGGL((heads_fwd_kernel<FT_, SB_, NT_>), dim3(rows), dim3(NT_), lds, s, slabs, S, B, fc_b,    \
+                       act, alpha, hp, temp, H, v, pi, rep, smp);                                            \
   } while (0)
   if (hp.F <= 256) {
-    if (S <= 1) MT_HEADS(1, 1);
-    else if (S <= 9) MT_HEADS(1, 9);
-    else MT_HEADS(1, 16);
+    if (S <= 1) MT_HEADS(1, 1, 256);
+    else if (S <= 9) MT_HEADS(1, 9, 256);
+    else MT_HEADS(1, 16, 256);
   } else {
-    if (S <= 1) MT_HEADS(2, 1);
-    else if (S <= 9) MT_HEADS(2, 9);
-    else MT_HEADS(2, 16);
+    if (S <= 1) MT_HEADS(1, 1, 512);
+    else if (S <= 9) MT_HEADS(1, 9, 512);
+    else MT_HEADS(1, 16, 512);
   }
 #undef MT_HEADS
   MT_LAUNCHED();
