@@ -585,10 +585,17 @@ __device__ __forceinline__ void heads_row(int b, const float *__restrict__ slabs
   const float z = lane < O ? zs[lane] : 0.f;
   if (lane == 0) v[b] = z;
   // actor logits sit in lanes 1..A, repetition logits in lanes 1+A..A+R: shift them to 0..
-  const float za = __shfl(z, (lane + 1) & 63, 64) / temp;
-  const float zr = __shfl(z, (lane + 1 + hp.A) & 63, 64) / temp;
+  // (wave-uniform shortcuts with identical results for finite logits: x / 1 = x, and a one-way
+  // softmax is exp(0) / 1 = 1 — the two IEEE divisions and the whole repetition softmax were a
+  // third of this single wave's instructions for the non-FiGAR heads)
+  float za = __shfl(z, (lane + 1) & 63, 64);
+  float zr = __shfl(z, (lane + 1 + hp.A) & 63, 64);
+  if (temp != 1.f) {
+    za = za / temp;
+    zr = zr / temp;
+  }
   const float pa = wave_softmax(za, lane, hp.A);
-  const float pr = wave_softmax(zr, lane, hp.R);
+  const float pr = hp.R == 1 ? (lane == 0 ? 1.f : 0.f) : wave_softmax(zr, lane, hp.R);
   if (lane < hp.A) pi[(size_t)b * hp.A + lane] = pa;
   if (lane < hp.R) rep[(size_t)b * hp.R + lane] = pr;
   if (smp.counters) {
